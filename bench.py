@@ -1,0 +1,212 @@
+"""Headline benchmark: AutoInt CTR training samples/sec (BASELINE.json metric; configs[1]:
+26 fields x 16-dim embeddings, batch 4096 per GPU, embedding + 3 x InteractingLayer + MLP).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: launched by torch.distributed.run, one process per GPU, RCCL over xGMI)
+
+A step = one full training step on one synthetic batch: embedding lookup, IL x3, deep + logits
+MLP, clip + cross_entropy, backward, (N > 1: dense all-reduce + sparse row exchange), dense Adam
+and sparse Adam on the touched rows.  Batches (Zipf(1.2) ids over 26 x 100k vocab, Bernoulli(0.25)
+labels) are pre-generated in HBM; each step copies the next one into the step's static input.
+Prints ONE JSON line on rank 0 (value = samples/s over all ranks, weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+# SURVEY §8(d) / BASELINE.md: algorithmic work of config 2
+IL_FWD_FLOPS_PER_SAMPLE = 289_536          # 3 iterations x (proj 53,248 + QK^T 21,632 + PV 21,632)
+TRAIN_FLOPS_PER_SAMPLE = 954_144           # IL 868,608 + MLP 85,536 (train = 3 x fwd)
+FP32_PEAK_TFLOPS = 157.3                   # MI355X dense fp32 (MFMA == vector rate)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (config 2: 4096)")
+    ap.add_argument("--pool", type=int, default=8, help="distinct pre-generated batches")
+    ap.add_argument("--cpu-baseline-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    return ap.parse_args()
+
+
+def zipf_ids(rng, B, F, vocab, a=1.2):
+    z = rng.zipf(a, size=(B, F)) - 1
+    return np.minimum(z, vocab - 1).astype(np.int64)
+
+
+def time_kernel(fn, reps):
+    """Average device duration of one launch of `fn` (HIP events on torch's current stream, which
+    is the stream the kernel is enqueued on)."""
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3  # seconds
+
+
+def cpu_baseline(cfg, model, batches_cpu, steps):
+    from oracle import torch_ref as tr
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    il = {k: v.detach().double().cpu().numpy() for k, v in
+          dict(W=model.interact.kernel, bias=model.interact.bias, gamma=model.interact.gamma,
+               beta=model.interact.beta).items()}
+    deep = [(l.kernel.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in model.deep.layers]
+    logits = [(l.kernel.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in model.logits.layers]
+    ocfg = dict(layer_num=cfg.layer_num, head_num=cfg.head_num, use_res=cfg.use_res,
+                mlp_activation=cfg.mlp_activation, logits_activation=cfg.logits_activation)
+    ref = tr.AutoIntCPU(model.table.weight.cpu().numpy(), model.embedding.row_base.cpu().numpy(),
+                        model.embedding.bucket.cpu().numpy(), il, deep, logits, ocfg,
+                        dtype=torch.float32)
+    ids, labels = batches_cpu[0]
+    ref.step(ids, labels)  # warm-up
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ids, labels = batches_cpu[i % len(batches_cpu)]
+        ref.step(ids, labels)
+    dt = time.perf_counter() - t0
+    B = ids.shape[0]
+    return {"value": round(B * steps / dt, 1), "unit": "samples/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{steps} AutoInt train steps at batch {B} (26x16, IL x3, MLP, Adam) of the "
+                      f"TF-semantics fp32 torch-CPU restatement (oracle/torch_ref.py), "
+                      f"{threads} threads, {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
+    _lib.load()
+
+    cfg = AutoIntConfig()  # config 2: 26 x 16, vocab 100k/field, IL(3, 16, 2), mlp [32,16], [1]
+    B, F = args.batch, cfg.num_fields
+    model = AutoInt(cfg, device=dev, seed=0, max_batch=B, world_size=world)
+    trainer = AutoIntTrainer(model, B, process_group=pg)
+
+    rng = np.random.default_rng(2 + 1000 * rank)
+    lab_rng = np.random.default_rng(3 + 1000 * rank)
+    pool_cpu = [(torch.from_numpy(zipf_ids(rng, B, F, cfg.vocab_per_field)),
+                 torch.from_numpy((lab_rng.uniform(size=(B, 1)) < 0.25).astype(np.float32)))
+                for _ in range(args.pool)]
+    pool = [(i.to(dev), l.to(dev)) for i, l in pool_cpu]
+
+    trainer.load_batch(*pool[0])
+    trainer.capture(warmup=max(1, min(args.warmup, 3)))
+    for i in range(args.warmup):
+        trainer.step(*pool[i % len(pool)])
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(*pool[i % len(pool)])
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    loss = float(trainer.loss.item())
+
+    # ---- roofline of the dominant kernel (IL backward), HIP events on its stream ----
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    il = model.interact
+    E, U, H, L = cfg.embed_dim, cfg.unit_num, cfg.head_num, cfg.layer_num
+
+    def il_bwd_once():
+        call("rs_il_bwd", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
+             trainer.dcat.data_ptr() + 4 * trainer.D, trainer.CW, B, F, E, U, H, L, ptr(il.kernel),
+             ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0, ptr(trainer.dx0), 0,
+             None, 0, ptr(trainer.il_ws), trainer.il_ws_n)
+
+    def il_fwd_once():
+        call("rs_il_fwd", stream_handle(), ptr(trainer.x0), B, F, E, U, H, L, ptr(il.kernel),
+             ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
+             trainer.cat.data_ptr() + 4 * trainer.D, trainer.CW, ptr(trainer.xsave))
+
+    t_bwd = time_kernel(il_bwd_once, args.kernel_reps)
+    t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
+    bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
+    achieved = bwd_flops / t_bwd / 1e12
+    traffic = None
+    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")
+    if os.path.exists(tf_path):
+        with open(tf_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    samples = B * args.steps * world
+    out = {
+        "metric": "samples/sec AutoInt CTR train, 26 fields×16-dim emb, batch 4096, 1/2/4/8 GPU",
+        "value": round(samples / dt, 1),
+        "unit": "samples/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Zipf(1.2) ids over 26x100k vocab, Bernoulli(0.25) labels; random-init weights)",
+        "config": {"workload": "configs[1]: AutoInt full train (embedding + 3xInteractingLayer + MLP), "
+                               "26 fields x emb 16, per-GPU batch 4096",
+                   "global_batch": B * world, "fields": F, "emb_dim": E, "layer_num": L,
+                   "head_num": H, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd_kernel (InteractingLayer backward)",
+                     "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "launch_us": round(t_bwd * 1e6, 2),
+                     "flops_per_launch": bwd_flops},
+        "il_fwd_us": round(t_fwd * 1e6, 2),
+        "step_tflops": round(TRAIN_FLOPS_PER_SAMPLE * samples / dt / 1e12, 3),
+        "final_loss": round(loss, 6),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_steps > 0:
+        out["cpu_baseline"] = cpu_baseline(cfg, model, pool_cpu, args.cpu_baseline_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * recsys_amd.h — C ABI of librecsys_amd.so, the MI355X (gfx950) kernels of the CTR
+ * feature-interaction training path of yueshifeng/recommendSystem.
+ *
+ * Conventions (every entry point):
+ *   - `stream` is a hipStream_t passed as void*; the call only enqueues work on it (no
+ *     allocation, no host synchronisation), so any sequence of calls can be captured into a
+ *     hipGraph by the caller.
+ *   - all pointers are device pointers to row-major buffers owned by the caller (the caller
+ *     allocates outputs and workspaces; the library never allocates or frees).
+ *   - fp32 everywhere ("float"); ids are int64; hashed table rows are int32.
+ *   - return value: 0 = OK, -1 = bad argument/shape, -2 = shape not compiled in,
+ *     -3 = kernel launch failed.  Callers raise on non-zero (the Python host layer raises the
+ *     reference's ValueError messages before launching).
+ *
+ * The reference is TensorFlow/Keras + tensornet Python; the "FFI" that binds this library is the
+ * Python host layer (recommendsystem_amd/_lib.py, ctypes).  Each declaration cites the reference
+ * interface it replaces.
+ */
+#ifndef RECSYS_AMD_H_
+#define RECSYS_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------------------
+ * H1/H2  Sparse embedding lookup + concat front end.
+ * Replaces tn.layers.EmbeddingFeatures(embedding_column(category_column(key, bucket_size),
+ * dimension, combiner))(inputs) and the expand + Concatenate(axis=1) that follows:
+ *   rank/ctr/base_model.py:203-217, rank/multi_head/multidnn.py:221-238,
+ *   staytime/VideoDnn.py:217-244, rough_rank/model.py:89-115, rank/finish/videodnn.py:53-68,
+ *   autoint:22-26, rank/multi_head/multidnn.py:25-27,50.
+ * Segment s = b*F + f holds ids[offsets[s] .. offsets[s+1]) (offsets == NULL: one id per
+ * segment).  row = row_base[f] + H(id) % bucket[f] with H = identity (hash_mode 0) or
+ * splitmix64 (1).  out[b*out_ld + f*out_fstride + e] = combiner(rows)[e], combiner 0 = sum,
+ * 1 = mean, 2 = sqrtn; empty segment -> 0.  rows_out[k] (nullable) receives the row of ids[k].
+ * ------------------------------------------------------------------------------------- */
+int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offsets, int64_t B,
+                            int F, const int64_t* row_base, const int64_t* bucket, int hash_mode,
+                            int combiner, const float* table, int64_t table_rows, int dim,
+                            float* out, int64_t out_ld, int64_t out_fstride, int32_t* rows_out);
+
+/* Sparse gradient push (the backward half of EmbeddingFeatures; tensornet pushes per-feature
+ * gradients to its PS): grad_table[rows[k]] += scale(s) * dout[s] for every id k of segment s.
+ * Rows touched for the first time this step are claimed (flag -1 -> -2) and appended to
+ * touched[*n_touched++] (capacity touched_cap).  flag[] must be all -1 between steps (the
+ * optimizer entry points restore it). */
+int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
+                              int64_t B, int F, const float* dout, int64_t dout_ld,
+                              int64_t dout_fstride, int dim, int combiner, float* grad_table,
+                              int32_t* flag, int32_t* touched, int32_t* n_touched,
+                              int32_t touched_cap);
+
+/* H11 sparse optimizers on the touched rows (tensornet tn.core.Adam / tn.core.AdaGrad handed to
+ * EmbeddingFeatures: rank/ctr/base_model.py:163, rank/multi_head/multidnn.py:235,
+ * staytime/VideoDnn.py:233).  Zero the gradient rows, release the flags, reset *n_touched.
+ * max_rows bounds the grid (>= the largest possible *n_touched). */
+int rs_sparse_adam(void* stream, float* table, float* m, float* v, float* grad_table,
+                   int32_t* flag, const int32_t* touched, int32_t* n_touched, int dim,
+                   int32_t max_rows, float lr, float beta1, float beta2, float eps,
+                   float grad_scale);
+int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* grad_table, int32_t* flag,
+                      const int32_t* touched, int32_t* n_touched, int dim, int32_t max_rows,
+                      float lr, float grad_scale);
+
+/* Data-parallel sparse exchange (replaces tensornet's PS push across workers):
+ * compact moves this rank's touched rows into (rows_out, grads_out) (padding rows = -1) and
+ * clears the table; merge adds one rank's list back (rows unique within a list, no atomics).
+ * Merging every rank's list in rank order gives bitwise-identical sums on every replica. */
+int rs_sparse_compact(void* stream, float* grad_table, int32_t* flag, const int32_t* touched,
+                      int32_t* n_touched, int dim, int32_t* rows_out, float* grads_out,
+                      int32_t cap);
+int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* grads, int32_t count,
+                         int dim, float* grad_table, int32_t* flag, int32_t* touched,
+                         int32_t* n_touched, int32_t touched_cap);
+
+/* ---------------------------------------------------------------------------------------
+ * H3  InteractingLayer (InteractingLayer.py:7-61; rank/multi_head/interacting_layer.py:7-61).
+ * x [B, F, E]; W [E, 4U] = [Wq | Wk | Wv | Wr] (Keras Dense kernels), bias [4U],
+ * gamma/beta [U] (LayerNormalization), layer_num L with tied weights (L > 1 needs E == U).
+ * y row stride y_ld (>= F*U).  xsave [(L-1), B, F, U] receives the inputs of iterations
+ * 1..L-1 for the backward (nullable when L == 1).  Dropout on the softmax weights
+ * (InteractingLayer.py:53-54) uses the counter-based mask documented in csrc/common.hpp.
+ * ------------------------------------------------------------------------------------- */
+int rs_il_param_count(int E, int U);
+int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
+              const float* W, const float* bias, const float* gamma, const float* beta,
+              float eps, int use_res, float drop_rate, uint64_t seed, float* y, int64_t y_ld,
+              float* xsave);
+/* Backward (TF autograd of the graph above).  dx [B, F, E] written (or accumulated).
+ * dparams = [dW (E*4U) | dbias (4U) | dgamma (U) | dbeta (U)] written (or accumulated);
+ * dparams == NULL skips the grid reduction (per-block partials stay in the workspace).
+ * workspace >= rs_il_bwd_workspace_floats(B, E, U) floats. */
+int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U);
+int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy, int64_t dy_ld,
+              int64_t B, int F, int E, int U, int H, int L, const float* W, const float* bias,
+              const float* gamma, const float* beta, float eps, int use_res, float drop_rate,
+              uint64_t seed, float* dx, int dx_accumulate, float* dparams,
+              int dparams_accumulate, float* workspace, int64_t workspace_floats);
+
+/* ---------------------------------------------------------------------------------------
+ * H4/H5/H8/H9  Keras Dense(units, activation) towers (autoint:36-52 MultiLayerDense,
+ * rank/multi_head/multidnn.py:60-127, rough_rank/layer.py:33-117 DNN,
+ * staytime/VideoDnn.py:130-191).  act: 0 linear, 1 relu, 2 sigmoid.
+ * Y[M, N] (ld ldy) = act(X[M, K] (ld ldx) @ W[K, N] + b).
+ * ------------------------------------------------------------------------------------- */
+int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t ldx, const float* W,
+                 const float* bias, int N, int act, float* Y, int64_t ldy);
+/* dX (+)= (dY * act'(Y)) @ W^T */
+int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const float* Y, int64_t ldy,
+                      int act, const float* W, int64_t M, int K, int N, float* dX,
+                      int64_t lddx, int accumulate);
+/* dW (+)= X^T (dY * act'(Y)), db (+)= colsum(dY * act'(Y)); deterministic */
+int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N);
+int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* dY, int64_t lddy,
+                        const float* Y, int64_t ldy, int act, int64_t M, int K, int N, float* dW,
+                        float* db, int accumulate, float* workspace, int64_t workspace_floats);
+
+/* H4/H10  tf.clip_by_value(s, lo, hi) (autoint:52) + cross_entropy (rank/ctr/base_model.py:7-12):
+ * loss[0] = mean_b sum_t [-y log(p+log_eps) - (1-y) log(1-p+log_eps)], p_out = clipped s,
+ * ds = gscale[0] * dloss/ds (zero outside [lo, hi]; gscale NULL = 1).  Any output pointer
+ * may be NULL. */
+int rs_bce_clip_loss(void* stream, const float* s, const float* y, int64_t M, int T,
+                     float clip_lo, float clip_hi, float log_eps, const float* gscale,
+                     float* p_out, float* loss, float* ds);
+
+/* ---------------------------------------------------------------------------------------
+ * H11  dense Adam over a flat parameter arena (tn.optimizer.Optimizer(tn.core.Adam(...)):
+ * rank/ctr/base_model.py:192-193, rank/multi_head/model.py:52-53, staytime/model.py:72,
+ * rough_rank/model.py:209).  step is a device int64 counter (read, then incremented).
+ * zero_grad != 0 zeroes each gradient after reading it (fused optimizer.zero_grad()).
+ * ------------------------------------------------------------------------------------- */
+int rs_dense_adam(void* stream, float* params, float* grads, float* m, float* v, int64_t n,
+                  int64_t* step, float lr, float beta1, float beta2, float eps, float grad_scale,
+                  int zero_grad);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RECSYS_AMD_H_ */

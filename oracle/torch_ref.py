@@ -1,0 +1,149 @@
+"""CPU ORACLE (autograd twin) — test infrastructure only; see oracle/ctr_oracle.py for status.
+
+The same TF-semantics restatement as ctr_oracle.py, written with torch CPU ops op-for-op
+(split/concat head shuffles, materialised [H*B, F, F] softmax, separate Dense/ReLU/LN ops), so
+that:
+  * torch autograd in float64 gives the reference gradients (TF's ReluGrad `x > 0`, ClipByValue
+    pass-through inside [lo, hi] and SigmoidGrad are what torch's relu/clamp/sigmoid backward
+    do), cross-checked against finite differences in tests/test_oracle.py;
+  * run in float32 with all host threads it is the unfused TF-CPU-style train step that
+    bench.py times as the CPU baseline ("kind": "port").
+PARITY STATUS: UNPINNED (no runnable reference, no reference fixtures).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ctr_oracle as npo
+
+
+def dense(x, W, b, activation=None):
+    y = torch.tensordot(x, W, dims=([x.dim() - 1], [0])) + b
+    if activation == "relu":
+        return torch.relu(y)
+    if activation == "sigmoid":
+        return torch.sigmoid(y)
+    return y
+
+
+def layer_norm(x, gamma, beta, eps=1e-14):
+    mean = x.mean(dim=-1, keepdim=True)
+    var = (x - mean).square().mean(dim=-1, keepdim=True)
+    return (x - mean) / torch.sqrt(var + eps) * gamma + beta
+
+
+def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=True, eps=1e-14,
+                      drop_rate=0.0, seed=0):
+    """InteractingLayer.py:37-61, op for op (tied weights across layer_num iterations)."""
+    U = W.shape[1] // 4
+    H = head_num
+    Wq, Wk, Wv, Wr = (W[:, j * U:(j + 1) * U] for j in range(4))
+    bq, bk, bv, br = (bias[j * U:(j + 1) * U] for j in range(4))
+    B = x.shape[0]
+    out = x
+    for it in range(layer_num):
+        q = dense(out, Wq, bq, "relu")
+        k = dense(out, Wk, bk, "relu")
+        v = dense(out, Wv, bv, "relu")
+        res = dense(out, Wr, br, "relu") if use_res else None
+        q = torch.cat(torch.split(q, U // H, dim=2), dim=0)
+        k = torch.cat(torch.split(k, U // H, dim=2), dim=0)
+        v = torch.cat(torch.split(v, U // H, dim=2), dim=0)
+        w = torch.matmul(q, k.transpose(1, 2))
+        w = w / float((U // H) ** 0.5)
+        w = torch.softmax(w, dim=-1)
+        if drop_rate > 0.0:
+            HB, Fq, Fk = w.shape
+            hh, bb = divmod(torch.arange(HB).numpy(), B)
+            keep = npo.dropout_keep(npo.layer_seed(seed, it), bb[:, None, None], hh[:, None, None],
+                                    torch.arange(Fq).numpy()[None, :, None],
+                                    torch.arange(Fk).numpy()[None, None, :], drop_rate)
+            w = torch.where(torch.from_numpy(keep), w * (1.0 / (1.0 - drop_rate)), torch.zeros_like(w))
+        o = torch.matmul(w, v)
+        o = torch.cat(torch.split(o, B, dim=0), dim=2)
+        if use_res:
+            o = o + res
+        o = torch.relu(o)
+        out = layer_norm(o, gamma, beta, eps)
+    return out
+
+
+def mlp(x, layers, activation):
+    for W, b in layers:
+        x = dense(x, W, b, activation)
+    return x
+
+
+def autoint_forward(x0, il, deep_layers, logit_layers, cfg):
+    B = x0.shape[0]
+    y = interacting_layer(x0, il["W"], il["bias"], il["gamma"], il["beta"], cfg["layer_num"],
+                          cfg["head_num"], cfg["use_res"], cfg.get("ln_eps", 1e-14))
+    deep = mlp(x0.reshape(B, -1), deep_layers, cfg["mlp_activation"])
+    result = torch.cat([deep, y.reshape(B, -1)], dim=1)
+    s = mlp(result, logit_layers, cfg["logits_activation"])
+    return s, torch.clamp(s, 1e-6, 1.0)
+
+
+def cross_entropy(y_true, y_pred, a=1):
+    y_true = y_true.to(y_pred.dtype)
+    loss = -y_true * torch.log(y_pred + 1e-6) - (a - y_true) * torch.log(1.0 - y_pred + 1e-6)
+    return torch.mean(torch.sum(loss, dim=1), dim=0)
+
+
+class AutoIntCPU:
+    """Unfused TF-CPU-style AutoInt train step: embedding gather (index_select + per-row sparse
+    gradient), InteractingLayer x layer_num, deep + logits MLP, clip, cross_entropy, backward,
+    dense Adam (bias-corrected) and sparse Adam on the touched rows (tensornet form)."""
+
+    def __init__(self, table, row_base, buckets, il, deep, logits, cfg, lr_dense=5e-5, lr_sparse=5e-5,
+                 dtype=torch.float32):
+        self.dtype = dtype
+        self.table = torch.as_tensor(table, dtype=dtype).clone()
+        self.m_tab = torch.zeros_like(self.table)
+        self.v_tab = torch.zeros_like(self.table)
+        self.row_base = torch.as_tensor(row_base, dtype=torch.int64)
+        self.buckets = torch.as_tensor(buckets, dtype=torch.int64)
+        self.cfg = cfg
+        self.params = {}
+        for k, v in il.items():
+            self.params["il_" + k] = torch.as_tensor(v, dtype=dtype).clone().requires_grad_(True)
+        self.deep = [(torch.as_tensor(W, dtype=dtype).clone().requires_grad_(True),
+                      torch.as_tensor(b, dtype=dtype).clone().requires_grad_(True)) for W, b in deep]
+        self.logits = [(torch.as_tensor(W, dtype=dtype).clone().requires_grad_(True),
+                        torch.as_tensor(b, dtype=dtype).clone().requires_grad_(True)) for W, b in logits]
+        self.dense_list = list(self.params.values()) + [t for l in self.deep + self.logits for t in l]
+        self.m = [torch.zeros_like(p) for p in self.dense_list]
+        self.v = [torch.zeros_like(p) for p in self.dense_list]
+        self.t = 0
+        self.lr_dense, self.lr_sparse = lr_dense, lr_sparse
+
+    def rows(self, ids):
+        F = ids.shape[1]
+        return self.row_base[None, :] + torch.remainder(ids, self.buckets[None, :])
+
+    def step(self, ids, labels):
+        B, F = ids.shape
+        rows = self.rows(ids).reshape(-1)
+        x0 = self.table.index_select(0, rows).reshape(B, F, -1).requires_grad_(True)
+        il = {k[3:]: v for k, v in self.params.items()}
+        _, p = autoint_forward(x0, il, self.deep, self.logits, self.cfg)
+        loss = cross_entropy(labels.reshape(B, -1), p)
+        grads = torch.autograd.grad(loss, [x0] + self.dense_list)
+        gx, gd = grads[0], grads[1:]
+        with torch.no_grad():
+            self.t += 1
+            b1, b2, eps = 0.9, 0.999, 1e-8
+            lr_t = self.lr_dense * (1 - b2 ** self.t) ** 0.5 / (1 - b1 ** self.t)
+            for p_, g, m, v in zip(self.dense_list, gd, self.m, self.v):
+                m.mul_(b1).add_(g, alpha=1 - b1)
+                v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                p_.sub_(lr_t * m / (v.sqrt() + eps))
+            uniq, inv = torch.unique(rows, return_inverse=True)
+            gsum = torch.zeros(uniq.numel(), self.table.shape[1], dtype=self.dtype)
+            gsum.index_add_(0, inv, gx.reshape(B * F, -1))
+            m = self.m_tab[uniq].mul_(b1).add_(gsum, alpha=1 - b1)
+            v = self.v_tab[uniq].mul_(b2).addcmul_(gsum, gsum, value=1 - b2)
+            self.m_tab[uniq] = m
+            self.v_tab[uniq] = v
+            self.table[uniq] -= self.lr_sparse * m / (eps + v.sqrt())
+        return float(loss)

@@ -1,0 +1,102 @@
+"""ctypes binding of ``librecsys_amd.so`` (the C ABI in ``include/recsys_amd.h``).
+
+This is the "reference-side binding" for a Python reference: the host layer passes raw device
+pointers, sizes and the current HIP stream; no torch types cross the boundary.  torch is imported
+FIRST so the process has exactly one HIP runtime (torch's ``libamdhip64.so.7``; the library's
+``DT_NEEDED libamdhip64.so.7`` then binds to it by soname).
+
+The product path has no fallback: if the library is missing or a call fails, this raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: one HIP runtime per process)
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG_DIR, "librecsys_amd.so")
+
+RS_OK, RS_ERR_ARG, RS_ERR_UNSUPPORTED, RS_ERR_LAUNCH = 0, -1, -2, -3
+_ERRS = {RS_ERR_ARG: "bad argument/shape", RS_ERR_UNSUPPORTED: "shape not compiled in",
+         RS_ERR_LAUNCH: "kernel launch failed"}
+
+_vp, _i32, _i64, _f32, _u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64
+
+# name -> (restype, argtypes); must match include/recsys_amd.h exactly
+SIGNATURES: dict[str, tuple] = {
+    "rs_embedding_lookup_fwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _vp, _i64,
+                                       _i32, _vp, _i64, _i64, _vp]),
+    "rs_sparse_grad_accumulate": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32,
+                                         _vp, _vp, _vp, _vp, _i32]),
+    "rs_sparse_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32, _f32,
+                              _f32, _f32]),
+    "rs_sparse_adagrad": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32]),
+    "rs_sparse_compact": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32]),
+    "rs_sparse_merge_rows": (_i32, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32]),
+    "rs_il_param_count": (_i32, [_i32, _i32]),
+    "rs_il_fwd": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32,
+                         _i32, _f32, _u64, _vp, _i64, _vp]),
+    "rs_il_bwd_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_il_bwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
+                         _vp, _vp, _f32, _i32, _f32, _u64, _vp, _i32, _vp, _i32, _vp, _i64]),
+    "rs_dense_fwd": (_i32, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _i64]),
+    "rs_dense_bwd_data": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _i64,
+                                 _i32]),
+    "rs_dense_bwd_weight_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_dense_bwd_weight": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _i32,
+                                   _vp, _vp, _i32, _vp, _i64]),
+    "rs_bce_clip_loss": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _vp, _vp, _vp]),
+    "rs_dense_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
+                             _i32]),
+}
+
+_LIB = None
+
+
+class RecsysKernelError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the shared library.  Raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RecsysKernelError(
+            f"{path} not found: build the HIP extension first (python -c "
+            "'import __graft_entry__ as g; g.build()' or python recommendsystem_amd/build.py)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(load(), name)(*args)
+    if SIGNATURES[name][0] is _i32 and rc != RS_OK and not name.endswith("_count"):
+        raise RecsysKernelError(f"{name} returned {rc} ({_ERRS.get(rc, 'hip error')})")
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle() -> int:
+    """hipStream_t of torch's current stream on the current device."""
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_device(*tensors) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RecsysKernelError("recommendsystem_amd kernels need tensors on a ROCm device "
+                                    "(there is no CPU fallback)")

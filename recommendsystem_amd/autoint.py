@@ -1,0 +1,328 @@
+"""AutoInt CTR model (autoint:11-60 on the rank/ctr BaseModel front end) and its training step.
+
+Two entry points share the same kernels:
+  * ``AutoInt`` — an nn.Module with the reference's structure (embedding concat -> InteractingLayer
+    -> flatten; deep MultiLayerDense on the flattened embeddings; concat [deep, autoint];
+    logits MultiLayerDense; clip_by_value(1e-6, 1)); ``forward`` is autograd-composable and
+    ``run()`` returns {"train": model, "predict": model} like autoint:58-60.
+  * ``AutoIntTrainer`` — the fused training step (what tensornet's model.fit runs per batch):
+    forward, cross_entropy, backward, dense Adam and sparse Adam, issued as ~20 launches into
+    preallocated buffers (no allocation, no host sync) and captured into one HIP graph.
+    Activations are laid out so that concats are free: the IL writes its flattened output and
+    the deep tower its last layer straight into the [B, D + F*U] concat buffer (autoint:44).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Sequence
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import call, ptr, stream_handle
+from .embedding import EmbeddingFeatures, SparseAdam, SparseTable
+from .layers import ACTIVATIONS, InteractingLayer, MultiLayerDense
+from .params import ParamArena
+
+
+@dataclass
+class AutoIntConfig:
+    """model_config['model_param'] of autoint:30-50 plus the front end.  The shipped
+    rank/ctr/model_parameter.json has no 'model_param' block, so defaults are the pinned config-2
+    values (SURVEY §8c decision 3): IL(3, 16, 2, res), mlp [32, 16] relu, logits [1] sigmoid."""
+    num_fields: int = 26
+    embed_dim: int = 16
+    vocab_per_field: int = 100_000
+    layer_num: int = 3
+    unit_num: int = 16
+    head_num: int = 2
+    use_dropout: bool = False
+    dropout_rate: float = 0.0
+    use_res: bool = True
+    ln_eps: float = 1e-14
+    mlp_hidden: Sequence[int] = (32, 16)
+    mlp_activation: str = "relu"
+    logits_hidden: Sequence[int] = (1,)
+    logits_activation: str = "sigmoid"
+    lr_dense: float = 5e-5    # rank/ctr/base_model.py:192
+    lr_sparse: float = 5e-5   # rank/ctr/base_model.py:163
+    hash_mode: str = "mod"
+    combiner: str = "mean"    # embedding_column(..., combiner='mean') base_model.py:211
+
+    @staticmethod
+    def from_model_config(model_config: dict, **front) -> "AutoIntConfig":
+        mp = model_config["model_param"]
+        it, ml, lg = mp["interact"], mp["mlp"], mp["logits"]
+        return AutoIntConfig(layer_num=it["layer_num"], unit_num=it["unit_num"],
+                             head_num=it["head_num"], use_dropout=it["use_dropout"],
+                             dropout_rate=it["dropout_rate"], use_res=it["use_res"],
+                             mlp_hidden=tuple(ml["hidden_units"]), mlp_activation=ml["activation"],
+                             logits_hidden=tuple(lg["hidden_units"]),
+                             logits_activation=lg["activation"], **front)
+
+
+class AutoInt(nn.Module):
+    def __init__(self, cfg: AutoIntConfig | dict | None = None, device=None, seed: int = 0,
+                 max_batch: int = 4096, world_size: int = 1):
+        super().__init__()
+        if isinstance(cfg, dict):
+            cfg = AutoIntConfig.from_model_config(cfg)
+        self.cfg = cfg = cfg or AutoIntConfig()
+        dev = torch.device(device or "cuda")
+        F, E, U = cfg.num_fields, cfg.embed_dim, cfg.unit_num
+        self.table = SparseTable(F * cfg.vocab_per_field, E, SparseAdam(cfg.lr_sparse), device=dev,
+                                 seed=seed, max_touched=max_batch * F * world_size)
+        self.embedding = EmbeddingFeatures(self.table, [cfg.vocab_per_field] * F,
+                                           combiner=cfg.combiner, hash_mode=cfg.hash_mode)
+        self.interact = InteractingLayer(cfg.layer_num, U, cfg.head_num, cfg.use_dropout,
+                                         cfg.dropout_rate, cfg.use_res, ln_epsilon=cfg.ln_eps,
+                                         seed=seed + 1, device=dev)
+        self.interact.build((1, F, E), device=dev)
+        self.deep = MultiLayerDense(cfg.mlp_hidden, cfg.mlp_activation, seed=seed + 10, device=dev)
+        d_in = F * E
+        for layer in self.deep.layers:
+            layer.build((1, d_in), device=dev)
+            d_in = layer.units
+        self.logits = MultiLayerDense(cfg.logits_hidden, cfg.logits_activation, seed=seed + 20,
+                                      device=dev)
+        d_in = cfg.mlp_hidden[-1] + F * U
+        for layer in self.logits.layers:
+            layer.build((1, d_in), device=dev)
+            d_in = layer.units
+        self.arena = ParamArena(self.parameters(), device=dev)
+
+    # autograd-composable forward (autoint:18-56); returns the clipped prediction p
+    def forward(self, ids: torch.Tensor, offsets: torch.Tensor | None = None) -> torch.Tensor:
+        x0 = self.embedding(ids, offsets)                       # [B, F, E]  (autoint:22-26)
+        B = x0.shape[0]
+        il = self.interact(x0).reshape(B, -1)                   # :30-36
+        deep = self.deep(x0.reshape(B, -1))                     # :39-41
+        result = torch.cat([deep, il], dim=1)                   # :44
+        s = self.logits(result)                                 # :48-50
+        return torch.clamp(s, 1e-6, 1.0)                        # :52
+
+    def run(self):
+        """autoint:58-60 / rank/ctr/base_model.py:169-201: {"train": model, "predict": model}."""
+        return {"train": self, "predict": self}
+
+
+def cross_entropy(y_true: torch.Tensor, y_pred: torch.Tensor, a: float = 1.0) -> torch.Tensor:
+    """rank/ctr/base_model.py:7-12 (autograd form, for the composable path)."""
+    y_true = y_true.to(torch.float32)
+    loss = -y_true * torch.log(y_pred + 1e-6) - (a - y_true) * torch.log(1.0 - y_pred + 1e-6)
+    return torch.mean(torch.sum(loss, dim=1), dim=0)
+
+
+class AutoIntTrainer:
+    """Fused AutoInt train step over fixed-shape batches (ids int64 [B, F], labels fp32 [B, T]).
+
+    Per step: lookup -> IL fwd -> deep fwd -> logits fwd -> clip+BCE (+ dloss) -> logits bwd ->
+    deep bwd -> IL bwd (accumulating into the embedding gradient) -> sparse push ->
+    [data-parallel exchange] -> dense Adam (one flat arena) -> sparse Adam (touched rows).
+    ``capture()`` records the step into a torch.cuda.CUDAGraph (hipGraph); ``step()`` replays it.
+    """
+
+    def __init__(self, model: AutoInt, batch_size: int, process_group=None):
+        self.model = m = model
+        cfg = m.cfg
+        self.B = B = int(batch_size)
+        self.F, self.E, self.U = F, E, U = cfg.num_fields, cfg.embed_dim, cfg.unit_num
+        self.L, self.H = cfg.layer_num, cfg.head_num
+        dev = m.table.weight.device
+        self.dev = dev
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.deep_layers = list(m.deep.layers)
+        self.logit_layers = list(m.logits.layers)
+        self.D = D = cfg.mlp_hidden[-1]
+        self.CW = CW = D + F * U
+        self.T = self.logit_layers[-1].units
+        # static inputs
+        self.ids = torch.zeros(B, F, device=dev, dtype=torch.int64)
+        self.labels = torch.zeros(B, self.T, **f32)
+        # activations
+        self.x0 = torch.empty(B, F * E, **f32)
+        self.rows = torch.empty(B * F, device=dev, dtype=torch.int32)
+        self.xsave = torch.empty(max(self.L - 1, 1), B, F, U, **f32)
+        self.cat = torch.empty(B, CW, **f32)
+        self.h = [torch.empty(B, l.units, **f32) for l in self.deep_layers[:-1]]
+        self.lh = [torch.empty(B, l.units, **f32) for l in self.logit_layers[:-1]]
+        self.s = torch.empty(B, self.T, **f32)
+        self.p = torch.empty(B, self.T, **f32)
+        self.loss = torch.zeros(1, **f32)
+        # gradients
+        self.ds = torch.empty(B, self.T, **f32)
+        self.dcat = torch.empty(B, CW, **f32)
+        self.dh = [torch.empty_like(t) for t in self.h]
+        self.dlh = [torch.empty_like(t) for t in self.lh]
+        self.dx0 = torch.empty(B, F * E, **f32)
+        lib = _lib.load()
+        self.il_ws_n = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+        ws_dense = max(int(lib.rs_dense_bwd_weight_workspace_floats(B, l.input_dim, l.units))
+                       for l in self.deep_layers + self.logit_layers)
+        self.dense_ws_n = ws_dense
+        self.il_ws = torch.empty(self.il_ws_n, **f32)
+        self.dense_ws = torch.empty(ws_dense, **f32)
+        # dense optimizer state on the flat arena
+        ar = m.arena
+        self.adam_m = torch.zeros_like(ar.data)
+        self.adam_v = torch.zeros_like(ar.data)
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.int64)
+        il = m.interact
+        self.il_dparams = ar.grad[self._offset(il.kernel):self._offset(il.kernel) +
+                                  il.kernel.numel() + il.bias.numel() + il.gamma.numel() + il.beta.numel()]
+        self.graph = None
+        if self.world > 1:
+            cap = m.table.touched_cap
+            self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
+            self.x_grads = torch.empty(cap, E, **f32)
+
+    def _offset(self, p: torch.Tensor) -> int:
+        return (p.data_ptr() - self.model.arena.data.data_ptr()) // 4
+
+    def _grad(self, p: torch.Tensor) -> int:
+        return self.model.arena.grad.data_ptr() + 4 * self._offset(p)
+
+    # ---------------------------------------------------------------------------------------
+    def _forward_backward(self):
+        m, cfg = self.model, self.model.cfg
+        B, F, E, U, L, H, D, CW = self.B, self.F, self.E, self.U, self.L, self.H, self.D, self.CW
+        s = stream_handle()
+        il = m.interact
+        emb = m.embedding
+        t = m.table
+        # ---- forward ----
+        call("rs_embedding_lookup_fwd", s, ptr(self.ids), None, B, F, ptr(emb.row_base),
+             ptr(emb.bucket), emb.hash_mode, emb.combiner, ptr(t.weight), t.rows, E, ptr(self.x0),
+             F * E, E, ptr(self.rows))
+        drop = il.dropout_rate if il.use_dropout else 0.0
+        call("rs_il_fwd", s, ptr(self.x0), B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+             ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
+             self.cat.data_ptr() + 4 * D, CW, ptr(self.xsave) if L > 1 else None)
+        x, ldx = self.x0, F * E
+        deep_io = []
+        for i, layer in enumerate(self.deep_layers):
+            last = i == len(self.deep_layers) - 1
+            y, ldy = (self.cat, CW) if last else (self.h[i], layer.units)
+            call("rs_dense_fwd", s, ptr(x), B, layer.input_dim, ldx, ptr(layer.kernel), ptr(layer.bias),
+                 layer.units, layer.act, ptr(y), ldy)
+            deep_io.append((x, ldx, y, ldy))
+            x, ldx = y, ldy
+        x, ldx = self.cat, CW
+        logit_io = []
+        for j, layer in enumerate(self.logit_layers):
+            last = j == len(self.logit_layers) - 1
+            y, ldy = (self.s, self.T) if last else (self.lh[j], layer.units)
+            call("rs_dense_fwd", s, ptr(x), B, layer.input_dim, ldx, ptr(layer.kernel), ptr(layer.bias),
+                 layer.units, layer.act, ptr(y), ldy)
+            logit_io.append((x, ldx, y, ldy))
+            x, ldx = y, ldy
+        call("rs_bce_clip_loss", s, ptr(self.s), ptr(self.labels), B, self.T, 1e-6, 1.0, 1e-6, None,
+             ptr(self.p), ptr(self.loss), ptr(self.ds))
+        # ---- backward ----
+        dy, lddy = self.ds, self.T
+        for j in reversed(range(len(self.logit_layers))):
+            layer = self.logit_layers[j]
+            x, ldx, y, ldy = logit_io[j]
+            dx, lddx = (self.dcat, CW) if j == 0 else (self.dlh[j - 1], self.logit_layers[j - 1].units)
+            call("rs_dense_bwd_data", s, ptr(dy), lddy, ptr(y), ldy, layer.act, ptr(layer.kernel), B,
+                 layer.input_dim, layer.units, ptr(dx), lddx, 0)
+            call("rs_dense_bwd_weight", s, ptr(x), ldx, ptr(dy), lddy, ptr(y), ldy, layer.act, B,
+                 layer.input_dim, layer.units, self._grad(layer.kernel), self._grad(layer.bias), 0,
+                 ptr(self.dense_ws), self.dense_ws_n)
+            dy, lddy = dx, lddx
+        dy_ptr, lddy = self.dcat.data_ptr(), CW   # deep part = dcat[:, :D]
+        for i in reversed(range(len(self.deep_layers))):
+            layer = self.deep_layers[i]
+            x, ldx, y, ldy = deep_io[i]
+            dx, lddx = (self.dx0, F * E) if i == 0 else (self.dh[i - 1], self.deep_layers[i - 1].units)
+            call("rs_dense_bwd_data", s, dy_ptr, lddy, ptr(y), ldy, layer.act, ptr(layer.kernel), B,
+                 layer.input_dim, layer.units, ptr(dx), lddx, 0)
+            call("rs_dense_bwd_weight", s, ptr(x), ldx, dy_ptr, lddy, ptr(y), ldy, layer.act, B,
+                 layer.input_dim, layer.units, self._grad(layer.kernel), self._grad(layer.bias), 0,
+                 ptr(self.dense_ws), self.dense_ws_n)
+            dy_ptr, lddy = ptr(dx), lddx
+        call("rs_il_bwd", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+             self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+             ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed, ptr(self.dx0),
+             1, ptr(self.il_dparams), 0, ptr(self.il_ws), self.il_ws_n)
+        t.accumulate(self.rows, None, B, F, self.dx0, F * E, E, emb.combiner)
+
+    def _exchange(self):
+        """Data-parallel gradient exchange: dense all-reduce of the flat arena
+        gradient (one RCCL bucket), sparse rows: compact -> all-gather -> rank-ordered merge."""
+        import torch.distributed as dist
+        m, t = self.model, self.model.table
+        dist.all_reduce(m.arena.grad, group=self.pg)
+        cnt = t.n_touched.clone()
+        call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
+             ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
+        t.n_touched.zero_()
+        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(counts, cnt, group=self.pg)
+        n = int(torch.stack(counts).max().item())
+        if n == 0:
+            return
+        rows_all = [torch.empty(n, device=self.dev, dtype=torch.int32) for _ in range(self.world)]
+        grads_all = [torch.empty(n, t.dim, device=self.dev, dtype=torch.float32) for _ in range(self.world)]
+        dist.all_gather(rows_all, self.x_rows[:n].contiguous(), group=self.pg)
+        dist.all_gather(grads_all, self.x_grads[:n].contiguous(), group=self.pg)
+        for r in range(self.world):
+            call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,
+                 t.dim, ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched), t.touched_cap)
+
+    def _optimize(self):
+        m, cfg = self.model, self.model.cfg
+        ar = m.arena
+        scale = 1.0 / self.world
+        call("rs_dense_adam", stream_handle(), ptr(ar.data), ptr(ar.grad), ptr(self.adam_m),
+             ptr(self.adam_v), ar.n, ptr(self.step_count), cfg.lr_dense, 0.9, 0.999, 1e-8, scale, 0)
+        m.table.step(grad_scale=scale)
+
+    def _step_eager(self):
+        self._forward_backward()
+        if self.world > 1:
+            self._exchange()
+        self._optimize()
+
+    # ---------------------------------------------------------------------------------------
+    def load_batch(self, ids: torch.Tensor, labels: torch.Tensor) -> None:
+        self.ids.copy_(ids, non_blocking=True)
+        self.labels.copy_(labels.reshape(self.B, self.T), non_blocking=True)
+
+    def capture(self, warmup: int = 2) -> None:
+        """Capture the single-GPU step into a HIP graph (N > 1 keeps collectives eager and
+        captures the compute-only halves)."""
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._step_eager()
+        torch.cuda.current_stream().wait_stream(side)
+        if self.world == 1:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._step_eager()
+        else:
+            self.graph_fb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_fb):
+                self._forward_backward()
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt):
+                self._optimize()
+            self.graph = True
+
+    def step(self, ids: torch.Tensor | None = None, labels: torch.Tensor | None = None) -> torch.Tensor:
+        if ids is not None:
+            self.load_batch(ids, labels)
+        if self.graph is None:
+            self._step_eager()
+        elif self.world == 1:
+            self.graph.replay()
+        else:
+            self.graph_fb.replay()
+            self._exchange()
+            self.graph_opt.replay()
+        return self.loss

@@ -1,0 +1,78 @@
+"""Build the gfx950 C-ABI library ``librecsys_amd.so`` in-tree with hipcc.
+
+Every ``csrc/*.hip`` file is compiled to an object for ``--offload-arch=gfx950`` (in parallel,
+skipping objects newer than their sources and headers), then linked into one shared library next
+to this file.  The library exports exactly the ``extern "C"`` entry points declared in
+``include/recsys_amd.h``; no torch headers are involved.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(PKG_DIR, "_build")
+LIB_PATH = os.path.join(PKG_DIR, "librecsys_amd.so")
+ARCH = os.environ.get("RS_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build recommendsystem_amd)")
+
+
+COMMON_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-munsafe-fp-atomics",
+    "-fvisibility=hidden",
+    "-Wno-unused-result",
+]
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src: str, headers: list[str], extra: list[str]) -> str:
+    obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+    if _newer(obj, [src] + headers):
+        cmd = [_hipcc(), *COMMON_FLAGS, *extra, "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False, extra: list[str] | None = None) -> str:
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(CSRC, "*.hpp")))
+    extra = list(extra or [])
+    workers = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        objs = list(ex.map(lambda s: _compile(s, headers, extra), srcs))
+    if _newer(LIB_PATH, objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB_PATH]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB_PATH}")
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(verbose=True, extra=sys.argv[1:])

@@ -1,0 +1,71 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of the CTR feature-interaction path.
+//
+// Every exported entry point is a plain C-ABI function (see include/recsys_amd.h): raw device
+// pointers, explicit sizes, a hipStream_t passed as void*, an int status.  Nothing here allocates,
+// frees or synchronises, so every launch can be captured into a hipGraph by the caller.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RS_API extern "C" __attribute__((visibility("default")))
+
+enum {
+  RS_OK = 0,
+  RS_ERR_ARG = -1,          // bad shape / null pointer / inconsistent sizes
+  RS_ERR_UNSUPPORTED = -2,  // shape outside the compiled instantiations
+  RS_ERR_LAUNCH = -3,       // hipLaunch failed (hipGetLastError != success)
+};
+
+static inline int rs_status_after_launch() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? RS_OK : RS_ERR_LAUNCH;
+}
+
+static inline hipStream_t rs_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Wave-local LDS hand-off: make every lane's earlier LDS writes visible to the other lanes of the
+// SAME wave and stop the compiler from moving LDS accesses across this point.  (DS instructions of
+// one wave execute in order; the fences emit the lgkmcnt wait and pin the program order.)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// xor-butterfly sum over aligned groups of `W` lanes (W power of two, <= 64)
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Counter-based dropout mask (shared bit-for-bit with oracle/ctr_oracle.py::dropout_keep).
+// TF's stateful RNG cannot be reproduced, so the framework pins its own: a SplitMix64 finaliser
+// over (seed, b, h, i, j); keep iff the top 24 bits / 2^24 >= rate.
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t b, uint32_t h, uint32_t i,
+                                             uint32_t j, float rate) {
+  uint64_t key = seed ^ (((uint64_t)b << 32) | ((uint64_t)h << 24) | ((uint64_t)i << 12) | j);
+  uint64_t r = splitmix64(key);
+  float u = (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
+  return u >= rate;
+}

@@ -1,0 +1,170 @@
+// H1/H2 — sparse embedding lookup + concat front end, and the sparse-gradient half of the
+// tensornet boundary.
+//
+// Reference behaviour being replaced:
+//   tn.feature_column.category_column(key, bucket_size) + tf.feature_column.embedding_column(
+//     dimension, combiner='mean') + tn.layers.EmbeddingFeatures(columns, sparse_opt)(inputs)
+//   rank/ctr/base_model.py:203-217, rank/multi_head/multidnn.py:221-238,
+//   staytime/VideoDnn.py:217-244, rough_rank/model.py:89-115, rank/finish/videodnn.py:53-68
+// and the expand + Concatenate(axis=1) that follows (autoint:22-26, multidnn.py:25-27,50),
+// which is folded into the store: every field's pooled row is written straight into its slot of
+// the [B, F, dim] (or wider) activation.
+//
+// id -> row: tensornet's key->row map is not vendored, so the framework pins a documented hash
+// (identical in oracle/ctr_oracle.py::hash_rows):
+//   RS_HASH_MOD      row = row_base[f] + (uint64)id % bucket[f]
+//   RS_HASH_SPLITMIX row = row_base[f] + splitmix64((uint64)id) % bucket[f]
+// Pooling ('mean' | 'sum' | 'sqrtn') sums rows in id order in fp32, then scales; an empty
+// segment yields zeros (tf.nn.embedding_lookup_sparse semantics).
+//
+// Layout in HBM: table [rows, dim] fp32 row-major (64 B rows at dim 16 -> one float4 per lane,
+// dim/4 lanes per segment, 64/(dim/4) segments per wave instruction: a wave reads 16 whole rows
+// and writes 1 KiB of contiguous [B, F, 16] output per step at config 2).
+#include "common.hpp"
+
+enum { RS_HASH_MOD = 0, RS_HASH_SPLITMIX = 1 };
+enum { RS_COMBINER_SUM = 0, RS_COMBINER_MEAN = 1, RS_COMBINER_SQRTN = 2 };
+
+__device__ __forceinline__ int64_t hash_row(int64_t id, int64_t base, int64_t bucket, int mode) {
+  uint64_t u = (uint64_t)id;
+  if (mode == RS_HASH_SPLITMIX) u = splitmix64(u);
+  return base + (int64_t)(u % (uint64_t)bucket);
+}
+
+__device__ __forceinline__ float combiner_scale(int n, int combiner) {
+  if (n <= 0) return 0.f;
+  if (combiner == RS_COMBINER_MEAN) return 1.0f / (float)n;
+  if (combiner == RS_COMBINER_SQRTN) return 1.0f / sqrtf((float)n);
+  return 1.0f;
+}
+
+// One group of G lanes (G = dim/4 capped at 64, float4 each) pools one (b, f) segment.
+template <int G>
+__global__ void __launch_bounds__(256) embed_lookup_fwd_kernel(
+    const int64_t* __restrict__ ids, const int32_t* __restrict__ offsets, int64_t nseg, int F,
+    const int64_t* __restrict__ row_base, const int64_t* __restrict__ bucket, int hash_mode,
+    int combiner, const float* __restrict__ table, int dim, float* __restrict__ out,
+    int64_t out_ld, int64_t out_fstride, int32_t* __restrict__ rows_out) {
+  const int groups_per_block = blockDim.x / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int nvec = dim >> 2;
+  for (int64_t s = (int64_t)blockIdx.x * groups_per_block + g; s < nseg;
+       s += (int64_t)gridDim.x * groups_per_block) {
+    const int f = (int)(s % F);
+    const int64_t b = s / F;
+    const int64_t beg = offsets ? offsets[s] : s;
+    const int64_t end = offsets ? offsets[s + 1] : s + 1;
+    const int64_t base = row_base[f], bk = bucket[f];
+    float* dst = out + b * out_ld + (int64_t)f * out_fstride;
+    for (int v0 = 0; v0 < nvec; v0 += G) {
+      const int v = v0 + l;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int64_t k = beg; k < end; ++k) {
+        const int64_t row = hash_row(ids[k], base, bk, hash_mode);
+        if (v0 == 0 && l == 0 && rows_out) rows_out[k] = (int32_t)row;
+        if (v < nvec) {
+          const float4 t = reinterpret_cast<const float4*>(table + row * dim)[v];
+          acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+        }
+      }
+      const float sc = combiner_scale((int)(end - beg), combiner);
+      if (v < nvec) {
+        if (combiner != RS_COMBINER_SUM) { acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc; }
+        reinterpret_cast<float4*>(dst)[v] = acc;
+      }
+    }
+  }
+}
+
+RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offsets,
+                                   int64_t B, int F, const int64_t* row_base,
+                                   const int64_t* bucket, int hash_mode, int combiner,
+                                   const float* table, int64_t table_rows, int dim, float* out,
+                                   int64_t out_ld, int64_t out_fstride, int32_t* rows_out) {
+  (void)table_rows;
+  if (!ids || !row_base || !bucket || !table || !out || B < 0 || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  if (dim % 4 != 0 || out_ld % 4 != 0 || out_fstride % 4 != 0) return RS_ERR_ARG;
+  const int64_t nseg = B * (int64_t)F;
+  if (nseg == 0) return RS_OK;
+  const int nvec = dim / 4;
+  int G = 1;
+  while (G < nvec && G < 64) G <<= 1;
+  const int block = 256;
+  int64_t grid = (nseg * G + block - 1) / block;
+  if (grid > 8192) grid = 8192;
+  hipStream_t s = rs_stream(stream);
+#define RS_LAUNCH_EMB(GG)                                                                         \
+  case GG:                                                                                        \
+    embed_lookup_fwd_kernel<GG><<<(int)grid, block, 0, s>>>(ids, offsets, nseg, F, row_base,      \
+                                                            bucket, hash_mode, combiner, table,  \
+                                                            dim, out, out_ld, out_fstride,        \
+                                                            rows_out);                            \
+    break;
+  switch (G) {
+    RS_LAUNCH_EMB(1) RS_LAUNCH_EMB(2) RS_LAUNCH_EMB(4) RS_LAUNCH_EMB(8) RS_LAUNCH_EMB(16)
+    RS_LAUNCH_EMB(32) RS_LAUNCH_EMB(64)
+    default: return RS_ERR_UNSUPPORTED;
+  }
+#undef RS_LAUNCH_EMB
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse gradient accumulation (the "push" half of EmbeddingFeatures): every occurrence k of
+// segment s adds scale(s) * dout[s] into grad_table[rows[k]].  The first occurrence of a row in
+// this step claims it (flag -1 -> -2) and appends it to `touched`, so the optimizer kernel visits
+// each touched row exactly once.  fp32 atomics: the row SET is exact, the summation order of a
+// row's contributions is not fixed (last-bit run-to-run differences).  Data-parallel replicas
+// stay identical because the cross-rank merge (rs_sparse_merge_rows) is rank-ordered.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ offsets, int64_t nseg,
+    const float* __restrict__ dout, int F, int64_t dout_ld, int64_t dout_fstride, int dim,
+    int combiner, int lanes_per_seg, float* __restrict__ grad_table, int32_t* __restrict__ flag,
+    int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
+  const int segs_per_block = blockDim.x / lanes_per_seg;
+  const int g = threadIdx.x / lanes_per_seg;
+  const int l = threadIdx.x % lanes_per_seg;
+  for (int64_t s = (int64_t)blockIdx.x * segs_per_block + g; s < nseg;
+       s += (int64_t)gridDim.x * segs_per_block) {
+    const int64_t beg = offsets ? offsets[s] : s;
+    const int64_t end = offsets ? offsets[s + 1] : s + 1;
+    if (end <= beg) continue;
+    const float sc = combiner_scale((int)(end - beg), combiner);
+    const int f = (int)(s % F);
+    const int64_t b = s / F;
+    const float* src = dout + b * dout_ld + (int64_t)f * dout_fstride;
+    for (int64_t k = beg; k < end; ++k) {
+      const int32_t row = rows[k];
+      if (l == 0) {
+        if (atomicCAS(&flag[row], -1, -2) == -1) {
+          const int32_t u = atomicAdd(n_touched, 1);
+          if (u < touched_cap) touched[u] = row;
+        }
+      }
+      float* dst = grad_table + (int64_t)row * dim;
+      for (int e = l; e < dim; e += lanes_per_seg) atomicAdd(dst + e, src[e] * sc);
+    }
+  }
+}
+
+RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
+                                     int64_t B, int F, const float* dout, int64_t dout_ld,
+                                     int64_t dout_fstride, int dim, int combiner,
+                                     float* grad_table, int32_t* flag, int32_t* touched,
+                                     int32_t* n_touched, int32_t touched_cap) {
+  if (!rows || !dout || !grad_table || !flag || !touched || !n_touched || F <= 0 || dim <= 0)
+    return RS_ERR_ARG;
+  const int64_t nseg = B * (int64_t)F;
+  if (nseg == 0) return RS_OK;
+  int lps = 1;
+  while (lps < dim && lps < 64) lps <<= 1;
+  const int block = 256;
+  int64_t grid = (nseg * lps + block - 1) / block;
+  if (grid > 8192) grid = 8192;
+  sparse_grad_accum_kernel<<<(int)grid, block, 0, rs_stream(stream)>>>(
+      rows, offsets, nseg, dout, F, dout_ld, dout_fstride, dim, combiner, lps, grad_table, flag,
+      touched, n_touched, touched_cap);
+  return rs_status_after_launch();
+}

@@ -1,0 +1,661 @@
+// H3 — AutoInt InteractingLayer (multi-head self-attention over field embeddings), fused.
+//
+// Reference: InteractingLayer.py:7-61 (byte-identical rank/multi_head/interacting_layer.py:7-61).
+// Per iteration it < layer_num, with the SAME Dense/LN objects every iteration (tied weights,
+// InteractingLayer.py:41-46):
+//   Q,K,V = relu(x Wq + bq), relu(x Wk + bk), relu(x Wv + bv)           :42-44
+//   R     = relu(x Wr + br)                    (use_res)                 :45-46
+//   heads = split(., H, axis=2) concat axis 0 -> [H*B, F, dh]            :47-49
+//   S     = Qh Kh^T / sqrt(dh)                 (dh = post-split width)   :50-51
+//   P     = softmax(S) ; dropout(P) when use_dropout (train)             :52-54
+//   O     = merge_heads(P Vh)                                            :55-56
+//   x     = LN(relu(O + R))                    (keras-layer-normalization form,
+//           (z - mean)/sqrt(var + eps) * gamma + beta; eps pinned by the caller)  :57-60
+//
+// MI355X mapping (one wave = one sample; samples are independent):
+//   * the sample's x, the four projections, the attention output (and in backward the softmax
+//     matrix and every gradient) live in LDS: only x_in, x_out and the per-iteration inputs saved
+//     for backward touch HBM.  The TF graph materialises ~15 intermediates per iteration
+//     including the [H*B, F, F] scores; here scores never leave LDS/VGPRs.
+//   * projections: lane = output column of [Wq|Wk|Wv|Wr] (4U = 64 columns at U = 16), the
+//     column's E weights in VGPRs, x rows broadcast from LDS (one address per wave).
+//   * attention: lane = (head, query row); the row's scores stay in VGPRs (softmax per lane:
+//     exp(s - max) * (1/sum), TF's order); K/V rows are broadcast LDS reads.  Key rows F..FMAX-1
+//     are zero and masked to -inf, so the j loops are unguarded and fully unrolled with
+//     compile-time LDS offsets (no per-key branch, no runtime stride arithmetic).
+//   * epilogue: U lanes per field row; LN mean/var by xor-butterfly inside the U-lane group.
+//   * backward recomputes the iteration from its saved input (only x_it is stored: 1.7 KB per
+//     sample per iteration), back-propagates LN, ReLU, attention and projections in LDS, keeps
+//     dW/db/dgamma/dbeta in VGPRs across every sample a wave visits, then reduces wave -> block
+//     (fixed order) -> grid (fixed order): deterministic weight gradients, no float atomics.
+// All arithmetic is fp32, as in the reference.
+#pragma once
+#include "common.hpp"
+
+namespace rs_il {
+
+struct FwdReq {
+  hipStream_t stream;
+  const float *x, *W, *bias, *gamma, *beta;
+  int64_t B;
+  int F, E, U, H, L, use_res;
+  float eps, drop_rate;
+  uint64_t seed;
+  float *y, *xsave;
+  int64_t y_ld;  // row stride of y (>= F*U): lets the layer write into a concat buffer
+};
+
+struct BwdReq {
+  hipStream_t stream;
+  const float *x, *xsave, *dy, *W, *bias, *gamma, *beta;
+  int64_t dy_ld;  // row stride of dy (>= F*U)
+  int64_t B;
+  int F, E, U, H, L, use_res;
+  float eps, drop_rate;
+  uint64_t seed;
+  float* dx;
+  int dx_accumulate;
+  float* dparams;
+  int dparams_accumulate;
+  float* workspace;
+  int64_t workspace_floats;
+};
+
+constexpr int kMaxFwdWaves = 4;
+constexpr int kMaxBwdWaves = 2;
+constexpr int kMaxBwdGrid = 1024;
+constexpr size_t kLdsBytes = 160 * 1024;
+
+template <int E_, int U_, int H_, int FMAX_, bool EXACT_ = false>
+struct Cfg {
+  static constexpr int E = E_, U = U_, H = H_, FMAX = FMAX_;
+  static constexpr bool EXACT = EXACT_;                // F == FMAX: no padded keys to mask
+  static constexpr int NC = 4 * U;                     // [Q | K | V | R] projection columns
+  static constexpr int DH = U / H;
+  static constexpr int NCOLW = NC < 64 ? NC : 64;      // lanes per projection row
+  static constexpr int RPI = 64 / NCOLW;               // rows per projection step
+  static constexpr int CPLP = NC / NCOLW;              // column chunks per lane
+  static constexpr int LPR = U < 64 ? U : 64;          // lanes per row in the LN epilogue
+  static constexpr int RG = 64 / LPR;                  // rows per epilogue step
+  static constexpr int CPLN = U / LPR;                 // LN columns per lane
+  static constexpr int RGE = 64 / E;                   // rows per dx step (E <= 64)
+  static constexpr int NPARAM = E * NC + NC + 2 * U;   // W | b | gamma | beta
+  // LDS row strides (floats), compile-time: every access inside an unrolled loop is
+  // base + immediate.  Region bases depend on the runtime F and are per-wave scalars.
+  static constexpr int PRS = NC + 4;                   // projection row stride (16-B aligned)
+  static constexpr int OS = U + 4;                     // attention-output row stride
+  static constexpr int PMS = FMAX + 1;                 // softmax-matrix row stride
+  static constexpr int BWD_FIXED = ((NC * E + 3) & ~3) + ((NPARAM + 3) & ~3);  // W^T + reduce
+  static_assert(U % H == 0, "unit_num must be divisible by head_num");
+  static_assert(E % 4 == 0 && DH % 4 == 0, "E and dh must be multiples of 4");
+  static_assert(E <= 64, "E <= 64");
+};
+
+struct Args {
+  int B, F, L, use_res, ncol;
+  float eps, sdh, drop_rate, drop_scale;
+  uint64_t seed;
+  int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
+};
+
+static inline int r4(int v) { return (v + 3) & ~3; }
+
+template <class C>
+Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate, uint64_t seed,
+               bool bwd) {
+  Args a;
+  a.B = (int)B; a.F = F; a.L = L; a.use_res = use_res;
+  a.ncol = use_res ? C::NC : 3 * C::U;
+  a.eps = eps;
+  a.sdh = (float)__builtin_sqrt((double)C::DH);   // Python float dh ** 0.5 -> fp32 constant
+  a.drop_rate = drop_rate;
+  a.drop_scale = drop_rate > 0.f ? (float)(1.0 / (1.0 - (double)drop_rate)) : 1.f;
+  a.seed = seed;
+  int off = 0;
+  a.l_x = off; off += r4(F * C::E);
+  a.l_pr = off; off += r4(C::FMAX * C::PRS);  // FMAX rows: padded key/value rows stay zero
+  a.l_o = off; off += r4(F * C::OS);
+  a.l_gpr = a.l_dy = a.l_pm = a.l_st = 0;
+  if (bwd) {
+    a.l_gpr = off; off += r4(F * C::PRS);
+    a.l_dy = off; off += r4(F * C::U);
+    a.l_pm = off; off += r4(C::H * F * C::PMS);
+    a.l_st = off; off += r4(2 * F);
+  }
+  a.per_wave = off;
+  return a;
+}
+
+// zero the padded projection rows F..FMAX-1 (done once per kernel; projections never write them)
+template <class C>
+__device__ __forceinline__ void zero_pad_rows(float* PR, int F) {
+  for (int k = F * C::PRS + lane_id(); k < C::FMAX * C::PRS; k += 64) PR[k] = 0.f;
+}
+
+// ---- phase: projections  PR[f][c] = relu(x[f] . W[:, c] + b[c]) ----------------------------
+template <class C>
+__device__ __forceinline__ void project(const float* X, float* PR, const Args& a,
+                                        const float* __restrict__ W,
+                                        const float* __restrict__ bias) {
+  const int lane = lane_id();
+  const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
+#pragma unroll
+  for (int cc = 0; cc < C::CPLP; ++cc) {
+    const int c = cc * C::NCOLW + col;
+    if (cc * C::NCOLW >= a.ncol) break;
+    const bool cact = c < a.ncol;
+    float w[C::E];
+#pragma unroll
+    for (int e = 0; e < C::E; ++e) w[e] = cact ? W[e * C::NC + c] : 0.f;
+    const float bc = cact ? bias[c] : 0.f;
+    for (int f = rsub; f < a.F; f += C::RPI) {
+      const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
+      float acc = 0.f;
+#pragma unroll
+      for (int e4 = 0; e4 < C::E / 4; ++e4) {
+        const float4 xv = xr[e4];
+        acc = fmaf(xv.x, w[4 * e4 + 0], acc);
+        acc = fmaf(xv.y, w[4 * e4 + 1], acc);
+        acc = fmaf(xv.z, w[4 * e4 + 2], acc);
+        acc = fmaf(xv.w, w[4 * e4 + 3], acc);
+      }
+      acc += bc;  // Keras Dense: tensordot, then bias_add, then activation
+      if (cact) PR[f * C::PRS + c] = fmaxf(acc, 0.f);
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void load_row(float (&v)[N], const float* p) {
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) {
+    const float4 t = p4[d4];
+    v[4 * d4] = t.x; v[4 * d4 + 1] = t.y; v[4 * d4 + 2] = t.z; v[4 * d4 + 3] = t.w;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ float dot_row(const float (&q)[N], const float* p) {
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+  float acc = 0.f;
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) {
+    const float4 k = p4[d4];
+    acc = fmaf(q[4 * d4], k.x, acc);
+    acc = fmaf(q[4 * d4 + 1], k.y, acc);
+    acc = fmaf(q[4 * d4 + 2], k.z, acc);
+    acc = fmaf(q[4 * d4 + 3], k.w, acc);
+  }
+  return acc;
+}
+
+template <int N>
+__device__ __forceinline__ void axpy_row(float (&o)[N], float p, const float* v) {
+  const float4* v4 = reinterpret_cast<const float4*>(v);
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) {
+    const float4 t = v4[d4];
+    o[4 * d4] = fmaf(p, t.x, o[4 * d4]);
+    o[4 * d4 + 1] = fmaf(p, t.y, o[4 * d4 + 1]);
+    o[4 * d4 + 2] = fmaf(p, t.z, o[4 * d4 + 2]);
+    o[4 * d4 + 3] = fmaf(p, t.w, o[4 * d4 + 3]);
+  }
+}
+
+// ---- phase: attention forward; optionally keeps P (pre-dropout) for backward ----------------
+template <class C, bool STORE_P, bool DROP>
+__device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* PM,
+                                              const Args& a, int64_t b, uint64_t lseed) {
+  const int lane = lane_id();
+  const int F = a.F;
+  for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+    const int r = r0 + lane;
+    const bool act = r < C::H * F;
+    const int h = act ? r / F : 0, i = act ? r % F : 0;
+    float q[C::DH];
+    load_row(q, PR + i * C::PRS + h * C::DH);
+    const float* kb = PR + C::U + h * C::DH;
+    float s[C::FMAX];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < C::FMAX; ++j) {
+      const float acc = dot_row(q, kb + j * C::PRS);
+      s[j] = (C::EXACT || j < F) ? acc / a.sdh : -INFINITY;
+      mx = fmaxf(mx, s[j]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < C::FMAX; ++j) { s[j] = expf(s[j] - mx); sum += s[j]; }
+    const float inv = 1.0f / sum;
+    float o[C::DH];
+#pragma unroll
+    for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
+    const float* vb = PR + 2 * C::U + h * C::DH;
+    float* pm_row = PM + (h * F + i) * C::PMS;
+#pragma unroll
+    for (int j = 0; j < C::FMAX; ++j) {
+      float p = s[j] * inv;
+      if (STORE_P && act) pm_row[j] = p;
+      if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+      axpy_row(o, p, vb + j * C::PRS);
+    }
+    if (act) {
+      float4* orow = reinterpret_cast<float4*>(O + i * C::OS + h * C::DH);
+#pragma unroll
+      for (int d4 = 0; d4 < C::DH / 4; ++d4)
+        orow[d4] = make_float4(o[4 * d4], o[4 * d4 + 1], o[4 * d4 + 2], o[4 * d4 + 3]);
+    }
+  }
+}
+
+// ---- phase: z = relu(O + R); y = LN(z).  MODE 0: write y (to LDS X or to global).
+//      MODE 1 (backward recompute): keep z in O, (mean, std) per row in ST. -----------------
+template <class C, int MODE>
+__device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, float* Y,
+                                         int y_stride, const Args& a,
+                                         const float* __restrict__ gamma,
+                                         const float* __restrict__ beta) {
+  const int lane = lane_id();
+  const int u0 = lane % C::LPR;
+  for (int f0 = 0; f0 < a.F; f0 += C::RG) {
+    const int f = f0 + lane / C::LPR;
+    const bool act = f < a.F;
+    float z[C::CPLN];
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < C::CPLN; ++c) {
+      const int u = u0 + c * C::LPR;
+      float t = act ? O[f * C::OS + u] : 0.f;
+      if (a.use_res && act) t += PR[f * C::PRS + 3 * C::U + u];
+      z[c] = fmaxf(t, 0.f);
+      sum += z[c];
+    }
+    const float mean = group_sum<C::LPR>(sum) / (float)C::U;
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
+    const float var = group_sum<C::LPR>(sq) / (float)C::U;
+    const float sd = sqrtf(var + a.eps);
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < C::CPLN; ++c) {
+        const int u = u0 + c * C::LPR;
+        if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) / sd * gamma[u] + beta[u];
+        else O[f * C::OS + u] = z[c];
+      }
+      if (MODE == 1 && u0 == 0) { ST[2 * f] = mean; ST[2 * f + 1] = sd; }
+    }
+  }
+}
+
+// ============================== forward kernel ===============================================
+template <class C, bool DROP>
+__global__ void __launch_bounds__(256, 3) fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y,
+    int64_t y_ld, float* __restrict__ xsave, Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* base = smem + wave_id() * a.per_wave;
+  float* X = base + a.l_x;
+  float* PR = base + a.l_pr;
+  float* O = base + a.l_o;
+  const int lane = lane_id();
+  const int wpb = blockDim.x >> 6;
+  const int F = a.F;
+  zero_pad_rows<C>(PR, F);
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_id(); b < a.B; b += (int64_t)gridDim.x * wpb) {
+    const float4* src = reinterpret_cast<const float4*>(x + b * F * C::E);
+    for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
+    wave_lds_sync();
+    for (int it = 0; it < a.L; ++it) {
+      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      project<C>(X, PR, a, W, bias);
+      wave_lds_sync();
+      attention_fwd<C, false, DROP>(PR, O, nullptr, a, b, lseed);
+      wave_lds_sync();
+      if (it == a.L - 1) {
+        epilogue<C, 0>(O, PR, nullptr, y + b * y_ld, C::U, a, gamma, beta);
+      } else {
+        epilogue<C, 0>(O, PR, nullptr, X, C::E, a, gamma, beta);  // E == U when L > 1
+        wave_lds_sync();
+        if (xsave) {
+          float4* dst = reinterpret_cast<float4*>(xsave + ((int64_t)it * a.B + b) * F * C::U);
+          for (int k = lane; k < F * C::U / 4; k += 64) dst[k] = reinterpret_cast<float4*>(X)[k];
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+// ============================== backward kernel ==============================================
+template <class C, bool DROP>
+__global__ void __launch_bounds__(128) bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
+    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ dx, int dx_accumulate,
+    float* __restrict__ partials, Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wpb = blockDim.x >> 6;
+  float* WT = smem;                                      // [NC][E]  (shared by the block)
+  float* RED = WT + ((C::NC * C::E + 3) & ~3);           // [NPARAM] block reduction buffer
+  float* base = smem + C::BWD_FIXED + wave_id() * a.per_wave;
+  float* X = base + a.l_x;
+  float* PR = base + a.l_pr;
+  float* GPR = base + a.l_gpr;
+  float* O = base + a.l_o;
+  float* DY = base + a.l_dy;
+  float* PM = base + a.l_pm;
+  float* ST = base + a.l_st;
+  const int lane = lane_id();
+  const int F = a.F;
+
+  for (int k = threadIdx.x; k < C::NC * C::E; k += blockDim.x) {
+    const int c = k / C::E, e = k % C::E;
+    WT[k] = W[e * C::NC + c];
+  }
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
+  zero_pad_rows<C>(PR, F);
+  __syncthreads();
+
+  // per-lane gradient accumulators, kept in VGPRs across every sample this wave visits
+  float dw[C::CPLP][C::E];
+  float db[C::CPLP];
+  float dg[C::CPLN], dbt[C::CPLN];
+#pragma unroll
+  for (int cc = 0; cc < C::CPLP; ++cc) {
+    db[cc] = 0.f;
+#pragma unroll
+    for (int e = 0; e < C::E; ++e) dw[cc][e] = 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; }
+
+  const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
+  const int u0 = lane % C::LPR;
+
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_id(); b < a.B; b += (int64_t)gridDim.x * wpb) {
+    {
+      const float* src = dy + b * dy_ld;
+      for (int k = lane; k < F * C::U; k += 64) DY[k] = src[k];  // dy_ld may be unaligned
+    }
+    for (int it = a.L - 1; it >= 0; --it) {
+      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      {
+        const float* xin = (it == 0) ? (x + b * F * C::E)
+                                     : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
+        const float4* src = reinterpret_cast<const float4*>(xin);
+        for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
+      }
+      wave_lds_sync();
+      // ---- recompute the iteration ----
+      project<C>(X, PR, a, W, bias);
+      wave_lds_sync();
+      attention_fwd<C, true, DROP>(PR, O, PM, a, b, lseed);
+      wave_lds_sync();
+      epilogue<C, 1>(O, PR, ST, nullptr, 0, a, gamma, beta);
+      wave_lds_sync();
+      // ---- LN + ReLU backward: O <- dt = dL/d(O+R);  GPR[R cols] <- dt * (R > 0) ----
+      for (int f0 = 0; f0 < F; f0 += C::RG) {
+        const int f = f0 + lane / C::LPR;
+        const bool act = f < F;
+        const float mean = act ? ST[2 * f] : 0.f;
+        const float sd = act ? ST[2 * f + 1] : 1.f;
+        float zv[C::CPLN], zh[C::CPLN], g[C::CPLN];
+        float sg = 0.f, sgz = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          zv[c] = act ? O[f * C::OS + u] : 0.f;
+          zh[c] = (zv[c] - mean) / sd;
+          const float dyv = act ? DY[f * C::U + u] : 0.f;
+          dg[c] = fmaf(dyv, zh[c], dg[c]);
+          dbt[c] += dyv;
+          g[c] = dyv * gamma[u];
+          sg += g[c];
+          sgz += g[c] * zh[c];
+        }
+        sg = group_sum<C::LPR>(sg) / (float)C::U;
+        sgz = group_sum<C::LPR>(sgz) / (float)C::U;
+        if (act) {
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            const float dz = (g[c] - sg - zh[c] * sgz) / sd;
+            const float dt = zv[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+            O[f * C::OS + u] = dt;
+            if (a.use_res)
+              GPR[f * C::PRS + 3 * C::U + u] = PR[f * C::PRS + 3 * C::U + u] > 0.f ? dt : 0.f;
+          }
+        }
+      }
+      wave_lds_sync();
+      // ---- dV_j = sum_i Pd_ij dO_i   (lane = (h, j)) ----
+      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < C::H * F;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dv[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
+        for (int i = 0; i < F; ++i) {
+          float p = PM[(h * F + i) * C::PMS + j];
+          if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+          axpy_row(dv, p, O + i * C::OS + h * C::DH);
+        }
+        if (act) {
+          const float* vr = PR + j * C::PRS + 2 * C::U + h * C::DH;
+          float* gv = GPR + j * C::PRS + 2 * C::U + h * C::DH;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] : 0.f;
+        }
+      }
+      wave_lds_sync();
+      // ---- dS (in place of P) and dQ   (lane = (h, i)) ----
+      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < C::H * F;
+        const int h = act ? r / F : 0, i = act ? r % F : 0;
+        float dO[C::DH];
+        load_row(dO, O + i * C::OS + h * C::DH);
+        const float* vb = PR + 2 * C::U + h * C::DH;
+        const float* kb = PR + C::U + h * C::DH;
+        float* pm_row = PM + (h * F + i) * C::PMS;
+        float s[C::FMAX];
+        float D = 0.f;
+#pragma unroll
+        for (int j = 0; j < C::FMAX; ++j) {
+          float dp = dot_row(dO, vb + j * C::PRS);  // padded V rows are zero -> dp = 0
+          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          const float p = pm_row[j];  // padded keys were stored as p = 0
+          D = fmaf(p, dp, D);
+          s[j] = dp;
+        }
+        float dq[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
+#pragma unroll
+        for (int j = 0; j < C::FMAX; ++j) {
+          const float ds = pm_row[j] * (s[j] - D) / a.sdh;
+          if (act) pm_row[j] = ds;
+          axpy_row(dq, ds, kb + j * C::PRS);
+        }
+        if (act) {
+          const float* qr = PR + i * C::PRS + h * C::DH;
+          float* gq = GPR + i * C::PRS + h * C::DH;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] : 0.f;
+        }
+      }
+      wave_lds_sync();
+      // ---- dK_j = sum_i dS_ij Q_i   (lane = (h, j)) ----
+      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < C::H * F;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dk[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
+        for (int i = 0; i < F; ++i) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+        if (act) {
+          const float* kr = PR + j * C::PRS + C::U + h * C::DH;
+          float* gk = GPR + j * C::PRS + C::U + h * C::DH;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] : 0.f;
+        }
+      }
+      wave_lds_sync();
+      // ---- dW[:, c] += X^T g ; db[c] += sum_f g   (lane = column) ----
+#pragma unroll
+      for (int cc = 0; cc < C::CPLP; ++cc) {
+        const int c = cc * C::NCOLW + col;
+        if (c < a.ncol) {
+          for (int f = rsub; f < F; f += C::RPI) {
+            const float gcol = GPR[f * C::PRS + c];
+            db[cc] += gcol;
+            const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
+#pragma unroll
+            for (int e4 = 0; e4 < C::E / 4; ++e4) {
+              const float4 xv = xr[e4];
+              dw[cc][4 * e4] = fmaf(xv.x, gcol, dw[cc][4 * e4]);
+              dw[cc][4 * e4 + 1] = fmaf(xv.y, gcol, dw[cc][4 * e4 + 1]);
+              dw[cc][4 * e4 + 2] = fmaf(xv.z, gcol, dw[cc][4 * e4 + 2]);
+              dw[cc][4 * e4 + 3] = fmaf(xv.w, gcol, dw[cc][4 * e4 + 3]);
+            }
+          }
+        }
+      }
+      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e)) ----
+      {
+        const int e = lane % C::E;
+        for (int f0 = 0; f0 < F; f0 += C::RGE) {
+          const int f = f0 + lane / C::E;
+          if (f < F) {
+            float acc = 0.f;
+            const float* gr = GPR + f * C::PRS;
+            for (int c = 0; c < a.ncol; ++c) acc = fmaf(gr[c], WT[c * C::E + e], acc);
+            if (it > 0) {
+              DY[f * C::U + e] = acc;  // gradient w.r.t. the previous iteration's output
+            } else {
+              float* d = dx + b * F * C::E + f * C::E + e;
+              *d = dx_accumulate ? (*d + acc) : acc;
+            }
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+
+  // ---- lanes -> wave (xor butterfly over row sub-groups) -> block (wave order) ----
+#pragma unroll
+  for (int cc = 0; cc < C::CPLP; ++cc) {
+#pragma unroll
+    for (int o = C::NCOLW; o < 64; o <<= 1) {
+      db[cc] += __shfl_xor(db[cc], o, 64);
+#pragma unroll
+      for (int e = 0; e < C::E; ++e) dw[cc][e] += __shfl_xor(dw[cc][e], o, 64);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) {
+#pragma unroll
+    for (int o = C::LPR; o < 64; o <<= 1) {
+      dg[c] += __shfl_xor(dg[c], o, 64);
+      dbt[c] += __shfl_xor(dbt[c], o, 64);
+    }
+  }
+  for (int w = 0; w < wpb; ++w) {
+    if (wave_id() == w) {
+      if (rsub == 0) {
+#pragma unroll
+        for (int cc = 0; cc < C::CPLP; ++cc) {
+          const int c = cc * C::NCOLW + col;
+#pragma unroll
+          for (int e = 0; e < C::E; ++e) RED[e * C::NC + c] += dw[cc][e];
+          RED[C::E * C::NC + c] += db[cc];
+        }
+      }
+      if (lane < C::LPR) {
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          RED[C::E * C::NC + C::NC + u] += dg[c];
+          RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
+    partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
+}
+
+// grid-level reduction of the per-block partials, fixed block order (deterministic)
+__global__ void reduce_params_kernel(const float* __restrict__ partials, int nblocks, int nparam,
+                                     float* __restrict__ out, int accumulate);
+
+// ---------------------------------------------------------------------------------------------
+template <class C, bool DROP>
+int fwd_launch(const FwdReq& q) {
+  if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
+  Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, false);
+  const size_t per_wave = (size_t)a.per_wave * sizeof(float);
+  int wpb = (int)(kLdsBytes / per_wave);
+  if (wpb > kMaxFwdWaves) wpb = kMaxFwdWaves;
+  if (wpb < 1) return RS_ERR_UNSUPPORTED;
+  int64_t grid = (q.B + wpb - 1) / wpb;
+  if (grid > 4096) grid = 4096;
+  if (grid == 0) return RS_OK;
+  fwd_kernel<C, DROP><<<(int)grid, 64 * wpb, per_wave * wpb, q.stream>>>(
+      q.x, q.W, q.bias, q.gamma, q.beta, q.y, q.y_ld, q.xsave, a);
+  return rs_status_after_launch();
+}
+
+template <class C, bool DROP>
+int bwd_launch(const BwdReq& q) {
+  if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
+  Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
+  const size_t fixed = (size_t)C::BWD_FIXED * sizeof(float);
+  const size_t per_wave = (size_t)a.per_wave * sizeof(float);
+  if (fixed + per_wave > kLdsBytes) return RS_ERR_UNSUPPORTED;
+  int wpb = (int)((kLdsBytes - fixed) / per_wave);
+  if (wpb > kMaxBwdWaves) wpb = kMaxBwdWaves;
+  int64_t grid = (q.B + wpb - 1) / wpb;
+  const int64_t max_grid = q.workspace_floats / C::NPARAM;
+  if (grid > kMaxBwdGrid) grid = kMaxBwdGrid;
+  if (grid > max_grid) grid = max_grid;
+  if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
+  bwd_kernel<C, DROP><<<(int)grid, 64 * wpb, fixed + per_wave * wpb, q.stream>>>(
+      q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
+      q.workspace, a);
+  if (q.dparams)  // NULL: leave the per-block partials in the workspace (kernel timing)
+    reduce_params_kernel<<<(C::NPARAM + 255) / 256, 256, 0, q.stream>>>(
+        q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+// EXACT instantiations (F == FMAX) drop the padded-key mask entirely.
+template <int E, int U, int H, int FMAX, bool EXACT = false>
+int try_fwd(const FwdReq& q) {
+  if (q.E != E || q.U != U || q.H != H || q.F > FMAX || (EXACT && q.F != FMAX))
+    return RS_ERR_UNSUPPORTED;
+  return q.drop_rate > 0.f ? fwd_launch<Cfg<E, U, H, FMAX, EXACT>, true>(q)
+                           : fwd_launch<Cfg<E, U, H, FMAX, EXACT>, false>(q);
+}
+
+template <int E, int U, int H, int FMAX, bool EXACT = false>
+int try_bwd(const BwdReq& q) {
+  if (q.E != E || q.U != U || q.H != H || q.F > FMAX || (EXACT && q.F != FMAX))
+    return RS_ERR_UNSUPPORTED;
+  return q.drop_rate > 0.f ? bwd_launch<Cfg<E, U, H, FMAX, EXACT>, true>(q)
+                           : bwd_launch<Cfg<E, U, H, FMAX, EXACT>, false>(q);
+}
+
+// Each instantiation unit (il_inst_*.hip) defines one pair of these.
+#define RS_IL_DECLARE_UNIT(name)          \
+  int name##_fwd(const rs_il::FwdReq& q); \
+  int name##_bwd(const rs_il::BwdReq& q);
+
+}  // namespace rs_il

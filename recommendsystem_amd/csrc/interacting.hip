@@ -1,0 +1,63 @@
+// C-ABI entry points of the fused InteractingLayer (kernels: il_kernels.hpp, instantiations:
+// il_inst_*.hip).  Replaces InteractingLayer.call (InteractingLayer.py:37-61) forward and the
+// TF autograd of that graph for backward.
+#include "il_kernels.hpp"
+
+namespace rs_il {
+RS_IL_DECLARE_UNIT(il_unit_a)
+RS_IL_DECLARE_UNIT(il_unit_b)
+RS_IL_DECLARE_UNIT(il_unit_c)
+
+__global__ void reduce_params_kernel(const float* __restrict__ partials, int nblocks, int nparam,
+                                     float* __restrict__ out, int accumulate) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nparam; k += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < nblocks; ++b) s += partials[(int64_t)b * nparam + k];
+    out[k] = accumulate ? out[k] + s : s;
+  }
+}
+}  // namespace rs_il
+
+RS_API int rs_il_param_count(int E, int U) { return E * 4 * U + 4 * U + 2 * U; }
+
+RS_API int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U) {
+  int64_t grid = B < 1 ? 1 : B;
+  if (grid > rs_il::kMaxBwdGrid) grid = rs_il::kMaxBwdGrid;
+  return grid * (int64_t)rs_il_param_count(E, U);
+}
+
+RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
+                     const float* W, const float* bias, const float* gamma, const float* beta,
+                     float eps, int use_res, float drop_rate, uint64_t seed, float* y,
+                     int64_t y_ld, float* xsave) {
+  if (!x || !W || !bias || !gamma || !beta || !y || B < 0 || F <= 0 || L <= 0 || H <= 0)
+    return RS_ERR_ARG;
+  if (U % H != 0 || (L > 1 && (E != U || !xsave))) return RS_ERR_ARG;
+  if (drop_rate < 0.f || drop_rate >= 1.f || y_ld < (int64_t)F * U) return RS_ERR_ARG;
+  rs_il::FwdReq q{rs_stream(stream), x, W, bias, gamma, beta, B, F, E, U, H, L, use_res,
+                  eps, drop_rate, seed, y, xsave, y_ld};
+  int r = rs_il::il_unit_a_fwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
+  return r;
+}
+
+RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
+                     int64_t dy_ld, int64_t B,
+                     int F, int E, int U, int H, int L, const float* W, const float* bias,
+                     const float* gamma, const float* beta, float eps, int use_res,
+                     float drop_rate, uint64_t seed, float* dx, int dx_accumulate,
+                     float* dparams, int dparams_accumulate, float* workspace,
+                     int64_t workspace_floats) {
+  if (!x || !dy || !W || !bias || !gamma || !beta || !dx || !workspace) return RS_ERR_ARG;
+  if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
+    return RS_ERR_ARG;
+  if (drop_rate < 0.f || drop_rate >= 1.f || dy_ld < (int64_t)F * U) return RS_ERR_ARG;
+  rs_il::BwdReq q{rs_stream(stream), x, xsave, dy, W, bias, gamma, beta, dy_ld, B, F, E, U, H, L,
+                  use_res, eps, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
+                  workspace, workspace_floats};
+  int r = rs_il::il_unit_a_bwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
+  return r;
+}

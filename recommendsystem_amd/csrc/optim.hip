@@ -1,0 +1,233 @@
+// H11 — optimizers on the path.
+//
+// Dense: tn.optimizer.Optimizer(tn.core.Adam(lr, beta1, beta2, epsilon)) at
+//   rank/ctr/base_model.py:192-193, rank/multi_head/model.py:52-53, staytime/model.py:72,
+//   rough_rank/model.py:209, rank/finish/model.py:41.
+// Sparse: tn.core.Adam handed to EmbeddingFeatures (rank/ctr/base_model.py:163,
+//   rank/multi_head/multidnn.py:235, rough_rank/model.py:106) and tn.core.AdaGrad
+//   (staytime/VideoDnn.py:233,259).
+// tensornet is not vendored, so the update forms are pinned here and restated in
+// oracle/ctr_oracle.py:
+//   dense Adam  : t += 1; lr_t = lr*sqrt(1-b2^t)/(1-b1^t); m = b1 m + (1-b1) g;
+//                 v = b2 v + (1-b2) g^2; w -= lr_t * m / (sqrt(v) + eps)      (tf.keras form)
+//   sparse Adam : per touched row, no bias correction (tensornet SparseAdamValue form):
+//                 m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; w -= lr * m / (eps + sqrt(v))
+//   sparse AdaGrad: g2 += g^2 (per element, initialised to initial_g2sum);
+//                 w -= lr * g / sqrt(g2)
+// The dense parameters of a model live in ONE flat fp32 arena (params | grads | m | v), so the
+// dense step is one launch and the data-parallel all-reduce is one bucket.
+#include "common.hpp"
+
+__global__ void __launch_bounds__(256) dense_adam_kernel(float* __restrict__ p,
+                                                        float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        int64_t n, const int64_t* __restrict__ step,
+                                                        float lr, float b1, float b2, float eps,
+                                                        float grad_scale, int zero_grad) {
+  const int64_t t = step[0] + 1;
+  const float bc1 = 1.0f - powf(b1, (float)t);
+  const float bc2 = 1.0f - powf(b2, (float)t);
+  const float lr_t = lr * sqrtf(bc2) / bc1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * grad_scale;
+    if (zero_grad) g[i] = 0.f;  // fused zero_grad: the next backward accumulates into g
+    const float mi = b1 * m[i] + (1.0f - b1) * gi;
+    const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+__global__ void step_increment_kernel(int64_t* step) { step[0] += 1; }
+
+RS_API int rs_dense_adam(void* stream, float* params, float* grads, float* m, float* v,
+                         int64_t n, int64_t* step, float lr, float beta1, float beta2, float eps,
+                         float grad_scale, int zero_grad) {
+  if (!params || !grads || !m || !v || !step || n < 0) return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  if (n > 0) {
+    int64_t grid = (n + 255) / 256;
+    if (grid > 2048) grid = 2048;
+    dense_adam_kernel<<<(int)grid, 256, 0, s>>>(params, grads, m, v, n, step, lr, beta1, beta2,
+                                                eps, grad_scale, zero_grad);
+  }
+  step_increment_kernel<<<1, 1, 0, s>>>(step);
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse Adam over the rows touched this step.  One group of `lps` lanes per row; the group also
+// zeroes the row's gradient slot and releases its claim flag so the next step starts clean.
+// The row count lives on the device (written by rs_sparse_grad_accumulate), so the grid is sized
+// by the capacity and idle groups exit: no host sync, graph-capturable.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sparse_adam_kernel(
+    float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
+    float* __restrict__ grad_table, int32_t* __restrict__ flag,
+    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched, int dim,
+    int lps, float lr, float b1, float b2, float eps, float grad_scale) {
+  const int nrows = *n_touched;
+  const int per_block = blockDim.x / lps;
+  const int gi = threadIdx.x / lps;
+  const int l = threadIdx.x % lps;
+  for (int u = blockIdx.x * per_block + gi; u < nrows; u += gridDim.x * per_block) {
+    const int64_t row = touched[u];
+    const int64_t base = row * dim;
+    for (int e = l; e < dim; e += lps) {
+      const float g = grad_table[base + e] * grad_scale;
+      const float mi = b1 * m[base + e] + (1.0f - b1) * g;
+      const float vi = b2 * v[base + e] + (1.0f - b2) * g * g;
+      m[base + e] = mi;
+      v[base + e] = vi;
+      table[base + e] -= lr * mi / (eps + sqrtf(vi));
+      grad_table[base + e] = 0.f;
+    }
+    if (l == 0) flag[row] = -1;
+  }
+}
+
+__global__ void __launch_bounds__(256) sparse_adagrad_kernel(
+    float* __restrict__ table, float* __restrict__ g2sum, float* __restrict__ grad_table,
+    int32_t* __restrict__ flag, const int32_t* __restrict__ touched,
+    const int32_t* __restrict__ n_touched, int dim, int lps, float lr, float grad_scale) {
+  const int nrows = *n_touched;
+  const int per_block = blockDim.x / lps;
+  const int gi = threadIdx.x / lps;
+  const int l = threadIdx.x % lps;
+  for (int u = blockIdx.x * per_block + gi; u < nrows; u += gridDim.x * per_block) {
+    const int64_t row = touched[u];
+    const int64_t base = row * dim;
+    for (int e = l; e < dim; e += lps) {
+      const float g = grad_table[base + e] * grad_scale;
+      const float s2 = g2sum[base + e] + g * g;
+      g2sum[base + e] = s2;
+      table[base + e] -= lr * g / sqrtf(s2);
+      grad_table[base + e] = 0.f;
+    }
+    if (l == 0) flag[row] = -1;
+  }
+}
+
+static int lanes_for_dim(int dim) {
+  int lps = 1;
+  while (lps < dim && lps < 64) lps <<= 1;
+  return lps;
+}
+
+RS_API int rs_sparse_adam(void* stream, float* table, float* m, float* v, float* grad_table,
+                          int32_t* flag, const int32_t* touched, int32_t* n_touched, int dim,
+                          int32_t max_rows, float lr, float beta1, float beta2, float eps,
+                          float grad_scale) {
+  if (!table || !m || !v || !grad_table || !flag || !touched || !n_touched || dim <= 0)
+    return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  const int lps = lanes_for_dim(dim);
+  if (max_rows > 0) {
+    int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    sparse_adam_kernel<<<(int)grid, 256, 0, s>>>(table, m, v, grad_table, flag, touched,
+                                                 n_touched, dim, lps, lr, beta1, beta2, eps,
+                                                 grad_scale);
+  }
+  hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* grad_table,
+                             int32_t* flag, const int32_t* touched, int32_t* n_touched, int dim,
+                             int32_t max_rows, float lr, float grad_scale) {
+  if (!table || !g2sum || !grad_table || !flag || !touched || !n_touched || dim <= 0)
+    return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  const int lps = lanes_for_dim(dim);
+  if (max_rows > 0) {
+    int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    sparse_adagrad_kernel<<<(int)grid, 256, 0, s>>>(table, g2sum, grad_table, flag, touched,
+                                                    n_touched, dim, lps, lr, grad_scale);
+  }
+  hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Data-parallel sparse exchange helpers.
+//   compact: move this rank's touched rows out of the gradient table into a dense list
+//            (rows_out[u], grads_out[u, :]), zero the slots and release the flags, so the
+//            table is clean for the rank-ordered merge.
+//   merge  : add one rank's list into the table (rows are unique within a list, so plain adds
+//            with no atomics), claiming rows into `touched`.  Called once per rank in rank
+//            order on every replica -> bitwise-identical sums on all replicas.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sparse_compact_kernel(
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, const int32_t* __restrict__ touched,
+    const int32_t* __restrict__ n_touched, int dim, int lps, int32_t* __restrict__ rows_out,
+    float* __restrict__ grads_out, int32_t cap) {
+  const int nrows = min(*n_touched, cap);
+  const int per_block = blockDim.x / lps;
+  const int gi = threadIdx.x / lps;
+  const int l = threadIdx.x % lps;
+  for (int u = blockIdx.x * per_block + gi; u < cap; u += gridDim.x * per_block) {
+    if (u < nrows) {
+      const int64_t row = touched[u];
+      for (int e = l; e < dim; e += lps) {
+        grads_out[(int64_t)u * dim + e] = grad_table[row * dim + e];
+        grad_table[row * dim + e] = 0.f;
+      }
+      if (l == 0) { rows_out[u] = (int32_t)row; flag[row] = -1; }
+    } else {
+      if (l == 0) rows_out[u] = -1;  // padding entries are skipped by the merge
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) sparse_merge_kernel(
+    const int32_t* __restrict__ rows, const float* __restrict__ grads, int32_t count, int dim,
+    int lps, float* __restrict__ grad_table, int32_t* __restrict__ flag,
+    int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
+  const int per_block = blockDim.x / lps;
+  const int gi = threadIdx.x / lps;
+  const int l = threadIdx.x % lps;
+  for (int u = blockIdx.x * per_block + gi; u < count; u += gridDim.x * per_block) {
+    const int32_t row = rows[u];
+    if (row < 0) continue;
+    if (l == 0 && atomicCAS(&flag[row], -1, -2) == -1) {
+      const int32_t k = atomicAdd(n_touched, 1);
+      if (k < touched_cap) touched[k] = row;
+    }
+    for (int e = l; e < dim; e += lps)
+      grad_table[(int64_t)row * dim + e] += grads[(int64_t)u * dim + e];
+  }
+}
+
+RS_API int rs_sparse_compact(void* stream, float* grad_table, int32_t* flag,
+                             const int32_t* touched, int32_t* n_touched, int dim,
+                             int32_t* rows_out, float* grads_out, int32_t cap) {
+  if (!grad_table || !flag || !touched || !n_touched || !rows_out || !grads_out || dim <= 0)
+    return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  const int lps = lanes_for_dim(dim);
+  if (cap > 0) {
+    int64_t grid = ((int64_t)cap * lps + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    sparse_compact_kernel<<<(int)grid, 256, 0, s>>>(grad_table, flag, touched, n_touched, dim,
+                                                    lps, rows_out, grads_out, cap);
+  }
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* grads,
+                                int32_t count, int dim, float* grad_table, int32_t* flag,
+                                int32_t* touched, int32_t* n_touched, int32_t touched_cap) {
+  if (!rows || !grads || !grad_table || !flag || !touched || !n_touched || dim <= 0)
+    return RS_ERR_ARG;
+  if (count <= 0) return RS_OK;
+  const int lps = lanes_for_dim(dim);
+  int64_t grid = ((int64_t)count * lps + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  sparse_merge_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(
+      rows, grads, count, dim, lps, grad_table, flag, touched, n_touched, touched_cap);
+  return rs_status_after_launch();
+}

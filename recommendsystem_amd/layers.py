@@ -1,0 +1,236 @@
+"""Drop-in layers for the CTR feature-interaction path, keeping the reference's constructor
+kwargs, call signatures and error messages; every compute step runs in librecsys_amd.so.
+
+    InteractingLayer   InteractingLayer.py:7-61 (== rank/multi_head/interacting_layer.py)
+    Dense              tf.keras.layers.Dense(units, activation) as used on the path
+    MultiLayerDense    common_module.multi_dense_layer.MultiLayerDense (absent from the reference;
+                       pinned: sequential Dense(u, activation) for every u, SURVEY §8c decision 2)
+
+Layers are torch.nn.Modules.  Like Keras, parameters are created on the first call from the
+input's last dimension (or by an explicit ``build(input_shape)``).  Gradients: when a layer's
+``.grad`` tensors live in one flat block (always, unless the caller replaced them), the backward
+kernels accumulate into them in place and autograd receives ``None`` for the weights -- no extra
+accumulate kernels.  Otherwise the gradients are returned to autograd normally.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _lib
+from ._lib import call, ptr, stream_handle
+from .params import FlatBlock, glorot_uniform_, grads_contiguous
+
+ACTIVATIONS = {None: 0, "linear": 0, "relu": 1, "sigmoid": 2}
+
+
+def _act_code(activation) -> int:
+    if activation in ACTIVATIONS:
+        return ACTIVATIONS[activation]
+    raise NotImplementedError(f"activation {activation!r} is not on the fused path "
+                              f"(supported: {sorted(k for k in ACTIVATIONS if k)})")
+
+
+# ============================================================================================
+# InteractingLayer
+# ============================================================================================
+class _InteractingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, bias, gamma, beta, layer, seed, drop_rate):
+        _lib.require_device(x, W)
+        x = x.contiguous()
+        B, F, E = x.shape
+        U, H, L = layer.unit_num, layer.head_num, layer.layer_num
+        y = torch.empty(B, F, U, device=x.device, dtype=torch.float32)
+        xsave = torch.empty(max(L - 1, 0), B, F, U, device=x.device, dtype=torch.float32)
+        call("rs_il_fwd", stream_handle(), ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma),
+             ptr(beta), layer.epsilon, int(layer.use_res), drop_rate, seed, ptr(y), F * U,
+             ptr(xsave) if L > 1 else None)
+        ctx.save_for_backward(x, xsave, W, bias, gamma, beta)
+        ctx.layer, ctx.seed, ctx.drop_rate = layer, seed, drop_rate
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xsave, W, bias, gamma, beta = ctx.saved_tensors
+        layer = ctx.layer
+        dy = dy.contiguous()
+        B, F, E = x.shape
+        U, H, L = layer.unit_num, layer.head_num, layer.layer_num
+        dx = torch.empty_like(x)
+        ws_n = int(_lib.load().rs_il_bwd_workspace_floats(B, E, U))
+        ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
+        params = (W, bias, gamma, beta)
+        block = grads_contiguous(params)
+        in_place = block is not None
+        dparams = block if in_place else torch.empty(
+            sum(p.numel() for p in params), device=x.device, dtype=torch.float32)
+        call("rs_il_bwd", stream_handle(), ptr(x), ptr(xsave) if L > 1 else None, ptr(dy), F * U,
+             B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), layer.epsilon,
+             int(layer.use_res), ctx.drop_rate, ctx.seed, ptr(dx), 0, ptr(dparams),
+             1 if in_place else 0, ptr(ws), ws_n)
+        if in_place:
+            return dx, None, None, None, None, None, None, None
+        outs, off = [], 0
+        for p in params:
+            outs.append(dparams[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+        return (dx, *outs, None, None, None)
+
+
+class InteractingLayer(nn.Module):
+    """AutoInt interacting layer, InteractingLayer.py:7-61.
+
+    Same kwargs/defaults as the reference (:9-16).  ``ln_epsilon`` pins the epsilon of the
+    missing ``layer_normalization.LayerNormalization`` (keras-layer-normalization default
+    K.epsilon()**2 = 1e-14; SURVEY §8c open decision 1).  ``seed`` seeds the counter-based
+    dropout mask (InteractingLayer.py:53-54; active only in training mode with use_dropout).
+    """
+
+    def __init__(self, layer_num=1, unit_num=128, head_num=1, use_dropout=False, dropout_rate=0.3,
+                 use_res=True, ln_epsilon=1e-14, seed=0, device=None, **kwargs):
+        super().__init__()
+        self.layer_num = int(layer_num)
+        self.unit_num = int(unit_num)
+        self.head_num = int(head_num)
+        self.use_dropout = bool(use_dropout)
+        self.dropout_rate = float(dropout_rate)
+        self.use_res = bool(use_res)
+        self.epsilon = float(ln_epsilon)
+        self.seed = int(seed)
+        self._calls = 0
+        self._device = device
+        self.built = False
+        self.name = kwargs.get("name", "interacting_layer")
+
+    # Keras Layer.build (InteractingLayer.py:33-35) + the Dense builds it triggers
+    def build(self, input_shape, device=None):
+        if len(input_shape) != 3:
+            raise ValueError('The rank of input of InteractingLayer must be 3, but now is %d'
+                             % len(input_shape))
+        E, U, H = int(input_shape[-1]), self.unit_num, self.head_num
+        if U % H != 0:  # tf.split(query, head_num, axis=2) (InteractingLayer.py:47)
+            raise ValueError(f"Dimension size must be evenly divisible by {H} but is {U}")
+        if self.layer_num > 1 and E != U:  # the tied Dense kernels are built for the first input
+            raise ValueError(f"layer_num > 1 needs unit_num == input dim (tied weights): "
+                             f"unit_num={U}, input dim={E}")
+        device = device or self._device or torch.device("cuda")
+        blk = FlatBlock([(E, 4 * U), (4 * U,), (U,), (U,)], device)
+        self.kernel, self.bias, self.gamma, self.beta = blk.params()
+        gen = torch.Generator().manual_seed(self.seed)
+        with torch.no_grad():
+            for j in range(4):  # query / key / value / res Dense kernels, each glorot_uniform
+                k = torch.empty(E, U)
+                glorot_uniform_(k, E, U, gen)
+                self.kernel[:, j * U:(j + 1) * U].copy_(k)
+            self.gamma.fill_(1.0)
+        self.input_dim = E
+        self.built = True
+
+    # Keras-named views of the fused [E, 4U] kernel
+    def dense_kernel(self, which: str) -> torch.Tensor:
+        j = {"query": 0, "key": 1, "value": 2, "res": 3}[which]
+        return self.kernel[:, j * self.unit_num:(j + 1) * self.unit_num]
+
+    def dense_bias(self, which: str) -> torch.Tensor:
+        j = {"query": 0, "key": 1, "value": 2, "res": 3}[which]
+        return self.bias[j * self.unit_num:(j + 1) * self.unit_num]
+
+    def forward(self, inputs):
+        if inputs.dim() != 3:
+            raise ValueError('The rank of input of InteractingLayer must be 3, but now is %d'
+                             % inputs.dim())
+        if not self.built:
+            self.build(tuple(inputs.shape), device=inputs.device)
+        drop = self.dropout_rate if (self.use_dropout and self.training) else 0.0
+        seed = (self.seed * 1000003 + self._calls) & 0xFFFFFFFFFFFFFFFF
+        self._calls += 1
+        return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
+                                    self, seed, drop)
+
+
+# ============================================================================================
+# Dense / MultiLayerDense
+# ============================================================================================
+class _DenseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        _lib.require_device(x, W)
+        x = x.contiguous()
+        M, K = x.shape
+        N = W.shape[1]
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        call("rs_dense_fwd", stream_handle(), ptr(x), M, K, K, ptr(W), ptr(b), N, act, ptr(y), N)
+        ctx.save_for_backward(x, y, W, b)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, W, b = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, K = x.shape
+        N = W.shape[1]
+        s = stream_handle()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            call("rs_dense_bwd_data", s, ptr(dy), N, ptr(y), N, ctx.act, ptr(W), M, K, N, ptr(dx),
+                 K, 0)
+        ws_n = int(_lib.load().rs_dense_bwd_weight_workspace_floats(M, K, N))
+        ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
+        in_place = W.grad is not None and b.grad is not None and W.grad.is_contiguous()
+        dW = W.grad if in_place else torch.empty_like(W)
+        db = b.grad if in_place else torch.empty_like(b)
+        call("rs_dense_bwd_weight", s, ptr(x), K, ptr(dy), N, ptr(y), N, ctx.act, M, K, N,
+             ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
+        if in_place:
+            return dx, None, None, None
+        return dx, dW, db, None
+
+
+class Dense(nn.Module):
+    """tf.keras.layers.Dense(units, activation): glorot_uniform kernel [in, units], zero bias."""
+
+    def __init__(self, units, activation=None, seed=0, device=None, name=None):
+        super().__init__()
+        self.units = int(units)
+        self.activation = activation
+        self.act = _act_code(activation)
+        self.seed = int(seed)
+        self._device = device
+        self.built = False
+        self.name = name
+
+    def build(self, input_shape, device=None):
+        K = int(input_shape[-1])
+        device = device or self._device or torch.device("cuda")
+        blk = FlatBlock([(K, self.units), (self.units,)], device)
+        self.kernel, self.bias = blk.params()
+        glorot_uniform_(self.kernel, K, self.units, torch.Generator().manual_seed(self.seed))
+        self.input_dim = K
+        self.built = True
+
+    def forward(self, x):
+        if not self.built:
+            self.build(tuple(x.shape), device=x.device)
+        lead = x.shape[:-1]  # Keras Dense = tensordot over the last axis
+        y = _DenseFn.apply(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act)
+        return y.reshape(*lead, self.units)
+
+
+class MultiLayerDense(nn.Module):
+    """MultiLayerDense(units=[...], activation=...) (imported at autoint:9, absent from the
+    reference): pinned as Dense(u, activation) for every u in order."""
+
+    def __init__(self, units, activation="relu", seed=0, device=None):
+        super().__init__()
+        self.units = [int(u) for u in units]
+        self.activation = activation
+        self.layers = nn.ModuleList(
+            Dense(u, activation, seed=seed + i, device=device) for i, u in enumerate(self.units))
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x

@@ -1,0 +1,333 @@
+"""GPU parity: every kernel of the path through the C ABI vs the CPU oracle on the same seeded
+inputs.  Tolerances (fp32 kernels vs the float64 oracle):
+  * index work (hashed rows, touched-row sets): bit-exact;
+  * forward activations / logits: |err| <= 1e-5 absolute (north_star: "fp32 logits within 1e-5");
+  * gradients and optimizer updates: |err| <= 1e-4 * (1 + |ref|) (fp32 accumulation order);
+The oracle is unpinned against the TF reference (oracle/ctr_oracle.py header).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as npo
+from oracle import torch_ref as tr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _np(t):
+    return t.detach().double().cpu().numpy()
+
+
+def assert_close(got, ref, atol, rtol=0.0, what=""):
+    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    err = np.abs(got - ref)
+    bound = atol + rtol * np.abs(ref)
+    worst = np.max(err - bound) if err.size else -1
+    assert worst <= 0, f"{what}: max|err|={err.max():.3e} (atol={atol}, rtol={rtol})"
+
+
+# ------------------------------------------------------------------------------------------
+# H1/H2 embedding lookup + sparse push
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("hash_mode", ["mod", "splitmix"])
+@pytest.mark.parametrize("combiner", ["mean", "sum", "sqrtn"])
+@pytest.mark.parametrize("ragged", [False, True])
+def test_embedding_lookup(hash_mode, combiner, ragged):
+    from recommendsystem_amd.embedding import EmbeddingFeatures, SparseTable
+    rng = np.random.default_rng(1)
+    B, F, dim, vocab = 37, 5, 16, 101
+    table = SparseTable(F * vocab, dim, device=DEV, seed=2)
+    emb = EmbeddingFeatures(table, [vocab] * F, combiner=combiner, hash_mode=hash_mode)
+    if ragged:
+        lens = rng.integers(0, 4, size=B * F)  # includes empty segments
+        offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        ids = rng.integers(-(1 << 40), 1 << 40, size=int(offsets[-1]), dtype=np.int64)
+        out = emb(torch.from_numpy(ids).to(DEV), torch.from_numpy(offsets).to(DEV))
+    else:
+        offsets = None
+        ids = rng.integers(0, 1 << 62, size=(B, F), dtype=np.int64)
+        out = emb(torch.from_numpy(ids).to(DEV))
+    W = table.weight.cpu().numpy()
+    ref, rows = npo.embedding_lookup(ids, offsets, B, F, emb.row_base.cpu().numpy(),
+                                     emb.bucket.cpu().numpy(), W.astype(np.float64), hash_mode, combiner)
+    assert_close(_np(out), ref, 1e-6, what="lookup")
+    # index work is bit-exact: the rows the kernel hashed == oracle rows
+    out_rows = torch.empty(ids.size, device=DEV, dtype=torch.int32)
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    idt = torch.from_numpy(ids.reshape(-1)).to(DEV)
+    offt = torch.from_numpy(offsets).to(DEV) if ragged else None
+    tmp = torch.empty(B, F, dim, device=DEV)
+    call("rs_embedding_lookup_fwd", stream_handle(), ptr(idt), ptr(offt), B, F, ptr(emb.row_base),
+         ptr(emb.bucket), emb.hash_mode, emb.combiner, ptr(table.weight), table.rows, dim, ptr(tmp),
+         F * dim, dim, ptr(out_rows))
+    torch.cuda.synchronize()
+    assert np.array_equal(out_rows.cpu().numpy().astype(np.int64), rows)
+
+
+def test_sparse_push_and_adam():
+    from recommendsystem_amd.embedding import EmbeddingFeatures, SparseAdam, SparseTable
+    rng = np.random.default_rng(3)
+    B, F, dim, vocab = 64, 4, 8, 13  # small vocab -> many collisions per row
+    opt = SparseAdam(learning_rate=1e-2)
+    table = SparseTable(F * vocab, dim, opt, device=DEV, seed=4)
+    emb = EmbeddingFeatures(table, [vocab] * F, combiner="mean")
+    lens = rng.integers(0, 3, size=B * F)
+    offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ids = rng.integers(0, 1000, size=int(offsets[-1]), dtype=np.int64)
+    W0 = table.weight.cpu().numpy().astype(np.float64)
+    out = emb(torch.from_numpy(ids).to(DEV), torch.from_numpy(offsets).to(DEV))
+    dout = torch.randn(B, F, dim, device=DEV)
+    out.backward(dout)
+    torch.cuda.synchronize()
+    n = int(table.n_touched.item())
+    touched = set(table.touched[:n].cpu().numpy().tolist())
+    _, rows = npo.embedding_lookup(ids, offsets, B, F, emb.row_base.cpu().numpy(),
+                                   emb.bucket.cpu().numpy(), W0, "mod", "mean")
+    gref = npo.sparse_grad_sum(rows, offsets, B, F, _np(dout), "mean")
+    assert touched == set(gref.keys())  # bit-exact row set
+    G = table.grad.cpu().numpy()
+    for r, g in gref.items():
+        assert_close(G[r], g, 1e-5, 1e-5, what=f"grad row {r}")
+    table.step()
+    torch.cuda.synchronize()
+    W1 = table.weight.cpu().numpy()
+    for r, g in gref.items():
+        w, _, _ = npo.adam_sparse(W0[r], g, np.zeros(dim), np.zeros(dim), 1e-2)
+        assert_close(W1[r], w, 1e-5, 1e-4, what=f"adam row {r}")
+    untouched = np.setdiff1d(np.arange(table.rows), list(gref.keys()))
+    assert np.array_equal(W1[untouched], W0[untouched].astype(np.float32))
+    assert int(table.n_touched.item()) == 0 and bool((table.flag == -1).all())
+    assert float(table.grad.abs().max()) == 0.0
+
+
+# ------------------------------------------------------------------------------------------
+# H3 InteractingLayer
+# ------------------------------------------------------------------------------------------
+IL_CASES = [  # (B, F, E, U, H, L, use_res)
+    (64, 26, 16, 16, 2, 3, True),    # config 2 (AutoInt CTR)
+    (33, 26, 16, 16, 2, 1, True),
+    (17, 7, 16, 16, 2, 2, False),
+    (9, 32, 16, 16, 1, 1, True),
+    (9, 40, 16, 16, 4, 2, True),     # F > 32 -> FMAX 64
+    (11, 19, 8, 8, 2, 1, True),      # multi_head IL(1, 8, 2)
+    (5, 26, 16, 8, 2, 1, True),
+    (6, 13, 32, 32, 2, 2, True),
+    (4, 26, 16, 128, 1, 1, True),    # constructor defaults (config 1): forward only
+]
+
+
+def _il_ref_params(il):
+    return (_np(il.kernel), _np(il.bias), _np(il.gamma), _np(il.beta))
+
+
+@pytest.mark.parametrize("case", IL_CASES)
+def test_interacting_forward(case):
+    from recommendsystem_amd.layers import InteractingLayer
+    B, F, E, U, H, L, res = case
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.5, 0.5, size=(B, F, E))
+    il = InteractingLayer(L, U, H, use_res=res, seed=7, device=DEV)
+    il.build((B, F, E), device=DEV)
+    with torch.no_grad():  # non-trivial LN affine + biases
+        il.bias.uniform_(-0.1, 0.1)
+        il.gamma.uniform_(0.5, 1.5)
+        il.beta.uniform_(-0.2, 0.2)
+    y = il(torch.from_numpy(x).float().to(DEV))
+    W, b, g, be = _il_ref_params(il)
+    ref = npo.interacting_layer(x.astype(np.float32).astype(np.float64), W, b, g, be, L, H, res)
+    assert_close(_np(y), ref, 2e-5, what=f"IL fwd {case}")
+
+
+@pytest.mark.parametrize("case", [c for c in IL_CASES if c[3] <= 32])
+def test_interacting_backward(case):
+    from recommendsystem_amd.layers import InteractingLayer
+    B, F, E, U, H, L, res = case
+    rng = np.random.default_rng(6)
+    x = rng.uniform(-0.5, 0.5, size=(B, F, E)).astype(np.float32)
+    dy = rng.normal(size=(B, F, U)).astype(np.float32)
+    il = InteractingLayer(L, U, H, use_res=res, seed=8, device=DEV)
+    il.build((B, F, E), device=DEV)
+    with torch.no_grad():
+        il.bias.uniform_(-0.1, 0.1)
+        il.gamma.uniform_(0.5, 1.5)
+        il.beta.uniform_(-0.2, 0.2)
+    xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    il(xd).backward(torch.from_numpy(dy).to(DEV))
+    torch.cuda.synchronize()
+    W, b, g, be = (torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il))
+    xr = torch.from_numpy(x).double().requires_grad_(True)
+    yr = tr.interacting_layer(xr, W, b, g, be, L, H, res)
+    yr.backward(torch.from_numpy(dy).double())
+    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dx")
+    assert_close(_np(il.kernel.grad), W.grad.numpy(), 1e-4, 1e-4, what="dW")
+    assert_close(_np(il.bias.grad), b.grad.numpy(), 1e-4, 1e-4, what="db")
+    assert_close(_np(il.gamma.grad), g.grad.numpy(), 1e-4, 1e-4, what="dgamma")
+    assert_close(_np(il.beta.grad), be.grad.numpy(), 1e-4, 1e-4, what="dbeta")
+
+
+def test_interacting_dropout_mask_matches_oracle():
+    from recommendsystem_amd.layers import InteractingLayer
+    B, F, E, U, H, L = 8, 26, 16, 16, 2, 2
+    rng = np.random.default_rng(9)
+    x = rng.uniform(-0.5, 0.5, size=(B, F, E)).astype(np.float32)
+    il = InteractingLayer(L, U, H, use_dropout=True, dropout_rate=0.2, seed=11, device=DEV)
+    il.train()
+    seed = (il.seed * 1000003 + il._calls) & 0xFFFFFFFFFFFFFFFF
+    y = il(torch.from_numpy(x).to(DEV))
+    W, b, g, be = _il_ref_params(il)
+    ref = npo.interacting_layer(x.astype(np.float64), W, b, g, be, L, H, True, drop_rate=0.2, seed=seed)
+    assert_close(_np(y), ref, 2e-5, what="IL dropout fwd")
+    # and its backward against autograd of the same masked graph
+    xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    il._calls -= 1
+    il(xd).sum().backward()
+    Wt, bt, gt, bet = (torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il))
+    xr = torch.from_numpy(x).double().requires_grad_(True)
+    tr.interacting_layer(xr, Wt, bt, gt, bet, L, H, True, drop_rate=0.2, seed=seed).sum().backward()
+    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dropout dx")
+    assert_close(_np(il.kernel.grad), Wt.grad.numpy(), 1e-4, 1e-4, what="dropout dW")
+
+
+def test_interacting_rank_error():
+    from recommendsystem_amd.layers import InteractingLayer
+    il = InteractingLayer(1, 16, 2, device=DEV)
+    with pytest.raises(ValueError, match="must be 3, but now is 2"):
+        il(torch.zeros(4, 16, device=DEV))
+
+
+# ------------------------------------------------------------------------------------------
+# Dense towers, loss, dense Adam
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("act", [None, "relu", "sigmoid"])
+@pytest.mark.parametrize("shape", [(4096, 416, 32), (77, 45, 3), (130, 432, 1), (64, 16, 70)])
+def test_dense_fwd_bwd(act, shape):
+    from recommendsystem_amd.layers import Dense
+    M, K, N = shape
+    rng = np.random.default_rng(12)
+    x = rng.normal(size=(M, K)).astype(np.float32)
+    dy = rng.normal(size=(M, N)).astype(np.float32)
+    layer = Dense(N, act, seed=3, device=DEV)
+    layer.build((M, K), device=DEV)
+    with torch.no_grad():
+        layer.bias.uniform_(-0.5, 0.5)
+    xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    y = layer(xd)
+    y.backward(torch.from_numpy(dy).to(DEV))
+    W = torch.from_numpy(_np(layer.kernel)).requires_grad_(True)
+    b = torch.from_numpy(_np(layer.bias)).requires_grad_(True)
+    xr = torch.from_numpy(x).double().requires_grad_(True)
+    yr = tr.dense(xr, W, b, act)
+    yr.backward(torch.from_numpy(dy).double())
+    assert_close(_np(y), yr.detach().numpy(), 1e-5, 1e-5, what="dense fwd")
+    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dense dx")
+    assert_close(_np(layer.kernel.grad), W.grad.numpy(), 1e-4, 1e-4, what="dense dW")
+    assert_close(_np(layer.bias.grad), b.grad.numpy(), 1e-4, 1e-4, what="dense db")
+
+
+def test_bce_clip_loss():
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(13)
+    M, T = 3000, 2
+    s = rng.uniform(-0.2, 1.2, size=(M, T)).astype(np.float32)  # exercises both clip edges
+    y = (rng.uniform(size=(M, T)) < 0.3).astype(np.float32)
+    sd, yd = torch.from_numpy(s).to(DEV), torch.from_numpy(y).to(DEV)
+    p, loss, ds = torch.empty_like(sd), torch.empty(1, device=DEV), torch.empty_like(sd)
+    call("rs_bce_clip_loss", stream_handle(), ptr(sd), ptr(yd), M, T, 1e-6, 1.0, 1e-6, None, ptr(p),
+         ptr(loss), ptr(ds))
+    st = torch.from_numpy(s).double().requires_grad_(True)
+    pr = torch.clamp(st, 1e-6, 1.0)
+    lr_ = tr.cross_entropy(torch.from_numpy(y).double(), pr)
+    lr_.backward()
+    assert_close(_np(loss), [float(lr_)], 1e-5, 1e-6, what="loss")
+    assert_close(_np(p), pr.detach().numpy(), 0, what="clip")
+    assert_close(_np(ds), st.grad.numpy(), 1e-7, 1e-4, what="dloss/ds")
+
+
+def test_dense_adam_matches_oracle():
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(14)
+    n = 10001
+    p0 = rng.normal(size=n)
+    m = np.zeros(n)
+    v = np.zeros(n)
+    pd = torch.from_numpy(p0).float().to(DEV)
+    md, vd = torch.zeros_like(pd), torch.zeros_like(pd)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    p = p0.astype(np.float32).astype(np.float64)
+    for t in range(1, 4):
+        g = rng.normal(size=n).astype(np.float32)
+        gd = torch.from_numpy(g).to(DEV)
+        call("rs_dense_adam", stream_handle(), ptr(pd), ptr(gd), ptr(md), ptr(vd), n, ptr(step),
+             1e-3, 0.9, 0.999, 1e-8, 1.0, 1)
+        p, m, v = npo.adam_dense(p, g.astype(np.float64), m, v, t, 1e-3)
+        assert float(gd.abs().max()) == 0.0  # fused zero_grad
+    assert int(step.item()) == 3
+    assert_close(_np(pd), p, 1e-6, 1e-5, what="adam")
+
+
+# ------------------------------------------------------------------------------------------
+# H4 AutoInt: full train step (fused trainer) vs the oracle train step
+# ------------------------------------------------------------------------------------------
+def _autoint_case(B=256, vocab=50, layer_num=3, seed=21):
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig
+    cfg = AutoIntConfig(vocab_per_field=vocab, layer_num=layer_num, lr_dense=1e-3, lr_sparse=1e-3)
+    model = AutoInt(cfg, device=DEV, seed=seed, max_batch=B)
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, 10 * vocab, size=(B, cfg.num_fields), dtype=np.int64)
+    labels = (rng.uniform(size=(B, 1)) < 0.25).astype(np.float32)
+    return cfg, model, ids, labels
+
+
+def _oracle_from_model(model, cfg, dtype=torch.float64):
+    il = {"W": _np(model.interact.kernel), "bias": _np(model.interact.bias),
+          "gamma": _np(model.interact.gamma), "beta": _np(model.interact.beta)}
+    deep = [(_np(l.kernel), _np(l.bias)) for l in model.deep.layers]
+    logits = [(_np(l.kernel), _np(l.bias)) for l in model.logits.layers]
+    ocfg = dict(layer_num=cfg.layer_num, head_num=cfg.head_num, use_res=cfg.use_res,
+                mlp_activation=cfg.mlp_activation, logits_activation=cfg.logits_activation)
+    return tr.AutoIntCPU(model.table.weight.cpu().numpy(), _np(model.embedding.row_base).astype(np.int64),
+                         _np(model.embedding.bucket).astype(np.int64), il, deep, logits, ocfg,
+                         lr_dense=cfg.lr_dense, lr_sparse=cfg.lr_sparse, dtype=dtype), il, deep, logits, ocfg
+
+
+def test_autoint_logits_within_1e5():
+    cfg, model, ids, labels = _autoint_case(B=512)
+    p = model(torch.from_numpy(ids).to(DEV))
+    ref, il, deep, logits, ocfg = _oracle_from_model(model, cfg)
+    rows = ref.rows(torch.from_numpy(ids)).numpy()
+    x0 = ref.table.numpy()[rows]
+    _, pref = npo.autoint_forward(x0, il, deep, logits, ocfg)
+    assert_close(_np(p), pref, 1e-5, what="AutoInt logits")
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_autoint_train_steps_match_oracle(graph):
+    from recommendsystem_amd.autoint import AutoIntTrainer
+    cfg, model, ids, labels = _autoint_case(B=256)
+    ref, *_ = _oracle_from_model(model, cfg)
+    trn = AutoIntTrainer(model, 256)
+    idt, lbt = torch.from_numpy(ids).to(DEV), torch.from_numpy(labels).to(DEV)
+    if graph:
+        trn.load_batch(idt, lbt)
+        # capture() runs 2 eager warm-up steps and records (does not run) one; replay = step 3
+        trn.capture(warmup=2)
+        steps = 3
+        trn.graph.replay()
+    else:
+        steps = 3
+        for _ in range(steps):
+            trn.step(idt, lbt)
+    torch.cuda.synchronize()
+    for _ in range(steps):
+        loss_ref = ref.step(torch.from_numpy(ids), torch.from_numpy(labels))
+    # step `steps`'s loss is computed before its update; compare the loss and the parameters
+    assert abs(float(trn.loss) - loss_ref) < 1e-5
+    got = torch.cat([p.detach().reshape(-1).double().cpu() for p in model.parameters()])
+    want = torch.cat([p.detach().reshape(-1) for p in ref.dense_list])
+    assert_close(got.numpy(), want.numpy(), 2e-6, 1e-4, what="dense params after steps")
+    assert_close(model.table.weight.cpu().numpy(), ref.table.numpy(), 2e-6, 1e-4, what="table after steps")
