@@ -65,7 +65,8 @@ def time_kernel(fn, reps):
 
 def cpu_baseline(cfg, model, batches_cpu, steps):
     from oracle import torch_ref as tr
-    threads = len(os.sched_getaffinity(0))
+    # the box's CPU share (OMP_NUM_THREADS is set to it; affinity shows the whole machine)
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     torch.set_num_threads(threads)
     il = {k: v.detach().double().cpu().numpy() for k, v in
           dict(W=model.interact.kernel, bias=model.interact.bias, gamma=model.interact.gamma,

@@ -46,8 +46,13 @@ def _newer(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _tag(extra: list[str]) -> str:
+    import hashlib
+    return hashlib.sha1(" ".join(extra).encode()).hexdigest()[:8]
+
+
 def _compile(src: str, headers: list[str], extra: list[str]) -> str:
-    obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+    obj = os.path.join(BUILD_DIR, f"{os.path.basename(src)}.{_tag(extra)}.o")
     if _newer(obj, [src] + headers):
         cmd = [_hipcc(), *COMMON_FLAGS, *extra, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -64,11 +69,15 @@ def build(verbose: bool = False, extra: list[str] | None = None) -> str:
     workers = min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(max_workers=workers) as ex:
         objs = list(ex.map(lambda s: _compile(s, headers, extra), srcs))
-    if _newer(LIB_PATH, objs):
+    stamp = os.path.join(BUILD_DIR, "lib.flags")
+    prev = open(stamp).read() if os.path.exists(stamp) else None
+    if _newer(LIB_PATH, objs) or prev != _tag(extra):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB_PATH]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        with open(stamp, "w") as f:
+            f.write(_tag(extra))
     if verbose:
         print(f"built {LIB_PATH}")
     return LIB_PATH

@@ -69,3 +69,42 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t b, uint32_t
   float u = (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
   return u >= rate;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Deterministic column reduction of per-block partial rows:
+//   out[c] (+)= sum_r part[r * ld + c]   (c < ncols; columns >= split go to out1[c - split])
+// Block = 64 columns x G row-groups; each thread sums rows r = g, g+G, ... in order, then the G
+// partial sums are combined in g order: a fixed summation order for a given (nrows, G), so the
+// result is bitwise reproducible.  Many columns per wave keep the loads coalesced; the G row
+// groups keep G independent load streams per column in flight.
+// ---------------------------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(64 * G) column_reduce_kernel(
+    const float* __restrict__ part, int nrows, int64_t ld, int64_t ncols, int64_t split,
+    float* __restrict__ out0, float* __restrict__ out1, int accumulate) {
+  __shared__ float red[G][64];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lc;
+  float s = 0.f;
+  if (c < ncols) {
+#pragma unroll 4
+    for (int r = g; r < nrows; r += G) s += part[(int64_t)r * ld + c];
+  }
+  red[g][lc] = s;
+  __syncthreads();
+  if (g == 0 && c < ncols) {
+    float t = red[0][lc];
+#pragma unroll
+    for (int k = 1; k < G; ++k) t += red[k][lc];
+    float* d = c < split ? out0 + c : out1 + (c - split);
+    *d = accumulate ? (*d + t) : t;
+  }
+}
+
+static inline void launch_column_reduce(hipStream_t s, const float* part, int nrows, int64_t ld,
+                                        int64_t ncols, int64_t split, float* out0, float* out1,
+                                        int accumulate) {
+  const unsigned grid = (unsigned)((ncols + 63) / 64);
+  column_reduce_kernel<16><<<grid, 64 * 16, 0, s>>>(part, nrows, ld, ncols, split, out0, out1,
+                                                    accumulate);
+}

@@ -43,48 +43,62 @@ constexpr int BT = 64;  // block tile (rows and columns)
 constexpr int BK = 32;  // K slab
 
 // ------------------------------- forward ------------------------------------------------------
+// Block = 16 rows x 64 columns, 4 waves splitting K (a batch-sized M with N <= 64 and K up to a
+// few thousand is the shape of every tower layer on the path, so the grid is M/16 blocks rather
+// than M/64).  X rows are staged through LDS in 256-deep slabs (coalesced); W is read straight
+// from L2 (it is a few KB to a few hundred KB and shared by every block).  The 4 wave partials
+// are summed in wave order (deterministic), then bias + activation.
+constexpr int FM = 16;    // rows per block
+constexpr int FKS = 256;  // K slab staged in LDS
+
 __global__ void __launch_bounds__(256) dense_fwd_kernel(const float* __restrict__ X, int64_t M,
                                                         int K, int64_t ldx,
                                                         const float* __restrict__ W,
                                                         const float* __restrict__ bias, int N,
                                                         int act, float* __restrict__ Y,
                                                         int64_t ldy) {
-  __shared__ float As[BT][BK + 1];
-  __shared__ float Bs[BK][BT + 1];
-  const int64_t m_blk = (int64_t)blockIdx.x * BT;
+  __shared__ float As[FM][FKS + 4];
+  __shared__ float red[4][FM][BT + 1];
+  const int64_t m_blk = (int64_t)blockIdx.x * FM;
   const int n_blk = blockIdx.y * BT;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int lr = l & 15, lk = l >> 4;
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    for (int t = threadIdx.x; t < BT * BK; t += 256) {
-      const int r = t / BK, c = t % BK;
+  for (int k0 = 0; k0 < K; k0 += FKS) {
+    for (int t = threadIdx.x; t < FM * FKS; t += 256) {
+      const int r = t / FKS, c = t % FKS;
       const int64_t m = m_blk + r;
       const int k = k0 + c;
       As[r][c] = (m < M && k < K) ? X[m * ldx + k] : 0.f;
     }
-    for (int t = threadIdx.x; t < BK * BT; t += 256) {
-      const int r = t / BT, c = t % BT;
-      const int k = k0 + r, n = n_blk + c;
-      Bs[r][c] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
-    }
     __syncthreads();
+    // wave w takes k-steps kk = w*4, w*4 + 16, ... of this slab (interleaved -> balanced tails)
+    for (int kk = w * 4; kk < FKS && k0 + kk < K; kk += 16) {
+      const int k = k0 + kk + lk;
+      const float a = As[lr][kk + lk];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      const float a = As[w * 16 + (l & 15)][kk + (l >> 4)];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma4(a, Bs[kk + (l >> 4)][nt * 16 + (l & 15)], acc[nt]);
+      for (int t = 0; t < 4; ++t) {
+        const int n = n_blk + t * 16 + lr;
+        const float bv = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
+        acc[t] = mfma4(a, bv, acc[t]);
+      }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int n = n_blk + nt * 16 + (l & 15);
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t m = m_blk + w * 16 + (l >> 4) * 4 + r;
-      if (m < M && n < N) Y[m * ldy + n] = act_fwd(acc[nt][r] + bias[n], act);
+    for (int r = 0; r < 4; ++r) red[w][lk * 4 + r][t * 16 + lr] = acc[t][r];
+  __syncthreads();
+  for (int o = threadIdx.x; o < FM * BT; o += 256) {
+    const int r = o / BT, c = o % BT;
+    const int64_t m = m_blk + r;
+    const int n = n_blk + c;
+    if (m < M && n < N) {
+      const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
+      Y[m * ldy + n] = act_fwd(v + bias[n], act);
     }
   }
 }
@@ -191,26 +205,12 @@ __global__ void __launch_bounds__(256) dense_bwd_weight_kernel(
   }
 }
 
-__global__ void dense_reduce_kernel(const float* __restrict__ partials, int nchunks, int K, int N,
-                                    float* __restrict__ dW, float* __restrict__ db,
-                                    int accumulate) {
-  const int64_t total = (int64_t)K * N + N;
-  const int64_t stride = total;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c) s += partials[(int64_t)c * stride + i];
-    float* d = (i < (int64_t)K * N) ? (dW + i) : (db + (i - (int64_t)K * N));
-    *d = accumulate ? (*d + s) : s;
-  }
-}
-
 RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t ldx,
                         const float* W, const float* bias, int N, int act, float* Y,
                         int64_t ldy) {
   if (!X || !W || !bias || !Y || M < 0 || K <= 0 || N <= 0 || ldx < K || ldy < N) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
-  dim3 grid((unsigned)((M + BT - 1) / BT), (unsigned)((N + BT - 1) / BT));
+  dim3 grid((unsigned)((M + FM - 1) / FM), (unsigned)((N + BT - 1) / BT));
   dense_fwd_kernel<<<grid, 256, 0, rs_stream(stream)>>>(X, M, K, ldx, W, bias, N, act, Y, ldy);
   return rs_status_after_launch();
 }
@@ -245,9 +245,7 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
                                                  workspace);
   }
   const int64_t total = (int64_t)K * N + N;
-  int64_t rgrid = (total + 255) / 256;
-  if (rgrid > 1024) rgrid = 1024;
-  dense_reduce_kernel<<<(int)rgrid, 256, 0, s>>>(workspace, nchunks, K, N, dW, db, accumulate);
+  launch_column_reduce(s, workspace, nchunks, total, total, (int64_t)K * N, dW, db, accumulate);
   return rs_status_after_launch();
 }
 

@@ -112,40 +112,80 @@ RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32
 
 // ---------------------------------------------------------------------------------------------
 // Sparse gradient accumulation (the "push" half of EmbeddingFeatures): every occurrence k of
-// segment s adds scale(s) * dout[s] into grad_table[rows[k]].  The first occurrence of a row in
-// this step claims it (flag -1 -> -2) and appends it to `touched`, so the optimizer kernel visits
-// each touched row exactly once.  fp32 atomics: the row SET is exact, the summation order of a
-// row's contributions is not fixed (last-bit run-to-run differences).  Data-parallel replicas
-// stay identical because the cross-rank merge (rs_sparse_merge_rows) is rank-ordered.
+// segment s adds scale(s) * dout[s] into grad_table[rows[k]].
+//
+// MI355X mapping: a block owns one field f and a tile of samples.  Phase 1 inserts each id's row
+// into an LDS open-addressing table (CAS on the key) and adds the scaled gradient row into the
+// slot with LDS float atomics; phase 2 flushes every occupied slot with ONE global float-atomic
+// row add and claims the row for the optimizer (flag -1 -> -2, append to `touched`).  Zipf-hot
+// ids (the top id of a field is ~18% of a Criteo-like batch) thus cost one global add per block
+// instead of one per occurrence -- global atomics on one row serialise at the memory side.
+// If the LDS table ever fills (long multi-hot tiles), the occurrence falls back to direct global
+// atomics.  The row SET is exact; the fp32 summation order is not fixed (last-bit run-to-run
+// differences).  Replicas stay identical because the cross-rank merge (rs_sparse_merge_rows)
+// is rank-ordered and atomic-free.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void claim_row(int32_t row, int32_t* flag, int32_t* touched,
+                                          int32_t* n_touched, int32_t touched_cap) {
+  if (atomicCAS(&flag[row], -1, -2) == -1) {
+    const int32_t u = atomicAdd(n_touched, 1);
+    if (u < touched_cap) touched[u] = row;
+  }
+}
+
 __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
-    const int32_t* __restrict__ rows, const int32_t* __restrict__ offsets, int64_t nseg,
-    const float* __restrict__ dout, int F, int64_t dout_ld, int64_t dout_fstride, int dim,
-    int combiner, int lanes_per_seg, float* __restrict__ grad_table, int32_t* __restrict__ flag,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ offsets, int64_t B, int F,
+    const float* __restrict__ dout, int64_t dout_ld, int64_t dout_fstride, int dim, int combiner,
+    int G, int tile, int cap, float* __restrict__ grad_table, int32_t* __restrict__ flag,
     int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
-  const int segs_per_block = blockDim.x / lanes_per_seg;
-  const int g = threadIdx.x / lanes_per_seg;
-  const int l = threadIdx.x % lanes_per_seg;
-  for (int64_t s = (int64_t)blockIdx.x * segs_per_block + g; s < nseg;
-       s += (int64_t)gridDim.x * segs_per_block) {
-    const int64_t beg = offsets ? offsets[s] : s;
-    const int64_t end = offsets ? offsets[s + 1] : s + 1;
+  extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+  int32_t* keys = sm;                                   // [cap]
+  float* vals = reinterpret_cast<float*>(sm + cap);     // [cap][dim]
+  for (int k = threadIdx.x; k < cap; k += blockDim.x) keys[k] = -1;
+  for (int k = threadIdx.x; k < cap * dim; k += blockDim.x) vals[k] = 0.f;
+  __syncthreads();
+  const int f = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * tile;
+  const int64_t b1 = b0 + tile < B ? b0 + tile : B;
+  const int per_pass = blockDim.x / G;
+  const int gsub = threadIdx.x / G, l = threadIdx.x % G;
+  const int leader = (threadIdx.x & 63) - l;  // lane of this group's leader within the wave
+  // ---- phase 1: aggregate this tile's occurrences per row in LDS ----
+  for (int64_t b = b0 + gsub; b < b1; b += per_pass) {
+    const int64_t sg = b * F + f;
+    const int64_t beg = offsets ? offsets[sg] : sg;
+    const int64_t end = offsets ? offsets[sg + 1] : sg + 1;
     if (end <= beg) continue;
     const float sc = combiner_scale((int)(end - beg), combiner);
-    const int f = (int)(s % F);
-    const int64_t b = s / F;
     const float* src = dout + b * dout_ld + (int64_t)f * dout_fstride;
     for (int64_t k = beg; k < end; ++k) {
       const int32_t row = rows[k];
+      int slot = -1;
       if (l == 0) {
-        if (atomicCAS(&flag[row], -1, -2) == -1) {
-          const int32_t u = atomicAdd(n_touched, 1);
-          if (u < touched_cap) touched[u] = row;
+        int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));
+        for (int probe = 0; probe < cap; ++probe) {
+          const int32_t old = atomicCAS(&keys[h], -1, row);
+          if (old == -1 || old == row) { slot = h; break; }
+          h = (h + 1) & (cap - 1);
         }
       }
-      float* dst = grad_table + (int64_t)row * dim;
-      for (int e = l; e < dim; e += lanes_per_seg) atomicAdd(dst + e, src[e] * sc);
+      slot = __shfl(slot, leader, 64);
+      if (slot >= 0) {
+        for (int e = l; e < dim; e += G) atomicAdd(&vals[slot * dim + e], src[e] * sc);
+      } else {  // LDS table full: direct global path
+        if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
+        for (int e = l; e < dim; e += G) atomicAdd(grad_table + (int64_t)row * dim + e, src[e] * sc);
+      }
     }
+  }
+  __syncthreads();
+  // ---- phase 2: one global row add per distinct row of the tile ----
+  for (int slot = gsub; slot < cap; slot += per_pass) {
+    const int32_t row = keys[slot];
+    if (row < 0) continue;
+    if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
+    float* dst = grad_table + (int64_t)row * dim;
+    for (int e = l; e < dim; e += G) atomicAdd(dst + e, vals[slot * dim + e]);
   }
 }
 
@@ -156,15 +196,18 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
                                      int32_t* n_touched, int32_t touched_cap) {
   if (!rows || !dout || !grad_table || !flag || !touched || !n_touched || F <= 0 || dim <= 0)
     return RS_ERR_ARG;
-  const int64_t nseg = B * (int64_t)F;
-  if (nseg == 0) return RS_OK;
-  int lps = 1;
-  while (lps < dim && lps < 64) lps <<= 1;
-  const int block = 256;
-  int64_t grid = (nseg * lps + block - 1) / block;
-  if (grid > 8192) grid = 8192;
-  sparse_grad_accum_kernel<<<(int)grid, block, 0, rs_stream(stream)>>>(
-      rows, offsets, nseg, dout, F, dout_ld, dout_fstride, dim, combiner, lps, grad_table, flag,
-      touched, n_touched, touched_cap);
+  if (B * (int64_t)F == 0) return RS_OK;
+  int G = 1;
+  while (G < dim && G < 64) G <<= 1;
+  // LDS table: cap slots of dim floats (<= 64 KB), tile = cap/2 samples (load factor <= 1/2
+  // for single-hot fields)
+  int cap = 1024;
+  while (cap > 32 && (size_t)cap * (dim + 1) * 4 > 64 * 1024) cap >>= 1;
+  const int tile = cap / 2;
+  dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
+  const size_t lds = (size_t)cap * (dim + 1) * 4;
+  sparse_grad_accum_kernel<<<grid, 256, lds, rs_stream(stream)>>>(
+      rows, offsets, B, F, dout, dout_ld, dout_fstride, dim, combiner, G, tile, cap, grad_table,
+      flag, touched, n_touched, touched_cap);
   return rs_status_after_launch();
 }

@@ -5,12 +5,18 @@ namespace rs_il {
 RS_IL_DECLARE_UNIT(il_unit_a)
 int il_unit_a_fwd(const FwdReq& q) {
   if (q.F == 26) return try_fwd<16, 16, 2, 26, true>(q);
+#ifndef RS_MIN_BUILD
   if (q.F <= 32) return try_fwd<16, 16, 2, 32>(q);
   return try_fwd<16, 16, 2, 64>(q);
+#endif
+  return RS_ERR_UNSUPPORTED;
 }
 int il_unit_a_bwd(const BwdReq& q) {
   if (q.F == 26) return try_bwd<16, 16, 2, 26, true>(q);
+#ifndef RS_MIN_BUILD
   if (q.F <= 32) return try_bwd<16, 16, 2, 32>(q);
   return try_bwd<16, 16, 2, 64>(q);
+#endif
+  return RS_ERR_UNSUPPORTED;
 }
 }  // namespace rs_il

@@ -20,7 +20,9 @@
 //   * projections: lane = output column of [Wq|Wk|Wv|Wr] (4U = 64 columns at U = 16), the
 //     column's E weights in VGPRs, x rows broadcast from LDS (one address per wave).
 //   * attention: lane = (head, query row); the row's scores stay in VGPRs (softmax per lane:
-//     exp(s - max) * (1/sum), TF's order); K/V rows are broadcast LDS reads.  Key rows F..FMAX-1
+//     exp(s - max) * (1/sum), TF's order, evaluated as v_exp_f32 in the base-2 domain with
+//     log2(e)/sqrt(dh) folded into one multiply; no fp32 divisions in any loop); K/V rows are
+//     broadcast LDS reads.  Key rows F..FMAX-1
 //     are zero and masked to -inf, so the j loops are unguarded and fully unrolled with
 //     compile-time LDS offsets (no per-key branch, no runtime stride arithmetic).
 //   * epilogue: U lanes per field row; LN mean/var by xor-butterfly inside the U-lane group.
@@ -85,7 +87,8 @@ struct Cfg {
   static constexpr int PRS = NC + 4;                   // projection row stride (16-B aligned)
   static constexpr int OS = U + 4;                     // attention-output row stride
   static constexpr int PMS = FMAX + 1;                 // softmax-matrix row stride
-  static constexpr int BWD_FIXED = ((NC * E + 3) & ~3) + ((NPARAM + 3) & ~3);  // W^T + reduce
+  static constexpr int WPS = NC + 4;                   // padded W row stride in LDS (dx phase)
+  static constexpr int BWD_FIXED = E * WPS + ((NPARAM + 3) & ~3);  // W image + reduction buffer
   static_assert(U % H == 0, "unit_num must be divisible by head_num");
   static_assert(E % 4 == 0 && DH % 4 == 0, "E and dh must be multiples of 4");
   static_assert(E <= 64, "E <= 64");
@@ -94,6 +97,8 @@ struct Cfg {
 struct Args {
   int B, F, L, use_res, ncol;
   float eps, sdh, drop_rate, drop_scale;
+  float inv_sdh;    // 1 / sqrt(dh)
+  float sc2;        // log2(e) / sqrt(dh): scores go straight to the exp2 domain
   uint64_t seed;
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
 };
@@ -108,6 +113,8 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.ncol = use_res ? C::NC : 3 * C::U;
   a.eps = eps;
   a.sdh = (float)__builtin_sqrt((double)C::DH);   // Python float dh ** 0.5 -> fp32 constant
+  a.inv_sdh = (float)(1.0 / __builtin_sqrt((double)C::DH));
+  a.sc2 = (float)(1.4426950408889634 / __builtin_sqrt((double)C::DH));
   a.drop_rate = drop_rate;
   a.drop_scale = drop_rate > 0.f ? (float)(1.0 / (1.0 - (double)drop_rate)) : 1.f;
   a.seed = seed;
@@ -141,26 +148,28 @@ __device__ __forceinline__ void project(const float* X, float* PR, const Args& a
   const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
 #pragma unroll
   for (int cc = 0; cc < C::CPLP; ++cc) {
-    const int c = cc * C::NCOLW + col;
-    if (cc * C::NCOLW >= a.ncol) break;
-    const bool cact = c < a.ncol;
+    const int c = cc * C::NCOLW + col;  // all 4U columns (R is computed even without use_res)
     float w[C::E];
 #pragma unroll
-    for (int e = 0; e < C::E; ++e) w[e] = cact ? W[e * C::NC + c] : 0.f;
-    const float bc = cact ? bias[c] : 0.f;
-    for (int f = rsub; f < a.F; f += C::RPI) {
-      const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
-      float acc = 0.f;
+    for (int e = 0; e < C::E; ++e) w[e] = W[e * C::NC + c];
+    const float bc = bias[c];
+#pragma unroll 2
+    for (int f0 = 0; f0 < C::FMAX; f0 += C::RPI) {
+      const int f = f0 + rsub;
+      if (C::EXACT ? (f < C::FMAX) : (f < a.F)) {
+        const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
+        float acc = 0.f;
 #pragma unroll
-      for (int e4 = 0; e4 < C::E / 4; ++e4) {
-        const float4 xv = xr[e4];
-        acc = fmaf(xv.x, w[4 * e4 + 0], acc);
-        acc = fmaf(xv.y, w[4 * e4 + 1], acc);
-        acc = fmaf(xv.z, w[4 * e4 + 2], acc);
-        acc = fmaf(xv.w, w[4 * e4 + 3], acc);
+        for (int e4 = 0; e4 < C::E / 4; ++e4) {
+          const float4 xv = xr[e4];
+          acc = fmaf(xv.x, w[4 * e4 + 0], acc);
+          acc = fmaf(xv.y, w[4 * e4 + 1], acc);
+          acc = fmaf(xv.z, w[4 * e4 + 2], acc);
+          acc = fmaf(xv.w, w[4 * e4 + 3], acc);
+        }
+        acc += bc;  // Keras Dense: tensordot, then bias_add, then activation
+        PR[f * C::PRS + c] = fmaxf(acc, 0.f);
       }
-      acc += bc;  // Keras Dense: tensordot, then bias_add, then activation
-      if (cact) PR[f * C::PRS + c] = fmaxf(acc, 0.f);
     }
   }
 }
@@ -216,17 +225,19 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
     float q[C::DH];
     load_row(q, PR + i * C::PRS + h * C::DH);
     const float* kb = PR + C::U + h * C::DH;
+    // softmax(QK^T / sqrt(dh)) as exp2((QK^T) * log2(e)/sqrt(dh) - max): one multiply per score,
+    // a hardware v_exp_f32 per key, one reciprocal per row (TF: exp(x - max) * (1 / sum)).
     float s[C::FMAX];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < C::FMAX; ++j) {
       const float acc = dot_row(q, kb + j * C::PRS);
-      s[j] = (C::EXACT || j < F) ? acc / a.sdh : -INFINITY;
+      s[j] = (C::EXACT || j < F) ? acc * a.sc2 : -INFINITY;
       mx = fmaxf(mx, s[j]);
     }
     float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < C::FMAX; ++j) { s[j] = expf(s[j] - mx); sum += s[j]; }
+    for (int j = 0; j < C::FMAX; ++j) { s[j] = __builtin_amdgcn_exp2f(s[j] - mx); sum += s[j]; }
     const float inv = 1.0f / sum;
     float o[C::DH];
 #pragma unroll
@@ -271,20 +282,20 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
       z[c] = fmaxf(t, 0.f);
       sum += z[c];
     }
-    const float mean = group_sum<C::LPR>(sum) / (float)C::U;
+    const float mean = group_sum<C::LPR>(sum) * (1.0f / (float)C::U);
     float sq = 0.f;
 #pragma unroll
     for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
-    const float var = group_sum<C::LPR>(sq) / (float)C::U;
-    const float sd = sqrtf(var + a.eps);
+    const float var = group_sum<C::LPR>(sq) * (1.0f / (float)C::U);
+    const float rstd = 1.0f / sqrtf(var + a.eps);  // (x - mean) / sqrt(var + eps)
     if (act) {
 #pragma unroll
       for (int c = 0; c < C::CPLN; ++c) {
         const int u = u0 + c * C::LPR;
-        if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) / sd * gamma[u] + beta[u];
+        if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) * rstd * gamma[u] + beta[u];
         else O[f * C::OS + u] = z[c];
       }
-      if (MODE == 1 && u0 == 0) { ST[2 * f] = mean; ST[2 * f + 1] = sd; }
+      if (MODE == 1 && u0 == 0) { ST[2 * f] = mean; ST[2 * f + 1] = rstd; }
     }
   }
 }
@@ -338,8 +349,8 @@ __global__ void __launch_bounds__(128) bwd_kernel(
     float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6;
-  float* WT = smem;                                      // [NC][E]  (shared by the block)
-  float* RED = WT + ((C::NC * C::E + 3) & ~3);           // [NPARAM] block reduction buffer
+  float* WP = smem;                                      // [E][NC+4] W image (shared)
+  float* RED = WP + C::E * C::WPS;                       // [NPARAM] block reduction buffer
   float* base = smem + C::BWD_FIXED + wave_id() * a.per_wave;
   float* X = base + a.l_x;
   float* PR = base + a.l_pr;
@@ -352,8 +363,8 @@ __global__ void __launch_bounds__(128) bwd_kernel(
   const int F = a.F;
 
   for (int k = threadIdx.x; k < C::NC * C::E; k += blockDim.x) {
-    const int c = k / C::E, e = k % C::E;
-    WT[k] = W[e * C::NC + c];
+    const int e = k / C::NC, c = k % C::NC;
+    WP[e * C::WPS + c] = W[k];
   }
   for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
   zero_pad_rows<C>(PR, F);
@@ -401,14 +412,14 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         const int f = f0 + lane / C::LPR;
         const bool act = f < F;
         const float mean = act ? ST[2 * f] : 0.f;
-        const float sd = act ? ST[2 * f + 1] : 1.f;
+        const float rstd = act ? ST[2 * f + 1] : 1.f;
         float zv[C::CPLN], zh[C::CPLN], g[C::CPLN];
         float sg = 0.f, sgz = 0.f;
 #pragma unroll
         for (int c = 0; c < C::CPLN; ++c) {
           const int u = u0 + c * C::LPR;
           zv[c] = act ? O[f * C::OS + u] : 0.f;
-          zh[c] = (zv[c] - mean) / sd;
+          zh[c] = (zv[c] - mean) * rstd;
           const float dyv = act ? DY[f * C::U + u] : 0.f;
           dg[c] = fmaf(dyv, zh[c], dg[c]);
           dbt[c] += dyv;
@@ -416,17 +427,17 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           sg += g[c];
           sgz += g[c] * zh[c];
         }
-        sg = group_sum<C::LPR>(sg) / (float)C::U;
-        sgz = group_sum<C::LPR>(sgz) / (float)C::U;
+        sg = group_sum<C::LPR>(sg) * (1.0f / (float)C::U);
+        sgz = group_sum<C::LPR>(sgz) * (1.0f / (float)C::U);
         if (act) {
 #pragma unroll
           for (int c = 0; c < C::CPLN; ++c) {
             const int u = u0 + c * C::LPR;
-            const float dz = (g[c] - sg - zh[c] * sgz) / sd;
+            const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
             const float dt = zv[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
             O[f * C::OS + u] = dt;
-            if (a.use_res)
-              GPR[f * C::PRS + 3 * C::U + u] = PR[f * C::PRS + 3 * C::U + u] > 0.f ? dt : 0.f;
+            GPR[f * C::PRS + 3 * C::U + u] =
+                (a.use_res && PR[f * C::PRS + 3 * C::U + u] > 0.f) ? dt : 0.f;
           }
         }
       }
@@ -439,10 +450,13 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         float dv[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
-        for (int i = 0; i < F; ++i) {
-          float p = PM[(h * F + i) * C::PMS + j];
-          if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
-          axpy_row(dv, p, O + i * C::OS + h * C::DH);
+#pragma unroll 4
+        for (int i = 0; i < C::FMAX; ++i) {
+          if (C::EXACT || i < F) {
+            float p = PM[(h * F + i) * C::PMS + j];
+            if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+            axpy_row(dv, p, O + i * C::OS + h * C::DH);
+          }
         }
         if (act) {
           const float* vr = PR + j * C::PRS + 2 * C::U + h * C::DH;
@@ -477,7 +491,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
 #pragma unroll
         for (int j = 0; j < C::FMAX; ++j) {
-          const float ds = pm_row[j] * (s[j] - D) / a.sdh;
+          const float ds = pm_row[j] * (s[j] - D) * a.inv_sdh;
           if (act) pm_row[j] = ds;
           axpy_row(dq, ds, kb + j * C::PRS);
         }
@@ -497,7 +511,9 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         float dk[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
-        for (int i = 0; i < F; ++i) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+#pragma unroll 4
+        for (int i = 0; i < C::FMAX; ++i)
+          if (C::EXACT || i < F) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
         if (act) {
           const float* kr = PR + j * C::PRS + C::U + h * C::DH;
           float* gk = GPR + j * C::PRS + C::U + h * C::DH;
@@ -510,8 +526,11 @@ __global__ void __launch_bounds__(128) bwd_kernel(
 #pragma unroll
       for (int cc = 0; cc < C::CPLP; ++cc) {
         const int c = cc * C::NCOLW + col;
-        if (c < a.ncol) {
-          for (int f = rsub; f < F; f += C::RPI) {
+        {
+#pragma unroll 2
+          for (int f0 = 0; f0 < C::FMAX; f0 += C::RPI) {
+            const int f = f0 + rsub;
+            if (!(C::EXACT ? (f < C::FMAX) : (f < F))) continue;
             const float gcol = GPR[f * C::PRS + c];
             db[cc] += gcol;
             const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
@@ -526,15 +545,23 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           }
         }
       }
-      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e)) ----
+      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e)); float4 over c ----
       {
         const int e = lane % C::E;
+        const float4* wr = reinterpret_cast<const float4*>(WP + e * C::WPS);
         for (int f0 = 0; f0 < F; f0 += C::RGE) {
           const int f = f0 + lane / C::E;
           if (f < F) {
+            const float4* gr = reinterpret_cast<const float4*>(GPR + f * C::PRS);
             float acc = 0.f;
-            const float* gr = GPR + f * C::PRS;
-            for (int c = 0; c < a.ncol; ++c) acc = fmaf(gr[c], WT[c * C::E + e], acc);
+#pragma unroll
+            for (int c4 = 0; c4 < C::NC / 4; ++c4) {
+              const float4 gv = gr[c4], wv = wr[c4];
+              acc = fmaf(gv.x, wv.x, acc);
+              acc = fmaf(gv.y, wv.y, acc);
+              acc = fmaf(gv.z, wv.z, acc);
+              acc = fmaf(gv.w, wv.w, acc);
+            }
             if (it > 0) {
               DY[f * C::U + e] = acc;  // gradient w.r.t. the previous iteration's output
             } else {
@@ -570,7 +597,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
     if (wave_id() == w) {
       if (rsub == 0) {
 #pragma unroll
-        for (int cc = 0; cc < C::CPLP; ++cc) {
+        for (int cc = 0; cc < C::CPLP; ++cc) {  // (R columns hold zeros when !use_res)
           const int c = cc * C::NCOLW + col;
 #pragma unroll
           for (int e = 0; e < C::E; ++e) RED[e * C::NC + c] += dw[cc][e];
@@ -592,9 +619,9 @@ __global__ void __launch_bounds__(128) bwd_kernel(
     partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
 }
 
-// grid-level reduction of the per-block partials, fixed block order (deterministic)
-__global__ void reduce_params_kernel(const float* __restrict__ partials, int nblocks, int nparam,
-                                     float* __restrict__ out, int accumulate);
+// grid-level reduction of the per-block partials, fixed order (deterministic); interacting.hip
+void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
+                   int accumulate);
 
 // ---------------------------------------------------------------------------------------------
 template <class C, bool DROP>
@@ -631,8 +658,7 @@ int bwd_launch(const BwdReq& q) {
       q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
       q.workspace, a);
   if (q.dparams)  // NULL: leave the per-block partials in the workspace (kernel timing)
-    reduce_params_kernel<<<(C::NPARAM + 255) / 256, 256, 0, q.stream>>>(
-        q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+    reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
   return rs_status_after_launch();
 }
 

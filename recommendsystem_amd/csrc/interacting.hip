@@ -8,13 +8,9 @@ RS_IL_DECLARE_UNIT(il_unit_a)
 RS_IL_DECLARE_UNIT(il_unit_b)
 RS_IL_DECLARE_UNIT(il_unit_c)
 
-__global__ void reduce_params_kernel(const float* __restrict__ partials, int nblocks, int nparam,
-                                     float* __restrict__ out, int accumulate) {
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nparam; k += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += partials[(int64_t)b * nparam + k];
-    out[k] = accumulate ? out[k] + s : s;
-  }
+void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
+                   int accumulate) {
+  launch_column_reduce(s, partials, nblocks, nparam, nparam, nparam, out, nullptr, accumulate);
 }
 }  // namespace rs_il
 

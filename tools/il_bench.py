@@ -1,0 +1,37 @@
+"""Time the InteractingLayer kernels alone at config-2 size (B=4096, F=26, E=U=16, H=2, L=3)."""
+import os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from recommendsystem_amd import _lib
+from recommendsystem_amd._lib import call, ptr, stream_handle
+
+def main(B=4096, F=26, E=16, U=16, H=2, L=3, reps=50):
+    lib = _lib.load()
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = (torch.rand(B, F, E, device=dev, generator=g) - 0.5)
+    W = (torch.rand(E, 4 * U, device=dev, generator=g) - 0.5) * 0.5
+    bias = torch.zeros(4 * U, device=dev); gamma = torch.ones(U, device=dev); beta = torch.zeros(U, device=dev)
+    y = torch.empty(B, F * U, device=dev); xs = torch.empty(max(L - 1, 1), B, F, U, device=dev)
+    dy = torch.randn(B, F * U, device=dev, generator=g); dx = torch.empty_like(x)
+    wsn = int(lib.rs_il_bwd_workspace_floats(B, E, U)); ws = torch.empty(wsn, device=dev)
+    dp = torch.empty(int(lib.rs_il_param_count(E, U)), device=dev)
+    s = stream_handle()
+    fwd = lambda: call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs))
+    bwd = lambda: call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
+    red = lambda: call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(dx), 0, ptr(dp), 0, ptr(ws), wsn)
+    out = {}
+    for name, fn in (("fwd", fwd), ("bwd", bwd), ("bwd+reduce", red)):
+        fn(); torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps): fn()
+        e1.record(); torch.cuda.synchronize()
+        out[name + "_us"] = round(e0.elapsed_time(e1) / reps * 1e3, 2)
+    fl = 289_536 * B
+    out["fwd_tflops"] = round(fl / out["fwd_us"] / 1e6, 2)
+    out["bwd_tflops"] = round(2 * fl / out["bwd_us"] / 1e6, 2)
+    print(json.dumps(out))
+
+if __name__ == "__main__":
+    main(reps=int(os.environ.get("REPS", "50")))
