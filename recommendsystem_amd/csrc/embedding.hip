@@ -139,8 +139,9 @@ __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
     int G, int tile, int cap, float* __restrict__ grad_table, int32_t* __restrict__ flag,
     int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
   extern __shared__ __attribute__((aligned(16))) int32_t sm[];
-  int32_t* keys = sm;                                   // [cap]
-  float* vals = reinterpret_cast<float*>(sm + cap);     // [cap][dim]
+  int32_t* ctl = sm;                                    // [4]: claim count, range base
+  int32_t* keys = sm + 4;                               // [cap]  (lidx[cap] follows)
+  float* vals = reinterpret_cast<float*>(sm + 4 + 2 * cap);  // [cap][dim]
   for (int k = threadIdx.x; k < cap; k += blockDim.x) keys[k] = -1;
   for (int k = threadIdx.x; k < cap * dim; k += blockDim.x) vals[k] = 0.f;
   __syncthreads();
@@ -179,11 +180,30 @@ __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
     }
   }
   __syncthreads();
-  // ---- phase 2: one global row add per distinct row of the tile ----
+  // ---- phase 2: claim each distinct row once (flag CAS); the claims of the whole block take ONE
+  //      global atomic on n_touched (a single counter word serialises ~11 ns per atomic at the
+  //      memory side: 30k per-row increments would cost ~0.3 ms) ----
+  int32_t* lidx = keys + cap;  // reuse: vals region follows; lidx lives in the extra cap ints
+  int32_t& nclaim = ctl[0];
+  int32_t& base = ctl[1];
+  if (threadIdx.x == 0) nclaim = 0;
+  __syncthreads();
+  for (int slot = threadIdx.x; slot < cap; slot += blockDim.x) {
+    const int32_t row = keys[slot];
+    int32_t li = -1;
+    if (row >= 0 && atomicCAS(&flag[row], -1, -2) == -1) li = atomicAdd(&nclaim, 1);
+    lidx[slot] = li;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) base = nclaim > 0 ? atomicAdd(n_touched, nclaim) : 0;
+  __syncthreads();
   for (int slot = gsub; slot < cap; slot += per_pass) {
     const int32_t row = keys[slot];
     if (row < 0) continue;
-    if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
+    if (l == 0) {
+      const int32_t li = lidx[slot];
+      if (li >= 0 && base + li < touched_cap) touched[base + li] = row;
+    }
     float* dst = grad_table + (int64_t)row * dim;
     for (int e = l; e < dim; e += G) atomicAdd(dst + e, vals[slot * dim + e]);
   }
@@ -202,10 +222,10 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
   // LDS table: cap slots of dim floats (<= 64 KB), tile = cap/2 samples (load factor <= 1/2
   // for single-hot fields)
   int cap = 1024;
-  while (cap > 32 && (size_t)cap * (dim + 1) * 4 > 64 * 1024) cap >>= 1;
+  while (cap > 32 && (size_t)cap * (dim + 2) * 4 > 64 * 1024) cap >>= 1;
   const int tile = cap / 2;
   dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
-  const size_t lds = (size_t)cap * (dim + 1) * 4;
+  const size_t lds = ((size_t)cap * (dim + 2) + 4) * 4;
   sparse_grad_accum_kernel<<<grid, 256, lds, rs_stream(stream)>>>(
       rows, offsets, B, F, dout, dout_ld, dout_fstride, dim, combiner, G, tile, cap, grad_table,
       flag, touched, n_touched, touched_cap);

@@ -88,7 +88,7 @@ struct Cfg {
   static constexpr int OS = U + 4;                     // attention-output row stride
   static constexpr int PMS = FMAX + 1;                 // softmax-matrix row stride
   static constexpr int WPS = NC + 4;                   // padded W row stride in LDS (dx phase)
-  static constexpr int BWD_FIXED = E * WPS + ((NPARAM + 3) & ~3);  // W image + reduction buffer
+
   static_assert(U % H == 0, "unit_num must be divisible by head_num");
   static_assert(E % 4 == 0 && DH % 4 == 0, "E and dh must be multiples of 4");
   static_assert(E <= 64, "E <= 64");
@@ -127,7 +127,7 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
     a.l_gpr = off; off += r4(F * C::PRS);
     a.l_dy = off; off += r4(F * C::U);
     a.l_pm = off; off += r4(C::H * F * C::PMS);
-    a.l_st = off; off += r4(2 * F);
+    a.l_st = off; off += r4(2 * C::H * F);   // LN stats / the split-j D partials
   }
   a.per_wave = off;
   return a;
@@ -341,17 +341,25 @@ __global__ void __launch_bounds__(256, 3) fwd_kernel(
 }
 
 // ============================== backward kernel ==============================================
+// One workgroup = one sample at a time, TWO waves sharing the sample's LDS (the per-sample state
+// is ~25 KB, so one wave per sample would cap occupancy at 1 wave/SIMD; two waves per sample give
+// ~10 waves/CU).  Row-parallel phases (projection, LN, dW, dx) split rows between the waves;
+// attention phases keep the lane = (head, row) mapping and split the inner loop (keys for the
+// row-oriented softmax / dS / dQ passes, queries for the column-oriented dV / dK passes), the
+// two partials meeting in LDS regions that are dead during that phase:
+//   fwd recompute : GPR region holds (m_w, l_w, o_w) per row
+//   dV / dQ / dK  : DY region holds the second wave's partial row vector, ST the partial D_i.
+// Every sum combines the partials in a fixed order (wave 0 + wave 1): deterministic.
 template <class C, bool DROP>
 __global__ void __launch_bounds__(128) bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
-    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ dx, int dx_accumulate,
-    float* __restrict__ partials, Args a) {
+    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
+    int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int wpb = blockDim.x >> 6;
-  float* WP = smem;                                      // [E][NC+4] W image (shared)
-  float* RED = WP + C::E * C::WPS;                       // [NPARAM] block reduction buffer
-  float* base = smem + C::BWD_FIXED + wave_id() * a.per_wave;
+  constexpr int JH = (C::FMAX + 1) / 2;  // keys per wave in the split-j passes
+  float* WP = smem;                       // [E][NC+4] W image (shared)
+  float* base = smem + C::E * C::WPS;
   float* X = base + a.l_x;
   float* PR = base + a.l_pr;
   float* GPR = base + a.l_gpr;
@@ -360,17 +368,18 @@ __global__ void __launch_bounds__(128) bwd_kernel(
   float* PM = base + a.l_pm;
   float* ST = base + a.l_st;
   const int lane = lane_id();
+  const int w = wave_id();  // 0 or 1
   const int F = a.F;
+  const int HF = C::H * F;
+  const int j0 = w * JH;    // this wave's key (or query) half
 
   for (int k = threadIdx.x; k < C::NC * C::E; k += blockDim.x) {
     const int e = k / C::NC, c = k % C::NC;
     WP[e * C::WPS + c] = W[k];
   }
-  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
-  zero_pad_rows<C>(PR, F);
+  for (int k = F * C::PRS + threadIdx.x; k < C::FMAX * C::PRS; k += blockDim.x) PR[k] = 0.f;
   __syncthreads();
 
-  // per-lane gradient accumulators, kept in VGPRs across every sample this wave visits
   float dw[C::CPLP][C::E];
   float db[C::CPLP];
   float dg[C::CPLN], dbt[C::CPLN];
@@ -382,14 +391,13 @@ __global__ void __launch_bounds__(128) bwd_kernel(
   }
 #pragma unroll
   for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; }
-
   const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
   const int u0 = lane % C::LPR;
 
-  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_id(); b < a.B; b += (int64_t)gridDim.x * wpb) {
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     {
       const float* src = dy + b * dy_ld;
-      for (int k = lane; k < F * C::U; k += 64) DY[k] = src[k];  // dy_ld may be unaligned
+      for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
     }
     for (int it = a.L - 1; it >= 0; --it) {
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
@@ -397,29 +405,115 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         const float* xin = (it == 0) ? (x + b * F * C::E)
                                      : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
         const float4* src = reinterpret_cast<const float4*>(xin);
-        for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
+        for (int k = threadIdx.x; k < F * C::E / 4; k += blockDim.x)
+          reinterpret_cast<float4*>(X)[k] = src[k];
       }
-      wave_lds_sync();
-      // ---- recompute the iteration ----
-      project<C>(X, PR, a, W, bias);
-      wave_lds_sync();
-      attention_fwd<C, true, DROP>(PR, O, PM, a, b, lseed);
-      wave_lds_sync();
-      epilogue<C, 1>(O, PR, ST, nullptr, 0, a, gamma, beta);
-      wave_lds_sync();
-      // ---- LN + ReLU backward: O <- dt = dL/d(O+R);  GPR[R cols] <- dt * (R > 0) ----
-      for (int f0 = 0; f0 < F; f0 += C::RG) {
+      __syncthreads();
+      // ---- recompute: projections (rows split between the waves) ----
+#pragma unroll
+      for (int cc = 0; cc < C::CPLP; ++cc) {
+        const int c = cc * C::NCOLW + col;
+        float wv[C::E];
+#pragma unroll
+        for (int e = 0; e < C::E; ++e) wv[e] = WP[e * C::WPS + c];
+        const float bc = bias[c];
+        for (int f = 2 * rsub + w; f < F; f += 2 * C::RPI) {
+          const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
+          float acc = 0.f;
+#pragma unroll
+          for (int e4 = 0; e4 < C::E / 4; ++e4) {
+            const float4 xv = xr[e4];
+            acc = fmaf(xv.x, wv[4 * e4 + 0], acc);
+            acc = fmaf(xv.y, wv[4 * e4 + 1], acc);
+            acc = fmaf(xv.z, wv[4 * e4 + 2], acc);
+            acc = fmaf(xv.w, wv[4 * e4 + 3], acc);
+          }
+          PR[f * C::PRS + c] = fmaxf(acc + bc, 0.f);
+        }
+      }
+      __syncthreads();
+      // ---- recompute: attention, keys split between the waves ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, i = act ? r % F : 0;
+        float q[C::DH];
+        load_row(q, PR + i * C::PRS + h * C::DH);
+        const float* kb = PR + C::U + h * C::DH;
+        float s[JH];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          const float acc = (j < C::FMAX) ? dot_row(q, kb + j * C::PRS) : 0.f;
+          s[jj] = (j < F) ? acc * a.sc2 : -INFINITY;
+          mx = fmaxf(mx, s[jj]);
+        }
+        float* xch = GPR + r * (4 + 2 * C::DH);  // [m0 m1 l0 l1 | o0[DH] | o1[DH]]
+        if (act) xch[w] = mx;
+        __syncthreads();
+        const float m = act ? fmaxf(xch[0], xch[1]) : 0.f;
+        float l = 0.f;
+        float o[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
+        const float* vb = PR + 2 * C::U + h * C::DH;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          s[jj] = __builtin_amdgcn_exp2f(s[jj] - m);
+          l += s[jj];
+          float e = s[jj];
+          if (DROP && j < F) e = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? e * a.drop_scale : 0.f;
+          if (j < C::FMAX) axpy_row(o, e, vb + j * C::PRS);
+        }
+        if (act) {
+          xch[2 + w] = l;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) xch[4 + w * C::DH + d] = o[d];
+        }
+        __syncthreads();
+        if (act) {
+          const float inv = 1.0f / (xch[2] + xch[3]);
+          float* pm_row = PM + (h * F + i) * C::PMS;
+#pragma unroll
+          for (int jj = 0; jj < JH; ++jj)
+            if (j0 + jj < C::FMAX) pm_row[j0 + jj] = s[jj] * inv;
+          if (w == 0) {
+            float* orow = O + i * C::OS + h * C::DH;
+#pragma unroll
+            for (int d = 0; d < C::DH; ++d) orow[d] = (xch[4 + d] + xch[4 + C::DH + d]) * inv;
+          }
+        }
+        __syncthreads();
+      }
+      // ---- recompute: z = relu(O + R), LN stats (rows split) ----
+      for (int f0 = w * C::RG; f0 < F; f0 += 2 * C::RG) {
         const int f = f0 + lane / C::LPR;
         const bool act = f < F;
-        const float mean = act ? ST[2 * f] : 0.f;
-        const float rstd = act ? ST[2 * f + 1] : 1.f;
-        float zv[C::CPLN], zh[C::CPLN], g[C::CPLN];
+        float z[C::CPLN];
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          float t = act ? O[f * C::OS + u] : 0.f;
+          if (a.use_res && act) t += PR[f * C::PRS + 3 * C::U + u];
+          z[c] = fmaxf(t, 0.f);
+          sum += z[c];
+        }
+        const float mean = group_sum<C::LPR>(sum) * (1.0f / (float)C::U);
+        float sq = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
+        const float var = group_sum<C::LPR>(sq) * (1.0f / (float)C::U);
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        // ---- LN + ReLU backward, fused: O <- dt; GPR[R] <- dt * (R > 0) ----
+        float zh[C::CPLN], g[C::CPLN];
         float sg = 0.f, sgz = 0.f;
 #pragma unroll
         for (int c = 0; c < C::CPLN; ++c) {
           const int u = u0 + c * C::LPR;
-          zv[c] = act ? O[f * C::OS + u] : 0.f;
-          zh[c] = (zv[c] - mean) * rstd;
+          zh[c] = (z[c] - mean) * rstd;
           const float dyv = act ? DY[f * C::U + u] : 0.f;
           dg[c] = fmaf(dyv, zh[c], dg[c]);
           dbt[c] += dyv;
@@ -434,133 +528,156 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           for (int c = 0; c < C::CPLN; ++c) {
             const int u = u0 + c * C::LPR;
             const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
-            const float dt = zv[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+            const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
             O[f * C::OS + u] = dt;
             GPR[f * C::PRS + 3 * C::U + u] =
                 (a.use_res && PR[f * C::PRS + 3 * C::U + u] > 0.f) ? dt : 0.f;
           }
         }
       }
-      wave_lds_sync();
-      // ---- dV_j = sum_i Pd_ij dO_i   (lane = (h, j)) ----
-      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+      __syncthreads();
+      // ---- dV_j = sum_i Pd_ij dO_i   (lane = (h, j); queries split between the waves) ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
-        const bool act = r < C::H * F;
+        const bool act = r < HF;
         const int h = act ? r / F : 0, j = act ? r % F : 0;
         float dv[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
 #pragma unroll 4
-        for (int i = 0; i < C::FMAX; ++i) {
-          if (C::EXACT || i < F) {
+        for (int ii = 0; ii < JH; ++ii) {
+          const int i = j0 + ii;
+          if (i < F) {
             float p = PM[(h * F + i) * C::PMS + j];
             if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
             axpy_row(dv, p, O + i * C::OS + h * C::DH);
           }
         }
-        if (act) {
+        float* part = DY + r * C::DH;
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) part[d] = dv[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
           const float* vr = PR + j * C::PRS + 2 * C::U + h * C::DH;
           float* gv = GPR + j * C::PRS + 2 * C::U + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] + part[d] : 0.f;
         }
+        __syncthreads();
       }
-      wave_lds_sync();
-      // ---- dS (in place of P) and dQ   (lane = (h, i)) ----
-      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+      // ---- dS (in place of P) and dQ   (lane = (h, i); keys split between the waves) ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
-        const bool act = r < C::H * F;
+        const bool act = r < HF;
         const int h = act ? r / F : 0, i = act ? r % F : 0;
         float dO[C::DH];
         load_row(dO, O + i * C::OS + h * C::DH);
         const float* vb = PR + 2 * C::U + h * C::DH;
         const float* kb = PR + C::U + h * C::DH;
         float* pm_row = PM + (h * F + i) * C::PMS;
-        float s[C::FMAX];
-        float D = 0.f;
+        float s[JH];
+        float Dw = 0.f;
 #pragma unroll
-        for (int j = 0; j < C::FMAX; ++j) {
-          float dp = dot_row(dO, vb + j * C::PRS);  // padded V rows are zero -> dp = 0
-          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          const float p = pm_row[j];  // padded keys were stored as p = 0
-          D = fmaf(p, dp, D);
-          s[j] = dp;
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          float dp = (j < C::FMAX) ? dot_row(dO, vb + j * C::PRS) : 0.f;  // padded V rows: 0
+          if (DROP && j < F) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          const float p = (j < C::FMAX) ? pm_row[j] : 0.f;                // padded keys: p = 0
+          Dw = fmaf(p, dp, Dw);
+          s[jj] = dp;
         }
+        if (act) ST[r * 2 + w] = Dw;
+        __syncthreads();
+        const float D = act ? ST[r * 2] + ST[r * 2 + 1] : 0.f;
         float dq[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
 #pragma unroll
-        for (int j = 0; j < C::FMAX; ++j) {
-          const float ds = pm_row[j] * (s[j] - D) * a.inv_sdh;
-          if (act) pm_row[j] = ds;
-          axpy_row(dq, ds, kb + j * C::PRS);
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          if (j < C::FMAX) {
+            const float ds = pm_row[j] * (s[jj] - D) * a.inv_sdh;
+            axpy_row(dq, ds, kb + j * C::PRS);
+            if (act) pm_row[j] = ds;
+          }
         }
-        if (act) {
+        float* part = DY + r * C::DH;
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) part[d] = dq[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
           const float* qr = PR + i * C::PRS + h * C::DH;
           float* gq = GPR + i * C::PRS + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] + part[d] : 0.f;
         }
+        __syncthreads();
       }
-      wave_lds_sync();
-      // ---- dK_j = sum_i dS_ij Q_i   (lane = (h, j)) ----
-      for (int r0 = 0; r0 < C::H * F; r0 += 64) {
+      // ---- dK_j = sum_i dS_ij Q_i   (lane = (h, j); queries split between the waves) ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
-        const bool act = r < C::H * F;
+        const bool act = r < HF;
         const int h = act ? r / F : 0, j = act ? r % F : 0;
         float dk[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
 #pragma unroll 4
-        for (int i = 0; i < C::FMAX; ++i)
-          if (C::EXACT || i < F) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
-        if (act) {
+        for (int ii = 0; ii < JH; ++ii) {
+          const int i = j0 + ii;
+          if (i < F) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+        }
+        float* part = DY + r * C::DH;
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) part[d] = dk[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
           const float* kr = PR + j * C::PRS + C::U + h * C::DH;
           float* gk = GPR + j * C::PRS + C::U + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] + part[d] : 0.f;
         }
+        __syncthreads();
       }
-      wave_lds_sync();
-      // ---- dW[:, c] += X^T g ; db[c] += sum_f g   (lane = column) ----
+      // ---- dW[:, c] += X^T g ; db[c] += sum_f g   (lane = column; rows split) ----
 #pragma unroll
       for (int cc = 0; cc < C::CPLP; ++cc) {
         const int c = cc * C::NCOLW + col;
-        {
-#pragma unroll 2
-          for (int f0 = 0; f0 < C::FMAX; f0 += C::RPI) {
-            const int f = f0 + rsub;
-            if (!(C::EXACT ? (f < C::FMAX) : (f < F))) continue;
-            const float gcol = GPR[f * C::PRS + c];
-            db[cc] += gcol;
-            const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
+        for (int f = 2 * rsub + w; f < F; f += 2 * C::RPI) {
+          const float gcol = GPR[f * C::PRS + c];
+          db[cc] += gcol;
+          const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
 #pragma unroll
-            for (int e4 = 0; e4 < C::E / 4; ++e4) {
-              const float4 xv = xr[e4];
-              dw[cc][4 * e4] = fmaf(xv.x, gcol, dw[cc][4 * e4]);
-              dw[cc][4 * e4 + 1] = fmaf(xv.y, gcol, dw[cc][4 * e4 + 1]);
-              dw[cc][4 * e4 + 2] = fmaf(xv.z, gcol, dw[cc][4 * e4 + 2]);
-              dw[cc][4 * e4 + 3] = fmaf(xv.w, gcol, dw[cc][4 * e4 + 3]);
-            }
+          for (int e4 = 0; e4 < C::E / 4; ++e4) {
+            const float4 xv = xr[e4];
+            dw[cc][4 * e4] = fmaf(xv.x, gcol, dw[cc][4 * e4]);
+            dw[cc][4 * e4 + 1] = fmaf(xv.y, gcol, dw[cc][4 * e4 + 1]);
+            dw[cc][4 * e4 + 2] = fmaf(xv.z, gcol, dw[cc][4 * e4 + 2]);
+            dw[cc][4 * e4 + 3] = fmaf(xv.w, gcol, dw[cc][4 * e4 + 3]);
           }
         }
       }
-      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e)); float4 over c ----
+      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e); rows split) ----
       {
         const int e = lane % C::E;
         const float4* wr = reinterpret_cast<const float4*>(WP + e * C::WPS);
-        for (int f0 = 0; f0 < F; f0 += C::RGE) {
+        for (int f0 = w * C::RGE; f0 < F; f0 += 2 * C::RGE) {
           const int f = f0 + lane / C::E;
           if (f < F) {
             const float4* gr = reinterpret_cast<const float4*>(GPR + f * C::PRS);
             float acc = 0.f;
 #pragma unroll
             for (int c4 = 0; c4 < C::NC / 4; ++c4) {
-              const float4 gv = gr[c4], wv = wr[c4];
-              acc = fmaf(gv.x, wv.x, acc);
-              acc = fmaf(gv.y, wv.y, acc);
-              acc = fmaf(gv.z, wv.z, acc);
-              acc = fmaf(gv.w, wv.w, acc);
+              const float4 gv = gr[c4], wv4 = wr[c4];
+              acc = fmaf(gv.x, wv4.x, acc);
+              acc = fmaf(gv.y, wv4.y, acc);
+              acc = fmaf(gv.z, wv4.z, acc);
+              acc = fmaf(gv.w, wv4.w, acc);
             }
             if (it > 0) {
               DY[f * C::U + e] = acc;  // gradient w.r.t. the previous iteration's output
@@ -571,7 +688,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           }
         }
       }
-      wave_lds_sync();
+      __syncthreads();
     }
   }
 
@@ -593,8 +710,11 @@ __global__ void __launch_bounds__(128) bwd_kernel(
       dbt[c] += __shfl_xor(dbt[c], o, 64);
     }
   }
-  for (int w = 0; w < wpb; ++w) {
-    if (wave_id() == w) {
+  float* RED = base;  // the sample region is dead now
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
+  __syncthreads();
+  for (int ww = 0; ww < 2; ++ww) {
+    if (w == ww) {
       if (rsub == 0) {
 #pragma unroll
         for (int cc = 0; cc < C::CPLP; ++cc) {  // (R columns hold zeros when !use_res)
@@ -644,17 +764,16 @@ template <class C, bool DROP>
 int bwd_launch(const BwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
   Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
-  const size_t fixed = (size_t)C::BWD_FIXED * sizeof(float);
-  const size_t per_wave = (size_t)a.per_wave * sizeof(float);
-  if (fixed + per_wave > kLdsBytes) return RS_ERR_UNSUPPORTED;
-  int wpb = (int)((kLdsBytes - fixed) / per_wave);
-  if (wpb > kMaxBwdWaves) wpb = kMaxBwdWaves;
-  int64_t grid = (q.B + wpb - 1) / wpb;
+  // exchange scratch fits: fwd partials (4 + 2*DH per row) in GPR, D partials in ST
+  if (C::H * q.F * (4 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
+  const size_t lds = ((size_t)C::E * C::WPS + a.per_wave) * sizeof(float);
+  if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
+  int64_t grid = q.B;
   const int64_t max_grid = q.workspace_floats / C::NPARAM;
   if (grid > kMaxBwdGrid) grid = kMaxBwdGrid;
   if (grid > max_grid) grid = max_grid;
   if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
-  bwd_kernel<C, DROP><<<(int)grid, 64 * wpb, fixed + per_wave * wpb, q.stream>>>(
+  bwd_kernel<C, DROP><<<(int)grid, 128, lds, q.stream>>>(
       q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
       q.workspace, a);
   if (q.dparams)  // NULL: leave the per-block partials in the workspace (kernel timing)

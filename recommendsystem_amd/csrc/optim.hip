@@ -187,18 +187,27 @@ __global__ void __launch_bounds__(256) sparse_merge_kernel(
     const int32_t* __restrict__ rows, const float* __restrict__ grads, int32_t count, int dim,
     int lps, float* __restrict__ grad_table, int32_t* __restrict__ flag,
     int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
+  // one global n_touched atomic per block (see sparse_grad_accum_kernel)
+  __shared__ int32_t nclaim, base;
+  __shared__ int32_t lidx[256];
   const int per_block = blockDim.x / lps;
   const int gi = threadIdx.x / lps;
   const int l = threadIdx.x % lps;
-  for (int u = blockIdx.x * per_block + gi; u < count; u += gridDim.x * per_block) {
-    const int32_t row = rows[u];
-    if (row < 0) continue;
-    if (l == 0 && atomicCAS(&flag[row], -1, -2) == -1) {
-      const int32_t k = atomicAdd(n_touched, 1);
-      if (k < touched_cap) touched[k] = row;
+  for (int u0 = blockIdx.x * per_block; u0 < count; u0 += gridDim.x * per_block) {
+    const int u = u0 + gi;
+    const int32_t row = u < count ? rows[u] : -1;
+    if (threadIdx.x == 0) nclaim = 0;
+    __syncthreads();
+    if (l == 0) lidx[gi] = (row >= 0 && atomicCAS(&flag[row], -1, -2) == -1) ? atomicAdd(&nclaim, 1) : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) base = nclaim > 0 ? atomicAdd(n_touched, nclaim) : 0;
+    __syncthreads();
+    if (row >= 0) {
+      if (l == 0 && lidx[gi] >= 0 && base + lidx[gi] < touched_cap) touched[base + lidx[gi]] = row;
+      for (int e = l; e < dim; e += lps)
+        grad_table[(int64_t)row * dim + e] += grads[(int64_t)u * dim + e];
     }
-    for (int e = l; e < dim; e += lps)
-      grad_table[(int64_t)row * dim + e] += grads[(int64_t)u * dim + e];
+    __syncthreads();
   }
 }
 
