@@ -251,25 +251,16 @@ class AutoIntTrainer:
         t.accumulate(self.rows, None, B, F, self.dx0, F * E, E, emb.combiner)
 
     def _exchange(self):
-        """Data-parallel gradient exchange: dense all-reduce of the flat arena
-        gradient (one RCCL bucket), sparse rows: compact -> all-gather -> rank-ordered merge."""
-        import torch.distributed as dist
+        """Data-parallel gradient exchange (recommendsystem_amd/dist.py)."""
+        from .dist import allreduce_flat, gather_sparse_lists
         m, t = self.model, self.model.table
-        dist.all_reduce(m.arena.grad, group=self.pg)
+        allreduce_flat(m.arena.grad, self.pg)
         cnt = t.n_touched.clone()
         call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
              ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
         t.n_touched.zero_()
-        counts = [torch.zeros_like(cnt) for _ in range(self.world)]
-        dist.all_gather(counts, cnt, group=self.pg)
-        n = int(torch.stack(counts).max().item())
-        if n == 0:
-            return
-        rows_all = [torch.empty(n, device=self.dev, dtype=torch.int32) for _ in range(self.world)]
-        grads_all = [torch.empty(n, t.dim, device=self.dev, dtype=torch.float32) for _ in range(self.world)]
-        dist.all_gather(rows_all, self.x_rows[:n].contiguous(), group=self.pg)
-        dist.all_gather(grads_all, self.x_grads[:n].contiguous(), group=self.pg)
-        for r in range(self.world):
+        rows_all, grads_all, n = gather_sparse_lists(self.x_rows, self.x_grads, cnt, self.pg)
+        for r in range(self.world if n else 0):  # rank order -> identical sums on every replica
             call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,
                  t.dim, ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched), t.touched_cap)
 

@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           s[jj] = (j < F) ? acc * a.sc2 : -INFINITY;
           mx = fmaxf(mx, s[jj]);
         }
-        float* xch = GPR + r * (4 + 2 * C::DH);  // [m0 m1 l0 l1 | o0[DH] | o1[DH]]
+        float* xch = GPR + r * (5 + 2 * C::DH);  // [m0 m1 l0 l1 | o0[DH] | o1[DH]], odd stride
         if (act) xch[w] = mx;
         __syncthreads();
         const float m = act ? fmaxf(xch[0], xch[1]) : 0.f;
@@ -553,17 +553,17 @@ __global__ void __launch_bounds__(128) bwd_kernel(
             axpy_row(dv, p, O + i * C::OS + h * C::DH);
           }
         }
-        float* part = DY + r * C::DH;
+        float* part = DY + r;  // [d][row]: element d at part[d * HF]
         if (act && w == 1) {
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d] = dv[d];
+          for (int d = 0; d < C::DH; ++d) part[d * HF] = dv[d];
         }
         __syncthreads();
         if (act && w == 0) {
           const float* vr = PR + j * C::PRS + 2 * C::U + h * C::DH;
           float* gv = GPR + j * C::PRS + 2 * C::U + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] + part[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] + part[d * HF] : 0.f;
         }
         __syncthreads();
       }
@@ -588,9 +588,9 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           Dw = fmaf(p, dp, Dw);
           s[jj] = dp;
         }
-        if (act) ST[r * 2 + w] = Dw;
+        if (act) ST[w * HF + r] = Dw;
         __syncthreads();
-        const float D = act ? ST[r * 2] + ST[r * 2 + 1] : 0.f;
+        const float D = act ? ST[r] + ST[HF + r] : 0.f;
         float dq[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
@@ -603,17 +603,17 @@ __global__ void __launch_bounds__(128) bwd_kernel(
             if (act) pm_row[j] = ds;
           }
         }
-        float* part = DY + r * C::DH;
+        float* part = DY + r;
         if (act && w == 1) {
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d] = dq[d];
+          for (int d = 0; d < C::DH; ++d) part[d * HF] = dq[d];
         }
         __syncthreads();
         if (act && w == 0) {
           const float* qr = PR + i * C::PRS + h * C::DH;
           float* gq = GPR + i * C::PRS + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] + part[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] + part[d * HF] : 0.f;
         }
         __syncthreads();
       }
@@ -630,17 +630,17 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           const int i = j0 + ii;
           if (i < F) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
         }
-        float* part = DY + r * C::DH;
+        float* part = DY + r;
         if (act && w == 1) {
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d] = dk[d];
+          for (int d = 0; d < C::DH; ++d) part[d * HF] = dk[d];
         }
         __syncthreads();
         if (act && w == 0) {
           const float* kr = PR + j * C::PRS + C::U + h * C::DH;
           float* gk = GPR + j * C::PRS + C::U + h * C::DH;
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] + part[d] : 0.f;
+          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] + part[d * HF] : 0.f;
         }
         __syncthreads();
       }
@@ -765,7 +765,7 @@ int bwd_launch(const BwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
   Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
   // exchange scratch fits: fwd partials (4 + 2*DH per row) in GPR, D partials in ST
-  if (C::H * q.F * (4 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
+  if (C::H * q.F * (5 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
   const size_t lds = ((size_t)C::E * C::WPS + a.per_wave) * sizeof(float);
   if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
   int64_t grid = q.B;

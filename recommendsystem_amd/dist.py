@@ -1,0 +1,59 @@
+"""Data-parallel gradient exchange: one process per GPU, torch.distributed with the
+'nccl' backend (= RCCL over xGMI on ROCm).  Replaces tensornet's dense MPI all-reduce
+(tn.optimizer.Optimizer) and its PS sparse push (tn.layers.EmbeddingFeatures) for DP training.
+
+  dense  : the model's flat gradient arena is ONE all-reduce bucket (AutoInt: 15.4 K floats,
+           latency-bound; staytime+rough_rank: ~3.5 M floats = 14 MB, still one bucket).
+  sparse : each rank pre-reduces its touched rows locally (rs_sparse_grad_accumulate), compacts
+           them into (rows, grads) lists, the lists are all-gathered (counts first, then lists
+           padded to the max count with row -1), and every rank merges the lists IN RANK ORDER
+           with atomic-free adds (rs_sparse_merge_rows): identical inputs + identical order ->
+           bitwise-identical sparse updates on every replica.
+
+The transport functions are device-agnostic (gloo on CPU tensors in tests/test_dist.py, RCCL
+on the GPU box); the merge itself runs in librecsys_amd.so.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def allreduce_flat(grad: torch.Tensor, group=None) -> None:
+    """Sum the flat dense gradient over ranks in place (the optimizer scales by 1/world)."""
+    dist.all_reduce(grad, group=group)
+
+
+def gather_sparse_lists(rows: torch.Tensor, grads: torch.Tensor, count: torch.Tensor, group=None):
+    """All-gather every rank's compacted (rows, grads) list.
+
+    rows [cap] int32 (-1 padded past `count`), grads [cap, dim], count [1] int32.
+    Returns (rows_all [world, n], grads_all [world, n, dim], n) with n = max count (n == 0 ->
+    nothing touched anywhere).  The host learns n through one small all-gather.
+    """
+    world = dist.get_world_size(group)
+    counts = [torch.zeros_like(count) for _ in range(world)]
+    dist.all_gather(counts, count, group=group)
+    n = int(torch.stack(counts).max().item())
+    if n == 0:
+        return None, None, 0
+    rows_all = torch.empty(world, n, dtype=rows.dtype, device=rows.device)
+    grads_all = torch.empty(world, n, grads.shape[1], dtype=grads.dtype, device=grads.device)
+    dist.all_gather(list(rows_all.unbind(0)), rows[:n].contiguous(), group=group)
+    dist.all_gather(list(grads_all.unbind(0)), grads[:n].contiguous(), group=group)
+    return rows_all, grads_all, n
+
+
+def merge_reference(rows_all, grads_all, table_grad):
+    """Host restatement of the rank-ordered merge (what rs_sparse_merge_rows does per rank),
+    used by the CPU tests: table_grad[row] += grads in rank order, skipping -1 padding."""
+    touched = []
+    for r in range(rows_all.shape[0]):
+        for u in range(rows_all.shape[1]):
+            row = int(rows_all[r, u])
+            if row < 0:
+                continue
+            if row not in touched:
+                touched.append(row)
+            table_grad[row] += grads_all[r, u]
+    return touched

@@ -1,0 +1,69 @@
+"""CPU, world_size 2 over gloo: the data-parallel exchange (dense bucket all-reduce, sparse list
+all-gather + rank-ordered merge) gives identical results on every rank, equal to the single-
+process sum over the union of the ranks' batches."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from recommendsystem_amd.dist import allreduce_flat, gather_sparse_lists, merge_reference
+
+ROWS, DIM, CAP = 50, 4, 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _local_lists(rank):
+    """What rs_sparse_compact leaves on rank `rank`: unique rows + their local sums, -1 padded."""
+    rng = np.random.default_rng(100 + rank)
+    n = 7 + 5 * rank
+    rows = rng.choice(ROWS, size=n, replace=False).astype(np.int32)
+    grads = rng.normal(size=(n, DIM)).astype(np.float32)
+    r = np.full(CAP, -1, np.int32)
+    g = np.zeros((CAP, DIM), np.float32)
+    r[:n], g[:n] = rows, grads
+    return r, g, n
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dense = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    allreduce_flat(dense)
+    r, g, n = _local_lists(rank)
+    rows_all, grads_all, nmax = gather_sparse_lists(torch.from_numpy(r), torch.from_numpy(g),
+                                                    torch.tensor([n], dtype=torch.int32))
+    table = np.zeros((ROWS, DIM), np.float32)
+    touched = merge_reference(rows_all.numpy(), grads_all.numpy(), table)
+    out[rank] = (dense.numpy().copy(), table.copy(), sorted(touched), nmax)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_exchange_two_ranks():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    d0, t0, tc0, n0 = out[0]
+    d1, t1, tc1, n1 = out[1]
+    assert np.array_equal(d0, d1) and np.array_equal(d0, np.arange(10) * 3.0)
+    assert np.array_equal(t0, t1) and tc0 == tc1  # replicas bitwise identical
+    assert n0 == n1 == 12
+    ref = np.zeros((ROWS, DIM), np.float64)
+    for rank in range(world):
+        r, g, n = _local_lists(rank)
+        for k in range(n):
+            ref[r[k]] += g[k]
+    assert np.allclose(t0, ref, atol=1e-6)
+    assert tc0 == sorted(set(int(v) for rank in range(world) for v in _local_lists(rank)[0] if v >= 0))
