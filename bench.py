@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (config 2: 4096)")
     ap.add_argument("--pool", type=int, default=8, help="distinct pre-generated batches")
-    ap.add_argument("--cpu-baseline-steps", type=int, default=3)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                    help="bounded CPU sample: run whole train steps until this much time passed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     return ap.parse_args()
@@ -63,7 +64,7 @@ def time_kernel(fn, reps):
     return e0.elapsed_time(e1) / reps * 1e-3  # seconds
 
 
-def cpu_baseline(cfg, model, batches_cpu, steps):
+def cpu_baseline(cfg, model, batches_cpu, seconds):
     from oracle import torch_ref as tr
     # the box's CPU share (OMP_NUM_THREADS is set to it; affinity shows the whole machine)
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
@@ -81,10 +82,13 @@ def cpu_baseline(cfg, model, batches_cpu, steps):
     ids, labels = batches_cpu[0]
     ref.step(ids, labels)  # warm-up
     t0 = time.perf_counter()
-    for i in range(steps):
-        ids, labels = batches_cpu[i % len(batches_cpu)]
+    n = 0
+    while n < 3 or time.perf_counter() - t0 < seconds:
+        ids, labels = batches_cpu[n % len(batches_cpu)]
         ref.step(ids, labels)
+        n += 1
     dt = time.perf_counter() - t0
+    steps = n
     B = ids.shape[0]
     return {"value": round(B * steps / dt, 1), "unit": "samples/sec", "cores": threads,
             "kind": "port",
@@ -168,7 +172,7 @@ def main():
     bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
     achieved = bwd_flops / t_bwd / 1e12
     traffic = None
-    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")
+    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")  # from tools/profile_round.sh
     if os.path.exists(tf_path):
         with open(tf_path) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -201,8 +205,8 @@ def main():
         "final_loss": round(loss, 6),
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_steps > 0:
-        out["cpu_baseline"] = cpu_baseline(cfg, model, pool_cpu, args.cpu_baseline_steps)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(cfg, model, pool_cpu, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -35,11 +35,24 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-// xor-butterfly sum over aligned groups of `W` lanes (W power of two, <= 64)
+// Sum over aligned groups of `W` lanes (W power of two, <= 64), result in every lane of the group.
+// W <= 16 uses DPP row operations only (VALU, no LDS round trip): quad_perm xor-1 / xor-2, then
+// row_half_mirror (lane i <-> 7 - i in each 8) and row_mirror (i <-> 15 - i in each 16): after
+// each step every lane holds the sum of a symmetric group, so mirrors complete the butterfly.
+// Wider groups finish with __shfl_xor (ds_bpermute / swizzle).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
+  if (W >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (W >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (W >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if (W >= 16) v += dpp_mov<0x140>(v); // row_mirror
 #pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 16; o < W; o <<= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 

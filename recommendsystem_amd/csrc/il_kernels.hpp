@@ -94,6 +94,28 @@ struct Cfg {
   static_assert(E <= 64, "E <= 64");
 };
 
+// Diagnostic build only (-DRS_IL_STAMPS): per-phase s_memtime deltas summed per wave and added to
+// a global u64 array (cdna_hip_programming.md §7 "In-kernel stamps"); shares, not absolute time.
+#ifdef RS_IL_STAMPS
+#define IL_STAMP_DECL uint64_t st_prev_ = 0, st_acc_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define IL_STAMP(k)                                                                    \
+  {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    uint64_t t_;                                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if ((k) > 0) st_acc_[(k)-1] += t_ - st_prev_;                                      \
+    st_prev_ = t_;                                                                     \
+  }
+#define IL_STAMP_FLUSH(ptr)                                                            \
+  if ((ptr) && lane_id() == 0)                                                         \
+    for (int k_ = 0; k_ < 10; ++k_) atomicAdd((unsigned long long*)(ptr) + k_, st_acc_[k_]);
+#else
+#define IL_STAMP_DECL
+#define IL_STAMP(k)
+#define IL_STAMP_FLUSH(ptr)
+#endif
+
 struct Args {
   int B, F, L, use_res, ncol;
   float eps, sdh, drop_rate, drop_scale;
@@ -101,6 +123,7 @@ struct Args {
   float sc2;        // log2(e) / sqrt(dh): scores go straight to the exp2 domain
   uint64_t seed;
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
+  unsigned long long* stamps;  // diagnostic build only
 };
 
 static inline int r4(int v) { return (v + 3) & ~3; }
@@ -130,6 +153,12 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
     a.l_st = off; off += r4(2 * C::H * F);   // LN stats / the split-j D partials
   }
   a.per_wave = off;
+#ifdef RS_IL_STAMPS
+  extern unsigned long long* g_il_stamps;
+  a.stamps = g_il_stamps;
+#else
+  a.stamps = nullptr;
+#endif
   return a;
 }
 
@@ -137,41 +166,6 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
 template <class C>
 __device__ __forceinline__ void zero_pad_rows(float* PR, int F) {
   for (int k = F * C::PRS + lane_id(); k < C::FMAX * C::PRS; k += 64) PR[k] = 0.f;
-}
-
-// ---- phase: projections  PR[f][c] = relu(x[f] . W[:, c] + b[c]) ----------------------------
-template <class C>
-__device__ __forceinline__ void project(const float* X, float* PR, const Args& a,
-                                        const float* __restrict__ W,
-                                        const float* __restrict__ bias) {
-  const int lane = lane_id();
-  const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
-#pragma unroll
-  for (int cc = 0; cc < C::CPLP; ++cc) {
-    const int c = cc * C::NCOLW + col;  // all 4U columns (R is computed even without use_res)
-    float w[C::E];
-#pragma unroll
-    for (int e = 0; e < C::E; ++e) w[e] = W[e * C::NC + c];
-    const float bc = bias[c];
-#pragma unroll 2
-    for (int f0 = 0; f0 < C::FMAX; f0 += C::RPI) {
-      const int f = f0 + rsub;
-      if (C::EXACT ? (f < C::FMAX) : (f < a.F)) {
-        const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
-        float acc = 0.f;
-#pragma unroll
-        for (int e4 = 0; e4 < C::E / 4; ++e4) {
-          const float4 xv = xr[e4];
-          acc = fmaf(xv.x, w[4 * e4 + 0], acc);
-          acc = fmaf(xv.y, w[4 * e4 + 1], acc);
-          acc = fmaf(xv.z, w[4 * e4 + 2], acc);
-          acc = fmaf(xv.w, w[4 * e4 + 3], acc);
-        }
-        acc += bc;  // Keras Dense: tensordot, then bias_add, then activation
-        PR[f * C::PRS + c] = fmaxf(acc, 0.f);
-      }
-    }
-  }
 }
 
 template <int N>
@@ -182,6 +176,13 @@ __device__ __forceinline__ void load_row(float (&v)[N], const float* p) {
     const float4 t = p4[d4];
     v[4 * d4] = t.x; v[4 * d4 + 1] = t.y; v[4 * d4 + 2] = t.z; v[4 * d4 + 3] = t.w;
   }
+}
+
+template <int N>
+__device__ __forceinline__ void store_row(float* p, const float (&v)[N]) {
+  float4* p4 = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) p4[d4] = make_float4(v[4 * d4], v[4 * d4 + 1], v[4 * d4 + 2], v[4 * d4 + 3]);
 }
 
 template <int N>
@@ -209,6 +210,162 @@ __device__ __forceinline__ void axpy_row(float (&o)[N], float p, const float* v)
     o[4 * d4 + 1] = fmaf(p, t.y, o[4 * d4 + 1]);
     o[4 * d4 + 2] = fmaf(p, t.z, o[4 * d4 + 2]);
     o[4 * d4 + 3] = fmaf(p, t.w, o[4 * d4 + 3]);
+  }
+}
+
+
+// =============================================================================================
+// GEMM-shaped phases on the matrix cores: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate,
+// exact: a k-ordered fma chain).  D[16x16] += A[16x4] B[4x16]; lane l = (q = l >> 4, j = l & 15)
+// supplies A[j][k_q] and B[k_q][j] and holds D[4q + r][j] (r < 4).  The k index is PERMUTED
+// consistently for A and B (k-step t takes k = 16s + 4q + t), so one ds_read_b128 of 4
+// consecutive floats feeds 4 k-steps.  W lives in VGPRs for the whole kernel in both layouts
+// (projection B operand and dx B operand), so only activations / gradients come from LDS:
+// this replaces the per-row broadcast ds_read_b128 streams of the VALU version, which made the
+// backward LDS-throughput bound (PMC: ~2.6K LDS instructions per sample-iteration).
+// =============================================================================================
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <class C>
+struct MfmaW {
+  static constexpr int KS = (C::E + 15) / 16;  // 16-wide k chunks of E
+  static constexpr int NT = C::NC / 16;        // 16-wide column tiles of [Wq|Wk|Wv|Wr]
+  static constexpr int ET = (C::E + 15) / 16;  // 16-wide e tiles (dx / dW rows)
+  static constexpr int CS = C::NC / 16;        // 16-wide c chunks (dx reduction)
+  float wp[KS][4][NT];  // projection B: W[16ks + 4q + t][16nt + j]
+  float wx[CS][4][ET];  // dx B       : W[16et + j][16cs + 4q + t]
+  float bp[NT];         // bias[16nt + j] (loop-invariant: kept out of the per-row loops)
+
+  __device__ __forceinline__ void load(const float* __restrict__ W, const float* __restrict__ bias) {
+    const int q = lane_id() >> 4, j = lane_id() & 15;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bp[nt] = bias[16 * nt + j];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int k = 16 * ks + 4 * q + t;
+          wp[ks][t][nt] = k < C::E ? W[k * C::NC + 16 * nt + j] : 0.f;
+        }
+#pragma unroll
+    for (int cs = 0; cs < CS; ++cs)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int et = 0; et < ET; ++et) {
+          const int e = 16 * et + j;
+          wx[cs][t][et] = e < C::E ? W[e * C::NC + 16 * cs + 4 * q + t] : 0.f;
+        }
+  }
+};
+
+// PR[f][c] = relu(X[f] . W[:, c] + b[c]) for the 16 rows of row tile rt (rows >= F skipped)
+template <class C>
+__device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, int rt,
+                                             const MfmaW<C>& w) {
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  using M = MfmaW<C>;
+  f32x4 acc[M::NT];
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = 16 * rt + j;  // A row of this lane (rows >= F give discarded outputs)
+#pragma unroll
+  for (int ks = 0; ks < M::KS; ++ks) {
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (16 * ks + 4 * q < C::E && arow < F) {
+      const float4 v = *reinterpret_cast<const float4*>(X + arow * C::E + 16 * ks + 4 * q);
+      a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int nt = 0; nt < M::NT; ++nt) acc[nt] = mfma_16x16x4(a4[t], w.wp[ks][t][nt], acc[nt]);
+  }
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) {
+    const int c = 16 * nt + j;
+    const float bc = w.bp[nt];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * rt + 4 * q + r;
+      if (f < F) PR[f * C::PRS + c] = fmaxf(acc[nt][r] + bc, 0.f);
+    }
+  }
+}
+
+// dW[e][c] += sum_{f in tile rt} X[f][e] G[f][c] (acc[et][nt], D row = e, col = c);
+// db partial: dbp[nt] += sum over this lane's 4 rows of G[f][16nt + j]
+template <class C>
+__device__ __forceinline__ void mfma_dw(const float* X, const float* G, int F, int rt,
+                                        f32x4 (&acc)[MfmaW<C>::ET][MfmaW<C>::NT],
+                                        float (&dbp)[MfmaW<C>::NT]) {
+  using M = MfmaW<C>;
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  float xa[4][M::ET];
+  float gb[4][M::NT];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int f = 16 * rt + 4 * q + t;
+    const bool ok = f < F;
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et) {
+      const int e = 16 * et + j;
+      xa[t][et] = (ok && e < C::E) ? X[f * C::E + e] : 0.f;
+    }
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) {
+      gb[t][nt] = ok ? G[f * C::PRS + 16 * nt + j] : 0.f;
+      dbp[nt] += gb[t][nt];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+      for (int nt = 0; nt < M::NT; ++nt)
+        acc[et][nt] = mfma_16x16x4(xa[t][et], gb[t][nt], acc[et][nt]);
+}
+
+// dx[f][e] = sum_c G[f][c] W[e][c] for row tile rt; writes rows < F to out[f * ld + e]
+template <class C>
+__device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const MfmaW<C>& w,
+                                        float* out, int ld, bool accumulate) {
+  using M = MfmaW<C>;
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  f32x4 acc[M::ET];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = 16 * rt + j;
+#pragma unroll
+  for (int cs = 0; cs < M::CS; ++cs) {
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (arow < F) {
+      const float4 v = *reinterpret_cast<const float4*>(G + arow * C::PRS + 16 * cs + 4 * q);
+      a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+  }
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et) {
+    const int e = 16 * et + j;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * rt + 4 * q + r;
+      if (f < F && e < C::E) {
+        float* d = out + f * ld + e;
+        *d = accumulate ? (*d + acc[et][r]) : acc[et][r];
+      }
+    }
   }
 }
 
@@ -264,9 +421,8 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
 //      MODE 1 (backward recompute): keep z in O, (mean, std) per row in ST. -----------------
 template <class C, int MODE>
 __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, float* Y,
-                                         int y_stride, const Args& a,
-                                         const float* __restrict__ gamma,
-                                         const float* __restrict__ beta) {
+                                         int y_stride, const Args& a, const float (&gam)[C::CPLN],
+                                         const float (&bet)[C::CPLN]) {
   const int lane = lane_id();
   const int u0 = lane % C::LPR;
   for (int f0 = 0; f0 < a.F; f0 += C::RG) {
@@ -292,7 +448,7 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
 #pragma unroll
       for (int c = 0; c < C::CPLN; ++c) {
         const int u = u0 + c * C::LPR;
-        if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) * rstd * gamma[u] + beta[u];
+        if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) * rstd * gam[c] + bet[c];
         else O[f * C::OS + u] = z[c];
       }
       if (MODE == 1 && u0 == 0) { ST[2 * f] = mean; ST[2 * f + 1] = rstd; }
@@ -315,20 +471,28 @@ __global__ void __launch_bounds__(256, 3) fwd_kernel(
   const int wpb = blockDim.x >> 6;
   const int F = a.F;
   zero_pad_rows<C>(PR, F);
+  MfmaW<C> mw;
+  mw.load(W, bias);
+  float gam[C::CPLN], bet[C::CPLN];
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) {
+    gam[c] = gamma[lane % C::LPR + c * C::LPR];
+    bet[c] = beta[lane % C::LPR + c * C::LPR];
+  }
   for (int64_t b = (int64_t)blockIdx.x * wpb + wave_id(); b < a.B; b += (int64_t)gridDim.x * wpb) {
     const float4* src = reinterpret_cast<const float4*>(x + b * F * C::E);
     for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
     wave_lds_sync();
     for (int it = 0; it < a.L; ++it) {
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
-      project<C>(X, PR, a, W, bias);
+      for (int rt = 0; rt * 16 < F; ++rt) mfma_project<C>(X, PR, F, rt, mw);
       wave_lds_sync();
       attention_fwd<C, false, DROP>(PR, O, nullptr, a, b, lseed);
       wave_lds_sync();
       if (it == a.L - 1) {
-        epilogue<C, 0>(O, PR, nullptr, y + b * y_ld, C::U, a, gamma, beta);
+        epilogue<C, 0>(O, PR, nullptr, y + b * y_ld, C::U, a, gam, bet);
       } else {
-        epilogue<C, 0>(O, PR, nullptr, X, C::E, a, gamma, beta);  // E == U when L > 1
+        epilogue<C, 0>(O, PR, nullptr, X, C::E, a, gam, bet);  // E == U when L > 1
         wave_lds_sync();
         if (xsave) {
           float4* dst = reinterpret_cast<float4*>(xsave + ((int64_t)it * a.B + b) * F * C::U);
@@ -358,8 +522,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int JH = (C::FMAX + 1) / 2;  // keys per wave in the split-j passes
-  float* WP = smem;                       // [E][NC+4] W image (shared)
-  float* base = smem + C::E * C::WPS;
+  float* base = smem;
   float* X = base + a.l_x;
   float* PR = base + a.l_pr;
   float* GPR = base + a.l_gpr;
@@ -373,33 +536,34 @@ __global__ void __launch_bounds__(128) bwd_kernel(
   const int HF = C::H * F;
   const int j0 = w * JH;    // this wave's key (or query) half
 
-  for (int k = threadIdx.x; k < C::NC * C::E; k += blockDim.x) {
-    const int e = k / C::NC, c = k % C::NC;
-    WP[e * C::WPS + c] = W[k];
-  }
   for (int k = F * C::PRS + threadIdx.x; k < C::FMAX * C::PRS; k += blockDim.x) PR[k] = 0.f;
   __syncthreads();
 
-  float dw[C::CPLP][C::E];
-  float db[C::CPLP];
-  float dg[C::CPLN], dbt[C::CPLN];
+  using M = MfmaW<C>;
+  MfmaW<C> mw;
+  mw.load(W, bias);
+  f32x4 dwacc[M::ET][M::NT];
+  float dbp[M::NT];
 #pragma unroll
-  for (int cc = 0; cc < C::CPLP; ++cc) {
-    db[cc] = 0.f;
+  for (int et = 0; et < M::ET; ++et)
 #pragma unroll
-    for (int e = 0; e < C::E; ++e) dw[cc][e] = 0.f;
-  }
+    for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; }
-  const int col = lane % C::NCOLW, rsub = lane / C::NCOLW;
+  for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
+  float dg[C::CPLN], dbt[C::CPLN], gam[C::CPLN];
   const int u0 = lane % C::LPR;
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
+  const int nrt = (F + 15) / 16;  // 16-row tiles; wave w takes tiles w, w + 2, ...
 
+  IL_STAMP_DECL
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     {
       const float* src = dy + b * dy_ld;
       for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
     }
     for (int it = a.L - 1; it >= 0; --it) {
+      IL_STAMP(0)
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
       {
         const float* xin = (it == 0) ? (x + b * F * C::E)
@@ -409,29 +573,11 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           reinterpret_cast<float4*>(X)[k] = src[k];
       }
       __syncthreads();
-      // ---- recompute: projections (rows split between the waves) ----
-#pragma unroll
-      for (int cc = 0; cc < C::CPLP; ++cc) {
-        const int c = cc * C::NCOLW + col;
-        float wv[C::E];
-#pragma unroll
-        for (int e = 0; e < C::E; ++e) wv[e] = WP[e * C::WPS + c];
-        const float bc = bias[c];
-        for (int f = 2 * rsub + w; f < F; f += 2 * C::RPI) {
-          const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
-          float acc = 0.f;
-#pragma unroll
-          for (int e4 = 0; e4 < C::E / 4; ++e4) {
-            const float4 xv = xr[e4];
-            acc = fmaf(xv.x, wv[4 * e4 + 0], acc);
-            acc = fmaf(xv.y, wv[4 * e4 + 1], acc);
-            acc = fmaf(xv.z, wv[4 * e4 + 2], acc);
-            acc = fmaf(xv.w, wv[4 * e4 + 3], acc);
-          }
-          PR[f * C::PRS + c] = fmaxf(acc + bc, 0.f);
-        }
-      }
+      IL_STAMP(1)
+      // ---- recompute: projections (row tiles split between the waves; MFMA) ----
+      for (int rt = w; rt < nrt; rt += 2) mfma_project<C>(X, PR, F, rt, mw);
       __syncthreads();
+      IL_STAMP(2)
       // ---- recompute: attention, keys split between the waves ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -480,13 +626,15 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           for (int jj = 0; jj < JH; ++jj)
             if (j0 + jj < C::FMAX) pm_row[j0 + jj] = s[jj] * inv;
           if (w == 0) {
-            float* orow = O + i * C::OS + h * C::DH;
+            float ov[C::DH];
 #pragma unroll
-            for (int d = 0; d < C::DH; ++d) orow[d] = (xch[4 + d] + xch[4 + C::DH + d]) * inv;
+            for (int d = 0; d < C::DH; ++d) ov[d] = (xch[4 + d] + xch[4 + C::DH + d]) * inv;
+            store_row(O + i * C::OS + h * C::DH, ov);
           }
         }
         __syncthreads();
       }
+      IL_STAMP(3)
       // ---- recompute: z = relu(O + R), LN stats (rows split) ----
       for (int f0 = w * C::RG; f0 < F; f0 += 2 * C::RG) {
         const int f = f0 + lane / C::LPR;
@@ -517,7 +665,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
           const float dyv = act ? DY[f * C::U + u] : 0.f;
           dg[c] = fmaf(dyv, zh[c], dg[c]);
           dbt[c] += dyv;
-          g[c] = dyv * gamma[u];
+          g[c] = dyv * gam[c];
           sg += g[c];
           sgz += g[c] * zh[c];
         }
@@ -536,6 +684,7 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         }
       }
       __syncthreads();
+      IL_STAMP(4)
       // ---- dV_j = sum_i Pd_ij dO_i   (lane = (h, j); queries split between the waves) ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -544,10 +693,10 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         float dv[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
-#pragma unroll 4
+#pragma unroll
         for (int ii = 0; ii < JH; ++ii) {
           const int i = j0 + ii;
-          if (i < F) {
+          if (C::EXACT ? (i < C::FMAX) : (i < F)) {  // compile-time for exact-F shapes
             float p = PM[(h * F + i) * C::PMS + j];
             if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
             axpy_row(dv, p, O + i * C::OS + h * C::DH);
@@ -560,13 +709,15 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         }
         __syncthreads();
         if (act && w == 0) {
-          const float* vr = PR + j * C::PRS + 2 * C::U + h * C::DH;
-          float* gv = GPR + j * C::PRS + 2 * C::U + h * C::DH;
+          float vr[C::DH];
+          load_row(vr, PR + j * C::PRS + 2 * C::U + h * C::DH);
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gv[d] = vr[d] > 0.f ? dv[d] + part[d * HF] : 0.f;
+          for (int d = 0; d < C::DH; ++d) vr[d] = vr[d] > 0.f ? dv[d] + part[d * HF] : 0.f;
+          store_row(GPR + j * C::PRS + 2 * C::U + h * C::DH, vr);
         }
         __syncthreads();
       }
+      IL_STAMP(5)
       // ---- dS (in place of P) and dQ   (lane = (h, i); keys split between the waves) ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -610,13 +761,15 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         }
         __syncthreads();
         if (act && w == 0) {
-          const float* qr = PR + i * C::PRS + h * C::DH;
-          float* gq = GPR + i * C::PRS + h * C::DH;
+          float qr[C::DH];
+          load_row(qr, PR + i * C::PRS + h * C::DH);
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gq[d] = qr[d] > 0.f ? dq[d] + part[d * HF] : 0.f;
+          for (int d = 0; d < C::DH; ++d) qr[d] = qr[d] > 0.f ? dq[d] + part[d * HF] : 0.f;
+          store_row(GPR + i * C::PRS + h * C::DH, qr);
         }
         __syncthreads();
       }
+      IL_STAMP(6)
       // ---- dK_j = sum_i dS_ij Q_i   (lane = (h, j); queries split between the waves) ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -625,10 +778,11 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         float dk[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
-#pragma unroll 4
+#pragma unroll
         for (int ii = 0; ii < JH; ++ii) {
           const int i = j0 + ii;
-          if (i < F) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+          if (C::EXACT ? (i < C::FMAX) : (i < F))
+            axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
         }
         float* part = DY + r;
         if (act && w == 1) {
@@ -637,70 +791,33 @@ __global__ void __launch_bounds__(128) bwd_kernel(
         }
         __syncthreads();
         if (act && w == 0) {
-          const float* kr = PR + j * C::PRS + C::U + h * C::DH;
-          float* gk = GPR + j * C::PRS + C::U + h * C::DH;
+          float kr[C::DH];
+          load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) gk[d] = kr[d] > 0.f ? dk[d] + part[d * HF] : 0.f;
+          for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] + part[d * HF] : 0.f;
+          store_row(GPR + j * C::PRS + C::U + h * C::DH, kr);
         }
         __syncthreads();
       }
-      // ---- dW[:, c] += X^T g ; db[c] += sum_f g   (lane = column; rows split) ----
-#pragma unroll
-      for (int cc = 0; cc < C::CPLP; ++cc) {
-        const int c = cc * C::NCOLW + col;
-        for (int f = 2 * rsub + w; f < F; f += 2 * C::RPI) {
-          const float gcol = GPR[f * C::PRS + c];
-          db[cc] += gcol;
-          const float4* xr = reinterpret_cast<const float4*>(X + f * C::E);
-#pragma unroll
-          for (int e4 = 0; e4 < C::E / 4; ++e4) {
-            const float4 xv = xr[e4];
-            dw[cc][4 * e4] = fmaf(xv.x, gcol, dw[cc][4 * e4]);
-            dw[cc][4 * e4 + 1] = fmaf(xv.y, gcol, dw[cc][4 * e4 + 1]);
-            dw[cc][4 * e4 + 2] = fmaf(xv.z, gcol, dw[cc][4 * e4 + 2]);
-            dw[cc][4 * e4 + 3] = fmaf(xv.w, gcol, dw[cc][4 * e4 + 3]);
-          }
-        }
-      }
-      // ---- dx[f][e] = sum_c g[f][c] W[e][c]   (lane = (row, e); rows split) ----
-      {
-        const int e = lane % C::E;
-        const float4* wr = reinterpret_cast<const float4*>(WP + e * C::WPS);
-        for (int f0 = w * C::RGE; f0 < F; f0 += 2 * C::RGE) {
-          const int f = f0 + lane / C::E;
-          if (f < F) {
-            const float4* gr = reinterpret_cast<const float4*>(GPR + f * C::PRS);
-            float acc = 0.f;
-#pragma unroll
-            for (int c4 = 0; c4 < C::NC / 4; ++c4) {
-              const float4 gv = gr[c4], wv4 = wr[c4];
-              acc = fmaf(gv.x, wv4.x, acc);
-              acc = fmaf(gv.y, wv4.y, acc);
-              acc = fmaf(gv.z, wv4.z, acc);
-              acc = fmaf(gv.w, wv4.w, acc);
-            }
-            if (it > 0) {
-              DY[f * C::U + e] = acc;  // gradient w.r.t. the previous iteration's output
-            } else {
-              float* d = dx + b * F * C::E + f * C::E + e;
-              *d = dx_accumulate ? (*d + acc) : acc;
-            }
-          }
-        }
+      IL_STAMP(7)
+      // ---- dW += X^T G, db += colsum G; dx = G W^T  (row tiles split between the waves; MFMA) ----
+      for (int rt = w; rt < nrt; rt += 2) {
+        mfma_dw<C>(X, GPR, F, rt, dwacc, dbp);
+        if (it > 0) mfma_dx<C>(GPR, F, rt, mw, DY, C::U, false);  // dL/d(previous output)
+        else mfma_dx<C>(GPR, F, rt, mw, dx + b * F * C::E, C::E, dx_accumulate != 0);
       }
       __syncthreads();
+      IL_STAMP(8)
     }
   }
+  IL_STAMP_FLUSH(a.stamps)
 
-  // ---- lanes -> wave (xor butterfly over row sub-groups) -> block (wave order) ----
+  // ---- lanes -> wave -> block (wave order): dW from the MFMA accumulators (D row = e,
+  //      col = c), db partials summed over the 4 lane groups, LN grads over the row groups ----
 #pragma unroll
-  for (int cc = 0; cc < C::CPLP; ++cc) {
-#pragma unroll
-    for (int o = C::NCOLW; o < 64; o <<= 1) {
-      db[cc] += __shfl_xor(db[cc], o, 64);
-#pragma unroll
-      for (int e = 0; e < C::E; ++e) dw[cc][e] += __shfl_xor(dw[cc][e], o, 64);
-    }
+  for (int nt = 0; nt < M::NT; ++nt) {
+    dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
+    dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
   }
 #pragma unroll
   for (int c = 0; c < C::CPLN; ++c) {
@@ -713,27 +830,34 @@ __global__ void __launch_bounds__(128) bwd_kernel(
   float* RED = base;  // the sample region is dead now
   for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
   __syncthreads();
-  for (int ww = 0; ww < 2; ++ww) {
-    if (w == ww) {
-      if (rsub == 0) {
+  {
+    const int q = lane >> 4, j = lane & 15;
+    for (int ww = 0; ww < 2; ++ww) {
+      if (w == ww) {
 #pragma unroll
-        for (int cc = 0; cc < C::CPLP; ++cc) {  // (R columns hold zeros when !use_res)
-          const int c = cc * C::NCOLW + col;
+        for (int et = 0; et < M::ET; ++et)
 #pragma unroll
-          for (int e = 0; e < C::E; ++e) RED[e * C::NC + c] += dw[cc][e];
-          RED[C::E * C::NC + c] += db[cc];
+          for (int nt = 0; nt < M::NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int e = 16 * et + 4 * q + r;
+              if (e < C::E) RED[e * C::NC + 16 * nt + j] += dwacc[et][nt][r];
+            }
+        if (q == 0) {
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + j] += dbp[nt];
+        }
+        if (lane < C::LPR) {
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            RED[C::E * C::NC + C::NC + u] += dg[c];
+            RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
+          }
         }
       }
-      if (lane < C::LPR) {
-#pragma unroll
-        for (int c = 0; c < C::CPLN; ++c) {
-          const int u = u0 + c * C::LPR;
-          RED[C::E * C::NC + C::NC + u] += dg[c];
-          RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
-        }
-      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
     partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
@@ -766,7 +890,7 @@ int bwd_launch(const BwdReq& q) {
   Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
   // exchange scratch fits: fwd partials (4 + 2*DH per row) in GPR, D partials in ST
   if (C::H * q.F * (5 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
-  const size_t lds = ((size_t)C::E * C::WPS + a.per_wave) * sizeof(float);
+  const size_t lds = (size_t)a.per_wave * sizeof(float);
   if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
   int64_t grid = q.B;
   const int64_t max_grid = q.workspace_floats / C::NPARAM;

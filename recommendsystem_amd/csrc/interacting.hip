@@ -14,6 +14,12 @@ void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam
 }
 }  // namespace rs_il
 
+#ifdef RS_IL_STAMPS
+namespace rs_il { unsigned long long* g_il_stamps = nullptr; }
+// diagnostic build only (not part of include/recsys_amd.h)
+RS_API void rs_il_debug_set_stamps(unsigned long long* p) { rs_il::g_il_stamps = p; }
+#endif
+
 RS_API int rs_il_param_count(int E, int U) { return E * 4 * U + 4 * U + 2 * U; }
 
 RS_API int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U) {

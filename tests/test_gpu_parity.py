@@ -2,7 +2,9 @@
 inputs.  Tolerances (fp32 kernels vs the float64 oracle):
   * index work (hashed rows, touched-row sets): bit-exact;
   * forward activations / logits: |err| <= 1e-5 absolute (north_star: "fp32 logits within 1e-5");
-  * gradients and optimizer updates: |err| <= 1e-4 * (1 + |ref|) (fp32 accumulation order);
+  * gradients and optimizer updates: |err| <= 1e-4 * |ref| + max(1e-4, 2e-6 * max|ref|)
+    (fp32 sums over B*F*layer_num terms: the absolute error scales with the tensor's magnitude,
+    e.g. dW entries reach ~450 at B=64 with random dy);
 The oracle is unpinned against the TF reference (oracle/ctr_oracle.py header).
 """
 from __future__ import annotations
@@ -20,6 +22,11 @@ DEV = "cuda"
 
 def _np(t):
     return t.detach().double().cpu().numpy()
+
+
+def assert_grad_close(got, ref, what=""):
+    ref = np.asarray(ref, dtype=np.float64)
+    assert_close(got, ref, max(1e-4, 2e-6 * float(np.abs(ref).max(initial=0.0))), 1e-4, what)
 
 
 def assert_close(got, ref, atol, rtol=0.0, what=""):
@@ -163,11 +170,11 @@ def test_interacting_backward(case):
     xr = torch.from_numpy(x).double().requires_grad_(True)
     yr = tr.interacting_layer(xr, W, b, g, be, L, H, res)
     yr.backward(torch.from_numpy(dy).double())
-    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dx")
-    assert_close(_np(il.kernel.grad), W.grad.numpy(), 1e-4, 1e-4, what="dW")
-    assert_close(_np(il.bias.grad), b.grad.numpy(), 1e-4, 1e-4, what="db")
-    assert_close(_np(il.gamma.grad), g.grad.numpy(), 1e-4, 1e-4, what="dgamma")
-    assert_close(_np(il.beta.grad), be.grad.numpy(), 1e-4, 1e-4, what="dbeta")
+    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dx")
+    assert_grad_close(_np(il.kernel.grad), W.grad.numpy(), what="dW")
+    assert_grad_close(_np(il.bias.grad), b.grad.numpy(), what="db")
+    assert_grad_close(_np(il.gamma.grad), g.grad.numpy(), what="dgamma")
+    assert_grad_close(_np(il.beta.grad), be.grad.numpy(), what="dbeta")
 
 
 def test_interacting_dropout_mask_matches_oracle():
@@ -189,8 +196,8 @@ def test_interacting_dropout_mask_matches_oracle():
     Wt, bt, gt, bet = (torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il))
     xr = torch.from_numpy(x).double().requires_grad_(True)
     tr.interacting_layer(xr, Wt, bt, gt, bet, L, H, True, drop_rate=0.2, seed=seed).sum().backward()
-    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dropout dx")
-    assert_close(_np(il.kernel.grad), Wt.grad.numpy(), 1e-4, 1e-4, what="dropout dW")
+    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dropout dx")
+    assert_grad_close(_np(il.kernel.grad), Wt.grad.numpy(), what="dropout dW")
 
 
 def test_interacting_rank_error():
@@ -224,9 +231,9 @@ def test_dense_fwd_bwd(act, shape):
     yr = tr.dense(xr, W, b, act)
     yr.backward(torch.from_numpy(dy).double())
     assert_close(_np(y), yr.detach().numpy(), 1e-5, 1e-5, what="dense fwd")
-    assert_close(_np(xd.grad), xr.grad.numpy(), 1e-4, 1e-4, what="dense dx")
-    assert_close(_np(layer.kernel.grad), W.grad.numpy(), 1e-4, 1e-4, what="dense dW")
-    assert_close(_np(layer.bias.grad), b.grad.numpy(), 1e-4, 1e-4, what="dense db")
+    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dense dx")
+    assert_grad_close(_np(layer.kernel.grad), W.grad.numpy(), what="dense dW")
+    assert_grad_close(_np(layer.bias.grad), b.grad.numpy(), what="dense db")
 
 
 def test_bce_clip_loss():
