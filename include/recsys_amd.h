@@ -43,6 +43,18 @@ int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32_t* off
                             int combiner, const float* table, int64_t table_rows, int dim,
                             float* out, int64_t out_ld, int64_t out_fstride, int32_t* rows_out);
 
+/* H1 sequence lookup: embedding_column(combiner=None, seq_max_len) -> (emb3d, mask)
+ * (staytime/VideoDnn.py:217-244, consumed at :58-68; the DIN keys of din.py at config 4).
+ * Sample b's ids are ids[offsets[b] .. offsets[b+1]) (offsets [B+1]); the first T are looked up
+ * (row = row_base + H(id) % bucket), out[b*out_ss + t*out_rs + e]; positions t >= n_b are zero,
+ * mask[b*mask_ld + t] = (t < n_b), lengths[b] = min(n_b, T), rows_out[b*T + t] = row or -1
+ * (all three nullable).  The sparse push skips rows < 0. */
+int rs_sequence_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offsets, int64_t B,
+                           int T, int64_t row_base, int64_t bucket, int hash_mode,
+                           const float* table, int dim, float* out, int64_t out_ss,
+                           int64_t out_rs, uint8_t* mask, int64_t mask_ld, int32_t* lengths,
+                           int32_t* rows_out);
+
 /* Sparse gradient push (the backward half of EmbeddingFeatures; tensornet pushes per-feature
  * gradients to its PS): grad_table[rows[k]] += scale(s) * dout[s] for every id k of segment s.
  * Rows touched for the first time this step are claimed (flag -1 -> -2) and appended to
@@ -100,6 +112,39 @@ int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
               const float* gamma, const float* beta, float eps, int use_res, float drop_rate,
               uint64_t seed, float* dx, int dx_accumulate, float* dparams,
               int dparams_accumulate, float* workspace, int64_t workspace_floats);
+
+/* ---------------------------------------------------------------------------------------
+ * H6/H7  DIN behaviour-sequence attention pooling.
+ *   variant 0: din.py:18-47 (DIN(**kwargs)(queries, keys, values, seq_length)):
+ *              s_t = relu(relu([q, k_t, q*k_t] W1 + b1) W2 + b2), masked to 0, out = sum s_t v_t
+ *   variant 1: staytime/layer.py:16-41 (DIN(**kwargs)(query, facts, mask)):
+ *              z_t = sigmoid([q, f_t, q-f_t, q*f_t] W1 + b1) W2 + b2, masked -> -2**32+1,
+ *              p = softmax_t(z), out = sum p_t f_t (values must be the keys tensor)
+ * q [B, H] (row stride q_ld); keys / values [B, T, H] with sample stride *_ss and row stride
+ * *_rs (floats; last dim contiguous, 16-byte aligned rows).  W1 [3H|4H, 16], b1 [16],
+ * W2 [16, 1], b2 [1] (Keras Dense kernels).  Position t of sample b is on iff
+ * (lengths == NULL || t < lengths[b]) && (mask == NULL || mask[b*mask_ld + t]).
+ * H = 16 is the compiled width (configs 4, 5).  probs [B, T] (variant 1, nullable in inference)
+ * receives the softmax for the backward.
+ * ------------------------------------------------------------------------------------- */
+int rs_din_param_count(int variant, int H);
+int rs_din_fwd(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
+               int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
+               int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
+               int64_t mask_ld, const float* W1, const float* b1, const float* W2,
+               const float* b2, float* out, int64_t out_ld, float* probs);
+/* Backward: dq [B, H] (row stride dq_ld) written; dkeys / dvalues [B, T, H] contiguous written
+ * (nullable; dkeys == dvalues writes their sum, always the case for variant 1); dparams =
+ * [dW1 | db1 | dW2 | db2] written or accumulated (nullable).  workspace >=
+ * rs_din_bwd_workspace_floats(variant, B, T, H) floats (required). */
+int64_t rs_din_bwd_workspace_floats(int variant, int64_t B, int T, int H);
+int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
+               int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
+               int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
+               int64_t mask_ld, const float* W1, const float* b1, const float* W2,
+               const float* b2, const float* probs, const float* dout, int64_t dout_ld,
+               float* dq, int64_t dq_ld, float* dkeys, float* dvalues, float* dparams,
+               int dparams_accumulate, float* workspace, int64_t workspace_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H4/H5/H8/H9  Keras Dense(units, activation) towers (autoint:36-52 MultiLayerDense,

@@ -252,3 +252,90 @@ def adam_sparse(w, g, m, v, lr, b1=0.9, b2=0.999, eps=1e-8):
 def adagrad_sparse(w, g, g2, lr):
     g2 = g2 + g * g
     return w - lr * g / np.sqrt(g2), g2
+
+
+# ------------------------------------------------------------------------------------------
+# H1 sequence lookup (tn embedding_column(combiner=None, seq_max_len) -> (emb3d, mask);
+# staytime/VideoDnn.py:217-244, consumed at :58-68).  Pinned: the first seq_max_len ids of a
+# sample are kept, positions past the sample's length are zero rows with mask False.
+# ------------------------------------------------------------------------------------------
+def sequence_lookup(ids, offsets, B, T, row_base, bucket, table, mode="mod"):
+    """ids [nnz] int64, offsets [B+1]; returns (emb [B, T, dim], mask [B, T] bool,
+    rows [B, T] int64 with -1 at padded positions)."""
+    table = np.asarray(table)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    ids = np.asarray(ids, dtype=np.int64).reshape(-1)
+    emb = np.zeros((B, T, table.shape[1]), dtype=table.dtype)
+    mask = np.zeros((B, T), dtype=bool)
+    rows = np.full((B, T), -1, dtype=np.int64)
+    for b in range(B):
+        n = min(int(offsets[b + 1] - offsets[b]), T)
+        if n == 0:
+            continue
+        r = hash_rows(ids[offsets[b]:offsets[b] + n], np.zeros(n, dtype=np.int64), [row_base],
+                      [bucket], mode)
+        rows[b, :n] = r
+        emb[b, :n] = table[r]
+        mask[b, :n] = True
+    return emb, mask, rows
+
+
+# ------------------------------------------------------------------------------------------
+# H6 DIN (din.py:18-47): ReLU-MLP scores, masked to zero, no softmax, weighted sum of values.
+# ------------------------------------------------------------------------------------------
+def sequence_mask(lengths, maxlen=None):
+    """tf.sequence_mask: maxlen defaults to max(lengths) (din.py:24)."""
+    lengths = np.asarray(lengths)
+    if maxlen is None:
+        maxlen = int(lengths.max()) if lengths.size else 0
+    return np.arange(maxlen)[None, :] < lengths[:, None]
+
+
+def din_pool(queries, keys, values, seq_length, W1, b1, W2, b2):
+    """queries [B, H], keys/values [B, T, H], seq_length [B] (None = no mask); W1 [3H, 16],
+    b1 [16], W2 [16, 1], b2 [1] (din_nn_0 / din_nn_1, both relu, din.py:12-15)."""
+    q = np.expand_dims(queries, axis=1)                                   # :19  [B, 1, H]
+    from_len, to_len = q.shape[1], keys.shape[1]                          # :21-22
+    q = np.expand_dims(q, axis=2)                                         # :26  [B, 1, 1, H]
+    k = np.expand_dims(keys, axis=1)                                      # :27  [B, 1, T, H]
+    q = np.tile(q, [1, 1, to_len, 1])                                     # :28
+    k = np.tile(k, [1, from_len, 1, 1])                                   # :29
+    deep = np.concatenate([q, k, q * k], axis=-1)                         # :31  [B, 1, T, 3H]
+    deep = dense(deep, W1, b1, "relu")                                    # :33-34
+    deep = dense(deep, W2, b2, "relu")
+    deep = np.squeeze(deep, axis=-1)                                      # :37  [B, 1, T]
+    if seq_length is not None:
+        masks = sequence_mask(seq_length, to_len)                         # :24 (maxlen = T)
+        masks = np.tile(np.expand_dims(masks, 1), [1, from_len, 1])       # :40-41
+        deep = np.where(masks, deep, np.zeros_like(deep))                 # :42
+    out = np.matmul(deep, values)                                         # :44  [B, 1, H]
+    return np.squeeze(out, 1)                                             # :45
+
+
+# ------------------------------------------------------------------------------------------
+# H7 staytime DIN (staytime/layer.py:16-41): [q, f, q-f, q*f] -> Dense(16, sigmoid) ->
+# Dense(1) -> masked (-2**32+1) softmax over T -> weighted sum of facts.
+# ------------------------------------------------------------------------------------------
+DIN_PAD = -2.0 ** 32 + 1
+
+
+def din_softmax_pool(query, facts, mask, W1, b1, W2, b2, return_probs=False):
+    """query [B, H], facts [B, T, H], mask [B, >=T] bool (None = no mask); W1 [4H, 16], b1 [16],
+    W2 [16, 1], b2 [1]."""
+    B, T, H = facts.shape
+    dt = facts.dtype.type
+    queries = np.tile(query, [1, T]).reshape(facts.shape)                 # :20-21
+    din_all = np.concatenate([queries, facts, queries - facts, queries * facts], axis=-1)  # :22-23
+    d1 = dense(din_all, W1, b1, "sigmoid")                                # :24
+    d2 = dense(d1, W2, b2, None)                                          # :25
+    scores = d2.reshape(-1, 1, T)                                         # :26-27
+    if mask is not None:
+        key_masks = np.expand_dims(np.asarray(mask)[:, :T], 1)            # :30-31
+        paddings = np.ones_like(scores) * dt(DIN_PAD)                     # :32
+        scores = np.where(key_masks, scores, paddings)                    # :34
+    probs = softmax(scores)                                               # :35
+    out = np.matmul(probs, facts)                                         # :36
+    out = np.squeeze(out, 1)                                              # :40
+    if return_probs:
+        return out, probs[:, 0, :]
+    return out

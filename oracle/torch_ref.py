@@ -147,3 +147,30 @@ class AutoIntCPU:
             self.v_tab[uniq] = v
             self.table[uniq] -= self.lr_sparse * m / (eps + v.sqrt())
         return float(loss)
+
+
+def din_pool(queries, keys, values, seq_length, W1, b1, W2, b2):
+    """din.py:18-47 op for op (tile + concat + two relu Dense + where + matmul)."""
+    T = keys.shape[1]
+    q = queries[:, None, None, :].expand(-1, 1, T, -1)
+    k = keys[:, None, :, :]
+    deep = torch.cat([q, k, q * k], dim=-1)
+    deep = dense(deep, W1, b1, "relu")
+    deep = dense(deep, W2, b2, "relu").squeeze(-1)              # [B, 1, T]
+    if seq_length is not None:
+        m = (torch.arange(T)[None, :] < torch.as_tensor(seq_length)[:, None])[:, None, :]
+        deep = torch.where(m, deep, torch.zeros_like(deep))
+    return torch.matmul(deep, values).squeeze(1)
+
+
+def din_softmax_pool(query, facts, mask, W1, b1, W2, b2):
+    """staytime/layer.py:16-41 op for op."""
+    B, T, H = facts.shape
+    q = query[:, None, :].expand(-1, T, -1)
+    din_all = torch.cat([q, facts, q - facts, q * facts], dim=-1)
+    d2 = dense(dense(din_all, W1, b1, "sigmoid"), W2, b2, None)
+    scores = d2.reshape(-1, 1, T)
+    if mask is not None:
+        km = torch.as_tensor(mask)[:, :T][:, None, :]
+        scores = torch.where(km, scores, torch.full_like(scores, npo.DIN_PAD))
+    return torch.matmul(torch.softmax(scores, dim=-1), facts).squeeze(1)

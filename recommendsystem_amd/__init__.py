@@ -4,7 +4,9 @@ MLP towers behind the reference's layer/model signatures.  See DESIGN.md.
 
 All compute runs in librecsys_amd.so (C ABI: include/recsys_amd.h); there is no CPU fallback.
 """
-from .embedding import EmbeddingFeatures, SparseAdaGrad, SparseAdam, SparseTable  # noqa: F401
+from .embedding import (EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam,  # noqa: F401
+                        SparseTable)
+from .din import DIN, StaytimeDIN  # noqa: F401
 from .layers import Dense, InteractingLayer, MultiLayerDense  # noqa: F401
 from .autoint import AutoInt, AutoIntConfig, AutoIntTrainer, cross_entropy  # noqa: F401
 

@@ -27,6 +27,8 @@ _vp, _i32, _i64, _f32, _u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, cty
 SIGNATURES: dict[str, tuple] = {
     "rs_embedding_lookup_fwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _i32, _vp, _i64,
                                        _i32, _vp, _i64, _i64, _vp]),
+    "rs_sequence_lookup_fwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _i64, _i64, _i32, _vp, _i32, _vp,
+                                      _i64, _i64, _vp, _i64, _vp, _vp]),
     "rs_sparse_grad_accumulate": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32,
                                          _vp, _vp, _vp, _vp, _i32]),
     "rs_sparse_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32, _f32,
@@ -49,6 +51,13 @@ SIGNATURES: dict[str, tuple] = {
     "rs_bce_clip_loss": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _vp, _vp, _vp]),
     "rs_dense_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
                              _i32]),
+    "rs_din_param_count": (_i32, [_i32, _i32]),
+    "rs_din_bwd_workspace_floats": (_i64, [_i32, _i64, _i32, _i32]),
+    "rs_din_fwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32, _i32,
+                          _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "rs_din_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32, _i32,
+                          _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
+                          _vp, _i32, _vp, _i64]),
 }
 
 _LIB = None

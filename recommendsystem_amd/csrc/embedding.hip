@@ -111,6 +111,80 @@ RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sequence lookup (embedding_column(combiner=None, seq_max_len) -> (emb3d, mask);
+// staytime/VideoDnn.py:217-244, consumed at :58-68; the DIN keys of din.py at config 4).
+// Sample b's ids are ids[offsets[b] .. offsets[b+1]); the first T are looked up (pinned), the
+// rest of the [T, dim] block is zero, mask[b, t] = t < n_b, rows_out = -1 on padding so the
+// sparse push (rows < 0 skipped) needs no separate path.  One G-lane group per position.
+// ---------------------------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(256) seq_lookup_fwd_kernel(
+    const int64_t* __restrict__ ids, const int32_t* __restrict__ offsets, int64_t B, int T,
+    int64_t row_base, int64_t bucket, int hash_mode, const float* __restrict__ table, int dim,
+    float* __restrict__ out, int64_t out_ss, int64_t out_rs, uint8_t* __restrict__ mask,
+    int64_t mask_ld, int32_t* __restrict__ lengths, int32_t* __restrict__ rows_out) {
+  const int groups_per_block = blockDim.x / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int nvec = dim >> 2;
+  const int64_t npos = B * (int64_t)T;
+  for (int64_t p = (int64_t)blockIdx.x * groups_per_block + g; p < npos;
+       p += (int64_t)gridDim.x * groups_per_block) {
+    const int64_t b = p / T;
+    const int t = (int)(p - b * T);
+    const int64_t beg = offsets[b];
+    int64_t n = offsets[b + 1] - beg;
+    if (n > T) n = T;
+    const bool on = t < n;
+    int64_t row = -1;
+    if (on) row = hash_row(ids[beg + t], row_base, bucket, hash_mode);
+    float* dst = out + b * out_ss + (int64_t)t * out_rs;
+    for (int v = l; v < nvec; v += G) {
+      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (on) val = reinterpret_cast<const float4*>(table + row * dim)[v];
+      reinterpret_cast<float4*>(dst)[v] = val;
+    }
+    if (l == 0) {
+      if (rows_out) rows_out[p] = (int32_t)row;
+      if (mask) mask[b * mask_ld + t] = on ? 1 : 0;
+      if (lengths && t == 0) lengths[b] = (int32_t)n;
+    }
+  }
+}
+
+RS_API int rs_sequence_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offsets,
+                                  int64_t B, int T, int64_t row_base, int64_t bucket,
+                                  int hash_mode, const float* table, int dim, float* out,
+                                  int64_t out_ss, int64_t out_rs, uint8_t* mask, int64_t mask_ld,
+                                  int32_t* lengths, int32_t* rows_out) {
+  if (!offsets || !table || !out || B < 0 || T <= 0 || dim <= 0 || bucket <= 0) return RS_ERR_ARG;
+  if (dim % 4 != 0 || out_ss % 4 != 0 || out_rs % 4 != 0) return RS_ERR_ARG;
+  const int64_t npos = B * (int64_t)T;
+  if (npos == 0) return RS_OK;
+  const int nvec = dim / 4;
+  int G = 1;
+  while (G < nvec && G < 64) G <<= 1;
+  const int block = 256;
+  int64_t grid = (npos * G + block - 1) / block;
+  if (grid > 8192) grid = 8192;
+  hipStream_t s = rs_stream(stream);
+#define RS_LAUNCH_SEQ(GG)                                                                         \
+  case GG:                                                                                        \
+    seq_lookup_fwd_kernel<GG><<<(int)grid, block, 0, s>>>(ids, offsets, B, T, row_base, bucket,   \
+                                                          hash_mode, table, dim, out, out_ss,     \
+                                                          out_rs, mask, mask_ld, lengths,         \
+                                                          rows_out);                              \
+    break;
+  switch (G) {
+    RS_LAUNCH_SEQ(1) RS_LAUNCH_SEQ(2) RS_LAUNCH_SEQ(4) RS_LAUNCH_SEQ(8) RS_LAUNCH_SEQ(16)
+    RS_LAUNCH_SEQ(32) RS_LAUNCH_SEQ(64)
+    default: return RS_ERR_UNSUPPORTED;
+  }
+#undef RS_LAUNCH_SEQ
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Sparse gradient accumulation (the "push" half of EmbeddingFeatures): every occurrence k of
 // segment s adds scale(s) * dout[s] into grad_table[rows[k]].
 //
@@ -161,6 +235,7 @@ __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
     const float* src = dout + b * dout_ld + (int64_t)f * dout_fstride;
     for (int64_t k = beg; k < end; ++k) {
       const int32_t row = rows[k];
+      if (row < 0) continue;  // padded sequence position (rs_sequence_lookup_fwd)
       int slot = -1;
       if (l == 0) {
         int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));

@@ -180,3 +180,59 @@ class EmbeddingFeatures(nn.Module):
         if offsets is not None:
             offsets = offsets.to(torch.int32).contiguous()
         return _LookupFn.apply(self.table.anchor, ids, offsets, self, out)
+
+
+class _SeqLookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, ids, offsets, layer):
+        t = layer.table
+        B, T = offsets.numel() - 1, layer.seq_max_len
+        dev = ids.device
+        out = torch.empty(B, T, t.dim, device=dev, dtype=torch.float32)
+        mask = torch.empty(B, T, device=dev, dtype=torch.uint8)
+        rows = torch.empty(B * T, device=dev, dtype=torch.int32)
+        call("rs_sequence_lookup_fwd", stream_handle(), ptr(ids), ptr(offsets), B, T,
+             layer.row_base, layer.bucket, layer.hash_mode, ptr(t.weight), t.dim, ptr(out), T * t.dim,
+             t.dim, ptr(mask), T, None, ptr(rows))
+        ctx.layer, ctx.B = layer, B
+        ctx.save_for_backward(rows)
+        ctx.mark_non_differentiable(mask)
+        return out, mask.view(torch.bool)
+
+    @staticmethod
+    def backward(ctx, dout, _dmask):
+        (rows,) = ctx.saved_tensors
+        layer = ctx.layer
+        T, dim = layer.seq_max_len, layer.table.dim
+        layer.table.accumulate(rows, None, ctx.B, T, dout.contiguous(), T * dim, dim, COMBINERS["sum"])
+        return None, None, None, None
+
+
+class SequenceEmbedding(nn.Module):
+    """embedding_column(categorical_column, dimension, combiner=None, seq_max_len) of
+    tn.layers.EmbeddingFeatures (staytime/VideoDnn.py:217-244): a VarLen id list per sample ->
+    (emb [B, seq_max_len, dim], mask [B, seq_max_len] bool).  Pinned: the first seq_max_len ids
+    are kept; padding rows are zero and receive no gradient.  Input: ids int64 [nnz] +
+    offsets int32 [B + 1], or a dense [B, n] id matrix (every row full)."""
+
+    def __init__(self, table: SparseTable, bucket: int, seq_max_len: int, row_base: int = 0,
+                 hash_mode: str = "mod"):
+        super().__init__()
+        if row_base < 0 or bucket <= 0 or row_base + bucket > table.rows:
+            raise ValueError(f"rows [{row_base}, {row_base + bucket}) outside the table")
+        self.table = table
+        self.bucket, self.row_base = int(bucket), int(row_base)
+        self.seq_max_len = int(seq_max_len)
+        self.hash_mode = HASH_MODES[hash_mode]
+
+    def forward(self, ids: torch.Tensor, offsets: torch.Tensor | None = None):
+        _lib.require_device(ids)
+        if ids.dtype != torch.int64:
+            raise TypeError("ids must be int64")
+        if offsets is None:
+            if ids.dim() != 2:
+                raise ValueError("ids must be [B, n] when no offsets are given")
+            B, n = ids.shape
+            offsets = torch.arange(0, B * n + 1, n, device=ids.device, dtype=torch.int32)
+        offsets = offsets.to(device=ids.device, dtype=torch.int32).contiguous()
+        return _SeqLookupFn.apply(self.table.anchor, ids.reshape(-1).contiguous(), offsets, self)

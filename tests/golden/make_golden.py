@@ -86,6 +86,41 @@ def lookup_case(seed, B=9, F=4, dim=8, vocab=31):
                 dout=dout, grad_rows=keys, grad_vals=np.stack([g[k] for k in keys]), **out)
 
 
+def din_case(seed, variant, B=6, T=9, H=16):
+    rng = np.random.default_rng(seed)
+    q = rng.uniform(-0.5, 0.5, size=(B, H)).astype(np.float32)
+    k = rng.uniform(-0.5, 0.5, size=(B, T, H)).astype(np.float32)
+    nb = 3 if variant == 0 else 4
+    W1 = glorot(rng, nb * H, 16).astype(np.float32)
+    b1 = rng.uniform(-0.1, 0.1, size=16).astype(np.float32)
+    W2 = glorot(rng, 16, 1).astype(np.float32)
+    b2 = np.array([0.05], dtype=np.float32)
+    f64 = lambda a: a.astype(np.float64)
+    if variant == 0:
+        v = rng.uniform(-0.5, 0.5, size=(B, T, H)).astype(np.float32)
+        lens = rng.integers(0, T + 1, size=B).astype(np.int32)
+        lens[0] = T
+        out = npo.din_pool(f64(q), f64(k), f64(v), lens, f64(W1), f64(b1), f64(W2), f64(b2))
+        return dict(seed=seed, q=q, keys=k, values=v, lengths=lens, W1=W1, b1=b1, W2=W2, b2=b2, out=out)
+    mask = rng.uniform(size=(B, T)) < 0.6
+    mask[1] = False
+    out, probs = npo.din_softmax_pool(f64(q), f64(k), mask, f64(W1), f64(b1), f64(W2), f64(b2),
+                                      return_probs=True)
+    return dict(seed=seed, q=q, facts=k, mask=mask, W1=W1, b1=b1, W2=W2, b2=b2, out=out, probs=probs)
+
+
+def seq_case(seed, B=7, T=5, dim=8, vocab=23):
+    rng = np.random.default_rng(seed)
+    table = rng.normal(size=(vocab, dim)).astype(np.float32)
+    lens = rng.integers(0, T + 3, size=B)
+    offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ids = rng.integers(-(1 << 62), 1 << 62, size=int(offsets[-1]), dtype=np.int64)
+    emb, mask, rows = npo.sequence_lookup(ids, offsets, B, T, 0, vocab, table.astype(np.float64),
+                                          "splitmix")
+    return dict(seed=seed, table=table, ids=ids, offsets=offsets, T=np.int64(T), emb=emb, mask=mask,
+                rows=rows)
+
+
 def main():
     os.makedirs(HERE, exist_ok=True)
     np.savez_compressed(os.path.join(HERE, "il_config2.npz"), **il_case(101, 4, 26, 16, 16, 2, 3, True))
@@ -94,6 +129,9 @@ def main():
     np.savez_compressed(os.path.join(HERE, "il_multihead_u8.npz"), **il_case(104, 3, 19, 8, 8, 2, 1, True))
     np.savez_compressed(os.path.join(HERE, "autoint_config2.npz"), **autoint_case(105))
     np.savez_compressed(os.path.join(HERE, "lookup_ragged.npz"), **lookup_case(106))
+    np.savez_compressed(os.path.join(HERE, "din_relu_sum.npz"), **din_case(107, 0))
+    np.savez_compressed(os.path.join(HERE, "din_staytime_softmax.npz"), **din_case(108, 1))
+    np.savez_compressed(os.path.join(HERE, "sequence_lookup.npz"), **seq_case(109))
     np.savez_compressed(os.path.join(HERE, "splitmix64_kat.npz"),
                         # SplitMix64 generator seeded with 0: outputs k = mix(state + gamma) with
                         # state = k * gamma; our finaliser adds gamma itself, so the inputs are

@@ -1,0 +1,184 @@
+"""GPU parity of the H6/H7 DIN pools and the H1 sequence lookup, through the C ABI, against the
+CPU oracle (forward: numpy float64 restatement of din.py:18-47 / staytime/layer.py:16-41;
+gradients: the op-for-op torch float64 twin in oracle/torch_ref.py).  Tolerances: forward
+|err| <= 1e-5 absolute; gradients as tests/_tol.py; index work (rows, masks) bit-exact.
+Parity unpinned against TF itself (oracle/ctr_oracle.py header)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as npo
+from oracle import torch_ref as tr
+from _tol import assert_close, assert_grad_close, to_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _inputs(rng, B, T, H=16, scale=0.5):
+    q = rng.uniform(-scale, scale, size=(B, H)).astype(np.float32)
+    k = rng.uniform(-scale, scale, size=(B, T, H)).astype(np.float32)
+    v = rng.uniform(-scale, scale, size=(B, T, H)).astype(np.float32)
+    return q, k, v
+
+
+def _set_weights(layer, rng):
+    with torch.no_grad():
+        for p in (layer.W1, layer.b1, layer.W2, layer.b2):
+            p.copy_(torch.from_numpy(rng.uniform(-0.5, 0.5, size=tuple(p.shape)).astype(np.float32)))
+
+
+def _weights64(layer):
+    return [to_np(p) for p in (layer.W1, layer.b1, layer.W2, layer.b2)]
+
+
+def _twin_grads(fn, tensors, dout):
+    ts = [torch.tensor(t, dtype=torch.float64, requires_grad=True) for t in tensors]
+    out = fn(*ts)
+    out.backward(torch.tensor(dout, dtype=torch.float64))
+    return out.detach().numpy(), [t.grad.numpy() for t in ts]
+
+
+@pytest.mark.parametrize("B,T", [(37, 23), (5, 100), (64, 16), (3, 1)])
+@pytest.mark.parametrize("alias", [False, True])
+def test_din_relu_sum(B, T, alias):
+    from recommendsystem_amd import DIN
+    rng = np.random.default_rng(100 + B + T)
+    q, k, v = _inputs(rng, B, T)
+    if alias:
+        v = k
+    lens = rng.integers(0, T + 1, size=B).astype(np.int32)
+    lens[0] = T  # tf.sequence_mask maxlen = max(lengths) must equal T (din.py:24)
+    layer = DIN(seed=3)
+    layer.build((B, T, 16), device=DEV)
+    _set_weights(layer, rng)
+    # small b2 shift so some scores are relu-clipped and some are not
+    W1, b1, W2, b2 = _weights64(layer)
+    qd = torch.from_numpy(q).to(DEV).requires_grad_(True)
+    kd = torch.from_numpy(k).to(DEV).requires_grad_(True)
+    vd = kd if alias else torch.from_numpy(v).to(DEV).requires_grad_(True)
+    out = layer(qd, kd, vd, torch.from_numpy(lens).to(DEV))
+    ref = npo.din_pool(q.astype(np.float64), k.astype(np.float64), v.astype(np.float64), lens,
+                       W1, b1, W2, b2)
+    assert_close(to_np(out), ref, 1e-5, 0, "din out")
+    dout = rng.normal(size=(B, 16))
+    layer.W1.grad.zero_(); layer.b1.grad.zero_(); layer.W2.grad.zero_(); layer.b2.grad.zero_()
+    out.backward(torch.from_numpy(dout.astype(np.float32)).to(DEV))
+    if alias:
+        fn = lambda q_, k_, W1_, b1_, W2_, b2_: tr.din_pool(q_, k_, k_, lens, W1_, b1_, W2_, b2_)
+        _, g = _twin_grads(fn, [q, k, W1, b1, W2, b2], dout)
+        gq, gk, gW1, gb1, gW2, gb2 = g
+    else:
+        fn = lambda q_, k_, v_, W1_, b1_, W2_, b2_: tr.din_pool(q_, k_, v_, lens, W1_, b1_, W2_, b2_)
+        _, g = _twin_grads(fn, [q, k, v, W1, b1, W2, b2], dout)
+        gq, gk, gv, gW1, gb1, gW2, gb2 = g
+        assert_grad_close(to_np(vd.grad), gv, "dvalues")
+    assert_grad_close(to_np(qd.grad), gq, "dq")
+    assert_grad_close(to_np(kd.grad), gk, "dkeys")
+    assert_grad_close(to_np(layer.W1.grad), gW1, "dW1")
+    assert_grad_close(to_np(layer.b1.grad), gb1, "db1")
+    assert_grad_close(to_np(layer.W2.grad), gW2, "dW2")
+    assert_grad_close(to_np(layer.b2.grad), gb2, "db2")
+
+
+@pytest.mark.parametrize("B,T,wide", [(37, 23, 0), (16, 50, 3), (4, 7, 1)])
+def test_staytime_din_softmax(B, T, wide):
+    from recommendsystem_amd import StaytimeDIN
+    rng = np.random.default_rng(200 + B + T)
+    q, f, _ = _inputs(rng, B, T)
+    mask = rng.uniform(size=(B, T + wide)) < 0.7
+    mask[1, :] = False          # fully masked row -> uniform average of the facts
+    mask[2, :] = True
+    layer = StaytimeDIN(seed=4)
+    layer.build((B, T, 16), device=DEV)
+    _set_weights(layer, rng)
+    W1, b1, W2, b2 = _weights64(layer)
+    # facts as the [:, :, 0:16] slice of a 32-wide sequence lookup (staytime/VideoDnn.py:68)
+    wide_f = np.concatenate([f, rng.normal(size=f.shape).astype(np.float32)], axis=2)
+    fd_full = torch.from_numpy(wide_f).to(DEV).requires_grad_(True)
+    fd = fd_full[:, :, 0:16]
+    qd = torch.from_numpy(q).to(DEV).requires_grad_(True)
+    out = layer(qd, fd, torch.from_numpy(mask).to(DEV))
+    ref = npo.din_softmax_pool(q.astype(np.float64), f.astype(np.float64), mask, W1, b1, W2, b2)
+    assert_close(to_np(out), ref, 1e-5, 0, "staytime din out")
+    assert_close(to_np(out)[1], f[1].astype(np.float64).mean(0), 1e-5, 0, "fully masked row")
+    dout = rng.normal(size=(B, 16))
+    out.backward(torch.from_numpy(dout.astype(np.float32)).to(DEV))
+    fn = lambda q_, f_, W1_, b1_, W2_, b2_: tr.din_softmax_pool(q_, f_, torch.from_numpy(mask),
+                                                                 W1_, b1_, W2_, b2_)
+    _, (gq, gf, gW1, gb1, gW2, gb2) = _twin_grads(fn, [q, f, W1, b1, W2, b2], dout)
+    assert_grad_close(to_np(qd.grad), gq, "dq")
+    assert_grad_close(to_np(fd_full.grad)[:, :, 0:16], gf, "dfacts")
+    assert np.all(to_np(fd_full.grad)[:, :, 16:] == 0)
+    assert_grad_close(to_np(layer.W1.grad), gW1, "dW1")
+    assert_grad_close(to_np(layer.b1.grad), gb1, "db1")
+    assert_grad_close(to_np(layer.W2.grad), gW2, "dW2")
+    assert_grad_close(to_np(layer.b2.grad), gb2, "db2")
+
+
+def test_din_config4_size_properties():
+    """Config 4 shape (B=4096, T=100, H=16, lengths U{1..100} with max 100): the first 48
+    samples against the oracle, the rest through size-independent properties (a sample's output
+    does not depend on its batch neighbours; linearity of the pool in the values)."""
+    from recommendsystem_amd import DIN
+    rng = np.random.default_rng(4)
+    B, T = 4096, 100
+    q, k, v = _inputs(rng, B, T, scale=0.3)
+    lens = rng.integers(1, T + 1, size=B).astype(np.int32)
+    lens[7] = T
+    layer = DIN(seed=5)
+    layer.build((B, T, 16), device=DEV)
+    qd, kd, vd = (torch.from_numpy(a).to(DEV) for a in (q, k, v))
+    ld = torch.from_numpy(lens).to(DEV)
+    out = layer(qd, kd, vd, ld)
+    W1, b1, W2, b2 = _weights64(layer)
+    n = 48
+    ref = npo.din_pool(q[:n].astype(np.float64), k[:n].astype(np.float64), v[:n].astype(np.float64),
+                       lens[:n], W1, b1, W2, b2)
+    assert_close(to_np(out)[:n], ref, 1e-5, 0, "first samples")
+    perm = torch.randperm(B, generator=torch.Generator().manual_seed(0)).to(DEV)
+    out_p = layer(qd[perm], kd[perm], vd[perm], ld[perm])
+    assert torch.equal(out_p, out[perm])
+    out2 = layer(qd, kd, 2.0 * vd, ld)
+    assert_close(to_np(out2), 2.0 * to_np(out), 1e-5, 1e-6, "linear in values")
+
+
+@pytest.mark.parametrize("hash_mode", ["mod", "splitmix"])
+def test_sequence_lookup_and_push(hash_mode):
+    from recommendsystem_amd.embedding import SequenceEmbedding, SparseAdaGrad, SparseTable
+    rng = np.random.default_rng(9)
+    B, T, dim, vocab = 29, 12, 32, 61
+    table = SparseTable(vocab + 5, dim, optimizer=SparseAdaGrad(), device=DEV, seed=3)
+    seq = SequenceEmbedding(table, vocab, T, row_base=5, hash_mode=hash_mode)
+    lens = rng.integers(0, T + 6, size=B)  # includes empty and over-long histories
+    offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ids = rng.integers(-(1 << 50), 1 << 50, size=int(offsets[-1]), dtype=np.int64)
+    emb, mask = seq(torch.from_numpy(ids).to(DEV), torch.from_numpy(offsets).to(DEV))
+    w = table.weight.detach().cpu().numpy()
+    ref_emb, ref_mask, ref_rows = npo.sequence_lookup(ids, offsets, B, T, 5, vocab, w, hash_mode)
+    assert np.array_equal(emb.detach().cpu().numpy(), ref_emb.astype(np.float32))
+    assert np.array_equal(mask.cpu().numpy(), ref_mask)
+    dout = rng.normal(size=(B, T, dim)).astype(np.float32)
+    emb.backward(torch.from_numpy(dout).to(DEV))
+    grad = table.grad.cpu().numpy()
+    expect = np.zeros_like(w, dtype=np.float64)
+    for b in range(B):
+        for t in range(T):
+            if ref_rows[b, t] >= 0:
+                expect[ref_rows[b, t]] += dout[b, t]
+    assert_close(grad, expect, 1e-5, 1e-6, "sequence push")
+    touched = set(table.touched[: int(table.n_touched.item())].cpu().numpy().tolist())
+    assert touched == set(int(r) for r in ref_rows[ref_rows >= 0].ravel())
+    # AdaGrad step on exactly those rows (tensornet AdaGrad form, csrc/optim.hip)
+    g2_before = table.g2sum.cpu().numpy().astype(np.float64)
+    table.step()
+    rows = sorted(touched)
+    w_ref, g2_ref = npo.adagrad_sparse(w[rows].astype(np.float64), expect[rows], g2_before[rows],
+                                       table.optimizer.learning_rate)
+    assert_close(table.weight.cpu().numpy()[rows], w_ref, 1e-6, 1e-5, "adagrad rows")
+    assert_close(table.g2sum.cpu().numpy()[rows], g2_ref, 1e-5, 1e-5, "adagrad g2sum")
+    untouched = np.setdiff1d(np.arange(table.rows), rows)
+    assert np.array_equal(table.weight.cpu().numpy()[untouched], w[untouched])
+    assert int(table.n_touched.item()) == 0 and bool((table.flag == -1).all())

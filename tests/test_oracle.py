@@ -141,3 +141,83 @@ def test_adam_forms():
     assert np.allclose(p - w1, 0.1 * 0.1 * g / (1e-8 + np.sqrt(0.001 * g * g)))
     w2, g2 = npo.adagrad_sparse(p, g, np.full(2, 0.1), 0.1)
     assert np.allclose(w2, p - 0.1 * g / np.sqrt(0.1 + g * g))
+
+
+# ------------------------------------------------------------------------------------------
+# H6/H7 DIN pools and the H1 sequence lookup
+# ------------------------------------------------------------------------------------------
+def test_golden_din_pools():
+    d = gold("din_relu_sum.npz")
+    f64 = lambda k: d[k].astype(np.float64)  # noqa: E731
+    out = npo.din_pool(f64("q"), f64("keys"), f64("values"), d["lengths"], f64("W1"), f64("b1"),
+                       f64("W2"), f64("b2"))
+    assert np.array_equal(out, d["out"])
+    d = gold("din_staytime_softmax.npz")
+    f64 = lambda k: d[k].astype(np.float64)  # noqa: E731
+    out, probs = npo.din_softmax_pool(f64("q"), f64("facts"), d["mask"], f64("W1"), f64("b1"),
+                                      f64("W2"), f64("b2"), return_probs=True)
+    assert np.array_equal(out, d["out"]) and np.array_equal(probs, d["probs"])
+
+
+def test_golden_sequence_lookup():
+    d = gold("sequence_lookup.npz")
+    T = int(d["T"])
+    B = d["offsets"].size - 1
+    emb, mask, rows = npo.sequence_lookup(d["ids"], d["offsets"], B, T, 0, d["table"].shape[0],
+                                          d["table"].astype(np.float64), "splitmix")
+    assert np.array_equal(emb, d["emb"]) and np.array_equal(mask, d["mask"])
+    assert np.array_equal(rows, d["rows"])
+    lens = np.diff(d["offsets"])
+    assert np.array_equal(mask.sum(1), np.minimum(lens, T))
+
+
+def test_din_semantics():
+    """din.py: masked positions contribute nothing (their keys/values are irrelevant);
+    staytime/layer.py: a fully masked row is the uniform mean of the facts, and masked facts
+    are ignored otherwise."""
+    rng = np.random.default_rng(3)
+    B, T, H = 4, 6, 16
+    q, k, v = rng.normal(size=(B, H)), rng.normal(size=(B, T, H)), rng.normal(size=(B, T, H))
+    W1, b1 = rng.normal(size=(3 * H, 16)) * 0.3, rng.normal(size=16) * 0.1
+    W2, b2 = rng.normal(size=(16, 1)), np.array([0.1])
+    lens = np.array([6, 2, 0, 4])
+    a = npo.din_pool(q, k, v, lens, W1, b1, W2, b2)
+    k2, v2 = k.copy(), v.copy()
+    k2[1, 2:] = 99.0
+    v2[1, 2:] = -99.0
+    assert np.allclose(a, npo.din_pool(q, k2, v2, lens, W1, b1, W2, b2))
+    assert np.all(a[2] == 0)
+    W1s = rng.normal(size=(4 * H, 16)) * 0.3
+    mask = np.ones((B, T), bool)
+    mask[0] = False
+    mask[3, 4:] = False
+    o = npo.din_softmax_pool(q, k, mask, W1s, b1, W2, b2)
+    assert np.allclose(o[0], k[0].mean(0))
+    k3 = k.copy()
+    k3[3, 4:] = 5.0
+    o3 = npo.din_softmax_pool(q, k3, mask, W1s, b1, W2, b2)
+    assert np.allclose(o3[3], o[3]) and np.allclose(o3[:3], o[:3])
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_din_twin_matches_numpy_and_finite_differences(variant):
+    rng = np.random.default_rng(5 + variant)
+    B, T, H = 3, 5, 4
+    q, k, v = rng.normal(size=(B, H)), rng.normal(size=(B, T, H)), rng.normal(size=(B, T, H))
+    nb = 3 if variant == 0 else 4
+    W1, b1 = rng.normal(size=(nb * H, 16)) * 0.4, rng.normal(size=16) * 0.2 + 0.1
+    W2, b2 = rng.normal(size=(16, 1)) * 0.5, np.array([0.3])
+    lens = np.array([5, 3, 1])
+    mask = np.arange(T)[None, :] < lens[:, None]
+    if variant == 0:
+        a = npo.din_pool(q, k, v, lens, W1, b1, W2, b2)
+        fn = lambda q_, k_, v_, W1_, b1_, W2_, b2_: tr.din_pool(q_, k_, v_, lens, W1_, b1_, W2_, b2_)  # noqa: E731
+        args = [q, k, v, W1, b1, W2, b2]
+    else:
+        a = npo.din_softmax_pool(q, k, mask, W1, b1, W2, b2)
+        fn = lambda q_, k_, W1_, b1_, W2_, b2_: tr.din_softmax_pool(q_, k_, torch.from_numpy(mask),  # noqa: E731
+                                                                    W1_, b1_, W2_, b2_)
+        args = [q, k, W1, b1, W2, b2]
+    ts = [torch.tensor(x, requires_grad=True) for x in args]
+    assert np.max(np.abs(fn(*ts).detach().numpy() - a)) < 1e-12
+    assert torch.autograd.gradcheck(fn, tuple(ts), eps=1e-6, atol=1e-5)
