@@ -164,6 +164,80 @@ int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* 
                         const float* Y, int64_t ldy, int act, int64_t M, int K, int N, float* dW,
                         float* db, int accumulate, float* workspace, int64_t workspace_floats);
 
+/* ---------------------------------------------------------------------------------------
+ * H5/H8/H9  Tower ops around the Dense GEMMs (csrc/towers.hip).  act codes as rs_dense_fwd.
+ * ------------------------------------------------------------------------------------- */
+/* Gate mixture (MMOE.call rough_rank/layer.py:149-162, PLE.call :212-226,
+ * rank/multi_head/multidnn.py:95-120, staytime/VideoDnn.py:150-164):
+ *   Y[m, t*D + d] = sum_k softmax_k(G[m, t*n_sel + k]) * act(E[m, sel[t*n_sel + k]*D + d]).
+ * E holds n_exp experts of width D (pre-activation when e_act != 0), G the gate logits; both
+ * may be column ranges of ONE concatenated GEMM output.  sel: device int32 [n_task*n_sel].
+ * P [m, t*n_sel + k] (nullable) receives the gate probabilities.
+ * Backward writes dE (= dL/d(pre-activation) when e_act != 0) and dG (gate logits). */
+int rs_gate_mix_fwd(void* stream, const float* E, int64_t lde, int e_act, const float* G,
+                    int64_t ldg, int64_t M, int n_exp, int D, int n_task, int n_sel,
+                    const int32_t* sel, float* Y, int64_t ldy, float* P, int64_t ldp);
+int rs_gate_mix_bwd(void* stream, const float* E, int64_t lde, int e_act, const float* G,
+                    int64_t ldg, int64_t M, int n_exp, int D, int n_task, int n_sel,
+                    const int32_t* sel, const float* dY, int64_t lddy, float* dE, int64_t ldde,
+                    float* dG, int64_t lddg);
+/* CrossNet (rough_rank/layer.py:236-270) / DeepCrossLayer (staytime/layer.py:44-80):
+ * x_{l+1} = x0 * (x_l . W[l]) + b[l] + x_l, W, b [L, D] (L <= 4, D <= 2048).
+ * Backward: dX0 written/accumulated, dparams = [dW (L*D) | db (L*D)] (nullable). */
+int rs_cross_fwd(void* stream, const float* X0, int64_t ldx, int64_t M, int D, int L,
+                 const float* W, const float* b, float* Y, int64_t ldy);
+int64_t rs_cross_bwd_workspace_floats(int64_t M, int D, int L);
+int rs_cross_bwd(void* stream, const float* X0, int64_t ldx, int64_t M, int D, int L,
+                 const float* W, const float* b, const float* dY, int64_t lddy, float* dX0,
+                 int64_t lddx, int dx_accumulate, float* dparams, int dparams_accumulate,
+                 float* workspace, int64_t workspace_floats);
+/* FM cross term with optional per-field scale (FMLayer staytime/layer.py:83-116; SENet
+ * reweight + FM of staytime/VideoDnn.py:81-115): field f of row m at X[m*ldx + f*fsx + e];
+ * y_f = x_f * a_scale * A[m*lda + f] (A nullable; SENet's 2 * sigmoid uses a_scale 2) -> Y[m*ldy + f*E + e] (nullable);
+ * cross_e = (sum_f y_f)^2 - sum_f y_f^2 -> C (nullable); fm = 0.5 sum_e cross_e -> fm[m*ldf]. */
+int rs_fm_fwd(void* stream, const float* X, int64_t ldx, int64_t fsx, int64_t M, int F, int E,
+              const float* A, int64_t lda, float a_scale, float* Y, int64_t ldy, float* C, int64_t ldc,
+              float* fm, int64_t ldf);
+int rs_fm_bwd(void* stream, const float* X, int64_t ldx, int64_t fsx, int64_t M, int F, int E,
+              const float* A, int64_t lda, float a_scale, const float* dY, int64_t lddy, const float* dC,
+              int64_t lddc, const float* dfm, int64_t lddf, float* dX, int64_t lddx,
+              int64_t fsdx, int dx_accumulate, float* dA, int64_t ldda);
+/* ffm_block (staytime/VideoDnn.py:11-25): pair p = (i, j), i < NU user fields, j < NI item
+ * fields (field k at column cols[k] of X, user fields first, E = 16):
+ * Y[m, p*Dff + c] = (x_i Wx[p] + bx[p])_c * (y_j Wy[p] + by[p])_c; Mult (nullable, NU == NI)
+ * = relu(x_i * y_i) (:99-105).  params = [Wx (P*E*Dff) | bx (P*Dff) | Wy | by]. */
+int64_t rs_ffm_param_count(int NU, int NI, int E, int Dff);
+int rs_ffm_fwd(void* stream, const float* X, int64_t ldx, int64_t M, int NU, int NI, int E,
+               int Dff, const int32_t* cols, const float* Wx, const float* bx, const float* Wy,
+               const float* by, float* Y, int64_t ldy, float* Mult, int64_t ldm);
+int64_t rs_ffm_bwd_workspace_floats(int64_t M, int NU, int NI, int E, int Dff);
+int rs_ffm_bwd(void* stream, const float* X, int64_t ldx, int64_t M, int NU, int NI, int E,
+               int Dff, const int32_t* cols, const float* Wx, const float* bx, const float* Wy,
+               const float* by, const float* dY, int64_t lddy, const float* dMult,
+               int64_t lddm, float* dX, int64_t lddx, int dx_accumulate, float* dparams,
+               int dparams_accumulate, float* workspace, int64_t workspace_floats);
+/* ppnet gating (staytime/VideoDnn.py:135-146): Y = A * (scale * G) and its backward. */
+int rs_mul_fwd(void* stream, const float* A, int64_t lda, const float* G, int64_t ldg, int64_t M,
+               int N, float scale, float* Y, int64_t ldy);
+int rs_mul_bwd(void* stream, const float* A, int64_t lda, const float* G, int64_t ldg, int64_t M,
+               int N, float scale, const float* dY, int64_t lddy, float* dA, int64_t ldda,
+               float* dG, int64_t lddg);
+/* H9/H10 staytime head (staytime/VideoDnn.py:168-179) + custom_kl_loss (staytime/model.py:20-30):
+ * P[m, 0:C] = softmax(Z[m]), P[m, C] = max(P . bins, 0) (P, bins nullable); with y_true:
+ * loss_rows[m] = w_m * sum_c yt log(yt / yp) (yt, yp clipped to [eps, 1]) and
+ * dZ = gscale * w_m * dKL/dZ (through the clip and the softmax). */
+int rs_softmax_kl(void* stream, const float* Z, int64_t ldz, int64_t M, int C, const float* bins,
+                  float* P, int64_t ldp, const float* y_true, int64_t ldt, const float* sample_w,
+                  float gscale, float eps, float* loss_rows, float* dZ, int64_t lddz);
+/* Similarity (rough_rank/layer.py:6-30): Y[m] = [sigmoid](U[m] . V[m]); with dY: dU, dV. */
+int rs_rowdot(void* stream, const float* U, int64_t ldu, const float* V, int64_t ldv, int64_t M,
+              int N, int use_sigmoid, float* Y, const float* dY, float* dU, int64_t lddu,
+              float* dV, int64_t lddv);
+/* KDLoss (rough_rank/layer.py:272-279): loss_rows[m] = mean_j (S - T)^2,
+ * dS = gscale * 2 (S - T) / N (nullable). */
+int rs_mse_rows(void* stream, const float* S, int64_t lds, const float* T, int64_t ldt, int64_t M,
+                int N, float gscale, float* loss_rows, float* dS, int64_t ldds);
+
 /* H4/H10  tf.clip_by_value(s, lo, hi) (autoint:52) + cross_entropy (rank/ctr/base_model.py:7-12):
  * loss[0] = mean_b sum_t [-y log(p+log_eps) - (1-y) log(1-p+log_eps)], p_out = clipped s,
  * ds = gscale[0] * dloss/ds (zero outside [lo, hi]; gscale NULL = 1).  Any output pointer

@@ -174,3 +174,168 @@ def din_softmax_pool(query, facts, mask, W1, b1, W2, b2):
         km = torch.as_tensor(mask)[:, :T][:, None, :]
         scores = torch.where(km, scores, torch.full_like(scores, npo.DIN_PAD))
     return torch.matmul(torch.softmax(scores, dim=-1), facts).squeeze(1)
+
+
+# ==========================================================================================
+# H8 rough_rank layers (rough_rank/layer.py), H9 staytime towers (staytime/VideoDnn.py,
+# staytime/layer.py), H5 multi_head gates (rank/multi_head/multidnn.py), H10 losses.
+# Written op for op with torch CPU ops (float64 in the tests); weights are passed in.
+# ==========================================================================================
+def _act(x, activation):
+    if activation in (None, "linear"):
+        return x
+    if activation == "relu":
+        return torch.relu(x)
+    if activation == "sigmoid":
+        return torch.sigmoid(x)
+    if activation == "softmax":
+        return torch.softmax(x, dim=-1)
+    raise ValueError(activation)
+
+
+def dnn(x, kernels, biases, activation="relu", output_activation=None):
+    """DNN.call (rough_rank/layer.py:99-107): tensordot + bias_add + Activation per layer; the
+    last layer uses output_activation when given (:86-91).  No BN / dropout (the call sites use
+    use_bn=False, dropout_rate=0)."""
+    n = len(kernels)
+    for i, (W, b) in enumerate(zip(kernels, biases)):
+        x = torch.tensordot(x, W, dims=([x.dim() - 1], [0])) + b
+        act = output_activation if (output_activation and i == n - 1) else activation
+        x = _act(x, act)
+    return x
+
+
+def mmoe(x, experts, gates, expert_activation="relu"):
+    """MMOE.call (rough_rank/layer.py:149-162): experts = [(kernels, biases)] DNNs, gates = DNNs
+    with softmax output; task_out = sum_e gate_e * expert_e."""
+    eo = torch.stack([dnn(x, k, b, expert_activation) for k, b in experts], dim=-2)   # :150-151
+    outs = []
+    for k, b in gates:
+        g = dnn(x, k, b, "relu", "softmax").unsqueeze(-1)                          # :154-155
+        outs.append(torch.sum(eo * g, dim=-2))                                       # :158
+    return outs
+
+
+def ple(x, shared, specific, gates, expert_activation="relu"):
+    """PLE.call (rough_rank/layer.py:212-226)."""
+    so = [dnn(x, k, b, expert_activation) for k, b in shared]                     # :213
+    outs = []
+    for t, (gk, gb) in enumerate(gates):
+        sp = [dnn(x, k, b, expert_activation) for k, b in specific[t]]            # :216
+        eo = torch.stack(so + sp, dim=-2)                                           # :217-218
+        g = dnn(x, gk, gb, "relu", "softmax").unsqueeze(-1)                        # :219,222
+        outs.append(torch.sum(eo * g, dim=-2))                                      # :223
+    return outs
+
+
+def crossnet(x, kernels, biases):
+    """CrossNet.call (rough_rank/layer.py:252-260): kernels [D, 1], biases [D, 1]."""
+    x0 = x.unsqueeze(2)
+    xl = x0
+    for W, b in zip(kernels, biases):
+        xw = torch.tensordot(xl, W, dims=([1], [0]))     # [B, 1, 1]
+        dot_ = torch.matmul(x0, xw)                      # [B, D, 1]
+        xl = dot_ + b + xl
+    return xl.squeeze(2)
+
+
+def deep_cross_layer(x, Ws, bs):
+    """DeepCrossLayer.call (staytime/layer.py:65-71): W_i [D, 1], b_i [D]."""
+    cross = None
+    for i, (W, b) in enumerate(zip(Ws, bs)):
+        if i == 0:
+            cross = x * torch.matmul(x, W) + b + x
+        else:
+            cross = x * torch.matmul(cross, W) + b + cross
+    return cross
+
+
+def kd_loss(student, teacher):
+    """KDLoss (rough_rank/layer.py:272-279): MeanSquaredError(reduction=NONE)(teacher, student)
+    = mean over the last axis of (teacher - student)^2."""
+    return torch.mean(torch.square(teacher - student), dim=-1)
+
+
+def similarity(u, i, use_sigmoid=False):
+    """Similarity.call (rough_rank/layer.py:19-24)."""
+    out = torch.sum(u * i, dim=-1, keepdim=True)
+    return torch.sigmoid(out) if use_sigmoid else out
+
+
+def fm_layer(x):
+    """FMLayer.call (staytime/layer.py:99-112): x [B, F, E] -> [B, 1]."""
+    square_of_sum = torch.square(torch.sum(x, dim=1, keepdim=True))
+    sum_of_square = torch.sum(x * x, dim=1, keepdim=True)
+    cross_term = square_of_sum - sum_of_square
+    return 0.5 * torch.sum(cross_term, dim=-1)
+
+
+def senet_fm(general, W1, b1, W2, b2):
+    """staytime/VideoDnn.py:81-115: SENet on the stop-gradient concat of the general inputs
+    (Dense(len/4 -> int, relu), 2 * Dense(len, sigmoid)), per-field reweight, then the FM cross
+    term (vector) and fm_logit.  general: list of [B, E].  Returns (reweighted list, cross, fm)."""
+    n = len(general)
+    sq = torch.cat(general, dim=-1).detach()                                        # :84-86
+    s1 = torch.relu(sq @ W1 + b1)                                                   # :87-88
+    s2 = 2 * torch.sigmoid(s1 @ W2 + b2)                                            # :90-91
+    splits = torch.split(s2, 1, dim=1)                                              # :93
+    rew = [g * s for g, s in zip(general, splits)]                                  # :95-96
+    sum_embs = torch.sum(torch.stack(rew), dim=0)                                   # :108
+    cross = sum_embs * sum_embs - torch.sum(torch.stack([r * r for r in rew]), dim=0)  # :109-112
+    fm = 0.5 * torch.sum(cross, dim=-1, keepdim=True)                               # :114
+    assert n == len(rew)
+    return rew, cross, fm
+
+
+def ffm_block(user, item, Wx, bx, Wy, by):
+    """ffm_block (staytime/VideoDnn.py:11-25) for one [x_list, y_list, dim] group: pair p =
+    (i, j) over user x item fields, Dense(dim)(x_i) * Dense(dim)(y_j), concatenated in p order.
+    Wx [P, E, dim], bx [P, dim] (same for y)."""
+    out, p = [], 0
+    for x in user:
+        for y in item:
+            out.append((x @ Wx[p] + bx[p]) * (y @ Wy[p] + by[p]))
+            p += 1
+    return torch.cat(out, dim=-1)
+
+
+def multiply_relu(user, item):
+    """staytime/VideoDnn.py:99-105: ReLU(concat(user) * concat(item))."""
+    return torch.relu(torch.cat(user, dim=-1) * torch.cat(item, dim=-1))
+
+
+def staytime_head(x, W, b, bins):
+    """staytime/VideoDnn.py:168-179: softmax(Dense(400)(x)), expected bins clamped at 0,
+    concatenated -> [B, 401]."""
+    p = torch.softmax(x @ W + b, dim=-1)
+    pred = p @ torch.as_tensor(bins, dtype=p.dtype).reshape(-1, 1)
+    pred = torch.where(pred < 0.0, torch.zeros_like(pred), pred)
+    return torch.cat([p, pred], dim=-1)
+
+
+def custom_kl_loss(y_true, y_pred, C=400, eps=1e-7):
+    """staytime/model.py:20-30 (K.epsilon() = 1e-7): per-sample KL over the first C columns."""
+    yt = torch.clamp(y_true[:, :C].to(y_pred.dtype), eps, 1.0)
+    yp = torch.clamp(y_pred[:, :C], eps, 1.0)
+    return torch.sum(yt * torch.log(yt / yp), dim=-1)
+
+
+def keras_bce(y_true, y_pred, eps=1e-7):
+    """tf.keras.losses.BinaryCrossentropy() (rough_rank/model.py:211-212): clip to
+    [eps, 1-eps], -(y log(p+eps) + (1-y) log(1-p+eps)), mean over the last axis, then over the
+    batch."""
+    p = torch.clamp(y_pred, eps, 1.0 - eps)
+    bce = y_true * torch.log(p + eps) + (1 - y_true) * torch.log(1 - p + eps)
+    return torch.mean(torch.mean(-bce, dim=-1))
+
+
+def multi_head_gates(result, We, be, Wg, bg, n_used=7):
+    """rank/multi_head/multidnn.py:77-120: 8 experts Dense(32, relu), only the first n_used
+    stacked; n_tasks gates Dense(n_used, softmax); task t = sum_e gate_te * expert_e.
+    We [8][K, 32], Wg [T][K, n_used]."""
+    eo = torch.stack([torch.relu(result @ W + b) for W, b in zip(We, be)][:n_used], dim=1)  # :82-92
+    outs = []
+    for W, b in zip(Wg, bg):
+        g = torch.softmax(result @ W + b, dim=-1).unsqueeze(-1)                     # :100-107
+        outs.append(torch.sum(eo * g, dim=1))                                        # :109-112
+    return outs

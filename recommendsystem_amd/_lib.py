@@ -58,6 +58,32 @@ SIGNATURES: dict[str, tuple] = {
     "rs_din_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32, _i32,
                           _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                           _vp, _i32, _vp, _i64]),
+    "rs_gate_mix_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
+                               _vp, _i64, _vp, _i64]),
+    "rs_gate_mix_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
+                               _vp, _i64, _vp, _i64, _vp, _i64]),
+    "rs_cross_bwd_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_cross_fwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64]),
+    "rs_cross_bwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64, _vp, _i64, _i32,
+                            _vp, _i32, _vp, _i64]),
+    "rs_fm_fwd": (_i32, [_vp, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _f32, _vp, _i64, _vp,
+                         _i64, _vp, _i64]),
+    "rs_fm_bwd": (_i32, [_vp, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _i64, _f32, _vp, _i64, _vp, _i64,
+                         _vp, _i64, _vp, _i64, _i64, _i32, _vp, _i64]),
+    "rs_ffm_param_count": (_i64, [_i32, _i32, _i32, _i32]),
+    "rs_ffm_bwd_workspace_floats": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "rs_ffm_fwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _i64, _vp, _i64]),
+    "rs_ffm_bwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i32, _vp, _i64]),
+    "rs_mul_fwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _i64]),
+    "rs_mul_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _i64, _vp, _i64, _vp,
+                          _i64]),
+    "rs_softmax_kl": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp, _f32, _f32,
+                             _vp, _vp, _i64]),
+    "rs_rowdot": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64, _vp,
+                         _i64]),
+    "rs_mse_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _i64]),
 }
 
 _LIB = None

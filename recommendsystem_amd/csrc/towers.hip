@@ -1,0 +1,1008 @@
+// H5/H8/H9/H10 — the tower-side ops around the MLP GEMMs (csrc/dense.hip), each fused into one
+// HBM pass over its rows, forward and backward:
+//
+//   gate_mix     MMOE / PLE / multi_head / staytime MMoE combine: out_t = sum_k softmax(g_t)_k *
+//                act(expert_{sel[t,k]}) (rough_rank/layer.py:155-166, 212-226;
+//                rank/multi_head/multidnn.py:95-120; staytime/VideoDnn.py:150-164).  Experts and
+//                gate logits come straight out of ONE concatenated GEMM when they share an input
+//                (all experts + all gates of a layer are one [K, sum N] Dense), so the mixture
+//                kernel is the only extra pass.
+//   cross        CrossNet (rough_rank/layer.py:236-270) == DeepCrossLayer (staytime/layer.py:44-80):
+//                x_{l+1} = x0 * (x_l . w_l) + b_l + x_l, all layers per row in registers.
+//   fm           FMLayer (staytime/layer.py:83-116, rank/finish/videodnn.py:23-52) and the SENet
+//                reweight + FM cross term of staytime/VideoDnn.py:81-115: y_f = x_f * a_f,
+//                cross = (sum_f y_f)^2 - sum_f y_f^2, fm = 0.5 * sum_e cross.
+//   ffm          ffm_block (staytime/VideoDnn.py:11-25,118-120): per (user, item) field pair,
+//                Dense(8)(x) * Dense(8)(y); plus the user x item multiply-ReLU (:99-105).
+//   mul          ppnet gating deep * (scale * gate) (staytime/VideoDnn.py:135-146).
+//   softmax_kl   400-bin staytime head softmax + expected bins (:168-179) and custom_kl_loss
+//                (staytime/model.py:20-30), fused forward + backward.
+//   rowdot       Similarity (rough_rank/layer.py:6-30); mse_rows: KDLoss (:272-279).
+//
+// All reductions over rows are per-block partials + column_reduce (fixed order, deterministic).
+#include "common.hpp"
+
+namespace rs_tw {
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2 };
+
+__device__ __forceinline__ float act_f(float z, int act) {
+  if (act == ACT_RELU) return fmaxf(z, 0.f);
+  if (act == ACT_SIGMOID) return 1.0f / (1.0f + expf(-z));
+  return z;
+}
+// d/dz given z (relu: TF ReluGrad on the output, y > 0 <=> z > 0)
+__device__ __forceinline__ float act_d(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_SIGMOID) { const float y = 1.0f / (1.0f + expf(-z)); return y * (1.f - y); }
+  return 1.f;
+}
+
+// Block-wide sum of one float per thread (256 threads = 4 waves); `red` = 8 floats of LDS,
+// double-buffered by `phase` so back-to-back reductions need one barrier each.
+__device__ __forceinline__ float block_sum256(float v, float* red, int phase) {
+  v = group_sum<64>(v);
+  float* r = red + (phase & 1) * 4;
+  if (lane_id() == 0) r[wave_id()] = v;
+  __syncthreads();
+  return (r[0] + r[1]) + (r[2] + r[3]);
+}
+
+// =============================================================================================
+// gate_mix
+// =============================================================================================
+constexpr int GM_MAXSEL = 16;
+constexpr int GM_MAXCH = 4;  // D <= 256
+
+struct GM {
+  const float* E; int64_t lde; int e_act;
+  const float* G; int64_t ldg;
+  int64_t M; int n_exp, D, n_task, n_sel;
+  const int32_t* sel;
+};
+
+template <int DP>
+__global__ void __launch_bounds__(256) gate_mix_fwd_kernel(GM a, float* __restrict__ Y, int64_t ldy,
+                                                           float* __restrict__ P, int64_t ldp) {
+  constexpr int RPB = 256 / DP;
+  __shared__ int32_t sel[GM_MAXSEL * 8];
+  for (int i = threadIdx.x; i < a.n_task * a.n_sel; i += blockDim.x) sel[i] = a.sel[i];
+  __syncthreads();
+  const int rl = threadIdx.x / DP, dl = threadIdx.x % DP;
+  for (int64_t m = (int64_t)blockIdx.x * RPB + rl; m < a.M; m += (int64_t)gridDim.x * RPB) {
+    const float* g = a.G + m * a.ldg;
+    const float* e = a.E + m * a.lde;
+    for (int t = 0; t < a.n_task; ++t) {
+      float mx = -INFINITY;
+      for (int k = 0; k < a.n_sel; ++k) mx = fmaxf(mx, g[t * a.n_sel + k]);
+      float sum = 0.f;
+      for (int k = 0; k < a.n_sel; ++k) sum += expf(g[t * a.n_sel + k] - mx);
+      const float inv = 1.0f / sum;
+      for (int d = dl; d < a.D; d += DP) {
+        float acc = 0.f;
+        for (int k = 0; k < a.n_sel; ++k) {
+          const float p = expf(g[t * a.n_sel + k] - mx) * inv;
+          acc = fmaf(p, act_f(e[(int64_t)sel[t * a.n_sel + k] * a.D + d], a.e_act), acc);
+        }
+        Y[m * ldy + (int64_t)t * a.D + d] = acc;
+      }
+      if (P) {
+        for (int k = dl; k < a.n_sel; k += DP) P[m * ldp + t * a.n_sel + k] = expf(g[t * a.n_sel + k] - mx) * inv;
+      }
+    }
+  }
+}
+
+template <int DP>
+__global__ void __launch_bounds__(256) gate_mix_bwd_kernel(GM a, const float* __restrict__ dY,
+                                                           int64_t lddy, float* __restrict__ dE,
+                                                           int64_t ldde, float* __restrict__ dG,
+                                                           int64_t lddg) {
+  constexpr int RPB = 256 / DP;
+  extern __shared__ float acc_all[];  // [RPB][n_exp][D]
+  __shared__ int32_t sel[GM_MAXSEL * 8];
+  for (int i = threadIdx.x; i < a.n_task * a.n_sel; i += blockDim.x) sel[i] = a.sel[i];
+  __syncthreads();
+  const int rl = threadIdx.x / DP, dl = threadIdx.x % DP;
+  float* acc = acc_all + (int64_t)rl * a.n_exp * a.D;
+  const int nch = (a.D + DP - 1) / DP;
+  // every thread walks the same number of rows (so the group reductions stay converged)
+  const int64_t nrow_iter = (a.M + (int64_t)gridDim.x * RPB - 1) / ((int64_t)gridDim.x * RPB);
+  for (int64_t it = 0; it < nrow_iter; ++it) {
+    const int64_t m = ((int64_t)it * gridDim.x + blockIdx.x) * RPB + rl;
+    const bool live = m < a.M;
+    const int64_t mm = live ? m : 0;
+    const float* g = a.G + mm * a.ldg;
+    const float* e = a.E + mm * a.lde;
+    for (int x = 0; x < a.n_exp; ++x)
+      for (int c = 0; c < nch; ++c) {
+        const int d = dl + c * DP;
+        if (d < a.D) acc[x * a.D + d] = 0.f;
+      }
+    for (int t = 0; t < a.n_task; ++t) {
+      float dy[GM_MAXCH];
+#pragma unroll
+      for (int c = 0; c < GM_MAXCH; ++c) {
+        const int d = dl + c * DP;
+        dy[c] = (c < nch && d < a.D && live) ? dY[mm * lddy + (int64_t)t * a.D + d] : 0.f;
+      }
+      float mx = -INFINITY;
+      for (int k = 0; k < a.n_sel; ++k) mx = fmaxf(mx, g[t * a.n_sel + k]);
+      float sum = 0.f;
+      for (int k = 0; k < a.n_sel; ++k) sum += expf(g[t * a.n_sel + k] - mx);
+      const float inv = 1.0f / sum;
+      float p[GM_MAXSEL], s[GM_MAXSEL];
+      float ps = 0.f;
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) {
+        p[k] = 0.f; s[k] = 0.f;
+        if (k < a.n_sel) {
+          p[k] = expf(g[t * a.n_sel + k] - mx) * inv;
+          const int64_t col = (int64_t)sel[t * a.n_sel + k] * a.D;
+          float part = 0.f;
+#pragma unroll
+          for (int c = 0; c < GM_MAXCH; ++c) {
+            const int d = dl + c * DP;
+            if (c < nch && d < a.D) part = fmaf(dy[c], act_f(e[col + d], a.e_act), part);
+          }
+          s[k] = group_sum<DP>(part);
+          ps = fmaf(p[k], s[k], ps);
+#pragma unroll
+          for (int c = 0; c < GM_MAXCH; ++c) {
+            const int d = dl + c * DP;
+            if (c < nch && d < a.D) acc[sel[t * a.n_sel + k] * a.D + d] += p[k] * dy[c];
+          }
+        }
+      }
+      if (live && dG) {
+#pragma unroll
+        for (int k = 0; k < GM_MAXSEL; ++k)
+          if (k < a.n_sel && (k % DP) == dl) dG[m * lddg + t * a.n_sel + k] = p[k] * (s[k] - ps);
+      }
+    }
+    if (live && dE) {
+      for (int x = 0; x < a.n_exp; ++x)
+        for (int c = 0; c < nch; ++c) {
+          const int d = dl + c * DP;
+          if (d < a.D) {
+            const float z = e[(int64_t)x * a.D + d];
+            dE[m * ldde + (int64_t)x * a.D + d] = acc[x * a.D + d] * act_d(z, a.e_act);
+          }
+        }
+    }
+  }
+}
+
+// =============================================================================================
+// cross (CrossNet / DeepCrossLayer)
+// =============================================================================================
+constexpr int CR_MAXL = 4;
+
+// Thread owns columns c = threadIdx.x + 256 v (v < NV); the layer count L is a template parameter
+// so the per-layer register arrays hold exactly L rows.
+template <int NV, int L>
+__global__ void __launch_bounds__(256) cross_fwd_kernel(const float* __restrict__ X0, int64_t ldx,
+                                                        int64_t M, int D,
+                                                        const float* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ Y, int64_t ldy) {
+  __shared__ float red[8];
+  float w[L][NV], b[L][NV];
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      w[l][v] = c < D ? W[(int64_t)l * D + c] : 0.f;
+      b[l][v] = c < D ? bias[(int64_t)l * D + c] : 0.f;
+    }
+  int phase = 0;
+  for (int64_t m = blockIdx.x; m < M; m += gridDim.x) {
+    float x0[NV], xl[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      x0[v] = c < D ? X0[m * ldx + c] : 0.f;
+      xl[v] = x0[v];
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float part = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) part = fmaf(xl[v], w[l][v], part);
+      const float s = block_sum256(part, red, phase++);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) xl[v] = fmaf(x0[v], s, b[l][v] + xl[v]);
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      if (c < D) Y[m * ldy + c] = xl[v];
+    }
+  }
+}
+
+// Backward: recompute x_1..x_{L-1} and s_l = x_l . w_l per row, then for l = L-1 .. 0 with
+// g = dL/dx_{l+1}:  dx0 += g s_l;  ds = g . x0;  dw_l += x_l ds;  db_l += g;  g += w_l ds.
+// dX0 = dx0 + g.  w and b live in LDS (read once per row), dw/db accumulate in registers across
+// the block's rows and leave as one partial row per block.
+template <int NV, int L>
+__global__ void __launch_bounds__(256) cross_bwd_kernel(
+    const float* __restrict__ X0, int64_t ldx, int64_t M, int D, const float* __restrict__ W,
+    const float* __restrict__ bias, const float* __restrict__ dY, int64_t lddy,
+    float* __restrict__ dX0, int64_t lddx, int dx_accumulate, float* __restrict__ part) {
+  extern __shared__ float wb[];  // [L][D] w | [L][D] b
+  __shared__ float red[8];
+  for (int i = threadIdx.x; i < L * D; i += blockDim.x) { wb[i] = W[i]; wb[L * D + i] = bias[i]; }
+  __syncthreads();
+  const float* ws = wb;
+  const float* bs = wb + L * D;
+  float dw[L][NV], db[L][NV];
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) { dw[l][v] = 0.f; db[l][v] = 0.f; }
+  int phase = 0;
+  for (int64_t m = blockIdx.x; m < M; m += gridDim.x) {
+    float x0[NV], xs[L][NV], s[L];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      x0[v] = c < D ? X0[m * ldx + c] : 0.f;
+    }
+    float xl[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xl[v] = x0[v];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float pp = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = threadIdx.x + 256 * v;
+        xs[l][v] = xl[v];
+        if (c < D) pp = fmaf(xl[v], ws[l * D + c], pp);
+      }
+      s[l] = block_sum256(pp, red, phase++);
+      if (l + 1 < L) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int c = threadIdx.x + 256 * v;
+          xl[v] = fmaf(x0[v], s[l], (c < D ? bs[l * D + c] : 0.f) + xl[v]);
+        }
+      }
+    }
+    float g[NV], dx0[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      g[v] = c < D ? dY[m * lddy + c] : 0.f;
+      dx0[v] = 0.f;
+    }
+#pragma unroll
+    for (int l = L - 1; l >= 0; --l) {
+      float pp = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        dx0[v] = fmaf(g[v], s[l], dx0[v]);
+        pp = fmaf(g[v], x0[v], pp);
+        db[l][v] += g[v];
+      }
+      const float ds = block_sum256(pp, red, phase++);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = threadIdx.x + 256 * v;
+        dw[l][v] = fmaf(xs[l][v], ds, dw[l][v]);
+        if (c < D) g[v] = fmaf(ws[l * D + c], ds, g[v]);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      if (c < D) {
+        const float val = dx0[v] + g[v];
+        float* dst = dX0 + m * lddx + c;
+        *dst = dx_accumulate ? *dst + val : val;
+      }
+    }
+  }
+  // per-block partial row [dW (L*D) | db (L*D)]
+  float* pr = part + (int64_t)blockIdx.x * 2 * L * D;
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      if (c < D) {
+        pr[(int64_t)l * D + c] = dw[l][v];
+        pr[(int64_t)(L + l) * D + c] = db[l][v];
+      }
+    }
+}
+
+static int cross_bwd_grid(int64_t M) { return (int)(M < 128 ? (M < 1 ? 1 : M) : 128); }
+
+// =============================================================================================
+// fm (+ optional per-field scale = SENet reweight)
+// =============================================================================================
+struct FM {
+  const float* X; int64_t ldx; int64_t fsx;      // x[m*ldx + f*fsx + e]
+  int64_t M; int F, E;
+  const float* A; int64_t lda;                   // scale a[m*lda + f] (nullable)
+  float as;                                      // y = x * (as * a)
+};
+
+template <int EW>
+__global__ void __launch_bounds__(256) fm_fwd_kernel(FM a, float* __restrict__ Y, int64_t ldy,
+                                                     float* __restrict__ C, int64_t ldc,
+                                                     float* __restrict__ FMo, int64_t ldf) {
+  constexpr int NG = 64 / EW;
+  const int l = lane_id(), e = l % EW, fg = l / EW;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < a.M; m += (int64_t)gridDim.x * 4) {
+    float S = 0.f, Q = 0.f;
+    if (e < a.E) {
+      for (int f = fg; f < a.F; f += NG) {
+        float y = a.X[m * a.ldx + (int64_t)f * a.fsx + e];
+        if (a.A) y *= a.as * a.A[m * a.lda + f];
+        if (Y) Y[m * ldy + (int64_t)f * a.E + e] = y;
+        S += y;
+        Q = fmaf(y, y, Q);
+      }
+    }
+#pragma unroll
+    for (int o = EW; o < 64; o <<= 1) {
+      S += __shfl_xor(S, o, 64);
+      Q += __shfl_xor(Q, o, 64);
+    }
+    const float cr = S * S - Q;
+    if (C && fg == 0 && e < a.E) C[m * ldc + e] = cr;
+    if (FMo) {
+      const float t = group_sum<EW>(e < a.E ? cr : 0.f);
+      if (l == 0) FMo[m * ldf] = 0.5f * t;
+    }
+  }
+}
+
+template <int EW>
+__global__ void __launch_bounds__(256) fm_bwd_kernel(FM a, const float* __restrict__ dY,
+                                                     int64_t lddy, const float* __restrict__ dC,
+                                                     int64_t lddc, const float* __restrict__ dFM,
+                                                     int64_t lddf, float* __restrict__ dX,
+                                                     int64_t lddx, int64_t fsdx, int dx_accumulate,
+                                                     float* __restrict__ dA, int64_t ldda) {
+  constexpr int NG = 64 / EW;
+  const int l = lane_id(), e = l % EW, fg = l / EW;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < a.M; m += (int64_t)gridDim.x * 4) {
+    float S = 0.f;
+    if (e < a.E) {
+      for (int f = fg; f < a.F; f += NG) {
+        float y = a.X[m * a.ldx + (int64_t)f * a.fsx + e];
+        if (a.A) y *= a.as * a.A[m * a.lda + f];
+        S += y;
+      }
+    }
+#pragma unroll
+    for (int o = EW; o < 64; o <<= 1) S += __shfl_xor(S, o, 64);
+    const float dc = (dC && e < a.E) ? dC[m * lddc + e] : 0.f;
+    const float dfm = dFM ? dFM[m * lddf] : 0.f;
+    // F is the same for every lane group; loop over field rounds so group reductions converge
+    for (int f0 = 0; f0 < a.F; f0 += NG) {
+      const int f = f0 + fg;
+      const bool ok = f < a.F && e < a.E;
+      float x = 0.f, sc = 1.f, dyt = 0.f;
+      if (ok) {
+        x = a.X[m * a.ldx + (int64_t)f * a.fsx + e];
+        if (a.A) sc = a.as * a.A[m * a.lda + f];
+        const float y = x * sc;
+        // d/dy of cross_e = 2 (S_e - y), of fm = (S_e - y)
+        dyt = (dY ? dY[m * lddy + (int64_t)f * a.E + e] : 0.f) + (2.f * dc + dfm) * (S - y);
+      }
+      if (dX && ok) {
+        float* dst = dX + m * lddx + (int64_t)f * fsdx + e;
+        const float v = dyt * sc;
+        *dst = dx_accumulate ? *dst + v : v;
+      }
+      if (dA) {
+        const float t = group_sum<EW>(dyt * x);
+        if (e == 0 && f < a.F) dA[m * ldda + f] = a.as * t;
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// ffm + user x item multiply-ReLU
+// =============================================================================================
+constexpr int FF_E = 16;      // field width (general inputs are the 0:16 column slice)
+constexpr int FF_MAXF = 8;    // user + item fields
+
+struct FFM {
+  const float* X; int64_t ldx;                 // field f at column cols[f] (user fields first)
+  int64_t M; int NU, NI, Dff;
+  const int32_t* cols;
+  const float *Wx, *bx, *Wy, *by;              // [P][E][Dff], [P][Dff]
+};
+
+__global__ void __launch_bounds__(256) ffm_fwd_kernel(FFM a, float* __restrict__ Y, int64_t ldy,
+                                                      float* __restrict__ Mu, int64_t ldm) {
+  extern __shared__ float sw[];  // Wx | bx | Wy | by
+  const int P = a.NU * a.NI, nw = P * FF_E * a.Dff, nb = P * a.Dff;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) { sw[i] = a.Wx[i]; sw[nw + nb + i] = a.Wy[i]; }
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) { sw[nw + i] = a.bx[i]; sw[2 * nw + nb + i] = a.by[i]; }
+  __shared__ int32_t cols[FF_MAXF];
+  if (threadIdx.x < a.NU + a.NI) cols[threadIdx.x] = a.cols[threadIdx.x];
+  __syncthreads();
+  const float* Wx = sw; const float* bx = sw + nw; const float* Wy = sw + nw + nb;
+  const float* by = sw + 2 * nw + nb;
+  const int l = lane_id();
+  const int nout = P * a.Dff;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < a.M; m += (int64_t)gridDim.x * 4) {
+    const float* row = a.X + m * a.ldx;
+    for (int o = l; o < nout; o += 64) {
+      const int p = o / a.Dff, c = o % a.Dff;
+      const int xi = p / a.NI, yi = p % a.NI;
+      const float* xe = row + cols[xi];
+      const float* ye = row + cols[a.NU + yi];
+      float xo = bx[p * a.Dff + c], yo = by[p * a.Dff + c];
+#pragma unroll
+      for (int e = 0; e < FF_E; ++e) {
+        xo = fmaf(xe[e], Wx[(p * FF_E + e) * a.Dff + c], xo);
+        yo = fmaf(ye[e], Wy[(p * FF_E + e) * a.Dff + c], yo);
+      }
+      Y[m * ldy + o] = xo * yo;
+    }
+    if (Mu) {
+      for (int o = l; o < a.NU * FF_E; o += 64) {
+        const int i = o / FF_E, e = o % FF_E;
+        Mu[m * ldm + o] = fmaxf(row[cols[i] + e] * row[cols[a.NU + i] + e], 0.f);
+      }
+    }
+  }
+}
+
+// Backward: phase 1 (lane = output o): dxo/dyo into LDS and the per-lane dW/db accumulators;
+// phase 2 (lane = (field, e)): dx of each field = sum over its pairs (fixed order) + multiply.
+constexpr int FF_MAXOUT = 2;  // outputs per lane: P * Dff <= 128
+
+__global__ void __launch_bounds__(256) ffm_bwd_kernel(FFM a, const float* __restrict__ dY,
+                                                      int64_t lddy, const float* __restrict__ dMu,
+                                                      int64_t lddm, float* __restrict__ dX,
+                                                      int64_t lddx, int dx_accumulate,
+                                                      float* __restrict__ part) {
+  extern __shared__ float sw[];  // Wx | bx | Wy | by | per-wave dxo/dyo [4][2][P*Dff]
+  const int P = a.NU * a.NI, nw = P * FF_E * a.Dff, nb = P * a.Dff;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) { sw[i] = a.Wx[i]; sw[nw + nb + i] = a.Wy[i]; }
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) { sw[nw + i] = a.bx[i]; sw[2 * nw + nb + i] = a.by[i]; }
+  __shared__ int32_t cols[FF_MAXF];
+  if (threadIdx.x < a.NU + a.NI) cols[threadIdx.x] = a.cols[threadIdx.x];
+  __syncthreads();
+  const float* Wx = sw; const float* bx = sw + nw; const float* Wy = sw + nw + nb;
+  const float* by = sw + 2 * nw + nb;
+  float* dxo_s = sw + 2 * (nw + nb) + wave_id() * 2 * nb;
+  float* dyo_s = dxo_s + nb;
+  const int l = lane_id();
+  const int nout = P * a.Dff;
+  float gWx[FF_MAXOUT][FF_E], gWy[FF_MAXOUT][FF_E], gbx[FF_MAXOUT], gby[FF_MAXOUT];
+#pragma unroll
+  for (int j = 0; j < FF_MAXOUT; ++j) {
+    gbx[j] = gby[j] = 0.f;
+#pragma unroll
+    for (int e = 0; e < FF_E; ++e) gWx[j][e] = gWy[j][e] = 0.f;
+  }
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < a.M; m += (int64_t)gridDim.x * 4) {
+    const float* row = a.X + m * a.ldx;
+#pragma unroll
+    for (int j = 0; j < FF_MAXOUT; ++j) {
+      const int o = l + 64 * j;
+      if (o < nout) {
+        const int p = o / a.Dff, c = o % a.Dff;
+        const int xi = p / a.NI, yi = p % a.NI;
+        const float* xe = row + cols[xi];
+        const float* ye = row + cols[a.NU + yi];
+        float xv[FF_E], yv[FF_E];
+        float xo = bx[p * a.Dff + c], yo = by[p * a.Dff + c];
+#pragma unroll
+        for (int e = 0; e < FF_E; ++e) {
+          xv[e] = xe[e]; yv[e] = ye[e];
+          xo = fmaf(xv[e], Wx[(p * FF_E + e) * a.Dff + c], xo);
+          yo = fmaf(yv[e], Wy[(p * FF_E + e) * a.Dff + c], yo);
+        }
+        const float d = dY[m * lddy + o];
+        const float dxo = d * yo, dyo = d * xo;
+        dxo_s[o] = dxo;
+        dyo_s[o] = dyo;
+        gbx[j] += dxo;
+        gby[j] += dyo;
+#pragma unroll
+        for (int e = 0; e < FF_E; ++e) {
+          gWx[j][e] = fmaf(xv[e], dxo, gWx[j][e]);
+          gWy[j][e] = fmaf(yv[e], dyo, gWy[j][e]);
+        }
+      }
+    }
+    wave_lds_sync();
+    // phase 2: lane -> (field i, e)
+    for (int q = l; q < (a.NU + a.NI) * FF_E; q += 64) {
+      const int i = q / FF_E, e = q % FF_E;
+      float v = 0.f;
+      if (i < a.NU) {
+        for (int yi = 0; yi < a.NI; ++yi) {
+          const int p = i * a.NI + yi;
+          for (int c = 0; c < a.Dff; ++c) v = fmaf(Wx[(p * FF_E + e) * a.Dff + c], dxo_s[p * a.Dff + c], v);
+        }
+      } else {
+        const int yi = i - a.NU;
+        for (int xi = 0; xi < a.NU; ++xi) {
+          const int p = xi * a.NI + yi;
+          for (int c = 0; c < a.Dff; ++c) v = fmaf(Wy[(p * FF_E + e) * a.Dff + c], dyo_s[p * a.Dff + c], v);
+        }
+      }
+      if (dMu) {  // multiply-ReLU: field i pairs with field i of the other side
+        const int k = i < a.NU ? i : i - a.NU;
+        const float u = row[cols[k] + e], w = row[cols[a.NU + k] + e];
+        const float dm = dMu[m * lddm + k * FF_E + e];
+        if (u * w > 0.f) v = fmaf(dm, i < a.NU ? w : u, v);
+      }
+      float* dst = dX + m * lddx + cols[i] + e;
+      *dst = dx_accumulate ? *dst + v : v;
+    }
+    wave_lds_sync();
+  }
+  // per-wave partials -> block partial via LDS (reuse the weight region after a barrier)
+  __syncthreads();
+  float* red = sw;  // [4][2*(nw+nb)]
+  const int np = 2 * (nw + nb);
+  float* mine = red + wave_id() * np;
+#pragma unroll
+  for (int j = 0; j < FF_MAXOUT; ++j) {
+    const int o = l + 64 * j;
+    if (o < nout) {
+      const int p = o / a.Dff, c = o % a.Dff;
+#pragma unroll
+      for (int e = 0; e < FF_E; ++e) {
+        mine[(p * FF_E + e) * a.Dff + c] = gWx[j][e];
+        mine[nw + nb + (p * FF_E + e) * a.Dff + c] = gWy[j][e];
+      }
+      mine[nw + o] = gbx[j];
+      mine[2 * nw + nb + o] = gby[j];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < np; i += blockDim.x)
+    part[(int64_t)blockIdx.x * np + i] = (red[i] + red[np + i]) + (red[2 * np + i] + red[3 * np + i]);
+}
+
+static int ffm_grid(int64_t M) {
+  int64_t g = (M + 15) / 16;
+  return (int)(g > 256 ? 256 : (g < 1 ? 1 : g));
+}
+
+// =============================================================================================
+// elementwise gate multiply, softmax-KL head, rowdot, mse
+// =============================================================================================
+__global__ void mul_fwd_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ G,
+                               int64_t ldg, int64_t M, int N, float scale, float* __restrict__ Y,
+                               int64_t ldy) {
+  const int64_t n = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N, c = i % N;
+    Y[m * ldy + c] = A[m * lda + c] * (scale * G[m * ldg + c]);
+  }
+}
+
+__global__ void mul_bwd_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ G,
+                               int64_t ldg, int64_t M, int N, float scale,
+                               const float* __restrict__ dY, int64_t lddy, float* __restrict__ dA,
+                               int64_t ldda, float* __restrict__ dG, int64_t lddg) {
+  const int64_t n = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N, c = i % N;
+    const float d = dY[m * lddy + c] * scale;
+    const float a = A[m * lda + c], g = G[m * ldg + c];
+    if (dA) dA[m * ldda + c] = d * g;
+    if (dG) dG[m * lddg + c] = d * a;
+  }
+}
+
+constexpr int SK_MAXCH = 8;  // C <= 512
+
+__global__ void __launch_bounds__(256) softmax_kl_kernel(
+    const float* __restrict__ Z, int64_t ldz, int64_t M, int C, const float* __restrict__ bins,
+    float* __restrict__ Pout, int64_t ldp, const float* __restrict__ Yt, int64_t ldt,
+    const float* __restrict__ sw, float gscale, float eps, float* __restrict__ loss_rows,
+    float* __restrict__ dZ, int64_t lddz) {
+  const int l = lane_id();
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < M; m += (int64_t)gridDim.x * 4) {
+    float z[SK_MAXCH];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < SK_MAXCH; ++c) {
+      const int j = l + 64 * c;
+      z[c] = j < C ? Z[m * ldz + j] : -INFINITY;
+      mx = fmaxf(mx, z[c]);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < SK_MAXCH; ++c) {
+      const int j = l + 64 * c;
+      z[c] = j < C ? expf(z[c] - mx) : 0.f;
+      sum += z[c];
+    }
+    sum = group_sum<64>(sum);
+    const float inv = 1.0f / sum;
+    float ev = 0.f;
+#pragma unroll
+    for (int c = 0; c < SK_MAXCH; ++c) {
+      const int j = l + 64 * c;
+      z[c] *= inv;  // p
+      if (j < C) {
+        if (Pout) Pout[m * ldp + j] = z[c];
+        if (bins) ev = fmaf(z[c], bins[j], ev);
+      }
+    }
+    if (Pout && bins) {
+      ev = group_sum<64>(ev);
+      if (l == 0) Pout[m * ldp + C] = ev < 0.f ? 0.f : ev;  // tf.where(pred < 0, 0, pred)
+    }
+    if (!Yt) continue;
+    const float w = sw ? sw[m] : 1.f;
+    float kl = 0.f, pdp = 0.f, dp[SK_MAXCH];
+#pragma unroll
+    for (int c = 0; c < SK_MAXCH; ++c) {
+      const int j = l + 64 * c;
+      dp[c] = 0.f;
+      if (j < C) {
+        const float yt = fminf(fmaxf(Yt[m * ldt + j], eps), 1.f);
+        const float p = z[c];
+        const float yp = fminf(fmaxf(p, eps), 1.f);
+        kl = fmaf(yt, logf(yt / yp), kl);
+        dp[c] = (p >= eps && p <= 1.f) ? -yt / yp * (w * gscale) : 0.f;
+        pdp = fmaf(p, dp[c], pdp);
+      }
+    }
+    kl = group_sum<64>(kl);
+    pdp = group_sum<64>(pdp);
+    if (loss_rows && l == 0) loss_rows[m] = kl * w;
+    if (dZ) {
+#pragma unroll
+      for (int c = 0; c < SK_MAXCH; ++c) {
+        const int j = l + 64 * c;
+        if (j < C) dZ[m * lddz + j] = z[c] * (dp[c] - pdp);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) rowdot_kernel(const float* __restrict__ U, int64_t ldu,
+                                                     const float* __restrict__ V, int64_t ldv,
+                                                     int64_t M, int N, int sigm,
+                                                     float* __restrict__ Y,
+                                                     const float* __restrict__ dY,
+                                                     float* __restrict__ dU, int64_t lddu,
+                                                     float* __restrict__ dV, int64_t lddv) {
+  const int l = lane_id();
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < M; m += (int64_t)gridDim.x * 4) {
+    float s = 0.f;
+    for (int j = l; j < N; j += 64) s = fmaf(U[m * ldu + j], V[m * ldv + j], s);
+    s = group_sum<64>(s);
+    const float y = sigm ? 1.0f / (1.0f + expf(-s)) : s;
+    if (Y && l == 0) Y[m] = y;
+    if (dY) {
+      const float d = dY[m] * (sigm ? y * (1.f - y) : 1.f);
+      for (int j = l; j < N; j += 64) {
+        const float u = U[m * ldu + j], v = V[m * ldv + j];
+        if (dU) dU[m * lddu + j] = d * v;
+        if (dV) dV[m * lddv + j] = d * u;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) mse_rows_kernel(const float* __restrict__ S, int64_t lds,
+                                                       const float* __restrict__ T, int64_t ldt,
+                                                       int64_t M, int N, float gscale,
+                                                       float* __restrict__ loss_rows,
+                                                       float* __restrict__ dS, int64_t ldds) {
+  const int l = lane_id();
+  const float invN = 1.0f / (float)N;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < M; m += (int64_t)gridDim.x * 4) {
+    float q = 0.f;
+    for (int j = l; j < N; j += 64) {
+      const float d = S[m * lds + j] - T[m * ldt + j];
+      q = fmaf(d, d, q);
+      if (dS) dS[m * ldds + j] = 2.f * d * invN * gscale;
+    }
+    q = group_sum<64>(q);
+    if (loss_rows && l == 0) loss_rows[m] = q * invN;
+  }
+}
+
+static int rows_grid(int64_t M, int rows_per_block) {
+  int64_t g = (M + rows_per_block - 1) / rows_per_block;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+}
+
+}  // namespace rs_tw
+
+using namespace rs_tw;
+
+// ------------------------------- gate_mix ------------------------------------------------------
+static int gm_dp(int D) {
+  int dp = 8;
+  while (dp < D && dp < 64) dp <<= 1;
+  return dp;
+}
+
+static int gm_check(const GM& a) {
+  if (!a.E || !a.G || !a.sel || a.M < 0 || a.D <= 0 || a.n_exp <= 0 || a.n_task <= 0 ||
+      a.n_sel <= 0)
+    return RS_ERR_ARG;
+  if (a.n_sel > GM_MAXSEL || a.n_task * a.n_sel > GM_MAXSEL * 8 || a.D > 64 * GM_MAXCH)
+    return RS_ERR_UNSUPPORTED;
+  return RS_OK;
+}
+
+RS_API int rs_gate_mix_fwd(void* stream, const float* E, int64_t lde, int e_act, const float* G,
+                           int64_t ldg, int64_t M, int n_exp, int D, int n_task, int n_sel,
+                           const int32_t* sel, float* Y, int64_t ldy, float* P, int64_t ldp) {
+  GM a{E, lde, e_act, G, ldg, M, n_exp, D, n_task, n_sel, sel};
+  int st = gm_check(a);
+  if (st || !Y) return st ? st : RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  const int dp = gm_dp(D);
+  const int grid = rows_grid(M, 256 / dp);
+  hipStream_t s = rs_stream(stream);
+  switch (dp) {
+    case 8: gate_mix_fwd_kernel<8><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
+    case 16: gate_mix_fwd_kernel<16><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
+    case 32: gate_mix_fwd_kernel<32><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
+    default: gate_mix_fwd_kernel<64><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
+  }
+  return rs_status_after_launch();
+}
+
+RS_API int rs_gate_mix_bwd(void* stream, const float* E, int64_t lde, int e_act, const float* G,
+                           int64_t ldg, int64_t M, int n_exp, int D, int n_task, int n_sel,
+                           const int32_t* sel, const float* dY, int64_t lddy, float* dE,
+                           int64_t ldde, float* dG, int64_t lddg) {
+  GM a{E, lde, e_act, G, ldg, M, n_exp, D, n_task, n_sel, sel};
+  int st = gm_check(a);
+  if (st || !dY) return st ? st : RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  const int dp = gm_dp(D);
+  const int rpb = 256 / dp;
+  const size_t lds = (size_t)rpb * n_exp * D * 4;
+  if (lds > 64 * 1024) return RS_ERR_UNSUPPORTED;
+  const int grid = rows_grid(M, rpb);
+  hipStream_t s = rs_stream(stream);
+  switch (dp) {
+    case 8: gate_mix_bwd_kernel<8><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
+    case 16: gate_mix_bwd_kernel<16><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
+    case 32: gate_mix_bwd_kernel<32><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
+    default: gate_mix_bwd_kernel<64><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
+  }
+  return rs_status_after_launch();
+}
+
+// ------------------------------- cross ---------------------------------------------------------
+RS_API int64_t rs_cross_bwd_workspace_floats(int64_t M, int D, int L) {
+  if (M <= 0 || D <= 0 || L <= 0) return 0;
+  return (int64_t)cross_bwd_grid(M) * 2 * L * D;
+}
+
+static int cross_nv(int D) {
+  const int nv = (D + 255) / 256;
+  return nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : 8;
+}
+
+#define RS_CROSS_SWITCH(NVV, LL, CALL) \
+  switch (NVV * 10 + LL) {              \
+    case 11: CALL(1, 1); break;         \
+    case 12: CALL(1, 2); break;         \
+    case 13: CALL(1, 3); break;         \
+    case 14: CALL(1, 4); break;         \
+    case 21: CALL(2, 1); break;         \
+    case 22: CALL(2, 2); break;         \
+    case 23: CALL(2, 3); break;         \
+    case 24: CALL(2, 4); break;         \
+    case 41: CALL(4, 1); break;         \
+    case 42: CALL(4, 2); break;         \
+    case 43: CALL(4, 3); break;         \
+    case 44: CALL(4, 4); break;         \
+    case 81: CALL(8, 1); break;         \
+    case 82: CALL(8, 2); break;         \
+    case 83: CALL(8, 3); break;         \
+    default: CALL(8, 4); break;         \
+  }
+
+RS_API int rs_cross_fwd(void* stream, const float* X0, int64_t ldx, int64_t M, int D, int L,
+                        const float* W, const float* b, float* Y, int64_t ldy) {
+  if (!X0 || !W || !b || !Y || M < 0 || D <= 0 || L <= 0) return RS_ERR_ARG;
+  if (L > CR_MAXL || D > 256 * 8) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  const int nv = cross_nv(D);
+  const int grid = (int)(M > 2048 ? 2048 : M);
+  hipStream_t s = rs_stream(stream);
+#define RS_CF(NV, LL) cross_fwd_kernel<NV, LL><<<grid, 256, 0, s>>>(X0, ldx, M, D, W, b, Y, ldy)
+  RS_CROSS_SWITCH(nv, L, RS_CF)
+#undef RS_CF
+  return rs_status_after_launch();
+}
+
+RS_API int rs_cross_bwd(void* stream, const float* X0, int64_t ldx, int64_t M, int D, int L,
+                        const float* W, const float* b, const float* dY, int64_t lddy, float* dX0,
+                        int64_t lddx, int dx_accumulate, float* dparams, int dparams_accumulate,
+                        float* workspace, int64_t workspace_floats) {
+  if (!X0 || !W || !b || !dY || !dX0 || M < 0 || D <= 0 || L <= 0) return RS_ERR_ARG;
+  if (L > CR_MAXL || D > 256 * 8) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  const int grid = cross_bwd_grid(M);
+  if (!workspace || workspace_floats < (int64_t)grid * 2 * L * D) return RS_ERR_ARG;
+  const int nv = cross_nv(D);
+  const size_t lds = (size_t)2 * L * D * 4;
+  hipStream_t s = rs_stream(stream);
+#define RS_CB(NV, LL)                                                                           \
+  cross_bwd_kernel<NV, LL><<<grid, 256, lds, s>>>(X0, ldx, M, D, W, b, dY, lddy, dX0, lddx,     \
+                                                  dx_accumulate, workspace)
+  RS_CROSS_SWITCH(nv, L, RS_CB)
+#undef RS_CB
+  int st = rs_status_after_launch();
+  if (st || !dparams) return st;
+  const int64_t n = 2 * (int64_t)L * D;
+  launch_column_reduce(s, workspace, grid, n, n, n, dparams, dparams, dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+// ------------------------------- fm ------------------------------------------------------------
+RS_API int rs_fm_fwd(void* stream, const float* X, int64_t ldx, int64_t fsx, int64_t M, int F,
+                     int E, const float* A, int64_t lda, float a_scale, float* Y, int64_t ldy, float* C,
+                     int64_t ldc, float* fm, int64_t ldf) {
+  if (!X || M < 0 || F <= 0 || E <= 0) return RS_ERR_ARG;
+  if (E > 64) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  FM a{X, ldx, fsx, M, F, E, A, lda, a_scale};
+  const int grid = rows_grid(M, 4);
+  hipStream_t s = rs_stream(stream);
+  if (E <= 8) fm_fwd_kernel<8><<<grid, 256, 0, s>>>(a, Y, ldy, C, ldc, fm, ldf);
+  else if (E <= 16) fm_fwd_kernel<16><<<grid, 256, 0, s>>>(a, Y, ldy, C, ldc, fm, ldf);
+  else if (E <= 32) fm_fwd_kernel<32><<<grid, 256, 0, s>>>(a, Y, ldy, C, ldc, fm, ldf);
+  else fm_fwd_kernel<64><<<grid, 256, 0, s>>>(a, Y, ldy, C, ldc, fm, ldf);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_fm_bwd(void* stream, const float* X, int64_t ldx, int64_t fsx, int64_t M, int F, int E,
+                     const float* A, int64_t lda, float a_scale, const float* dY, int64_t lddy, const float* dC,
+                     int64_t lddc, const float* dfm, int64_t lddf, float* dX, int64_t lddx,
+                     int64_t fsdx, int dx_accumulate, float* dA, int64_t ldda) {
+  if (!X || M < 0 || F <= 0 || E <= 0) return RS_ERR_ARG;
+  if (E > 64) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  FM a{X, ldx, fsx, M, F, E, A, lda, a_scale};
+  const int grid = rows_grid(M, 4);
+  hipStream_t s = rs_stream(stream);
+#define RS_FMB(EW)                                                                              \
+  fm_bwd_kernel<EW><<<grid, 256, 0, s>>>(a, dY, lddy, dC, lddc, dfm, lddf, dX, lddx, fsdx,      \
+                                         dx_accumulate, dA, ldda)
+  if (E <= 8) RS_FMB(8);
+  else if (E <= 16) RS_FMB(16);
+  else if (E <= 32) RS_FMB(32);
+  else RS_FMB(64);
+#undef RS_FMB
+  return rs_status_after_launch();
+}
+
+// ------------------------------- ffm -----------------------------------------------------------
+static int ffm_check(int64_t M, int NU, int NI, int E, int Dff) {
+  if (M < 0 || NU <= 0 || NI <= 0 || Dff <= 0) return RS_ERR_ARG;
+  if (E != FF_E || NU + NI > FF_MAXF || NU * NI * Dff > 64 * FF_MAXOUT) return RS_ERR_UNSUPPORTED;
+  return RS_OK;
+}
+
+RS_API int64_t rs_ffm_param_count(int NU, int NI, int E, int Dff) {
+  return 2 * ((int64_t)NU * NI * E * Dff + (int64_t)NU * NI * Dff);
+}
+
+RS_API int64_t rs_ffm_bwd_workspace_floats(int64_t M, int NU, int NI, int E, int Dff) {
+  if (ffm_check(M, NU, NI, E, Dff)) return 0;
+  return (int64_t)ffm_grid(M) * rs_ffm_param_count(NU, NI, E, Dff);
+}
+
+RS_API int rs_ffm_fwd(void* stream, const float* X, int64_t ldx, int64_t M, int NU, int NI, int E,
+                      int Dff, const int32_t* cols, const float* Wx, const float* bx,
+                      const float* Wy, const float* by, float* Y, int64_t ldy, float* Mult,
+                      int64_t ldm) {
+  int st = ffm_check(M, NU, NI, E, Dff);
+  if (st) return st;
+  if (!X || !cols || !Wx || !bx || !Wy || !by || !Y) return RS_ERR_ARG;
+  if (Mult && NU != NI) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  FFM a{X, ldx, M, NU, NI, Dff, cols, Wx, bx, Wy, by};
+  const size_t lds = (size_t)rs_ffm_param_count(NU, NI, E, Dff) * 4;
+  ffm_fwd_kernel<<<rows_grid(M, 4), 256, lds, rs_stream(stream)>>>(a, Y, ldy, Mult, ldm);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_ffm_bwd(void* stream, const float* X, int64_t ldx, int64_t M, int NU, int NI, int E,
+                      int Dff, const int32_t* cols, const float* Wx, const float* bx,
+                      const float* Wy, const float* by, const float* dY, int64_t lddy,
+                      const float* dMult, int64_t lddm, float* dX, int64_t lddx,
+                      int dx_accumulate, float* dparams, int dparams_accumulate, float* workspace,
+                      int64_t workspace_floats) {
+  int st = ffm_check(M, NU, NI, E, Dff);
+  if (st) return st;
+  if (!X || !cols || !Wx || !bx || !Wy || !by || !dY || !dX) return RS_ERR_ARG;
+  if (dMult && NU != NI) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  const int grid = ffm_grid(M);
+  const int64_t np = rs_ffm_param_count(NU, NI, E, Dff);
+  if (!workspace || workspace_floats < grid * np) return RS_ERR_ARG;
+  FFM a{X, ldx, M, NU, NI, Dff, cols, Wx, bx, Wy, by};
+  const int nb = NU * NI * Dff;
+  size_t lds = (size_t)(np + 4 * 2 * nb) * 4;
+  if (lds < (size_t)4 * np * 4) lds = (size_t)4 * np * 4;
+  hipStream_t s = rs_stream(stream);
+  ffm_bwd_kernel<<<grid, 256, lds, s>>>(a, dY, lddy, dMult, lddm, dX, lddx, dx_accumulate,
+                                        workspace);
+  st = rs_status_after_launch();
+  if (st || !dparams) return st;
+  launch_column_reduce(s, workspace, grid, np, np, np, dparams, dparams, dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+// ------------------------------- elementwise / heads / losses ---------------------------------
+RS_API int rs_mul_fwd(void* stream, const float* A, int64_t lda, const float* G, int64_t ldg,
+                      int64_t M, int N, float scale, float* Y, int64_t ldy) {
+  if (!A || !G || !Y || M < 0 || N <= 0) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  int64_t grid = (M * N + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  mul_fwd_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(A, lda, G, ldg, M, N, scale, Y, ldy);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_mul_bwd(void* stream, const float* A, int64_t lda, const float* G, int64_t ldg,
+                      int64_t M, int N, float scale, const float* dY, int64_t lddy, float* dA,
+                      int64_t ldda, float* dG, int64_t lddg) {
+  if (!A || !G || !dY || M < 0 || N <= 0) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  int64_t grid = (M * N + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  mul_bwd_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(A, lda, G, ldg, M, N, scale, dY, lddy,
+                                                           dA, ldda, dG, lddg);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_softmax_kl(void* stream, const float* Z, int64_t ldz, int64_t M, int C,
+                         const float* bins, float* P, int64_t ldp, const float* y_true,
+                         int64_t ldt, const float* sample_w, float gscale, float eps,
+                         float* loss_rows, float* dZ, int64_t lddz) {
+  if (!Z || M < 0 || C <= 0) return RS_ERR_ARG;
+  if (C > 64 * SK_MAXCH) return RS_ERR_UNSUPPORTED;
+  if ((loss_rows || dZ) && !y_true) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  softmax_kl_kernel<<<rows_grid(M, 4), 256, 0, rs_stream(stream)>>>(
+      Z, ldz, M, C, bins, P, ldp, y_true, ldt, sample_w, gscale, eps, loss_rows, dZ, lddz);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_rowdot(void* stream, const float* U, int64_t ldu, const float* V, int64_t ldv,
+                     int64_t M, int N, int use_sigmoid, float* Y, const float* dY, float* dU,
+                     int64_t lddu, float* dV, int64_t lddv) {
+  if (!U || !V || M < 0 || N <= 0) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  rowdot_kernel<<<rows_grid(M, 4), 256, 0, rs_stream(stream)>>>(U, ldu, V, ldv, M, N, use_sigmoid,
+                                                               Y, dY, dU, lddu, dV, lddv);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_mse_rows(void* stream, const float* S, int64_t lds, const float* T, int64_t ldt,
+                       int64_t M, int N, float gscale, float* loss_rows, float* dS, int64_t ldds) {
+  if (!S || !T || M < 0 || N <= 0) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  mse_rows_kernel<<<rows_grid(M, 4), 256, 0, rs_stream(stream)>>>(S, lds, T, ldt, M, N, gscale,
+                                                                 loss_rows, dS, ldds);
+  return rs_status_after_launch();
+}

@@ -1,0 +1,241 @@
+"""GPU parity of the tower ops through the C ABI vs the op-for-op torch
+float64 restatements in oracle/torch_ref.py (rough_rank/layer.py, staytime/layer.py,
+staytime/VideoDnn.py, rank/multi_head/multidnn.py, staytime/model.py).  Tolerances: forward
+|err| <= 1e-5 absolute (2e-5 after 1000+-term fp32 sums); gradients as tests/_tol.py.
+Parity unpinned against TF itself (oracle/ctr_oracle.py header)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import torch_ref as tr
+from _tol import assert_close, assert_grad_close, to_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _x(rng, *shape, scale=0.5):
+    return rng.uniform(-scale, scale, size=shape).astype(np.float32)
+
+
+def _cpu(t):
+    return torch.tensor(to_np(t), dtype=torch.float64, requires_grad=True)
+
+
+def _check(out_gpu, out_ref, pairs, R, fwd_atol=1e-5):
+    """out_gpu / out_ref: tensors (or lists); R: numpy weights for the scalar loss sum(out * R).
+    pairs: [(gpu_tensor_with_grad, cpu_tensor_with_grad, name)]."""
+    if isinstance(out_gpu, (list, tuple)):
+        out_gpu = torch.cat([o.reshape(o.shape[0], -1) for o in out_gpu], 1)
+        out_ref = torch.cat([o.reshape(o.shape[0], -1) for o in out_ref], 1)
+    assert_close(to_np(out_gpu), to_np(out_ref), fwd_atol, 0, "forward")
+    (out_gpu * torch.from_numpy(R.astype(np.float32)).to(DEV)).sum().backward()
+    (out_ref * torch.from_numpy(R)).sum().backward()
+    for g, c, name in pairs:
+        assert_grad_close(to_np(g.grad), c.grad.numpy(), name)
+
+
+def test_dnn_tower():
+    from recommendsystem_amd.towers import DNN
+    rng = np.random.default_rng(1)
+    x = torch.from_numpy(_x(rng, 300, 832)).to(DEV).requires_grad_(True)
+    net = DNN((128, 64, 16), activation="relu", output_activation="linear", seed=3)
+    out = net(x)
+    xc = _cpu(x)
+    Ks = [_cpu(l.kernel) for l in net.layers]
+    Bs = [_cpu(l.bias) for l in net.layers]
+    ref = tr.dnn(xc, Ks, Bs, "relu", "linear")
+    R = rng.normal(size=tuple(out.shape))
+    pairs = [(x, xc, "dx")] + [(l.kernel, k, f"dW{i}") for i, (l, k) in enumerate(zip(net.layers, Ks))] \
+        + [(l.bias, b, f"db{i}") for i, (l, b) in enumerate(zip(net.layers, Bs))]
+    _check(out, ref, pairs, R)
+
+
+def _randomise(params, rng, scale=0.3):
+    with torch.no_grad():
+        for p in params:
+            p.copy_(torch.from_numpy(rng.uniform(-scale, scale, size=tuple(p.shape)).astype(np.float32)))
+
+
+@pytest.mark.parametrize("kind", ["mmoe", "ple", "multi_head"])
+def test_expert_gate_mixtures(kind):
+    from recommendsystem_amd.towers import MMOE, PLE, ExpertGateLayer
+    rng = np.random.default_rng(2)
+    if kind == "mmoe":
+        M, K = 257, 100
+        layer = MMOE(num_tasks=3, num_experts=4, expert_dnn_units=(32,))
+    elif kind == "ple":
+        M, K = 200, 528
+        layer = PLE(num_tasks=2, num_shared_experts=4, num_specific_experts=4, expert_dnn_units=(32,))
+    else:  # rank/multi_head/multidnn.py:77-120: 7 experts x 32 relu, 7 softmax gates over 7
+        M, K = 130, 1616
+        layer = ExpertGateLayer(7, 32, [list(range(7))] * 7, "relu")
+    x = torch.from_numpy(_x(rng, M, K)).to(DEV).requires_grad_(True)
+    mix = layer.mix if hasattr(layer, "mix") else layer
+    mix.build((M, K), device=x.device)
+    _randomise([mix.kernel, mix.bias], rng, 0.1)
+    outs = layer(x)
+    xc = _cpu(x)
+    Wc, bc = _cpu(mix.kernel), _cpu(mix.bias)
+    D, E, ns = mix.D, mix.n_exp, mix.n_sel
+    ek = lambda e: ([Wc[:, e * D:(e + 1) * D]], [bc[e * D:(e + 1) * D]])  # noqa: E731
+    gk = lambda t: ([Wc[:, E * D + t * ns:E * D + (t + 1) * ns]], [bc[E * D + t * ns:E * D + (t + 1) * ns]])  # noqa: E731
+    if kind == "mmoe":
+        ref = tr.mmoe(xc, [ek(e) for e in range(E)], [gk(t) for t in range(mix.n_task)])
+    elif kind == "ple":
+        S, P, T = 4, 4, 2
+        ref = tr.ple(xc, [ek(e) for e in range(S)], [[ek(S + t * P + j) for j in range(P)] for t in range(T)],
+                     [gk(t) for t in range(T)])
+    else:
+        We = [Wc[:, e * D:(e + 1) * D] for e in range(7)]
+        be = [bc[e * D:(e + 1) * D] for e in range(7)]
+        Wg = [Wc[:, E * D + t * ns:E * D + (t + 1) * ns] for t in range(7)]
+        bg = [bc[E * D + t * ns:E * D + (t + 1) * ns] for t in range(7)]
+        ref = tr.multi_head_gates(xc, We, be, Wg, bg, n_used=7)
+    R = rng.normal(size=(M, mix.n_task * D))
+    _check(outs, ref, [(x, xc, "dx"), (mix.kernel, Wc, "dW"), (mix.bias, bc, "db")], R, 2e-5)
+
+
+@pytest.mark.parametrize("kind,D,L", [("crossnet", 832, 2), ("deepcross", 1712, 3), ("crossnet", 40, 1),
+                                      ("deepcross", 300, 4)])
+def test_cross_layers(kind, D, L):
+    from recommendsystem_amd.towers import CrossNet, DeepCrossLayer
+    rng = np.random.default_rng(3)
+    M = 97
+    x = torch.from_numpy(_x(rng, M, D, scale=0.2)).to(DEV).requires_grad_(True)
+    layer = CrossNet(layer_num=L) if kind == "crossnet" else DeepCrossLayer(num_layer=L)
+    layer.build((M, D), device=x.device)
+    _randomise([layer.W, layer.b], rng, 0.05)
+    out = layer(x)
+    xc, Wc, bc = _cpu(x), _cpu(layer.W), _cpu(layer.b)
+    if kind == "crossnet":
+        ref = tr.crossnet(xc, [Wc[l].reshape(D, 1) for l in range(L)], [bc[l].reshape(D, 1) for l in range(L)])
+    else:
+        ref = tr.deep_cross_layer(xc, [Wc[l].reshape(D, 1) for l in range(L)], [bc[l] for l in range(L)])
+    R = rng.normal(size=(M, D))
+    _check(out, ref, [(x, xc, "dx"), (layer.W, Wc, "dW"), (layer.b, bc, "db")], R, 2e-5)
+
+
+def test_fm_layer_and_senet_fm():
+    from recommendsystem_amd.towers import FMLayer, SENetFM
+    rng = np.random.default_rng(4)
+    B, F, E = 77, 91, 16
+    full = torch.from_numpy(_x(rng, B, F, 32)).to(DEV).requires_grad_(True)
+    x = full[:, :, 0:16]                       # the general-input slice of staytime/VideoDnn.py:47
+    fm = FMLayer()(x)
+    fullc = _cpu(full)
+    ref = tr.fm_layer(fullc[:, :, 0:16])
+    R = rng.normal(size=(B, 1))
+    _check(fm, ref, [(full, fullc, "dx")], R, 2e-5)
+    # SENet + FM (staytime/VideoDnn.py:81-115)
+    full.grad = None
+    sen = SENetFM(F)
+    y, cross, fml = sen(x)
+    W1, b1 = _cpu(sen.squeeze.kernel), _cpu(sen.squeeze.bias)
+    W2, b2 = _cpu(sen.excite.kernel), _cpu(sen.excite.bias)
+    fullc = _cpu(full)
+    general = [fullc[:, f, 0:16] for f in range(F)]
+    rew, cr, fmr = tr.senet_fm(general, W1, b1, W2, b2)
+    outs = [y, cross, fml]
+    refs = [torch.cat(rew, 1), cr, fmr]
+    R = rng.normal(size=(B, F * E + E + 1))
+    pairs = [(full, fullc, "dx"), (sen.squeeze.kernel, W1, "dW1"), (sen.squeeze.bias, b1, "db1"),
+             (sen.excite.kernel, W2, "dW2"), (sen.excite.bias, b2, "db2")]
+    _check(outs, refs, pairs, R, 5e-5)
+    assert sen.squeeze.units == 22  # int(91 / 4): the float units of :82 coerced by Keras (pinned)
+
+
+def test_ffm_and_multiply():
+    from recommendsystem_amd.towers import FFMBlock
+    rng = np.random.default_rng(5)
+    B, F = 90, 12
+    user, item = [0, 3, 5, 7], [1, 2, 9, 11]
+    x = torch.from_numpy(_x(rng, B, F * 16)).to(DEV).requires_grad_(True)
+    blk = FFMBlock(user, item, dim=8)
+    _randomise([blk.bx, blk.by], rng, 0.1)
+    y, mu = blk(x)
+    xc = _cpu(x)
+    Wx, bx, Wy, by = (_cpu(t) for t in (blk.Wx, blk.bx, blk.Wy, blk.by))
+    fields = [xc[:, f * 16:(f + 1) * 16] for f in range(F)]
+    ref_y = tr.ffm_block([fields[i] for i in user], [fields[j] for j in item], Wx, bx, Wy, by)
+    ref_m = tr.multiply_relu([fields[i] for i in user], [fields[j] for j in item])
+    R = rng.normal(size=(B, 128 + 64))
+    _check([y, mu], [ref_y, ref_m], [(x, xc, "dx"), (blk.Wx, Wx, "dWx"), (blk.bx, bx, "dbx"),
+                                     (blk.Wy, Wy, "dWy"), (blk.by, by, "dby")], R)
+
+
+def test_ppnet_gate_multiply():
+    from recommendsystem_amd.towers import gated
+    rng = np.random.default_rng(6)
+    a = torch.from_numpy(_x(rng, 64, 256)).to(DEV).requires_grad_(True)
+    g = torch.from_numpy(_x(rng, 64, 256)).to(DEV).requires_grad_(True)
+    y = gated(a, g, 2.0)
+    ac, gc = _cpu(a), _cpu(g)
+    _check(y, ac * (2 * gc), [(a, ac, "da"), (g, gc, "dg")], rng.normal(size=(64, 256)))
+
+
+def test_staytime_head_and_kl_loss():
+    from recommendsystem_amd.towers import StaytimeHead
+    rng = np.random.default_rng(7)
+    B, K = 129, 1840
+    bins = [-19.0 + 0.5 * i for i in range(400)]
+    x = torch.from_numpy(_x(rng, B, K, scale=0.3)).to(DEV).requires_grad_(True)
+    head = StaytimeHead(bins)
+    P = head(x)
+    xc = _cpu(x)
+    W, b = _cpu(head.dense.kernel), _cpu(head.dense.bias)
+    ref = tr.staytime_head(xc, W, b, bins)
+    assert_close(to_np(P), to_np(ref), 1e-5, 1e-5, "head")
+    # soft labels as staytime/parse.py:40-62 builds them (gaussian over the bins, sigma 4)
+    wt = rng.uniform(0, 160, size=(B, 1))
+    yt = np.exp(-np.square(np.array(bins)[None] - wt) / 32.0) / (np.sqrt(2 * np.pi) * 4) * 0.5
+    yt = np.concatenate([yt, wt], 1)
+    sw = np.where(rng.uniform(size=B) < 0.2, 5.0, 1.0)
+    loss, P2 = head.loss(x, torch.from_numpy(yt.astype(np.float32)).to(DEV),
+                         torch.from_numpy(sw.astype(np.float32)).to(DEV), loss_weight=2.0)
+    kl = tr.custom_kl_loss(torch.from_numpy(yt), tr.staytime_head(xc, W, b, bins))
+    ref_loss = 2.0 * torch.mean(kl * torch.from_numpy(sw))
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    loss.backward()
+    ref_loss.backward()
+    assert_grad_close(to_np(x.grad), xc.grad.numpy(), "dx")
+    assert_grad_close(to_np(head.dense.kernel.grad), W.grad.numpy(), "dW")
+    assert_grad_close(to_np(head.dense.bias.grad), b.grad.numpy(), "db")
+
+
+def test_similarity_kd_and_losses():
+    from recommendsystem_amd.towers import KDLoss, Similarity, cross_entropy_sum, keras_bce
+    rng = np.random.default_rng(8)
+    u = torch.from_numpy(_x(rng, 50, 16)).to(DEV).requires_grad_(True)
+    v = torch.from_numpy(_x(rng, 50, 16)).to(DEV).requires_grad_(True)
+    for sig in (False, True):
+        u.grad = v.grad = None
+        uc, vc = _cpu(u), _cpu(v)
+        _check(Similarity(sig)([u, v]), tr.similarity(uc, vc, sig), [(u, uc, "du"), (v, vc, "dv")],
+               rng.normal(size=(50, 1)))
+    s = torch.from_numpy(_x(rng, 50, 1)).to(DEV).requires_grad_(True)
+    t = torch.from_numpy(_x(rng, 50, 1)).to(DEV).requires_grad_(True)
+    sc, tc = _cpu(s), _cpu(t)
+    _check(KDLoss()(s, t), tr.kd_loss(sc, tc), [(s, sc, "ds"), (t, tc, "dt")], rng.normal(size=(50,)))
+    p = torch.from_numpy(rng.uniform(0, 1, size=(60, 1)).astype(np.float32))
+    p[0, 0], p[1, 0] = 0.0, 1.0                # clip edges
+    p = p.to(DEV).requires_grad_(True)
+    y = torch.from_numpy((rng.uniform(size=(60, 1)) < 0.3).astype(np.float32)).to(DEV)
+    pc = _cpu(p)
+    l1 = keras_bce(y, p)
+    r1 = tr.keras_bce(torch.from_numpy(to_np(y)), pc)
+    assert abs(float(l1) - float(r1)) < 1e-5
+    l1.backward()
+    r1.backward()
+    assert_grad_close(to_np(p.grad), pc.grad.numpy(), "dbce")
+    p7 = torch.from_numpy(rng.uniform(0.01, 0.99, size=(40, 7)).astype(np.float32)).to(DEV).requires_grad_(True)
+    y7 = torch.from_numpy((rng.uniform(size=(40, 7)) < 0.2).astype(np.float32)).to(DEV)
+    p7c = _cpu(p7)
+    l7 = cross_entropy_sum(y7, p7)
+    r7 = tr.cross_entropy(torch.from_numpy(to_np(y7)), p7c)
+    assert abs(float(l7) - float(r7)) < 1e-5
+    l7.backward()
+    r7.backward()
+    assert_grad_close(to_np(p7.grad), p7c.grad.numpy(), "dce7")
