@@ -130,13 +130,29 @@ def layer_norm(x, gamma, beta, eps=1e-14):
     return (x - mean) / std * gamma + beta
 
 
+def fmix32(h):
+    """murmur3 32-bit finaliser on uint32 arrays (wrapping arithmetic)."""
+    h = np.asarray(h, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x85EBCA6B)
+        h = h ^ (h >> np.uint32(13))
+        h = h * np.uint32(0xC2B2AE35)
+        return h ^ (h >> np.uint32(16))
+
+
 def dropout_keep(seed: int, b, h, i, j, rate: float) -> np.ndarray:
-    """Counter-based dropout mask shared bit-for-bit with csrc/common.hpp::dropout_keep."""
-    b = np.asarray(b, dtype=np.uint64)
-    key = (U64(seed & MASK64) ^ ((b << U64(32)) | (np.asarray(h, np.uint64) << U64(24))
-                                 | (np.asarray(i, np.uint64) << U64(12)) | np.asarray(j, np.uint64)))
-    r = splitmix64(key)
-    u = (r >> U64(40)).astype(np.float64) * (1.0 / 16777216.0)
+    """Counter-based dropout mask shared bit-for-bit with csrc/common.hpp::dropout_keep:
+    kb = fmix32(lo32(seed) ^ fmix32(hi32(seed) + b)); r = fmix32(kb ^ (h<<24 | i<<12 | j));
+    keep iff (r >> 8) / 2^24 >= rate."""
+    seed = int(seed) & MASK64
+    lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    with np.errstate(over="ignore"):
+        kb = fmix32(lo ^ fmix32(hi + np.asarray(b, dtype=np.uint32)))
+    ctr = ((np.asarray(h, np.uint32) << np.uint32(24)) | (np.asarray(i, np.uint32) << np.uint32(12))
+           | np.asarray(j, np.uint32))
+    r = fmix32(kb ^ ctr)
+    u = (r >> np.uint32(8)).astype(np.float64) * (1.0 / 16777216.0)
     return u >= np.float32(rate)
 
 

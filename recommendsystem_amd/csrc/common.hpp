@@ -65,8 +65,12 @@ __device__ __forceinline__ float group_max(float v) {
 
 // ---------------------------------------------------------------------------------------------
 // Counter-based dropout mask (shared bit-for-bit with oracle/ctr_oracle.py::dropout_keep).
-// TF's stateful RNG cannot be reproduced, so the framework pins its own: a SplitMix64 finaliser
-// over (seed, b, h, i, j); keep iff the top 24 bits / 2^24 >= rate.
+// TF's stateful RNG cannot be reproduced, so the framework pins its own.  For the 64-bit layer
+// seed s (splitmix64(seed + iteration)) and sample b, a per-sample key
+//   kb = fmix32(lo32(s) ^ fmix32(hi32(s) + b))
+// then per element r = fmix32(kb ^ (h << 24 | i << 12 | j))  (h < 256, i, j < 4096);
+// keep iff (r >> 8) / 2^24 >= rate.  fmix32 is the murmur3 finaliser: two 32-bit multiplies per
+// element (a 64-bit SplitMix per element costs ~3x more on the VALU), and kb is hoisted per sample.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -75,12 +79,28 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t dropout_sample_key(uint64_t seed, uint32_t b) {
+  return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) + b));
+}
+
+__device__ __forceinline__ bool dropout_keep_k(uint32_t kb, uint32_t h, uint32_t i, uint32_t j,
+                                               float rate) {
+  const uint32_t r = fmix32(kb ^ ((h << 24) | (i << 12) | j));
+  return (float)(r >> 8) * (1.0f / 16777216.0f) >= rate;
+}
+
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t b, uint32_t h, uint32_t i,
                                              uint32_t j, float rate) {
-  uint64_t key = seed ^ (((uint64_t)b << 32) | ((uint64_t)h << 24) | ((uint64_t)i << 12) | j);
-  uint64_t r = splitmix64(key);
-  float u = (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
-  return u >= rate;
+  return dropout_keep_k(dropout_sample_key(seed, b), h, i, j, rate);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,0 +1,529 @@
+// H3/H5 — InteractingLayer for many fields (F in (64, 256]): the rank/multi_head ranker runs
+// IL(layer_num 1, unit_num 8, head_num 2, dropout 0.2, res) over 200 fields
+// (rank/multi_head/multidnn.py:54).  Same math as il_kernels.hpp
+// (InteractingLayer.py:37-61, tied weights, keras-layer-normalization LN, the counter-based
+// dropout mask of common.hpp), different MI355X mapping:
+//
+//   * one 256-thread workgroup per sample (grid-stride): at F = 200 the sample's x, Q, K, V, R
+//     and attention output are 38 KB of LDS (4 blocks / CU in forward);
+//   * projections: thread = (column of [Wq|Wk|Wv|Wr], row group), the column's E weights in
+//     VGPRs, x rows as broadcast float4 LDS reads;
+//   * attention: thread = (head, query row); the F x F scores are never stored: a max pass and
+//     an exp pass (one v_exp_f32 per score, base-2 domain) over K/V rows read as broadcast float4
+//     (all lanes of a wave share the head, so every K/V read is one address per wave);
+//   * backward recomputes the iteration, then two passes over the score matrix: pass A with
+//     thread = query row (dQ), pass B with thread = key row (dK, dV), each row's gradient in
+//     VGPRs -- no F x F buffer, no atomics.  The dropout mask is hashed once per iteration into an
+//     LDS bitmask (F x F x H bits = 10 KB at F = 200) read by both passes;
+//   * weight gradients in registers across the block's samples, one partial row per block,
+//     column_reduce over blocks (deterministic).
+#include "il_kernels.hpp"
+
+namespace rs_il {
+namespace large {
+
+constexpr int NT = 256;
+constexpr int FMAXL = 256;
+
+template <int E_, int U_, int H_>
+struct LC {
+  static constexpr int E = E_, U = U_, H = H_, NC = 4 * U, DH = U / H;
+  static constexpr int NPARAM = E * NC + NC + 2 * U;
+  static constexpr int NRG = NT / NC;   // projection row groups
+  static constexpr int WK = (E * NC + NT - 1) / NT;  // dW entries per thread
+  static_assert(DH % 4 == 0 && E % 4 == 0 && U % 4 == 0, "16-byte rows");
+  static_assert(NC <= NT && NT % NC == 0, "projection mapping");
+  static_assert(NT % E == 0, "dx mapping");
+};
+
+struct LFwd {
+  const float *x, *W, *bias, *gamma, *beta;
+  int64_t B;
+  int F, L, use_res, drop;
+  float eps, drop_rate, inv_keep, sc2, inv_sdh;
+  uint64_t seed;
+  float *y, *xsave;
+  int64_t y_ld;
+};
+
+struct LBwd {
+  const float *x, *xsave, *dy, *W, *bias, *gamma, *beta;
+  int64_t dy_ld, B;
+  int F, L, use_res, drop;
+  float eps, drop_rate, inv_keep, sc2, inv_sdh;
+  uint64_t seed;
+  float* dx;
+  int dx_accumulate;
+  float* part;
+};
+
+template <int N>
+__device__ __forceinline__ void ld(float (&v)[N], const float* p) {
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) {
+    const float4 t = reinterpret_cast<const float4*>(p)[k];
+    v[4 * k] = t.x; v[4 * k + 1] = t.y; v[4 * k + 2] = t.z; v[4 * k + 3] = t.w;
+  }
+}
+template <int N>
+__device__ __forceinline__ void st(float* p, const float (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k)
+    reinterpret_cast<float4*>(p)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+template <int N>
+__device__ __forceinline__ float dot(const float (&a)[N], const float (&b)[N]) {
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < N; ++d) s = fmaf(a[d], b[d], s);
+  return s;
+}
+
+// projection: P_c[f] = relu(x_f . W[:, c] + b_c) into the Q|K|V|R region of column c
+template <class C>
+__device__ __forceinline__ void project(const float* xs, float* Qs, int F, const float (&wcol)[C::E],
+                                        float bc) {
+  const int t = threadIdx.x, c = t % C::NC, rg = t / C::NC;
+  float* dst = Qs + (c / C::U) * F * C::U + (c % C::U);
+  for (int f = rg; f < F; f += C::NRG) {
+    float xr[C::E];
+    ld<C::E>(xr, xs + f * C::E);
+    float acc = bc;
+#pragma unroll
+    for (int e = 0; e < C::E; ++e) acc = fmaf(xr[e], wcol[e], acc);
+    dst[f * C::U] = fmaxf(acc, 0.f);
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int F = a.F;
+  float* xs = sm;                          // [F][E]
+  float* Qs = xs + F * C::E;               // [F][U] x {Q, K, V, R}
+  float* Ks = Qs + F * C::U;
+  float* Vs = Ks + F * C::U;
+  float* Rs = Vs + F * C::U;
+  float* Os = Rs + F * C::U;               // [F][U]
+  const int t = threadIdx.x;
+  float wcol[C::E];
+  {
+    const int c = t % C::NC;
+#pragma unroll
+    for (int e = 0; e < C::E; ++e) wcol[e] = a.W[e * C::NC + c];
+  }
+  const float bc = a.bias[t % C::NC];
+  float gam[C::U], bet[C::U];
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) { gam[u] = a.gamma[u]; bet[u] = a.beta[u]; }
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const float4* xg = reinterpret_cast<const float4*>(a.x + b * F * C::E);
+    for (int k = t; k < F * C::E / 4; k += NT) reinterpret_cast<float4*>(xs)[k] = xg[k];
+    __syncthreads();
+    for (int it = 0; it < a.L; ++it) {
+      const uint32_t kb = a.drop ? dropout_sample_key(splitmix64(a.seed + (uint64_t)it), (uint32_t)b) : 0u;
+      project<C>(xs, Qs, F, wcol, bc);
+      __syncthreads();
+      for (int p = t; p < F * C::H; p += NT) {
+        const int h = p / F, i = p % F;
+        float q[C::DH];
+        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
+        float mx = -INFINITY;
+        for (int j = 0; j < F; ++j) {
+          float k[C::DH];
+          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+          mx = fmaxf(mx, dot<C::DH>(q, k));
+        }
+        const float msc = mx * a.sc2;
+        float l = 0.f, o[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
+        for (int j = 0; j < F; ++j) {
+          float k[C::DH], v[C::DH];
+          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
+          const float e = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc));
+          l += e;
+          const float ek = (!a.drop || dropout_keep_k(kb, h, i, j, a.drop_rate)) ? e : 0.f;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) o[d] = fmaf(ek, v[d], o[d]);
+        }
+        const float inv = (a.drop ? a.inv_keep : 1.f) / l;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] *= inv;
+        st<C::DH>(Os + i * C::U + h * C::DH, o);
+      }
+      __syncthreads();
+      const bool last = it == a.L - 1;
+      for (int i = t; i < F; i += NT) {
+        float z[C::U], r[C::U];
+        ld<C::U>(z, Os + i * C::U);
+        ld<C::U>(r, Rs + i * C::U);
+        float mean = 0.f;
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) {
+          z[u] = fmaxf(a.use_res ? z[u] + r[u] : z[u], 0.f);
+          mean += z[u];
+        }
+        mean *= 1.0f / C::U;
+        float var = 0.f;
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) var = fmaf(z[u] - mean, z[u] - mean, var);
+        var *= 1.0f / C::U;
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) z[u] = fmaf((z[u] - mean) * rstd, gam[u], bet[u]);
+        if (last) {
+          st<C::U>(a.y + b * a.y_ld + i * C::U, z);
+        } else {  // E == U (tied weights): the output is the next iteration's input
+          st<C::U>(xs + i * C::E, z);
+          st<C::U>(a.xsave + ((int64_t)it * a.B + b) * F * C::U + i * C::U, z);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int F = a.F;
+  const int W32 = (F + 31) / 32;
+  float* xs = sm;                          // [F][E]
+  float* Qs = xs + F * C::E;               // Q | K | V | R (R becomes dR)
+  float* Ks = Qs + F * C::U;
+  float* Vs = Ks + F * C::U;
+  float* Rs = Vs + F * C::U;
+  float* Os = Rs + F * C::U;               // O, then dQ
+  float* Gs = Os + F * C::U;               // dY -> dA (= dO) -> dx of this iteration
+  float* DKs = Gs + F * C::U;
+  float* DVs = DKs + F * C::U;
+  float* stm = DVs + F * C::U;             // [H][F] scaled max
+  float* sti = stm + C::H * F;             // [H][F] 1 / sum
+  float* std_ = sti + C::H * F;            // [H][F] D = dO . O
+  uint32_t* mask = reinterpret_cast<uint32_t*>(std_ + C::H * F);  // [H][F][W32]
+  const int t = threadIdx.x;
+  float wcol[C::E];
+  {
+    const int c = t % C::NC;
+#pragma unroll
+    for (int e = 0; e < C::E; ++e) wcol[e] = a.W[e * C::NC + c];
+  }
+  const float bc = a.bias[t % C::NC];
+  float gam[C::U];
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) gam[u] = a.gamma[u];
+  float bet[C::U];
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) bet[u] = a.beta[u];
+  // dx mapping: thread -> (row group, e); the row of W for e in registers
+  const int xe = t % C::E, xrg = t / C::E;
+  constexpr int XRG = NT / C::E;
+  float wrow[C::NC];
+#pragma unroll
+  for (int c = 0; c < C::NC; ++c) wrow[c] = a.W[xe * C::NC + c];
+  float dw[C::WK];
+#pragma unroll
+  for (int k = 0; k < C::WK; ++k) dw[k] = 0.f;
+  float dbc = 0.f, dg[C::U], dbt[C::U];
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) { dg[u] = 0.f; dbt[u] = 0.f; }
+
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    for (int it = a.L - 1; it >= 0; --it) {
+      const float* xin = it == 0 ? a.x + b * F * C::E : a.xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U;
+      for (int k = t; k < F * C::E / 4; k += NT)
+        reinterpret_cast<float4*>(xs)[k] = reinterpret_cast<const float4*>(xin)[k];
+      if (it == a.L - 1) {
+        for (int k = t; k < F * C::U / 4; k += NT) {
+          const int i = k / (C::U / 4), q4 = k % (C::U / 4);
+          reinterpret_cast<float4*>(Gs)[k] =
+              reinterpret_cast<const float4*>(a.dy + b * a.dy_ld + i * C::U)[q4];
+        }
+      }
+      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint32_t kb = a.drop ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
+      __syncthreads();
+      project<C>(xs, Qs, F, wcol, bc);
+      if (a.drop) {
+        for (int p = t; p < F * C::H; p += NT) {
+          const int h = p / F, i = p % F;
+          for (int w = 0; w < W32; ++w) {
+            uint32_t bits = 0;
+            for (int jj = 0; jj < 32; ++jj) {
+              const int j = 32 * w + jj;
+              if (j < F && dropout_keep_k(kb, h, i, j, a.drop_rate)) bits |= 1u << jj;
+            }
+            mask[(h * F + i) * W32 + w] = bits;
+          }
+        }
+      }
+      __syncthreads();
+      // ---- recompute the attention forward: stats and O ----
+      for (int p = t; p < F * C::H; p += NT) {
+        const int h = p / F, i = p % F;
+        float q[C::DH];
+        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
+        float mx = -INFINITY;
+        for (int j = 0; j < F; ++j) {
+          float k[C::DH];
+          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+          mx = fmaxf(mx, dot<C::DH>(q, k));
+        }
+        const float msc = mx * a.sc2;
+        float l = 0.f, o[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
+        const uint32_t* mrow = mask + (h * F + i) * W32;
+        for (int j = 0; j < F; ++j) {
+          float k[C::DH], v[C::DH];
+          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
+          const float e = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc));
+          l += e;
+          const float ek = (!a.drop || ((mrow[j >> 5] >> (j & 31)) & 1u)) ? e : 0.f;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) o[d] = fmaf(ek, v[d], o[d]);
+        }
+        const float il = 1.0f / l;
+        const float inv = (a.drop ? a.inv_keep : 1.f) * il;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] *= inv;
+        st<C::DH>(Os + i * C::U + h * C::DH, o);
+        stm[h * F + i] = msc;
+        sti[h * F + i] = il;
+      }
+      __syncthreads();
+      // ---- epilogue backward: LN, ReLU, residual; D = dO . O per (head, row) ----
+      for (int i = t; i < F; i += NT) {
+        float o[C::U], r[C::U], z[C::U], g[C::U];
+        ld<C::U>(o, Os + i * C::U);
+        ld<C::U>(r, Rs + i * C::U);
+        ld<C::U>(g, Gs + i * C::U);
+        float mean = 0.f;
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) {
+          z[u] = fmaxf(a.use_res ? o[u] + r[u] : o[u], 0.f);
+          mean += z[u];
+        }
+        mean *= 1.0f / C::U;
+        float var = 0.f;
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) var = fmaf(z[u] - mean, z[u] - mean, var);
+        var *= 1.0f / C::U;
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        float m1 = 0.f, m2 = 0.f, xh[C::U];
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) {
+          xh[u] = (z[u] - mean) * rstd;
+          dg[u] = fmaf(g[u], xh[u], dg[u]);
+          dbt[u] += g[u];
+          const float gd = g[u] * gam[u];
+          m1 += gd;
+          m2 = fmaf(gd, xh[u], m2);
+        }
+        m1 *= 1.0f / C::U;
+        m2 *= 1.0f / C::U;
+        float da[C::U], dr[C::U];
+#pragma unroll
+        for (int u = 0; u < C::U; ++u) {
+          const float dz = rstd * (g[u] * gam[u] - m1 - xh[u] * m2);
+          da[u] = z[u] > 0.f ? dz : 0.f;
+          dr[u] = (a.use_res && r[u] > 0.f) ? da[u] : 0.f;
+        }
+        st<C::U>(Gs + i * C::U, da);
+        st<C::U>(Rs + i * C::U, dr);
+#pragma unroll
+        for (int h = 0; h < C::H; ++h) {
+          float dsum = 0.f;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) dsum = fmaf(da[h * C::DH + d], o[h * C::DH + d], dsum);
+          std_[h * F + i] = dsum;
+        }
+      }
+      __syncthreads();
+      // ---- pass A (thread = query row): dQ; pass B (thread = key row): dK, dV ----
+      for (int p = t; p < F * C::H; p += NT) {
+        const int h = p / F, i = p % F;
+        float q[C::DH], g[C::DH], dq[C::DH];
+        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
+        ld<C::DH>(g, Gs + i * C::U + h * C::DH);
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
+        const float msc = stm[h * F + i], il = sti[h * F + i], D = std_[h * F + i];
+        const uint32_t* mrow = mask + (h * F + i) * W32;
+        for (int j = 0; j < F; ++j) {
+          float k[C::DH], v[C::DH];
+          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
+          const float pe = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc)) * il;
+          float dP = dot<C::DH>(g, v);
+          if (a.drop) dP = ((mrow[j >> 5] >> (j & 31)) & 1u) ? dP * a.inv_keep : 0.f;
+          const float dS = pe * (dP - D);
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) dq[d] = fmaf(dS, k[d], dq[d]);
+        }
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dq[d] = q[d] > 0.f ? dq[d] * a.inv_sdh : 0.f;
+        st<C::DH>(Os + i * C::U + h * C::DH, dq);
+      }
+      for (int p = t; p < F * C::H; p += NT) {
+        const int h = p / F, j = p % F;
+        float k[C::DH], v[C::DH], dk[C::DH], dv[C::DH];
+        ld<C::DH>(k, Ks + j * C::U + h * C::DH);
+        ld<C::DH>(v, Vs + j * C::U + h * C::DH);
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+        const int jw = j >> 5;
+        const uint32_t jb = 1u << (j & 31);
+        for (int i = 0; i < F; ++i) {
+          float q[C::DH], g[C::DH];
+          ld<C::DH>(q, Qs + i * C::U + h * C::DH);
+          ld<C::DH>(g, Gs + i * C::U + h * C::DH);
+          const float pe = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -stm[h * F + i])) *
+                           sti[h * F + i];
+          float dP = dot<C::DH>(g, v), pd = pe;
+          if (a.drop) {
+            const bool keep = (mask[(h * F + i) * W32 + jw] & jb) != 0u;
+            dP = keep ? dP * a.inv_keep : 0.f;
+            pd = keep ? pe * a.inv_keep : 0.f;
+          }
+          const float dS = pe * (dP - std_[h * F + i]);
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) {
+            dk[d] = fmaf(dS, q[d], dk[d]);
+            dv[d] = fmaf(pd, g[d], dv[d]);
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) {
+          dk[d] = k[d] > 0.f ? dk[d] * a.inv_sdh : 0.f;
+          dv[d] = v[d] > 0.f ? dv[d] : 0.f;
+        }
+        st<C::DH>(DKs + j * C::U + h * C::DH, dk);
+        st<C::DH>(DVs + j * C::U + h * C::DH, dv);
+      }
+      __syncthreads();
+      // ---- projection backward: dZ = [dQ (Os) | dK | dV | dR (Rs)] ----
+      auto dzb = [&](int c) -> const float* {
+        const int g = c / C::U;
+        return (g == 0 ? Os : g == 1 ? DKs : g == 2 ? DVs : Rs) + (c % C::U);
+      };
+#pragma unroll
+      for (int k = 0; k < C::WK; ++k) {
+        const int idx = t + NT * k;
+        if (idx < C::E * C::NC) {
+          const int e = idx / C::NC, c = idx % C::NC;
+          const float* dz = dzb(c);
+          float s = 0.f;
+          for (int f = 0; f < F; ++f) s = fmaf(xs[f * C::E + e], dz[f * C::U], s);
+          dw[k] += s;
+        }
+      }
+      if (t < C::NC) {
+        const float* dz = dzb(t);
+        float s = 0.f;
+        for (int f = 0; f < F; ++f) s += dz[f * C::U];
+        dbc += s;
+      }
+      for (int f = xrg; f < F; f += XRG) {
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::NC; ++c) s = fmaf(dzb(c)[f * C::U], wrow[c], s);
+        if (it == 0) {
+          float* dst = a.dx + b * F * C::E + f * C::E + xe;
+          *dst = a.dx_accumulate ? *dst + s : s;
+        } else {
+          Gs[f * C::U + xe] = s;  // E == U: dY of iteration it - 1
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // ---- block partial: [dW (E*NC) | db (NC) | dgamma (U) | dbeta (U)] ----
+  float* red = sm;  // [NT][2U]
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) {
+    red[t * 2 * C::U + u] = dg[u];
+    red[t * 2 * C::U + C::U + u] = dbt[u];
+  }
+  __syncthreads();
+  float* pr = a.part + (int64_t)blockIdx.x * C::NPARAM;
+#pragma unroll
+  for (int k = 0; k < C::WK; ++k) {
+    const int idx = t + NT * k;
+    if (idx < C::E * C::NC) pr[idx] = dw[k];
+  }
+  if (t < C::NC) pr[C::E * C::NC + t] = dbc;
+  if (t < 2 * C::U) {
+    float s = 0.f;
+    for (int r = 0; r < NT; ++r) s += red[r * 2 * C::U + t];
+    pr[C::E * C::NC + C::NC + t] = s;
+  }
+}
+
+inline size_t fwd_lds(int F, int E, int U) { return (size_t)F * (E + 5 * U) * 4; }
+inline size_t bwd_lds(int F, int E, int U, int H) {
+  const size_t main = (size_t)F * (E + 8 * U) * 4 + (size_t)3 * H * F * 4 +
+                      (size_t)H * F * ((F + 31) / 32) * 4;
+  const size_t red = (size_t)NT * 2 * U * 4;
+  return main > red ? main : red;
+}
+
+template <int E, int U, int H>
+int run_fwd(const FwdReq& q) {
+  using C = LC<E, U, H>;
+  LFwd a{q.x, q.W, q.bias, q.gamma, q.beta, q.B, q.F, q.L, q.use_res, q.drop_rate > 0.f,
+         q.eps, q.drop_rate, q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
+         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, q.y,
+         q.xsave, q.y_ld};
+  if (q.B == 0) return RS_OK;
+  const size_t lds = fwd_lds(q.F, E, U);
+  int64_t grid = q.B < 4096 ? q.B : 4096;
+  fwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
+  return rs_status_after_launch();
+}
+
+template <int E, int U, int H>
+int run_bwd(const BwdReq& q) {
+  using C = LC<E, U, H>;
+  if (q.B == 0) return RS_OK;
+  int64_t grid = q.B < kMaxBwdGrid ? q.B : kMaxBwdGrid;
+  if (q.workspace_floats < grid * C::NPARAM) return RS_ERR_ARG;
+  LBwd a{q.x, q.xsave, q.dy, q.W, q.bias, q.gamma, q.beta, q.dy_ld, q.B, q.F, q.L, q.use_res,
+         q.drop_rate > 0.f, q.eps, q.drop_rate,
+         q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
+         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, q.dx,
+         q.dx_accumulate, q.workspace};
+  const size_t lds = bwd_lds(q.F, E, U, H);
+  bwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
+  int st = rs_status_after_launch();
+  if (st || !q.dparams) return st;
+  launch_column_reduce(q.stream, q.workspace, (int)grid, C::NPARAM, C::NPARAM, C::NPARAM,
+                       q.dparams, nullptr, q.dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+}  // namespace large
+
+// F in (64, 256]: the many-field instantiations (config 3 is E = U = 8, H = 2).
+int il_large_fwd(const FwdReq& q) {
+  if (q.F > large::FMAXL || (q.L > 1 && q.E != q.U)) return RS_ERR_UNSUPPORTED;
+  if (large::fwd_lds(q.F, q.E, q.U) > 64 * 1024) return RS_ERR_UNSUPPORTED;
+  if (q.E == 8 && q.U == 8 && q.H == 2) return large::run_fwd<8, 8, 2>(q);
+  if (q.E == 8 && q.U == 8 && q.H == 1) return large::run_fwd<8, 8, 1>(q);
+  if (q.E == 16 && q.U == 16 && q.H == 2) return large::run_fwd<16, 16, 2>(q);
+  return RS_ERR_UNSUPPORTED;
+}
+
+int il_large_bwd(const BwdReq& q) {
+  if (q.F > large::FMAXL || (q.L > 1 && q.E != q.U)) return RS_ERR_UNSUPPORTED;
+  if (large::bwd_lds(q.F, q.E, q.U, q.H) > 160 * 1024) return RS_ERR_UNSUPPORTED;
+  if (q.E == 8 && q.U == 8 && q.H == 2) return large::run_bwd<8, 8, 2>(q);
+  if (q.E == 8 && q.U == 8 && q.H == 1) return large::run_bwd<8, 8, 1>(q);
+  if (q.E == 16 && q.U == 16 && q.H == 2) return large::run_bwd<16, 16, 2>(q);
+  return RS_ERR_UNSUPPORTED;
+}
+
+}  // namespace rs_il

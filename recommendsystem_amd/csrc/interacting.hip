@@ -7,6 +7,8 @@ namespace rs_il {
 RS_IL_DECLARE_UNIT(il_unit_a)
 RS_IL_DECLARE_UNIT(il_unit_b)
 RS_IL_DECLARE_UNIT(il_unit_c)
+int il_large_fwd(const FwdReq& q);  // il_large.hip: F in (64, 256]
+int il_large_bwd(const BwdReq& q);
 
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
                    int accumulate) {
@@ -38,6 +40,7 @@ RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int 
   if (drop_rate < 0.f || drop_rate >= 1.f || y_ld < (int64_t)F * U) return RS_ERR_ARG;
   rs_il::FwdReq q{rs_stream(stream), x, W, bias, gamma, beta, B, F, E, U, H, L, use_res,
                   eps, drop_rate, seed, y, xsave, y_ld};
+  if (F > 64) return rs_il::il_large_fwd(q);
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
@@ -58,6 +61,7 @@ RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const flo
   rs_il::BwdReq q{rs_stream(stream), x, xsave, dy, W, bias, gamma, beta, dy_ld, B, F, E, U, H, L,
                   use_res, eps, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
                   workspace, workspace_floats};
+  if (F > 64) return rs_il::il_large_bwd(q);
   int r = rs_il::il_unit_a_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);

@@ -125,6 +125,10 @@ IL_CASES = [  # (B, F, E, U, H, L, use_res)
     (5, 26, 16, 8, 2, 1, True),
     (6, 13, 32, 32, 2, 2, True),
     (4, 26, 16, 128, 1, 1, True),    # constructor defaults (config 1): forward only
+    (5, 200, 8, 8, 2, 1, True),      # config 3 multi_head IL(1, 8, 2) over 200 fields (il_large)
+    (3, 130, 8, 8, 2, 2, True),      # many fields, tied iterations
+    (4, 97, 16, 16, 2, 2, False),
+    (3, 256, 8, 8, 1, 1, True),
 ]
 
 
@@ -198,6 +202,40 @@ def test_interacting_dropout_mask_matches_oracle():
     tr.interacting_layer(xr, Wt, bt, gt, bet, L, H, True, drop_rate=0.2, seed=seed).sum().backward()
     assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dropout dx")
     assert_grad_close(_np(il.kernel.grad), Wt.grad.numpy(), what="dropout dW")
+
+
+@pytest.mark.parametrize("F,L", [(200, 1), (150, 2)])
+def test_interacting_many_fields_dropout(F, L):
+    """The config-3 layer as used in training: IL(1, 8, 2, use_dropout=True, dropout_rate=0.2)
+    over 200 fields (rank/multi_head/multidnn.py:54): forward and backward through the same
+    counter-based mask as the oracle."""
+    from recommendsystem_amd.layers import InteractingLayer
+    B, E, U, H = 4, 8, 8, 2
+    rng = np.random.default_rng(12)
+    x = rng.uniform(-0.5, 0.5, size=(B, F, E)).astype(np.float32)
+    il = InteractingLayer(L, U, H, use_dropout=True, dropout_rate=0.2, seed=13, device=DEV)
+    il.train()
+    il.build((B, F, E), device=DEV)
+    with torch.no_grad():
+        il.bias.uniform_(-0.1, 0.1)
+        il.gamma.uniform_(0.5, 1.5)
+    seed = (il.seed * 1000003 + il._calls) & 0xFFFFFFFFFFFFFFFF
+    xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    y = il(xd)
+    W, b, g, be = _il_ref_params(il)
+    ref = npo.interacting_layer(x.astype(np.float64), W, b, g, be, L, H, True, drop_rate=0.2, seed=seed)
+    assert_close(_np(y), ref, 2e-5, what="IL many-field dropout fwd")
+    dy = rng.normal(size=(B, F, U)).astype(np.float32)
+    y.backward(torch.from_numpy(dy).to(DEV))
+    Wt, bt, gt, bet = (torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il))
+    xr = torch.from_numpy(x).double().requires_grad_(True)
+    tr.interacting_layer(xr, Wt, bt, gt, bet, L, H, True, drop_rate=0.2, seed=seed).backward(
+        torch.from_numpy(dy).double())
+    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dx")
+    assert_grad_close(_np(il.kernel.grad), Wt.grad.numpy(), what="dW")
+    assert_grad_close(_np(il.bias.grad), bt.grad.numpy(), what="db")
+    assert_grad_close(_np(il.gamma.grad), gt.grad.numpy(), what="dgamma")
+    assert_grad_close(_np(il.beta.grad), bet.grad.numpy(), what="dbeta")
 
 
 def test_interacting_rank_error():

@@ -16,6 +16,19 @@ def gold(name):
     return np.load(os.path.join(GOLD, name), allow_pickle=False)
 
 
+def test_fmix32_known_answers():
+    """murmur3 fmix32 (the dropout-mask finaliser): published values fmix32(0) = 0,
+    fmix32(1) = 0x514E28B7."""
+    out = npo.fmix32(np.array([0, 1], dtype=np.uint32))
+    assert out.tolist() == [0, 0x514E28B7]
+
+
+def test_dropout_mask_rate():
+    keep = npo.dropout_keep(npo.layer_seed(7, 0), np.arange(64)[:, None, None, None], 1,
+                            np.arange(40)[None, :, None, None], np.arange(40)[None, None, :, None], 0.2)
+    assert abs(1.0 - keep.mean() - 0.2) < 0.01
+
+
 def test_splitmix64_known_answers():
     d = gold("splitmix64_kat.npz")
     assert np.array_equal(npo.splitmix64(d["seeds"]), d["expect"])
