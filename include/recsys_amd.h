@@ -238,6 +238,33 @@ int rs_rowdot(void* stream, const float* U, int64_t ldu, const float* V, int64_t
 int rs_mse_rows(void* stream, const float* S, int64_t lds, const float* T, int64_t ldt, int64_t M,
                 int N, float gscale, float* loss_rows, float* dS, int64_t ldds);
 
+/* T independent Dense(1, act) heads (rank/multi_head/multidnn.py:122-204 towers): head t reads
+ * X columns [t*D, t*D + D), kernel W[t*D .. t*D + D), bias b[t]; Y[m*ldy + t].  T*D <= 256,
+ * D a power of two <= 64.  Backward: dX (nullable), dparams = [dW (T*D) | db (T)]. */
+int rs_grouped_head_fwd(void* stream, const float* X, int64_t ldx, int64_t M, int T, int D,
+                        const float* W, const float* b, int act, float* Y, int64_t ldy);
+int64_t rs_grouped_head_bwd_workspace_floats(int64_t M, int T, int D);
+int rs_grouped_head_bwd(void* stream, const float* X, int64_t ldx, int64_t M, int T, int D,
+                        const float* W, const float* Y, int64_t ldy, int act, const float* dY,
+                        int64_t lddy, float* dX, int64_t lddx, float* dparams,
+                        int dparams_accumulate, float* workspace, int64_t workspace_floats);
+/* tf.where(mask == 1, A, B) per row (rough_rank/model.py:52-53): forward Y, or with dY the
+ * routed gradients dA / dB ([M, N] contiguous, nullable). */
+int rs_row_select(void* stream, const float* mask, const float* A, int64_t lda, const float* B,
+                  int64_t ldb, int64_t M, int N, float* Y, int64_t ldy, const float* dY,
+                  float* dA, float* dB);
+
+/* Per-row (sample-weighted) binary cross entropy, contiguous [M, T]: staytime/model.py:33-36
+ * cross_entropy with Keras sample weights; rough_rank BinaryCrossentropy with lo = eps,
+ * hi = 1 - eps.  loss_rows[m] = w_m sum_t ce (nullable), dP = gscale w_m dce/dp (nullable). */
+int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, int T, float lo, float hi,
+                float log_eps, const float* W, float gscale, float* loss_rows, float* dP);
+
+/* Elementwise activation of a contiguous [n] tensor (tf.sigmoid of the rough_rank logits,
+ * rough_rank/model.py:80,146): Y = act(X); backward dX = dY * act'(Y). */
+int rs_act_fwd(void* stream, const float* X, int64_t n, int act, float* Y);
+int rs_act_bwd(void* stream, const float* Y, const float* dY, int64_t n, int act, float* dX);
+
 /* H4/H10  tf.clip_by_value(s, lo, hi) (autoint:52) + cross_entropy (rank/ctr/base_model.py:7-12):
  * loss[0] = mean_b sum_t [-y log(p+log_eps) - (1-y) log(1-p+log_eps)], p_out = clipped s,
  * ds = gscale[0] * dloss/ds (zero outside [lo, hi]; gscale NULL = 1).  Any output pointer
@@ -255,6 +282,10 @@ int rs_bce_clip_loss(void* stream, const float* s, const float* y, int64_t M, in
 int rs_dense_adam(void* stream, float* params, float* grads, float* m, float* v, int64_t n,
                   int64_t* step, float lr, float beta1, float beta2, float eps, float grad_scale,
                   int zero_grad);
+
+/* Keras kernel regularisers as a gradient term (L1L2 at rank/multi_head/multidnn.py:62-63,
+ * L2 at :85,103 and rough_rank/layer.py:77): grads += l1 * sign(w) + 2 * l2 * w. */
+int rs_l1l2_grad(void* stream, const float* params, float* grads, int64_t n, float l1, float l2);
 
 #ifdef __cplusplus
 }

@@ -84,6 +84,15 @@ SIGNATURES: dict[str, tuple] = {
     "rs_rowdot": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64, _vp,
                          _i64]),
     "rs_mse_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _i64]),
+    "rs_grouped_head_bwd_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_grouped_head_fwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _i64]),
+    "rs_grouped_head_bwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _i64, _i32, _vp,
+                                   _i64, _vp, _i64, _vp, _i32, _vp, _i64]),
+    "rs_row_select": (_i32, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "rs_l1l2_grad": (_i32, [_vp, _vp, _vp, _i64, _f32, _f32]),
+    "rs_act_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
+    "rs_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "rs_bce_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _f32, _vp, _vp]),
 }
 
 _LIB = None

@@ -240,3 +240,26 @@ RS_API int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* 
       rows, grads, count, dim, lps, grad_table, flag, touched, n_touched, touched_cap);
   return rs_status_after_launch();
 }
+
+// Keras kernel regularisers folded into the gradient (rank/multi_head/multidnn.py:62-63
+// L1L2(1e-5, 1e-5); :85,103 L2(0.01); rough_rank/layer.py:77 L2(l2_reg)):
+//   loss += l1 * sum|w| + l2 * sum w^2   =>   grad += l1 * sign(w) + 2 * l2 * w  (tf.sign(0) = 0)
+__global__ void l1l2_grad_kernel(const float* __restrict__ w, float* __restrict__ g, int64_t n,
+                                 float l1, float l2) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float x = w[i];
+    const float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+    g[i] += fmaf(l1, sg, 2.f * l2 * x);
+  }
+}
+
+RS_API int rs_l1l2_grad(void* stream, const float* params, float* grads, int64_t n, float l1,
+                        float l2) {
+  if (!params || !grads || n < 0) return RS_ERR_ARG;
+  if (n == 0) return RS_OK;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  l1l2_grad_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(params, grads, n, l1, l2);
+  return rs_status_after_launch();
+}

@@ -1006,3 +1006,235 @@ RS_API int rs_mse_rows(void* stream, const float* S, int64_t lds, const float* T
                                                                  loss_rows, dS, ldds);
   return rs_status_after_launch();
 }
+
+// ------------------------------- grouped per-task heads ----------------------------------------
+// T independent Dense(1, act) heads, head t reading columns [t*D, (t+1)*D) of X
+// (rank/multi_head/multidnn.py:122-204: one Dense(1, sigmoid) tower per gated task output).
+// W [T*D] (head t's kernel is W[t*D .. t*D+D)), b [T].  One wave per row, D-lane groups reduce.
+namespace rs_tw {
+template <int D>
+__global__ void __launch_bounds__(256) grouped_head_fwd_kernel(const float* __restrict__ X,
+                                                               int64_t ldx, int64_t M, int T,
+                                                               const float* __restrict__ W,
+                                                               const float* __restrict__ b,
+                                                               int act, float* __restrict__ Y,
+                                                               int64_t ldy) {
+  const int l = lane_id();
+  const int n = T * D;
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < M; m += (int64_t)gridDim.x * 4) {
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int idx = c0 + l;
+      const float v = idx < n ? X[m * ldx + idx] * W[idx] : 0.f;
+      const float s = group_sum<D>(v);
+      const int t = idx / D;
+      if (idx < n && (idx % D) == 0) Y[m * ldy + t] = act_f(s + b[t], act);
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) grouped_head_bwd_kernel(
+    const float* __restrict__ X, int64_t ldx, int64_t M, int T, const float* __restrict__ W,
+    const float* __restrict__ Y, int64_t ldy, int act, const float* __restrict__ dY, int64_t lddy,
+    float* __restrict__ dX, int64_t lddx, float* __restrict__ part) {
+  // part[block][T*D + T]: dW then db; lanes own columns idx = c0 + lane
+  constexpr int MAXC = 4;  // T*D <= 256
+  const int l = lane_id();
+  const int n = T * D;
+  float gw[MAXC] = {0.f, 0.f, 0.f, 0.f}, gb[MAXC] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < M; m += (int64_t)gridDim.x * 4) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int idx = c * 64 + l;
+      if (idx < n) {
+        const int t = idx / D;
+        const float y = Y[m * ldy + t];
+        float dz = dY[m * lddy + t];
+        if (act == ACT_RELU) dz = y > 0.f ? dz : 0.f;
+        else if (act == ACT_SIGMOID) dz *= y * (1.f - y);
+        const float x = X[m * ldx + idx];
+        if (dX) dX[m * lddx + idx] = dz * W[idx];
+        gw[c] = fmaf(x, dz, gw[c]);
+        if (idx % D == 0) gb[c] += dz;
+      }
+    }
+  }
+  __shared__ float red[4][256 + 64];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int idx = c * 64 + l;
+    red[wave_id()][idx] = gw[c];
+    if (idx % D == 0 && idx < n) red[wave_id()][256 + idx / D] = gb[c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n + T; i += blockDim.x) {
+    const int src = i < n ? i : 256 + (i - n);
+    part[(int64_t)blockIdx.x * (n + T) + i] = (red[0][src] + red[1][src]) + (red[2][src] + red[3][src]);
+  }
+}
+
+__global__ void row_select_kernel(const float* __restrict__ mask, const float* __restrict__ A,
+                                  int64_t lda, const float* __restrict__ Bm, int64_t ldb,
+                                  int64_t M, int N, float* __restrict__ Y, int64_t ldy,
+                                  const float* __restrict__ dY, float* __restrict__ dA,
+                                  float* __restrict__ dB) {
+  const int64_t n = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N, c = i % N;
+    const bool on = mask[m] == 1.0f;
+    if (Y) Y[m * ldy + c] = on ? A[m * lda + c] : Bm[m * ldb + c];
+    if (dY) {
+      const float d = dY[m * ldy + c];
+      if (dA) dA[m * N + c] = on ? d : 0.f;
+      if (dB) dB[m * N + c] = on ? 0.f : d;
+    }
+  }
+}
+}  // namespace rs_tw
+
+static int gh_grid(int64_t M) { return (int)(M < 4 * 256 ? (M + 3) / 4 : 256); }
+
+RS_API int64_t rs_grouped_head_bwd_workspace_floats(int64_t M, int T, int D) {
+  if (M <= 0 || T <= 0 || D <= 0) return 0;
+  return (int64_t)gh_grid(M) * (T * D + T);
+}
+
+#define RS_GH_SWITCH(DD, CALL) \
+  switch (DD) {                \
+    case 1: CALL(1); break;    \
+    case 2: CALL(2); break;    \
+    case 4: CALL(4); break;    \
+    case 8: CALL(8); break;    \
+    case 16: CALL(16); break;  \
+    case 32: CALL(32); break;  \
+    case 64: CALL(64); break;  \
+    default: return RS_ERR_UNSUPPORTED; \
+  }
+
+RS_API int rs_grouped_head_fwd(void* stream, const float* X, int64_t ldx, int64_t M, int T, int D,
+                               const float* W, const float* b, int act, float* Y, int64_t ldy) {
+  if (!X || !W || !b || !Y || M < 0 || T <= 0 || D <= 0) return RS_ERR_ARG;
+  if (T * D > 256) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  hipStream_t s = rs_stream(stream);
+  const int grid = rows_grid(M, 4);
+#define RS_GHF(DD) grouped_head_fwd_kernel<DD><<<grid, 256, 0, s>>>(X, ldx, M, T, W, b, act, Y, ldy)
+  RS_GH_SWITCH(D, RS_GHF)
+#undef RS_GHF
+  return rs_status_after_launch();
+}
+
+RS_API int rs_grouped_head_bwd(void* stream, const float* X, int64_t ldx, int64_t M, int T, int D,
+                               const float* W, const float* Y, int64_t ldy, int act,
+                               const float* dY, int64_t lddy, float* dX, int64_t lddx,
+                               float* dparams, int dparams_accumulate, float* workspace,
+                               int64_t workspace_floats) {
+  if (!X || !W || !Y || !dY || M < 0 || T <= 0 || D <= 0) return RS_ERR_ARG;
+  if (T * D > 256) return RS_ERR_UNSUPPORTED;
+  if (M == 0) return RS_OK;
+  const int grid = gh_grid(M);
+  const int64_t np = (int64_t)T * D + T;
+  if (!workspace || workspace_floats < grid * np) return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+#define RS_GHB(DD)                                                                               \
+  grouped_head_bwd_kernel<DD><<<grid, 256, 0, s>>>(X, ldx, M, T, W, Y, ldy, act, dY, lddy, dX,   \
+                                                   lddx, workspace)
+  RS_GH_SWITCH(D, RS_GHB)
+#undef RS_GHB
+  int st = rs_status_after_launch();
+  if (st || !dparams) return st;
+  launch_column_reduce(s, workspace, grid, np, np, np, dparams, dparams, dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_row_select(void* stream, const float* mask, const float* A, int64_t lda,
+                         const float* Bm, int64_t ldb, int64_t M, int N, float* Y, int64_t ldy,
+                         const float* dY, float* dA, float* dB) {
+  if (!mask || M < 0 || N <= 0 || (!Y && !dY)) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  int64_t grid = (M * N + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  row_select_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(mask, A, lda, Bm, ldb, M, N, Y, ldy,
+                                                            dY, dA, dB);
+  return rs_status_after_launch();
+}
+
+// ------------------------------- elementwise activation ----------------------------------------
+// tf.sigmoid / relu on a [M, N] tensor (rough_rank/model.py:30-33,80 teacher / student
+// probabilities from their logits).
+namespace rs_tw {
+__global__ void act_fwd_kernel(const float* __restrict__ X, int64_t n, int act, float* __restrict__ Y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    Y[i] = act_f(X[i], act);
+}
+__global__ void act_bwd_kernel(const float* __restrict__ Y, const float* __restrict__ dY, int64_t n,
+                               int act, float* __restrict__ dX) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float y = Y[i];
+    float d = dY[i];
+    if (act == ACT_RELU) d = y > 0.f ? d : 0.f;
+    else if (act == ACT_SIGMOID) d *= y * (1.f - y);
+    dX[i] = d;
+  }
+}
+}  // namespace rs_tw
+
+RS_API int rs_act_fwd(void* stream, const float* X, int64_t n, int act, float* Y) {
+  if (!X || !Y || n < 0) return RS_ERR_ARG;
+  if (n == 0) return RS_OK;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  act_fwd_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(X, n, act, Y);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_act_bwd(void* stream, const float* Y, const float* dY, int64_t n, int act, float* dX) {
+  if (!Y || !dY || !dX || n < 0) return RS_ERR_ARG;
+  if (n == 0) return RS_OK;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  act_bwd_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(Y, dY, n, act, dX);
+  return rs_status_after_launch();
+}
+
+// ------------------------------- per-row weighted cross entropy --------------------------------
+// staytime/model.py:33-36 cross_entropy (per element, p unclipped, +1e-6 inside the logs) with
+// Keras sample weights (parse.py:64): loss_rows[m] = w_m * sum_t ce(y, clip(p)); ds = gscale *
+// w_m * dce/dp (zero outside [lo, hi], TF ClipByValue gradient).
+namespace rs_tw {
+__global__ void bce_rows_kernel(const float* __restrict__ P, const float* __restrict__ Y, int64_t M,
+                                int T, float lo, float hi, float log_eps,
+                                const float* __restrict__ W, float gscale,
+                                float* __restrict__ loss_rows, float* __restrict__ dP) {
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M;
+       m += (int64_t)gridDim.x * blockDim.x) {
+    const float w = W ? W[m] : 1.f;
+    float l = 0.f;
+    for (int t = 0; t < T; ++t) {
+      const float p0 = P[m * T + t], y = Y[m * T + t];
+      const float p = fminf(fmaxf(p0, lo), hi);
+      l += -y * logf(p + log_eps) - (1.f - y) * logf(1.f - p + log_eps);
+      if (dP) {
+        const float d = -y / (p + log_eps) + (1.f - y) / (1.f - p + log_eps);
+        dP[m * T + t] = (p0 >= lo && p0 <= hi) ? gscale * w * d : 0.f;
+      }
+    }
+    if (loss_rows) loss_rows[m] = w * l;
+  }
+}
+}  // namespace rs_tw
+
+RS_API int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, int T, float lo,
+                       float hi, float log_eps, const float* W, float gscale, float* loss_rows,
+                       float* dP) {
+  if (!P || !Y || M < 0 || T <= 0) return RS_ERR_ARG;
+  if (M == 0) return RS_OK;
+  int64_t grid = (M + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  bce_rows_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(P, Y, M, T, lo, hi, log_eps, W, gscale,
+                                                          loss_rows, dP);
+  return rs_status_after_launch();
+}

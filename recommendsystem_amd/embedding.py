@@ -190,17 +190,18 @@ class _SeqLookupFn(torch.autograd.Function):
         dev = ids.device
         out = torch.empty(B, T, t.dim, device=dev, dtype=torch.float32)
         mask = torch.empty(B, T, device=dev, dtype=torch.uint8)
+        lengths = torch.empty(B, device=dev, dtype=torch.int32)
         rows = torch.empty(B * T, device=dev, dtype=torch.int32)
         call("rs_sequence_lookup_fwd", stream_handle(), ptr(ids), ptr(offsets), B, T,
              layer.row_base, layer.bucket, layer.hash_mode, ptr(t.weight), t.dim, ptr(out), T * t.dim,
-             t.dim, ptr(mask), T, None, ptr(rows))
+             t.dim, ptr(mask), T, ptr(lengths), ptr(rows))
         ctx.layer, ctx.B = layer, B
         ctx.save_for_backward(rows)
-        ctx.mark_non_differentiable(mask)
-        return out, mask.view(torch.bool)
+        ctx.mark_non_differentiable(mask, lengths)
+        return out, mask.view(torch.bool), lengths
 
     @staticmethod
-    def backward(ctx, dout, _dmask):
+    def backward(ctx, dout, _dmask, _dlen):
         (rows,) = ctx.saved_tensors
         layer = ctx.layer
         T, dim = layer.seq_max_len, layer.table.dim
@@ -225,7 +226,9 @@ class SequenceEmbedding(nn.Module):
         self.seq_max_len = int(seq_max_len)
         self.hash_mode = HASH_MODES[hash_mode]
 
-    def forward(self, ids: torch.Tensor, offsets: torch.Tensor | None = None):
+    def forward(self, ids: torch.Tensor, offsets: torch.Tensor | None = None,
+                return_lengths: bool = False):
+        """-> (emb, mask) like tensornet, or (emb, mask, lengths int32 [B]) with return_lengths."""
         _lib.require_device(ids)
         if ids.dtype != torch.int64:
             raise TypeError("ids must be int64")
@@ -235,4 +238,5 @@ class SequenceEmbedding(nn.Module):
             B, n = ids.shape
             offsets = torch.arange(0, B * n + 1, n, device=ids.device, dtype=torch.int32)
         offsets = offsets.to(device=ids.device, dtype=torch.int32).contiguous()
-        return _SeqLookupFn.apply(self.table.anchor, ids.reshape(-1).contiguous(), offsets, self)
+        emb, mask, lengths = _SeqLookupFn.apply(self.table.anchor, ids.reshape(-1).contiguous(), offsets, self)
+        return (emb, mask, lengths) if return_lengths else (emb, mask)

@@ -462,7 +462,8 @@ class FFMBlock(nn.Module):
     Dense(dim) 'ffm_x_*' on x_i and 'ffm_y_*' on y_j (glorot_uniform, zero bias).
     Returns (ffm [B, NU*NI*dim], multiply [B, NU*16] or None)."""
 
-    def __init__(self, user_fields, item_fields, dim=8, with_multiply=True, seed=0, device=None):
+    def __init__(self, user_fields, item_fields, dim=8, with_multiply=True, seed=0, device=None,
+                 field_stride=16):
         super().__init__()
         self.user_fields, self.item_fields = list(user_fields), list(item_fields)
         self.NU, self.NI, self.dim = len(self.user_fields), len(self.item_fields), int(dim)
@@ -478,11 +479,11 @@ class FFMBlock(nn.Module):
                 glorot_uniform_(t, E, self.dim, gen)
                 with torch.no_grad():
                     W[p].copy_(t)
-        self.cols = torch.tensor([f * E for f in self.user_fields + self.item_fields],
+        self.cols = torch.tensor([f * int(field_stride) for f in self.user_fields + self.item_fields],
                                  dtype=torch.int32, device=device)
 
     def forward(self, x):
-        x = _rows(x)
+        x = _rows(x)  # [B, fields * field_stride]; field k's 16 columns start at k * field_stride
         y, mu = _FFMFn.apply(x, self.Wx, self.bx, self.Wy, self.by, self.cols, self.NU, self.NI,
                              self.dim, self.with_multiply)
         return y, (mu if self.with_multiply else None)

@@ -1,0 +1,72 @@
+"""Generic training step for the composed models (rank/multi_head, rough_rank, staytime, DIN
+harness): what tensornet's ``model.fit`` runs per batch (SURVEY §3 call stacks).
+
+    loss = model.loss(*batch)           (forward: librecsys_amd.so kernels via autograd)
+    loss.backward()                     (kernels write weight grads in place into the arena)
+    grads += l1 sign(w) + 2 l2 w        (Keras kernel regularisers, rs_l1l2_grad)
+    [DP] all-reduce the flat dense gradient (one RCCL bucket), rank-ordered sparse exchange
+    dense Adam over the arena (one launch, zero_grad fused), sparse optimizer per table
+
+Dense Adam follows tn.optimizer.Optimizer(tn.core.Adam(lr, .9, .999, 1e-8)) with tf.keras bias
+correction (pinned); sparse tables use the optimizer they were created with.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, ptr, stream_handle
+from .params import ParamArena
+
+
+def exchange_sparse(table, pg, world, x_rows, x_grads):
+    """Data-parallel sparse exchange of one table (dist.py protocol): compact -> all-gather ->
+    merge in rank order."""
+    from .dist import gather_sparse_lists
+    cnt = table.n_touched.clone()
+    call("rs_sparse_compact", stream_handle(), ptr(table.grad), ptr(table.flag), ptr(table.touched),
+         ptr(table.n_touched), table.dim, ptr(x_rows), ptr(x_grads), table.touched_cap)
+    table.n_touched.zero_()
+    rows_all, grads_all, n = gather_sparse_lists(x_rows, x_grads, cnt, pg)
+    for r in range(world if n else 0):
+        call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,
+             table.dim, ptr(table.grad), ptr(table.flag), ptr(table.touched), ptr(table.n_touched),
+             table.touched_cap)
+
+
+class Trainer:
+    def __init__(self, model, lr_dense: float, tables=(), process_group=None, beta1=0.9,
+                 beta2=0.999, eps=1e-8):
+        self.model = model
+        self.arena = ParamArena(model.parameters())
+        dev = self.arena.data.device
+        self.m = torch.zeros_like(self.arena.data)
+        self.v = torch.zeros_like(self.arena.data)
+        self.step_count = torch.zeros(1, device=dev, dtype=torch.int64)
+        self.lr, self.b1, self.b2, self.eps = float(lr_dense), beta1, beta2, eps
+        self.tables = list(tables)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.regs = list(model.regularizers()) if hasattr(model, "regularizers") else []
+        self.xbuf = {}
+        if self.world > 1:
+            for t in self.tables:
+                self.xbuf[id(t)] = (torch.empty(t.touched_cap, device=dev, dtype=torch.int32),
+                                    torch.empty(t.touched_cap, t.dim, device=dev))
+
+    def step(self, *batch):
+        loss = self.model.loss(*batch)
+        loss.backward()
+        s = stream_handle()
+        for p, l1, l2 in self.regs:
+            call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
+        if self.world > 1:
+            from .dist import allreduce_flat
+            allreduce_flat(self.arena.grad, self.pg)
+            for t in self.tables:
+                exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])
+        scale = 1.0 / self.world
+        call("rs_dense_adam", s, ptr(self.arena.data), ptr(self.arena.grad), ptr(self.m), ptr(self.v),
+             self.arena.n, ptr(self.step_count), self.lr, self.b1, self.b2, self.eps, scale, 1)
+        for t in self.tables:
+            t.step(grad_scale=scale)
+        return loss
