@@ -42,6 +42,10 @@ def parse():
                     help="bounded CPU sample: run whole train steps until this much time passed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--workload", default="autoint",
+                    choices=["autoint", "multi_head", "din", "staytime"],
+                    help="autoint = the headline (configs[1]); the others are configs 3-5 at their "
+                         "per-GPU batch (global batch / stated DP degree), same timing contract")
     return ap.parse_args()
 
 
@@ -97,6 +101,69 @@ def cpu_baseline(cfg, model, batches_cpu, seconds):
                       f"{threads} threads, {dt:.1f}s"}
 
 
+WORKLOADS = {
+    # name: (config index, per-GPU batch, description)
+    "multi_head": (2, 4096, "configs[2]: rank/multi_head AUTOINT train (200 fields x dim 8 multi-hot, "
+                            "IL(1,8,2,dropout .2) + 7 experts/gates + 7 towers), global 8192 / DP2"),
+    "din": (3, 1024, "configs[3]: din.py DIN pool train (seq 100, 1M x 16 table, query ++ pool -> "
+                     "Dense(1)), global 4096 / DP4"),
+    "staytime": (4, 2048, "configs[4]: staytime mtl_net + rough_rank DSSM joint train, 10M x 32 "
+                          "hashed table, global 16384 / DP8"),
+}
+
+
+def run_workload(args, world, rank, dev, pg):
+    """Configs 3-5 through the generic Trainer (eager autograd composition of the kernels)."""
+    from recommendsystem_amd.models import MultiHeadConfig, MultiHeadRanker
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd import workloads as W
+    ci, B, desc = WORKLOADS[args.workload]
+    if args.batch != 4096:
+        B = args.batch
+    rng = np.random.default_rng(10 + 1000 * rank)
+    if args.workload == "multi_head":
+        cfg = MultiHeadConfig()
+        model = MultiHeadRanker(cfg, device=dev, seed=0)
+        trainer = Trainer(model, cfg.lr_dense, model.tables(), process_group=pg)
+        pool = [W.multi_head_batch(rng, B, cfg, dev) for _ in range(args.pool)]
+    elif args.workload == "din":
+        model = W.DINPool(device=dev, seed=0)
+        trainer = Trainer(model, 5e-5, [model.table], process_group=pg)
+        pool = [W.din_batch(rng, B, 100, 1_000_000, dev) for _ in range(args.pool)]
+    else:
+        model = W.StaytimeRoughRank(device=dev, seed=0)
+        trainer = Trainer(model, 5e-4, [model.table], process_group=pg)
+        pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
+    for i in range(args.warmup):
+        trainer.step(*pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = trainer.step(*pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    samples = B * args.steps * world
+    out = {"metric": f"samples/sec {args.workload} train ({desc})", "value": round(samples / dt, 1),
+           "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (SURVEY §8d config generators; random-init weights)",
+           "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
+                      "parallelism": f"dp{world}", "execution": "eager autograd (not graph-captured)"},
+           "roofline": None, "cpu_baseline": None, "final_loss": round(float(loss), 6)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,6 +181,11 @@ def main():
     from recommendsystem_amd import _lib
     from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
     _lib.load()
+    if args.workload != "autoint":
+        run_workload(args, world, rank, dev, pg)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     cfg = AutoIntConfig()  # config 2: 26 x 16, vocab 100k/field, IL(3, 16, 2), mlp [32,16], [1]
     B, F = args.batch, cfg.num_fields

@@ -7,10 +7,9 @@
 //
 // MI355X mapping: fp32 in / fp32 accumulate on the matrix cores (v_mfma_f32_16x16x4_f32: exact
 // f32, a k-ordered fma chain, so the numerics equal an fp32 CPU dot product up to summation
-// order).  64x64 block tile, 4 waves x (16 rows x 64 columns), K staged through LDS in 32-deep
-// slabs with coalesced row loads.  Leading dimensions are explicit so a layer reads a slice of
-// a concatenated activation and writes straight into its slot of the next concat (the
-// tf.concat on autoint:44 costs nothing).
+// order).  One tiled GEMM engine (below) serves forward, data and weight gradients.  Leading
+// dimensions are explicit so a layer reads a slice of a concatenated activation and writes
+// straight into its slot of the next concat (the tf.concat on autoint:44 costs nothing).
 //   forward      Y  = act(X W + b)
 //   backward     dZ = dY * act'(Y) (recomputed on load, never stored)
 //                dX = dZ W^T       (optionally accumulated)
@@ -39,179 +38,254 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-constexpr int BT = 64;  // block tile (rows and columns)
-constexpr int BK = 32;  // K slab
+// ---------------------------------------------------------------------------------------------
+// One MFMA GEMM engine for all three products (C[Mo, No] = sum_r A(m, r) B(r, n)):
+//   forward       Y  = act(X W + b)          A = X  (row-major)      B = W  (row-major)
+//   bwd data      dX (+)= dZ W^T             A = dZ (row-major, Z)   B(r=n, c=k) = W[k][n] (col)
+//   bwd weight    dW = X^T dZ, db = colsum   A(k, m) = X[m][k] (col) B = dZ (row-major, Z)
+// "Z" operands are dY * act'(Y) computed on load (dZ is never stored).
+// Block = 256 threads (4 waves), tile BM x BN in {32, 64}^2, reduction staged through LDS in
+// 16-deep slabs, double-buffered (the next slab's global loads are in flight while the current
+// one feeds the MFMAs; one barrier per slab).  Each lane's float4 fragment read from LDS covers
+// four k-steps of v_mfma_f32_16x16x4_f32 (the k index is permuted consistently in A and B), so a
+// slab costs one ds_read_b128 per operand tile and 4 MFMAs per output tile.  The reduction can
+// be split over gridDim.z (bwd weight with a small [K, N] and a batch-sized M): per-split
+// partial rows, then column_reduce in split order (deterministic).
+// ---------------------------------------------------------------------------------------------
+enum { LAY_ROW = 0, LAY_COL = 1 };
+enum { EPI_FWD = 0, EPI_STORE = 1, EPI_PARTIAL = 2 };
 
-// ------------------------------- forward ------------------------------------------------------
-// Block = 16 rows x 64 columns, 4 waves splitting K (a batch-sized M with N <= 64 and K up to a
-// few thousand is the shape of every tower layer on the path, so the grid is M/16 blocks rather
-// than M/64).  X rows are staged through LDS in 256-deep slabs (coalesced); W is read straight
-// from L2 (it is a few KB to a few hundred KB and shared by every block).  The 4 wave partials
-// are summed in wave order (deterministic), then bias + activation.
-constexpr int FM = 16;    // rows per block
-constexpr int FKS = 256;  // K slab staged in LDS
+constexpr int GBK = 32;       // reduction slab
+constexpr int LDP = GBK + 4;  // LDS row stride (floats): 16-byte aligned rows
+constexpr int RQ = GBK / 4;   // float4s per row along r
 
-__global__ void __launch_bounds__(256) dense_fwd_kernel(const float* __restrict__ X, int64_t M,
-                                                        int K, int64_t ldx,
-                                                        const float* __restrict__ W,
-                                                        const float* __restrict__ bias, int N,
-                                                        int act, float* __restrict__ Y,
-                                                        int64_t ldy) {
-  __shared__ float As[FM][FKS + 4];
-  __shared__ float red[4][FM][BT + 1];
-  const int64_t m_blk = (int64_t)blockIdx.x * FM;
-  const int n_blk = blockIdx.y * BT;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int lr = l & 15, lk = l >> 4;
-  f32x4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += FKS) {
-    for (int t = threadIdx.x; t < FM * FKS; t += 256) {
-      const int r = t / FKS, c = t % FKS;
-      const int64_t m = m_blk + r;
-      const int k = k0 + c;
-      As[r][c] = (m < M && k < K) ? X[m * ldx + k] : 0.f;
-    }
-    __syncthreads();
-    // wave w takes k-steps kk = w*4, w*4 + 16, ... of this slab (interleaved -> balanced tails)
-    for (int kk = w * 4; kk < FKS && k0 + kk < K; kk += 16) {
-      const int k = k0 + kk + lk;
-      const float a = As[lr][kk + lk];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = n_blk + t * 16 + lr;
-        const float bv = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
-        acc[t] = mfma4(a, bv, acc[t]);
-      }
-    }
-    __syncthreads();
+struct GemmArgs {
+  const float* a; int64_t lda; const float* ay; int64_t lday;   // ay: Y of a Z operand
+  const float* b; int64_t ldb; const float* by; int64_t ldby;
+  int64_t M, N, R, rchunk;
+  int act_z;          // activation of the Z operand
+  int epi, act;       // epilogue mode, forward activation
+  const float* bias;
+  float* out; int64_t ldo; int accumulate;
+  float* db;          // bwd weight: column sums of B (row m-chunk z) or NULL
+};
+
+template <bool Z>
+__device__ __forceinline__ float opval(const float* p, const float* y, int64_t i, int64_t iy, int act) {
+  if (!Z) return p[i];
+  return act_bwd(p[i], y[iy], act);
+}
+
+template <bool Z>
+__device__ __forceinline__ float4 opval4(const float* p, const float* y, int64_t i, int64_t iy, int act) {
+  float4 v = *reinterpret_cast<const float4*>(p + i);
+  if (Z) {
+    const float4 yv = *reinterpret_cast<const float4*>(y + iy);
+    v.x = act_bwd(v.x, yv.x, act); v.y = act_bwd(v.y, yv.y, act);
+    v.z = act_bwd(v.z, yv.z, act); v.w = act_bwd(v.w, yv.w, act);
   }
+  return v;
+}
+
+// Load one operand slab (tile rows [x0, x0 + BX) x reduction [r0, r0 + GBK)) into NL = BX/32
+// float4 registers per thread.  ALONG_R: contiguous along r (A row / B col layouts), else
+// contiguous along x (A col / B row).
+template <int BX, bool ALONG_R, bool Z, bool VEC>
+__device__ __forceinline__ float4 load_one(const float* p, int64_t ld, const float* y, int64_t ldy,
+                                           int act, int64_t x0, int64_t X, int64_t r0, int64_t R,
+                                           int idx) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t x, r;
+  if (ALONG_R) {
+    x = x0 + idx / RQ;
+    r = r0 + 4 * (idx % RQ);
+    if (x >= X) return v;
+    if (VEC && r + 3 < R) return opval4<Z>(p, y, x * ld + r, x * ldy + r, act);
+    float e[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int i = 0; i < 4; ++i) e[i] = (r + i < R) ? opval<Z>(p, y, x * ld + r + i, x * ldy + r + i, act) : 0.f;
+    return make_float4(e[0], e[1], e[2], e[3]);
+  } else {
+    r = r0 + idx / (BX / 4);
+    x = x0 + 4 * (idx % (BX / 4));
+    if (r >= R) return v;
+    if (VEC && x + 3 < X) return opval4<Z>(p, y, r * ld + x, r * ldy + x, act);
+    float e[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[w][lk * 4 + r][t * 16 + lr] = acc[t][r];
+    for (int i = 0; i < 4; ++i) e[i] = (x + i < X) ? opval<Z>(p, y, r * ld + x + i, r * ldy + x + i, act) : 0.f;
+    return make_float4(e[0], e[1], e[2], e[3]);
+  }
+}
+
+template <int BX>
+struct Slab {
+  static constexpr int NL = BX * GBK / 4 / 256;  // float4 per thread
+  float4 v[NL];
+};
+
+template <int BX, bool ALONG_R, bool Z, bool VEC>
+__device__ __forceinline__ void load_slab(Slab<BX>& sl, const float* p, int64_t ld, const float* y,
+                                          int64_t ldy, int act, int64_t x0, int64_t X, int64_t r0,
+                                          int64_t R, int t) {
+#pragma unroll
+  for (int u = 0; u < Slab<BX>::NL; ++u)
+    sl.v[u] = load_one<BX, ALONG_R, Z, VEC>(p, ld, y, ldy, act, x0, X, r0, R, t + 256 * u);
+}
+
+template <int BX, bool ALONG_R>
+__device__ __forceinline__ void store_slab(float* s, const Slab<BX>& sl, int t) {
+#pragma unroll
+  for (int u = 0; u < Slab<BX>::NL; ++u) {
+    const int idx = t + 256 * u;
+    const float4 v = sl.v[u];
+    if (ALONG_R) {
+      *reinterpret_cast<float4*>(s + (idx / RQ) * LDP + 4 * (idx % RQ)) = v;
+    } else {
+      const int ri = idx / (BX / 4), xq = idx % (BX / 4);
+      s[(4 * xq + 0) * LDP + ri] = v.x;
+      s[(4 * xq + 1) * LDP + ri] = v.y;
+      s[(4 * xq + 2) * LDP + ri] = v.z;
+      s[(4 * xq + 3) * LDP + ri] = v.w;
+    }
+  }
+}
+
+template <int BM, int BN, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+  constexpr int TM = BM / 16, TN = BN / 16, WT = TM * TN / 4;
+  static_assert(WT >= 1, "tile too small for 4 waves");
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDP];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
+  const int64_t rb = (int64_t)blockIdx.z * g.rchunk;
+  const int64_t re = rb + g.rchunk < g.R ? rb + g.rchunk : g.R;
+  const bool do_db = g.db != nullptr && blockIdx.x == 0;
+  float csum = 0.f;
+  f32x4 acc[WT];
+#pragma unroll
+  for (int i = 0; i < WT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr bool A_ALONG_R = ALAY == LAY_ROW, B_ALONG_R = BLAY == LAY_COL;
+  Slab<BM> ra;
+  Slab<BN> rbv;
+  load_slab<BM, A_ALONG_R, AZ, VEC>(ra, g.a, g.lda, g.ay, g.lday, g.act_z, m0, g.M, rb, re, t);
+  load_slab<BN, B_ALONG_R, BZ, VEC>(rbv, g.b, g.ldb, g.by, g.ldby, g.act_z, n0, g.N, rb, re, t);
+  store_slab<BM, A_ALONG_R>(As[0], ra, t);
+  store_slab<BN, B_ALONG_R>(Bs[0], rbv, t);
   __syncthreads();
-  for (int o = threadIdx.x; o < FM * BT; o += 256) {
-    const int r = o / BT, c = o % BT;
-    const int64_t m = m_blk + r;
-    const int n = n_blk + c;
-    if (m < M && n < N) {
-      const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
-      Y[m * ldy + n] = act_fwd(v + bias[n], act);
+  int buf = 0;
+  for (int64_t r0 = rb; r0 < re; r0 += GBK) {
+    const bool more = r0 + GBK < re;
+    if (more) {
+      load_slab<BM, A_ALONG_R, AZ, VEC>(ra, g.a, g.lda, g.ay, g.lday, g.act_z, m0, g.M, r0 + GBK, re, t);
+      load_slab<BN, B_ALONG_R, BZ, VEC>(rbv, g.b, g.ldb, g.by, g.ldby, g.act_z, n0, g.N, r0 + GBK, re, t);
     }
-  }
-}
-
-// ------------------------------- backward: data ----------------------------------------------
-// dX[m][k] (+)= sum_n dZ[m][n] W[k][n]
-__global__ void __launch_bounds__(256) dense_bwd_data_kernel(
-    const float* __restrict__ dY, int64_t lddy, const float* __restrict__ Y, int64_t ldy, int act,
-    const float* __restrict__ W, int64_t M, int K, int N, float* __restrict__ dX, int64_t lddx,
-    int accumulate) {
-  __shared__ float As[BT][BK + 1];  // dZ[m][n]
-  __shared__ float Bs[BK][BT + 1];  // W^T[n][k]
-  const int64_t m_blk = (int64_t)blockIdx.x * BT;
-  const int k_blk = blockIdx.y * BT;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  f32x4 acc[4];
+    if (do_db && t < BN) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int n0 = 0; n0 < N; n0 += BK) {
-    for (int t = threadIdx.x; t < BT * BK; t += 256) {
-      const int r = t / BK, c = t % BK;
-      const int64_t m = m_blk + r;
-      const int n = n0 + c;
-      As[r][c] = (m < M && n < N) ? act_bwd(dY[m * lddy + n], Y[m * ldy + n], act) : 0.f;
+      for (int k = 0; k < GBK; ++k) csum += Bs[buf][t * LDP + k];
     }
-    for (int t = threadIdx.x; t < BK * BT; t += 256) {
-      const int kr = t / BK, c = t % BK;  // coalesced along n within a W row
-      const int k = k_blk + kr, n = n0 + c;
-      Bs[c][kr] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
+#pragma unroll
+    for (int kg = 0; kg < GBK / 16; ++kg) {
+#pragma unroll
+      for (int i = 0; i < WT; ++i) {
+        const int q = w * WT + i, rt = q / TN, ct = q % TN;
+        const float4 af = *reinterpret_cast<const float4*>(
+            &As[buf][(rt * 16 + (l & 15)) * LDP + kg * 16 + 4 * (l >> 4)]);
+        const float4 bf = *reinterpret_cast<const float4*>(
+            &Bs[buf][(ct * 16 + (l & 15)) * LDP + kg * 16 + 4 * (l >> 4)]);
+        acc[i] = mfma4(af.x, bf.x, acc[i]);
+        acc[i] = mfma4(af.y, bf.y, acc[i]);
+        acc[i] = mfma4(af.z, bf.z, acc[i]);
+        acc[i] = mfma4(af.w, bf.w, acc[i]);
+      }
+    }
+    if (more) {
+      store_slab<BM, A_ALONG_R>(As[buf ^ 1], ra, t);
+      store_slab<BN, B_ALONG_R>(Bs[buf ^ 1], rbv, t);
     }
     __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      const float a = As[w * 16 + (l & 15)][kk + (l >> 4)];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = mfma4(a, Bs[kk + (l >> 4)][t * 16 + (l & 15)], acc[t]);
-    }
-    __syncthreads();
+    buf ^= 1;
   }
+  // ---- epilogue ----
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int k = k_blk + t * 16 + (l & 15);
+  for (int i = 0; i < WT; ++i) {
+    const int q = w * WT + i, rt = q / TN, ct = q % TN;
+    const int64_t n = n0 + ct * 16 + (l & 15);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t m = m_blk + w * 16 + (l >> 4) * 4 + r;
-      if (m < M && k < K) {
-        float* d = dX + m * lddx + k;
-        *d = accumulate ? (*d + acc[t][r]) : acc[t][r];
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + rt * 16 + (l >> 4) * 4 + j;
+      if (m < g.M && n < g.N) {
+        const float v = acc[i][j];
+        if (g.epi == EPI_FWD) {
+          g.out[m * g.ldo + n] = act_fwd(v + g.bias[n], g.act);
+        } else if (g.epi == EPI_STORE) {
+          float* d = g.out + m * g.ldo + n;
+          *d = g.accumulate ? *d + v : v;
+        } else {
+          g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + m * g.N + n] = v;
+        }
       }
     }
   }
-}
-
-// ------------------------------- backward: weights -------------------------------------------
-// partial[chunk][k][n] = sum_{m in chunk} X[m][k] dZ[m][n];  partial[chunk][K*N + n] = colsum dZ
-constexpr int MCH = 64;  // rows per M chunk (2 x 64 x 65 floats of LDS)
-
-__global__ void __launch_bounds__(256) dense_bwd_weight_kernel(
-    const float* __restrict__ X, int64_t ldx, const float* __restrict__ dY, int64_t lddy,
-    const float* __restrict__ Y, int64_t ldy, int act, int64_t M, int K, int N,
-    float* __restrict__ partials) {
-  __shared__ float Xs[MCH][BT + 1];
-  __shared__ float Zs[MCH][BT + 1];
-  const int64_t m_blk = (int64_t)blockIdx.x * MCH;
-  const int k_blk = blockIdx.y * BT;
-  const int n_blk = blockIdx.z * BT;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int t = threadIdx.x; t < MCH * BT; t += 256) {
-    const int r = t / BT, c = t % BT;
-    const int64_t m = m_blk + r;
-    const int k = k_blk + c, n = n_blk + c;
-    Xs[r][c] = (m < M && k < K) ? X[m * ldx + k] : 0.f;
-    Zs[r][c] = (m < M && n < N) ? act_bwd(dY[m * lddy + n], Y[m * ldy + n], act) : 0.f;
-  }
-  __syncthreads();
-  f32x4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int mm = 0; mm < MCH; mm += 4) {
-    const float a = Xs[mm + (l >> 4)][w * 16 + (l & 15)];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = mfma4(a, Zs[mm + (l >> 4)][t * 16 + (l & 15)], acc[t]);
-  }
-  float* part = partials + (int64_t)blockIdx.x * ((int64_t)K * N + N);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int n = n_blk + t * 16 + (l & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = k_blk + w * 16 + (l >> 4) * 4 + r;
-      if (k < K && n < N) part[(int64_t)k * N + n] = acc[t][r];
-    }
-  }
-  if (blockIdx.y == 0) {  // column sums of dZ (bias gradient), in row order
-    for (int c = threadIdx.x; c < BT; c += 256) {
-      const int n = n_blk + c;
-      if (n < N) {
-        float s = 0.f;
-        for (int r = 0; r < MCH; ++r) s += Zs[r][c];
-        part[(int64_t)K * N + n] = s;
-      }
-    }
+  if (do_db && t < BN && n0 + t < g.N) {
+    if (g.epi == EPI_PARTIAL) g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + g.M * g.N + n0 + t] = csum;
+    else g.db[n0 + t] = g.accumulate ? g.db[n0 + t] + csum : csum;
   }
 }
+
+struct GemmPlan { int bm, bn, splits; int64_t rchunk; };
+
+static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
+  GemmPlan p;
+  p.bn = N <= 32 ? 32 : 64;
+  const int64_t tn = (N + p.bn - 1) / p.bn;
+  p.bm = ((M + 63) / 64) * tn >= 240 ? 64 : 32;
+  const int64_t tiles = ((M + p.bm - 1) / p.bm) * tn;
+  p.splits = 1;
+  if (allow_split && tiles < 128) {
+    int64_t s = (256 + tiles - 1) / tiles;
+    const int64_t max_s = (R + 255) / 256;  // keep >= 256 reduction rows per split
+    if (s > max_s) s = max_s;
+    p.splits = (int)(s < 1 ? 1 : s);
+  }
+  int64_t rc = (R + p.splits - 1) / p.splits;
+  rc = (rc + GBK - 1) / GBK * GBK;
+  p.rchunk = rc < GBK ? GBK : rc;
+  p.splits = (int)((R + p.rchunk - 1) / p.rchunk);
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+template <int ALAY, int BLAY, bool AZ, bool BZ>
+static void launch_gemm(hipStream_t s, const GemmPlan& p, const GemmArgs& g, bool vec) {
+  dim3 grid((unsigned)((g.M + p.bm - 1) / p.bm), (unsigned)((g.N + p.bn - 1) / p.bn), (unsigned)p.splits);
+#define RS_GEMM(BMM, BNN, V) gemm_kernel<BMM, BNN, ALAY, BLAY, AZ, BZ, V><<<grid, 256, 0, s>>>(g)
+  if (vec) {
+    if (p.bm == 64 && p.bn == 64) RS_GEMM(64, 64, true);
+    else if (p.bm == 64) RS_GEMM(64, 32, true);
+    else if (p.bn == 64) RS_GEMM(32, 64, true);
+    else RS_GEMM(32, 32, true);
+  } else {
+    if (p.bm == 64 && p.bn == 64) RS_GEMM(64, 64, false);
+    else if (p.bm == 64) RS_GEMM(64, 32, false);
+    else if (p.bn == 64) RS_GEMM(32, 64, false);
+    else RS_GEMM(32, 32, false);
+  }
+#undef RS_GEMM
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t ldx,
                         const float* W, const float* bias, int N, int act, float* Y,
                         int64_t ldy) {
   if (!X || !W || !bias || !Y || M < 0 || K <= 0 || N <= 0 || ldx < K || ldy < N) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
-  dim3 grid((unsigned)((M + FM - 1) / FM), (unsigned)((N + BT - 1) / BT));
-  dense_fwd_kernel<<<grid, 256, 0, rs_stream(stream)>>>(X, M, K, ldx, W, bias, N, act, Y, ldy);
+  GemmArgs g{X, ldx, nullptr, 0, W, N, nullptr, 0, M, N, K, 0, 0, EPI_FWD, act, bias, Y, ldy, 0, nullptr};
+  GemmPlan p = plan_gemm(M, N, K, false);
+  g.rchunk = p.rchunk;
+  const bool vec = aligned16(X) && aligned16(W) && ldx % 4 == 0 && N % 4 == 0;
+  launch_gemm<LAY_ROW, LAY_ROW, false, false>(rs_stream(stream), p, g, vec);
   return rs_status_after_launch();
 }
 
@@ -220,32 +294,50 @@ RS_API int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const 
                              float* dX, int64_t lddx, int accumulate) {
   if (!dY || !Y || !W || !dX || M < 0 || K <= 0 || N <= 0 || lddx < K) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
-  dim3 grid((unsigned)((M + BT - 1) / BT), (unsigned)((K + BT - 1) / BT));
-  dense_bwd_data_kernel<<<grid, 256, 0, rs_stream(stream)>>>(dY, lddy, Y, ldy, act, W, M, K, N,
-                                                              dX, lddx, accumulate);
+  // C[M, K] = dZ[M, N] . W^T : B(r = n, c = k) = W[k * N + n] (column layout, ldb = N)
+  GemmArgs g{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, 0, act, EPI_STORE, 0, nullptr, dX, lddx,
+             accumulate, nullptr};
+  GemmPlan p = plan_gemm(M, K, N, false);
+  g.rchunk = p.rchunk;
+  const bool vec = aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 && ldy % 4 == 0 &&
+                   N % 4 == 0;
+  launch_gemm<LAY_ROW, LAY_COL, true, false>(rs_stream(stream), p, g, vec);
   return rs_status_after_launch();
 }
 
 RS_API int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N) {
-  const int64_t nchunks = (M + MCH - 1) / MCH;
-  return (nchunks < 1 ? 1 : nchunks) * ((int64_t)K * N + N);
+  const GemmPlan p = plan_gemm(K, N, M, true);
+  return (int64_t)p.splits * ((int64_t)K * N + N);
 }
 
 RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* dY,
                                int64_t lddy, const float* Y, int64_t ldy, int act, int64_t M,
                                int K, int N, float* dW, float* db, int accumulate,
                                float* workspace, int64_t workspace_floats) {
-  if (!X || !dY || !Y || !dW || !db || !workspace || M < 0 || K <= 0 || N <= 0) return RS_ERR_ARG;
-  if (workspace_floats < rs_dense_bwd_weight_workspace_floats(M, K, N)) return RS_ERR_ARG;
+  if (!X || !dY || !Y || !dW || !db || M < 0 || K <= 0 || N <= 0) return RS_ERR_ARG;
   hipStream_t s = rs_stream(stream);
-  const int nchunks = (int)((M + MCH - 1) / MCH);
-  if (nchunks > 0) {
-    dim3 grid((unsigned)nchunks, (unsigned)((K + BT - 1) / BT), (unsigned)((N + BT - 1) / BT));
-    dense_bwd_weight_kernel<<<grid, 256, 0, s>>>(X, ldx, dY, lddy, Y, ldy, act, M, K, N,
-                                                 workspace);
+  if (M == 0) {
+    if (!accumulate) {
+      (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)K * N, s);
+      (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)N, s);
+    }
+    return rs_status_after_launch();
   }
-  const int64_t total = (int64_t)K * N + N;
-  launch_column_reduce(s, workspace, nchunks, total, total, (int64_t)K * N, dW, db, accumulate);
+  // C[K, N] = sum_m X[m][k] dZ[m][n]: A(k, m) = X[m * ldx + k] (column layout), B = dZ rows
+  const GemmPlan p = plan_gemm(K, N, M, true);
+  const bool split = p.splits > 1;
+  if (split && (!workspace || workspace_floats < (int64_t)p.splits * ((int64_t)K * N + N)))
+    return RS_ERR_ARG;
+  GemmArgs g{X, ldx, nullptr, 0, dY, lddy, Y, ldy, K, N, M, p.rchunk, act,
+             split ? EPI_PARTIAL : EPI_STORE, 0, nullptr, split ? workspace : dW, N, accumulate,
+             db};
+  const bool vec = aligned16(X) && aligned16(dY) && aligned16(Y) && ldx % 4 == 0 && lddy % 4 == 0 &&
+                   ldy % 4 == 0;
+  launch_gemm<LAY_COL, LAY_ROW, false, true>(s, p, g, vec);
+  if (split) {
+    const int64_t total = (int64_t)K * N + N;
+    launch_column_reduce(s, workspace, p.splits, total, total, (int64_t)K * N, dW, db, accumulate);
+  }
   return rs_status_after_launch();
 }
 
