@@ -68,8 +68,10 @@ int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* 
 
 /* H11 sparse optimizers on the touched rows (tensornet tn.core.Adam / tn.core.AdaGrad handed to
  * EmbeddingFeatures: rank/ctr/base_model.py:163, rank/multi_head/multidnn.py:235,
- * staytime/VideoDnn.py:233).  Zero the gradient rows, release the flags, reset *n_touched.
- * max_rows bounds the grid (>= the largest possible *n_touched). */
+ * staytime/VideoDnn.py:233).  Zero the gradient rows, release the flags, reset the count.
+ * n_touched points at int32[1 + 288] = {count, completion counters} (all zero between steps):
+ * the last workgroup of the launch resets them, so no separate memset is needed.
+ * max_rows bounds the grid (>= the largest possible count). */
 int rs_sparse_adam(void* stream, float* table, float* m, float* v, float* grad_table,
                    int32_t* flag, const int32_t* touched, int32_t* n_touched, int dim,
                    int32_t max_rows, float lr, float beta1, float beta2, float eps,
@@ -286,6 +288,50 @@ int rs_dense_adam(void* stream, float* params, float* grads, float* m, float* v,
 /* Keras kernel regularisers as a gradient term (L1L2 at rank/multi_head/multidnn.py:62-63,
  * L2 at :85,103 and rough_rank/layer.py:77): grads += l1 * sign(w) + 2 * l2 * w. */
 int rs_l1l2_grad(void* stream, const float* params, float* grads, int64_t n, float l1, float l2);
+
+/* ---------------------------------------------------------------------------------------
+ * H4 + H10 fused: the AutoInt head training pass (autoint:38-52 + rank/ctr/base_model.py:7-12).
+ * Replaces, for the training step, the chain rs_dense_fwd x (deep + logits) -> rs_bce_clip_loss
+ * -> rs_dense_bwd_data / rs_dense_bwd_weight x (logits + deep) that mirrors
+ *   deep = MultiLayerDense([N1, N2], act)(Flatten(x0));  result = concat([deep, il], axis=1)
+ *   p = clip(MultiLayerDense([T], act3)(result), lo, hi);  loss = cross_entropy(labels, p)
+ * N2 = 0 means a single deep layer.  Supported (N1, N2): (32,16) (64,32) (16,0) (32,0) (64,0)
+ * (16,16) (32,32) (64,16) (64,64); T <= 4; K0 % 16 == 0; S % 4 == 0; x0 / il 16-byte aligned
+ * (RS_ERR_UNSUPPORTED otherwise: use the per-layer entry points).
+ * Writes p_out [B, T] (may be NULL), dil = dL/d il [B, S] (row stride ld_dil), dx0 = dL/dx0 from
+ * the deep tower (overwrite, or += when dx_accumulate).  Weight gradients and the loss are left
+ * as per-block partial rows in `workspace` (rs_mlp_head_partial_blocks(B) rows of
+ * rs_mlp_head_param_floats(...) + 1 floats, arena order [W1 b1 W2 b2 W3 b3 | loss_sum]) for
+ * rs_partials_reduce_adam.  The loss partials are sums; the batch mean is sum / B.
+ * ------------------------------------------------------------------------------------- */
+int64_t rs_mlp_head_param_floats(int K0, int N1, int N2, int S, int T);
+int64_t rs_mlp_head_workspace_floats(int64_t B, int K0, int N1, int N2, int S, int T);
+int rs_mlp_head_partial_blocks(int64_t B);
+int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const float* il, int64_t ld_il,
+                      int64_t B, int K0, int S, int N1, int act1, int N2, int act2, int T,
+                      int act3, const float* W1, const float* b1, const float* W2,
+                      const float* b2, const float* W3, const float* b3, const float* labels,
+                      float clip_lo, float clip_hi, float log_eps, float* p_out, float* dil,
+                      int64_t ld_dil, float* dx0, int64_t ld_dx, int dx_accumulate,
+                      float* workspace, int64_t workspace_floats);
+
+/* Per-block gradient partials -> gradients (-> dense Adam), one launch (replaces the
+ * column-reduce launches of the fused backward kernels plus rs_dense_adam and its step-increment
+ * launch).  Segment k: partial rows parts[k][r * lds[k] + c] (r < nrows[k], c < ncols[k]) are
+ * summed over r in a fixed order, scaled by scales[k] and written to outs[k][c]; if adam != 0 and
+ * adam_offs[k] >= 0 the tf.keras-form Adam of rs_dense_adam is applied to arena element
+ * adam_offs[k] + c with that gradient times grad_scale.  nseg <= 4.  step: device int64 Adam
+ * counter (advanced once per launch); done: device int32[288] completion counters, zero between
+ * launches (reset by the launch itself). */
+int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
+                            const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
+                            float* const* outs, const float* scales, const int64_t* adam_offs,
+                            float* params, float* m, float* v, int64_t* step, int32_t* done,
+                            float lr, float beta1, float beta2, float eps, float grad_scale,
+                            int adam);
+
+/* Grid (= number of per-block partial rows) rs_il_bwd uses for a given batch and workspace. */
+int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats);
 
 #ifdef __cplusplus
 }

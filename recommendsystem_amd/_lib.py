@@ -93,6 +93,15 @@ SIGNATURES: dict[str, tuple] = {
     "rs_act_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "rs_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "rs_bce_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _f32, _vp, _vp]),
+    "rs_mlp_head_param_floats": (_i64, [_i32, _i32, _i32, _i32, _i32]),
+    "rs_mlp_head_workspace_floats": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32]),
+    "rs_mlp_head_partial_blocks": (_i32, [_i64]),
+    "rs_mlp_head_train": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
+                                 _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32,
+                                 _f32, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
+    "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
+    "rs_il_bwd_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i64]),
 }
 
 _LIB = None
@@ -122,7 +131,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
 
 def call(name: str, *args) -> int:
     rc = getattr(load(), name)(*args)
-    if SIGNATURES[name][0] is _i32 and rc != RS_OK and not name.endswith("_count"):
+    if SIGNATURES[name][0] is _i32 and rc != RS_OK and not name.endswith(("_count", "_blocks")):
         raise RecsysKernelError(f"{name} returned {rc} ({_ERRS.get(rc, 'hip error')})")
     return rc
 
@@ -144,3 +153,34 @@ def require_device(*tensors) -> None:
         if t is not None and not t.is_cuda:
             raise RecsysKernelError("recommendsystem_amd kernels need tensors on a ROCm device "
                                     "(there is no CPU fallback)")
+
+
+def c_array(ctype, values):
+    """A ctypes array (keep a reference while the call runs) and its address for a `_vp` slot."""
+    arr = (ctype * len(values))(*values)
+    return arr, ctypes.addressof(arr)
+
+
+def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=None, done=None,
+                         lr=0.0, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0,
+                         adam=False) -> int:
+    """rs_partials_reduce_adam over a list of segments
+    (part_ptr, ld, nrows, ncols, out_ptr, scale, adam_off)."""
+    n = len(segments)
+    keep = []
+
+    def arr(ct, vals):
+        a, addr = c_array(ct, vals)
+        keep.append(a)
+        return addr
+
+    parts = arr(ctypes.c_void_p, [s[0] for s in segments])
+    lds = arr(ctypes.c_int64, [s[1] for s in segments])
+    nrows = arr(ctypes.c_int32, [s[2] for s in segments])
+    ncols = arr(ctypes.c_int64, [s[3] for s in segments])
+    outs = arr(ctypes.c_void_p, [s[4] for s in segments])
+    scales = arr(ctypes.c_float, [s[5] for s in segments])
+    offs = arr(ctypes.c_int64, [s[6] for s in segments])
+    return call("rs_partials_reduce_adam", stream, n, parts, lds, nrows, ncols, outs, scales, offs,
+                ptr(params), ptr(m), ptr(v), ptr(step), ptr(done), lr, beta1, beta2, eps,
+                grad_scale, int(adam))

@@ -174,6 +174,7 @@ class AutoIntTrainer:
         self.il_dparams = ar.grad[self._offset(il.kernel):self._offset(il.kernel) +
                                   il.kernel.numel() + il.bias.numel() + il.gamma.numel() + il.beta.numel()]
         self.graph = None
+        self.head = self._plan_head()
         if self.world > 1:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
@@ -186,7 +187,102 @@ class AutoIntTrainer:
         return self.model.arena.grad.data_ptr() + 4 * self._offset(p)
 
     # ---------------------------------------------------------------------------------------
+    def _plan_head(self):
+        """Use the fused head kernel (rs_mlp_head_train) when the towers fit its instantiations:
+        deep [N1] or [N1, N2], logits [T <= 4], parameters laid out [W1 b1 (W2 b2) W3 b3] in the
+        arena right after the InteractingLayer's [W b gamma beta].  Otherwise the per-layer
+        Dense entry points run (same math)."""
+        supported = {(32, 16), (64, 32), (16, 0), (32, 0), (64, 0), (16, 16), (32, 32), (64, 16),
+                     (64, 64)}
+        deep, logit = self.deep_layers, self.logit_layers
+        if len(deep) not in (1, 2) or len(logit) != 1 or logit[0].units > 4:
+            return None
+        N1 = deep[0].units
+        N2 = deep[1].units if len(deep) == 2 else 0
+        if (N1, N2) not in supported or (self.F * self.E) % 16 or (self.F * self.U) % 4:
+            return None
+        params = [deep[0].kernel, deep[0].bias] + ([deep[1].kernel, deep[1].bias] if N2 else []) + \
+                 [logit[0].kernel, logit[0].bias]
+        off = self._offset(params[0])
+        o = off
+        for p in params:
+            if self._offset(p) != o:
+                return None
+            o += p.numel()
+        il = self.model.interact
+        il_off = self._offset(il.kernel)
+        il_n = il.kernel.numel() + il.bias.numel() + il.gamma.numel() + il.beta.numel()
+        if il_off + il_n > self.model.arena.n:
+            return None
+        lib = _lib.load()
+        K0, S, T = self.F * self.E, self.F * self.U, logit[0].units
+        npar = int(lib.rs_mlp_head_param_floats(K0, N1, N2, S, T))
+        if npar != o - off:
+            return None
+        dev = self.dev
+        ws = torch.empty(int(lib.rs_mlp_head_workspace_floats(self.B, K0, N1, N2, S, T)),
+                         device=dev, dtype=torch.float32)
+        return dict(N1=N1, N2=N2, T=T, K0=K0, S=S, off=off, npar=npar, ws=ws,
+                    blocks=int(lib.rs_mlp_head_partial_blocks(self.B)),
+                    il_off=il_off, il_n=il_n,
+                    il_blocks=int(lib.rs_il_bwd_partial_blocks(self.B, self.F, self.E, self.U,
+                                                               self.il_ws_n)),
+                    done=torch.zeros(288, device=dev, dtype=torch.int32))
+
+    def _forward_backward_fused(self):
+        """lookup -> IL fwd -> fused head (MLP fwd, clip+BCE, MLP bwd) -> IL bwd -> sparse push:
+        five launches; dense gradients stay as per-block partials until _reduce_dense."""
+        m, hd = self.model, self.head
+        B, F, E, U, L, H, D, CW = self.B, self.F, self.E, self.U, self.L, self.H, self.D, self.CW
+        s = stream_handle()
+        il, emb, t = m.interact, m.embedding, m.table
+        call("rs_embedding_lookup_fwd", s, ptr(self.ids), None, B, F, ptr(emb.row_base),
+             ptr(emb.bucket), emb.hash_mode, emb.combiner, ptr(t.weight), t.rows, E, ptr(self.x0),
+             F * E, E, ptr(self.rows))
+        drop = il.dropout_rate if il.use_dropout else 0.0
+        call("rs_il_fwd", s, ptr(self.x0), B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+             ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
+             self.cat.data_ptr() + 4 * D, CW, ptr(self.xsave) if L > 1 else None)
+        d = self.deep_layers
+        lg = self.logit_layers[0]
+        d2 = d[1] if hd["N2"] else None
+        call("rs_mlp_head_train", s, ptr(self.x0), F * E, self.cat.data_ptr() + 4 * D, CW, B,
+             hd["K0"], hd["S"], hd["N1"], d[0].act, hd["N2"], d2.act if d2 is not None else 0,
+             hd["T"], lg.act, ptr(d[0].kernel), ptr(d[0].bias),
+             ptr(d2.kernel) if d2 is not None else None, ptr(d2.bias) if d2 is not None else None,
+             ptr(lg.kernel), ptr(lg.bias), ptr(self.labels), 1e-6, 1.0, 1e-6, ptr(self.p),
+             self.dcat.data_ptr() + 4 * D, CW, ptr(self.dx0), F * E, 0, ptr(hd["ws"]),
+             hd["ws"].numel())
+        call("rs_il_bwd", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+             self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+             ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed, ptr(self.dx0),
+             1, None, 0, ptr(self.il_ws), self.il_ws_n)
+        t.accumulate(self.rows, None, B, F, self.dx0, F * E, E, emb.combiner)
+
+    def _reduce_dense(self, adam: bool):
+        """Sum the IL and head partials (fixed order) into the arena gradient and the loss; with
+        adam, apply the dense Adam in the same launch."""
+        m, hd, cfg = self.model, self.head, self.model.cfg
+        ar = m.arena
+        g0 = ar.grad.data_ptr()
+        npl = hd["npar"] + 1
+        segs = [
+            (self.il_ws.data_ptr(), hd["il_n"], hd["il_blocks"], hd["il_n"], g0 + 4 * hd["il_off"],
+             1.0, hd["il_off"]),
+            (hd["ws"].data_ptr(), npl, hd["blocks"], hd["npar"], g0 + 4 * hd["off"], 1.0, hd["off"]),
+            (hd["ws"].data_ptr() + 4 * hd["npar"], npl, hd["blocks"], 1, self.loss.data_ptr(),
+             1.0 / self.B, -1),
+        ]
+        _lib.partials_reduce_adam(stream_handle(), segs, ar.data, self.adam_m, self.adam_v,
+                                  self.step_count, hd["done"], cfg.lr_dense, 0.9, 0.999, 1e-8,
+                                  1.0 / self.world, adam)
+
     def _forward_backward(self):
+        if self.head is not None:
+            self._forward_backward_fused()
+            if self.world > 1:
+                self._reduce_dense(adam=False)
+            return
         m, cfg = self.model, self.model.cfg
         B, F, E, U, L, H, D, CW = self.B, self.F, self.E, self.U, self.L, self.H, self.D, self.CW
         s = stream_handle()
@@ -255,7 +351,7 @@ class AutoIntTrainer:
         from .dist import allreduce_flat, gather_sparse_lists
         m, t = self.model, self.model.table
         allreduce_flat(m.arena.grad, self.pg)
-        cnt = t.n_touched.clone()
+        cnt = t.n_touched[:1].clone()
         call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
              ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
         t.n_touched.zero_()
@@ -267,6 +363,10 @@ class AutoIntTrainer:
     def _optimize(self):
         m, cfg = self.model, self.model.cfg
         ar = m.arena
+        if self.head is not None and self.world == 1:
+            self._reduce_dense(adam=True)   # partials -> grads -> Adam, one launch
+            m.table.step(grad_scale=1.0)
+            return
         scale = 1.0 / self.world
         call("rs_dense_adam", stream_handle(), ptr(ar.data), ptr(ar.grad), ptr(self.adam_m),
              ptr(self.adam_v), ar.n, ptr(self.step_count), cfg.lr_dense, 0.9, 0.999, 1e-8, scale, 0)

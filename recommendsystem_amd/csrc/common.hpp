@@ -141,3 +141,31 @@ static inline void launch_column_reduce(hipStream_t s, const float* part, int nr
   column_reduce_kernel<16><<<grid, 64 * 16, 0, s>>>(part, nrows, ld, ncols, split, out0, out1,
                                                     accumulate);
 }
+
+// ---------------------------------------------------------------------------------------------
+// "The last workgroup of this launch" without a second launch: a completion counter sharded over
+// 8 sub-counters (blockIdx % 8, one 128-B line each) plus a top counter, so at most
+// ceil(grid / 8) + 8 arrivals meet on any one word (one device-scope atomic serialises ~12 ns at
+// the memory side; 1024 arrivals on one word would cost ~13 us).  The counters live in
+// caller-owned memory, int32[RS_DONE_WORDS], all zero between launches: each sub-counter is reset
+// by its own last arriver and the top counter by the global last arriver (atomic exchanges, the
+// same memory-side path as the adds).  Every thread of the block must call this; it returns true
+// in thread 0 of the last block only.  No memory fence: callers use it only to order their own
+// earlier LOADS (consumed values) before a reset done by the last block.
+// ---------------------------------------------------------------------------------------------
+#define RS_DONE_STRIDE 32
+#define RS_DONE_WORDS (9 * RS_DONE_STRIDE)
+__device__ __forceinline__ bool rs_last_block(int32_t* ctr) {
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  const unsigned G = gridDim.x, k = blockIdx.x & 7u;
+  const int nk = (int)((G - k + 7u) / 8u);
+  const int nsub = (int)(G < 8u ? G : 8u);
+  int32_t* sub = ctr + k * RS_DONE_STRIDE;
+  int32_t* top = ctr + 8 * RS_DONE_STRIDE;
+  if (atomicAdd(sub, 1) != nk - 1) return false;
+  atomicExch(sub, 0);
+  if (atomicAdd(top, 1) != nsub - 1) return false;
+  atomicExch(top, 0);
+  return true;
+}

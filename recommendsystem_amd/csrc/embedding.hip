@@ -21,6 +21,7 @@
 // dim/4 lanes per segment, 64/(dim/4) segments per wave instruction: a wave reads 16 whole rows
 // and writes 1 KiB of contiguous [B, F, 16] output per step at config 2).
 #include "common.hpp"
+#include <stdlib.h>
 
 enum { RS_HASH_MOD = 0, RS_HASH_SPLITMIX = 1 };
 enum { RS_COMBINER_SUM = 0, RS_COMBINER_MEAN = 1, RS_COMBINER_SQRTN = 2 };
@@ -226,31 +227,62 @@ __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
   const int gsub = threadIdx.x / G, l = threadIdx.x % G;
   const int leader = (threadIdx.x & 63) - l;  // lane of this group's leader within the wave
   // ---- phase 1: aggregate this tile's occurrences per row in LDS ----
-  for (int64_t b = b0 + gsub; b < b1; b += per_pass) {
-    const int64_t sg = b * F + f;
-    const int64_t beg = offsets ? offsets[sg] : sg;
-    const int64_t end = offsets ? offsets[sg + 1] : sg + 1;
-    if (end <= beg) continue;
-    const float sc = combiner_scale((int)(end - beg), combiner);
-    const float* src = dout + b * dout_ld + (int64_t)f * dout_fstride;
-    for (int64_t k = beg; k < end; ++k) {
-      const int32_t row = rows[k];
-      if (row < 0) continue;  // padded sequence position (rs_sequence_lookup_fwd)
-      int slot = -1;
-      if (l == 0) {
-        int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));
-        for (int probe = 0; probe < cap; ++probe) {
-          const int32_t old = atomicCAS(&keys[h], -1, row);
-          if (old == -1 || old == row) { slot = h; break; }
-          h = (h + 1) & (cap - 1);
+  // insert one occurrence (the group's leader probes the LDS table; the group adds its elements)
+  auto insert = [&](int32_t row, const float* src, float sc, float v0) {
+    int slot = -1;
+    if (l == 0) {
+      int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));
+      for (int probe = 0; probe < cap; ++probe) {
+        const int32_t old = atomicCAS(&keys[h], -1, row);
+        if (old == -1 || old == row) { slot = h; break; }
+        h = (h + 1) & (cap - 1);
+      }
+    }
+    slot = __shfl(slot, leader, 64);
+    if (slot >= 0) {
+      if (src) for (int e = l; e < dim; e += G) atomicAdd(&vals[slot * dim + e], src[e] * sc);
+      else if (l < dim) atomicAdd(&vals[slot * dim + l], v0);
+    } else {  // LDS table full: direct global path
+      if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
+      if (src) for (int e = l; e < dim; e += G) atomicAdd(grad_table + (int64_t)row * dim + e, src[e] * sc);
+      else if (l < dim) atomicAdd(grad_table + (int64_t)row * dim + l, v0);
+    }
+  };
+  if (!offsets && dim <= G) {
+    // single-hot fast path: the rows and gradient elements of CH passes are loaded before any of
+    // them is inserted, so one HBM/L2 round trip covers CH samples per group (the per-pass
+    // dependent load -> probe -> add chain made this launch latency-bound)
+    constexpr int CH = 8;
+    const float sc = combiner_scale(1, combiner);
+    for (int64_t bb = b0 + gsub; bb < b1; bb += (int64_t)per_pass * CH) {
+      int32_t rw[CH];
+      float vv[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int64_t b = bb + (int64_t)u * per_pass;
+        rw[u] = -1;
+        vv[u] = 0.f;
+        if (b < b1) {
+          rw[u] = rows[b * F + f];
+          if (l < dim) vv[u] = dout[b * dout_ld + (int64_t)f * dout_fstride + l] * sc;
         }
       }
-      slot = __shfl(slot, leader, 64);
-      if (slot >= 0) {
-        for (int e = l; e < dim; e += G) atomicAdd(&vals[slot * dim + e], src[e] * sc);
-      } else {  // LDS table full: direct global path
-        if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
-        for (int e = l; e < dim; e += G) atomicAdd(grad_table + (int64_t)row * dim + e, src[e] * sc);
+#pragma unroll
+      for (int u = 0; u < CH; ++u)
+        if (rw[u] >= 0) insert(rw[u], nullptr, 0.f, vv[u]);
+    }
+  } else {
+    for (int64_t b = b0 + gsub; b < b1; b += per_pass) {
+      const int64_t sg = b * F + f;
+      const int64_t beg = offsets ? offsets[sg] : sg;
+      const int64_t end = offsets ? offsets[sg + 1] : sg + 1;
+      if (end <= beg) continue;
+      const float sc = combiner_scale((int)(end - beg), combiner);
+      const float* src = dout + b * dout_ld + (int64_t)f * dout_fstride;
+      for (int64_t k = beg; k < end; ++k) {
+        const int32_t row = rows[k];
+        if (row < 0) continue;  // padded sequence position (rs_sequence_lookup_fwd)
+        insert(row, src, sc, 0.f);
       }
     }
   }
@@ -263,11 +295,21 @@ __global__ void __launch_bounds__(256) sparse_grad_accum_kernel(
   int32_t& base = ctl[1];
   if (threadIdx.x == 0) nclaim = 0;
   __syncthreads();
-  for (int slot = threadIdx.x; slot < cap; slot += blockDim.x) {
-    const int32_t row = keys[slot];
-    int32_t li = -1;
-    if (row >= 0 && atomicCAS(&flag[row], -1, -2) == -1) li = atomicAdd(&nclaim, 1);
-    lidx[slot] = li;
+  for (int s0 = threadIdx.x; s0 < cap; s0 += 4 * blockDim.x) {
+    // four returning flag CASes in flight per thread (each is a memory-side round trip)
+    int32_t rw[4], old[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int slot = s0 + u * blockDim.x;
+      rw[u] = slot < cap ? keys[slot] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) old[u] = rw[u] >= 0 ? atomicCAS(&flag[rw[u]], -1, -2) : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int slot = s0 + u * blockDim.x;
+      if (slot < cap) lidx[slot] = (rw[u] >= 0 && old[u] == -1) ? atomicAdd(&nclaim, 1) : -1;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) base = nclaim > 0 ? atomicAdd(n_touched, nclaim) : 0;
@@ -298,6 +340,10 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
   // for single-hot fields)
   int cap = 1024;
   while (cap > 32 && (size_t)cap * (dim + 2) * 4 > 64 * 1024) cap >>= 1;
+  if (const char* e = getenv("RS_ACCUM_CAP")) {  // tuning experiment only
+    const int c = atoi(e);
+    if (c >= 32 && c <= cap && (c & (c - 1)) == 0) cap = c;
+  }
   const int tile = cap / 2;
   dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
   const size_t lds = ((size_t)cap * (dim + 2) + 4) * 4;

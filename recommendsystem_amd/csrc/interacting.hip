@@ -67,3 +67,11 @@ RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const flo
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
   return r;
 }
+
+RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats) {
+  (void)F;  // both kernel families use the same grid rule
+  int64_t grid = B < rs_il::kMaxBwdGrid ? B : rs_il::kMaxBwdGrid;
+  const int64_t by_ws = workspace_floats / rs_il_param_count(E, U);
+  if (grid > by_ws) grid = by_ws;
+  return (int)(grid < 0 ? 0 : grid);
+}

@@ -63,10 +63,17 @@ RS_API int rs_dense_adam(void* stream, float* params, float* grads, float* m, fl
 // The row count lives on the device (written by rs_sparse_grad_accumulate), so the grid is sized
 // by the capacity and idle groups exit: no host sync, graph-capturable.
 // ---------------------------------------------------------------------------------------------
+// n_touched = int32[1 + RS_DONE_WORDS]: {count, completion counters}.  Every block of a sparse
+// optimizer launch reads count first; the last block to finish resets it (rs_last_block), so the
+// next step's accumulate starts from zero without a separate memset launch.
+__device__ __forceinline__ void release_touched_count(int32_t* n_touched) {
+  if (rs_last_block(n_touched + 1)) atomicExch(n_touched, 0);
+}
+
 __global__ void __launch_bounds__(256) sparse_adam_kernel(
     float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ grad_table, int32_t* __restrict__ flag,
-    const int32_t* __restrict__ touched, const int32_t* __restrict__ n_touched, int dim,
+    const int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int dim,
     int lps, float lr, float b1, float b2, float eps, float grad_scale) {
   const int nrows = *n_touched;
   const int per_block = blockDim.x / lps;
@@ -86,12 +93,13 @@ __global__ void __launch_bounds__(256) sparse_adam_kernel(
     }
     if (l == 0) flag[row] = -1;
   }
+  release_touched_count(n_touched);
 }
 
 __global__ void __launch_bounds__(256) sparse_adagrad_kernel(
     float* __restrict__ table, float* __restrict__ g2sum, float* __restrict__ grad_table,
     int32_t* __restrict__ flag, const int32_t* __restrict__ touched,
-    const int32_t* __restrict__ n_touched, int dim, int lps, float lr, float grad_scale) {
+    int32_t* __restrict__ n_touched, int dim, int lps, float lr, float grad_scale) {
   const int nrows = *n_touched;
   const int per_block = blockDim.x / lps;
   const int gi = threadIdx.x / lps;
@@ -108,6 +116,7 @@ __global__ void __launch_bounds__(256) sparse_adagrad_kernel(
     }
     if (l == 0) flag[row] = -1;
   }
+  release_touched_count(n_touched);
 }
 
 static int lanes_for_dim(int dim) {
@@ -126,12 +135,13 @@ RS_API int rs_sparse_adam(void* stream, float* table, float* m, float* v, float*
   const int lps = lanes_for_dim(dim);
   if (max_rows > 0) {
     int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
-    if (grid > 4096) grid = 4096;
+    if (grid > 1024) grid = 1024;
     sparse_adam_kernel<<<(int)grid, 256, 0, s>>>(table, m, v, grad_table, flag, touched,
                                                  n_touched, dim, lps, lr, beta1, beta2, eps,
                                                  grad_scale);
   }
-  hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+  else
+    (void)hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
   return rs_status_after_launch();
 }
 
@@ -144,11 +154,12 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
   const int lps = lanes_for_dim(dim);
   if (max_rows > 0) {
     int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
-    if (grid > 4096) grid = 4096;
+    if (grid > 1024) grid = 1024;
     sparse_adagrad_kernel<<<(int)grid, 256, 0, s>>>(table, g2sum, grad_table, flag, touched,
                                                     n_touched, dim, lps, lr, grad_scale);
   }
-  hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+  else
+    (void)hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
   return rs_status_after_launch();
 }
 
@@ -261,5 +272,127 @@ RS_API int rs_l1l2_grad(void* stream, const float* params, float* grads, int64_t
   int64_t grid = (n + 255) / 256;
   if (grid > 4096) grid = 4096;
   l1l2_grad_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(params, grads, n, l1, l2);
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-block gradient partials -> gradients -> dense Adam, one launch.
+// The fused training kernels (InteractingLayer backward, the MLP head) leave one partial row per
+// workgroup in a workspace; this kernel sums every column over its rows in a FIXED order (16 row
+// groups, each in row order, then the groups in order: bitwise reproducible), writes the
+// gradient, and, when adam != 0, applies the tf.keras-form Adam of rs_dense_adam to that element
+// in the same pass.  Up to RS_RED_MAXSEG column segments, each mapped to an arena offset (Adam
+// applies) or to a plain output (e.g. the per-block loss column -> the batch-mean loss).
+// The Adam step counter is read by every block and advanced by the last block to finish
+// (completion counter `done`, zero between launches), so no separate increment launch.
+// ---------------------------------------------------------------------------------------------
+#define RS_RED_MAXSEG 4
+struct RedSeg {
+  const float* part;
+  int64_t ld;
+  int32_t nrows;
+  int64_t ncols;
+  float* out;       // gradient / output destination
+  float scale;      // out = sum * scale
+  int64_t adam_off; // arena index of column 0 (Adam applies), or -1
+};
+struct RedArgs {
+  RedSeg seg[RS_RED_MAXSEG];
+  int64_t col0[RS_RED_MAXSEG + 1];
+  int nseg;
+  float *params, *m, *v;
+  const int64_t* step_in;
+  int64_t* step;
+  int32_t* done;
+  float lr, b1, b2, eps, grad_scale;
+  int adam;
+};
+
+__global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
+  // 32 columns x 32 row groups per block (partial rows are up to ~1024 deep: more groups keep
+  // the per-thread chain short); each group sums its rows with 4 independent partial sums
+  constexpr int G = 32, NCB = 32;
+  __shared__ float red[G][NCB];
+  const int lc = threadIdx.x & (NCB - 1), g = threadIdx.x / NCB;
+  const int64_t c = (int64_t)blockIdx.x * NCB + lc;
+  int si = -1;
+#pragma unroll
+  for (int k = 0; k < RS_RED_MAXSEG; ++k)
+    if (k < a.nseg && c >= a.col0[k] && c < a.col0[k + 1]) si = k;
+  float s = 0.f;
+  int64_t cc = 0;
+  if (si >= 0) {
+    const RedSeg& sg = a.seg[si];
+    cc = c - a.col0[si];
+    const float* p = sg.part + cc;
+    // rows g, g+G, g+2G, g+3G, ... into four independent sums (loads in flight, not a chain);
+    // the combine order is fixed (deterministic)
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int r = g;
+#pragma unroll 2
+    for (; r + 3 * G < sg.nrows; r += 4 * G) {
+      s0 += p[(int64_t)r * sg.ld];
+      s1 += p[(int64_t)(r + G) * sg.ld];
+      s2 += p[(int64_t)(r + 2 * G) * sg.ld];
+      s3 += p[(int64_t)(r + 3 * G) * sg.ld];
+    }
+    for (; r < sg.nrows; r += G) s0 += p[(int64_t)r * sg.ld];
+    s = (s0 + s1) + (s2 + s3);
+  }
+  red[g][lc] = s;
+  __syncthreads();
+  if (g == 0 && si >= 0) {
+    const RedSeg& sg = a.seg[si];
+    float t = red[0][lc];
+#pragma unroll
+    for (int k = 1; k < G; ++k) t += red[k][lc];
+    t *= sg.scale;
+    sg.out[cc] = t;
+    if (a.adam && sg.adam_off >= 0) {
+      const int64_t i = sg.adam_off + cc;
+      const int64_t step = a.step_in[0] + 1;
+      const float bc1 = 1.0f - powf(a.b1, (float)step);
+      const float bc2 = 1.0f - powf(a.b2, (float)step);
+      const float lr_t = a.lr * sqrtf(bc2) / bc1;
+      const float gi = t * a.grad_scale;
+      const float mi = a.b1 * a.m[i] + (1.0f - a.b1) * gi;
+      const float vi = a.b2 * a.v[i] + (1.0f - a.b2) * gi * gi;
+      a.m[i] = mi;
+      a.v[i] = vi;
+      a.params[i] -= lr_t * mi / (sqrtf(vi) + a.eps);
+    }
+  }
+  if (a.adam && a.step) {
+    // every block has consumed step_in (the Adam reads above) before it arrives
+    if (rs_last_block(a.done)) a.step[0] = a.step_in[0] + 1;
+  }
+}
+
+RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
+                                   const int64_t* lds, const int32_t* nrows,
+                                   const int64_t* ncols, float* const* outs, const float* scales,
+                                   const int64_t* adam_offs, float* params, float* m, float* v,
+                                   int64_t* step, int32_t* done, float lr, float beta1,
+                                   float beta2, float eps, float grad_scale, int adam) {
+  if (nseg <= 0 || nseg > RS_RED_MAXSEG || !parts || !lds || !nrows || !ncols || !outs || !scales ||
+      !adam_offs)
+    return RS_ERR_ARG;
+  if (adam && (!params || !m || !v || !step || !done)) return RS_ERR_ARG;
+  RedArgs a{};
+  a.nseg = nseg;
+  int64_t tot = 0;
+  for (int k = 0; k < nseg; ++k) {
+    if (!parts[k] || !outs[k] || nrows[k] < 0 || ncols[k] < 0 || lds[k] < ncols[k]) return RS_ERR_ARG;
+    a.seg[k] = RedSeg{parts[k], lds[k], nrows[k], ncols[k], outs[k], scales[k], adam_offs[k]};
+    a.col0[k] = tot;
+    tot += ncols[k];
+  }
+  for (int k = nseg; k <= RS_RED_MAXSEG; ++k) a.col0[k] = tot;
+  a.params = params; a.m = m; a.v = v;
+  a.step_in = step; a.step = step; a.done = done;
+  a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.grad_scale = grad_scale; a.adam = adam;
+  if (tot == 0) return RS_OK;
+  const unsigned grid = (unsigned)((tot + 31) / 32);
+  partials_reduce_adam_kernel<<<grid, 1024, 0, rs_stream(stream)>>>(a);
   return rs_status_after_launch();
 }

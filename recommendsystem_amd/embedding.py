@@ -74,7 +74,7 @@ class SparseTable:
         cap = int(min(self.rows, max_touched)) if max_touched else self.rows
         self.touched_cap = cap
         self.touched = torch.zeros(cap, device=device, dtype=torch.int32)
-        self.n_touched = torch.zeros(1, device=device, dtype=torch.int32)
+        self.n_touched = torch.zeros(1 + 288, device=device, dtype=torch.int32)  # {count, completion counters}
         if isinstance(self.optimizer, SparseAdam):
             self.m = torch.zeros_like(self.weight)
             self.v = torch.zeros_like(self.weight)

@@ -22,7 +22,7 @@ def exchange_sparse(table, pg, world, x_rows, x_grads):
     """Data-parallel sparse exchange of one table (dist.py protocol): compact -> all-gather ->
     merge in rank order."""
     from .dist import gather_sparse_lists
-    cnt = table.n_touched.clone()
+    cnt = table.n_touched[:1].clone()
     call("rs_sparse_compact", stream_handle(), ptr(table.grad), ptr(table.flag), ptr(table.touched),
          ptr(table.n_touched), table.dim, ptr(x_rows), ptr(x_grads), table.touched_cap)
     table.n_touched.zero_()

@@ -169,7 +169,7 @@ def test_sequence_lookup_and_push(hash_mode):
             if ref_rows[b, t] >= 0:
                 expect[ref_rows[b, t]] += dout[b, t]
     assert_close(grad, expect, 1e-5, 1e-6, "sequence push")
-    touched = set(table.touched[: int(table.n_touched.item())].cpu().numpy().tolist())
+    touched = set(table.touched[: int(table.n_touched[0].item())].cpu().numpy().tolist())
     assert touched == set(int(r) for r in ref_rows[ref_rows >= 0].ravel())
     # AdaGrad step on exactly those rows (tensornet AdaGrad form, csrc/optim.hip)
     g2_before = table.g2sum.cpu().numpy().astype(np.float64)
@@ -181,4 +181,4 @@ def test_sequence_lookup_and_push(hash_mode):
     assert_close(table.g2sum.cpu().numpy()[rows], g2_ref, 1e-5, 1e-5, "adagrad g2sum")
     untouched = np.setdiff1d(np.arange(table.rows), rows)
     assert np.array_equal(table.weight.cpu().numpy()[untouched], w[untouched])
-    assert int(table.n_touched.item()) == 0 and bool((table.flag == -1).all())
+    assert int(table.n_touched[0].item()) == 0 and bool((table.flag == -1).all())
