@@ -386,12 +386,13 @@ class AutoIntTrainer:
     def capture(self, warmup: int = 2) -> None:
         """Capture the single-GPU step into a HIP graph (N > 1 keeps collectives eager and
         captures the compute-only halves)."""
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self._step_eager()
-        torch.cuda.current_stream().wait_stream(side)
+        if warmup > 0:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self._step_eager()
+            torch.cuda.current_stream().wait_stream(side)
         if self.world == 1:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
@@ -404,6 +405,30 @@ class AutoIntTrainer:
             with torch.cuda.graph(self.graph_opt):
                 self._optimize()
             self.graph = True
+
+    def capture_pool(self, batches, warmup: int = 2) -> None:
+        """One graph per device-resident batch [(ids, labels), ...]: each graph's lookup and loss
+        read that batch's own buffers, so replaying batch i needs no copy into a static input
+        (what a double-buffered loader hands over).  ``step_pool(i)`` replays batch i."""
+        self.pool_graphs = []
+        for k, (ids, labels) in enumerate(batches):
+            if ids.shape != (self.B, self.F) or ids.dtype != torch.int64 or not ids.is_contiguous():
+                raise ValueError("pool ids must be contiguous int64 [B, F]")
+            self.ids = ids
+            self.labels = labels.reshape(self.B, self.T).float().contiguous()
+            self.graph = None
+            self.capture(warmup=warmup if k == 0 else 0)
+            self.pool_graphs.append((self.graph, getattr(self, "graph_fb", None)))
+
+    def step_pool(self, i: int) -> torch.Tensor:
+        g, gfb = self.pool_graphs[i % len(self.pool_graphs)]
+        if self.world == 1:
+            g.replay()
+        else:
+            gfb.replay()
+            self._exchange()
+            self.graph_opt.replay()
+        return self.loss
 
     def step(self, ids: torch.Tensor | None = None, labels: torch.Tensor | None = None) -> torch.Tensor:
         if ids is not None:

@@ -295,10 +295,11 @@ struct RedSeg {
   float* out;       // gradient / output destination
   float scale;      // out = sum * scale
   int64_t adam_off; // arena index of column 0 (Adam applies), or -1
+  int32_t lg;       // log2 of the row groups per block (G); columns per block = 1024 / G
+  int32_t blk0;     // first block of this segment
 };
 struct RedArgs {
   RedSeg seg[RS_RED_MAXSEG];
-  int64_t col0[RS_RED_MAXSEG + 1];
   int nseg;
   float *params, *m, *v;
   const int64_t* step_in;
@@ -308,58 +309,66 @@ struct RedArgs {
   int adam;
 };
 
+// Block shape per segment (host-chosen): G row groups x (1024 / G) columns, G the smallest power
+// of two with <= 16 rows per thread (IL partials: 1024 rows -> 64 groups x 16 columns over 70
+// blocks; head partials: 256 rows -> 16 x 64 over 224 blocks: the whole launch is one round).  Spreading deep segments over many CUs matters:
+// one CU keeps only ~72 KB of loads in flight, so 1024 rows x 32 columns on one CU took ~11 us.
 __global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
-  // 32 columns x 32 row groups per block (partial rows are up to ~1024 deep: more groups keep
-  // the per-thread chain short); each group sums its rows with 4 independent partial sums
-  constexpr int G = 32, NCB = 32;
-  __shared__ float red[G][NCB];
-  const int lc = threadIdx.x & (NCB - 1), g = threadIdx.x / NCB;
-  const int64_t c = (int64_t)blockIdx.x * NCB + lc;
-  int si = -1;
+  __shared__ float red[1024];
+  int si = 0;
 #pragma unroll
-  for (int k = 0; k < RS_RED_MAXSEG; ++k)
-    if (k < a.nseg && c >= a.col0[k] && c < a.col0[k + 1]) si = k;
-  float s = 0.f;
-  int64_t cc = 0;
-  if (si >= 0) {
-    const RedSeg& sg = a.seg[si];
-    cc = c - a.col0[si];
-    const float* p = sg.part + cc;
-    // rows g, g+G, g+2G, g+3G, ... into four independent sums (loads in flight, not a chain);
-    // the combine order is fixed (deterministic)
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int r = g;
-#pragma unroll 2
-    for (; r + 3 * G < sg.nrows; r += 4 * G) {
-      s0 += p[(int64_t)r * sg.ld];
-      s1 += p[(int64_t)(r + G) * sg.ld];
-      s2 += p[(int64_t)(r + 2 * G) * sg.ld];
-      s3 += p[(int64_t)(r + 3 * G) * sg.ld];
-    }
-    for (; r < sg.nrows; r += G) s0 += p[(int64_t)r * sg.ld];
-    s = (s0 + s1) + (s2 + s3);
+  for (int k = 1; k < RS_RED_MAXSEG; ++k)
+    if (k < a.nseg && (int)blockIdx.x >= a.seg[k].blk0) si = k;  // block-uniform
+  const RedSeg sg = a.seg[si];
+  const int G = 1 << sg.lg, NC = 1024 >> sg.lg;
+  const int lc = threadIdx.x & (NC - 1), g = threadIdx.x >> (10 - sg.lg);
+  const int64_t cc = (int64_t)(blockIdx.x - sg.blk0) * NC + lc;
+  const bool col_ok = cc < sg.ncols;
+  // Adam operands are fetched before the partial rows, so their round trip overlaps the sums
+  const bool do_adam = a.adam && sg.adam_off >= 0 && g == 0 && col_ok;
+  float m0 = 0.f, v0 = 0.f, p0 = 0.f, lr_t = 0.f;
+  if (do_adam) {
+    const int64_t i = sg.adam_off + cc;
+    m0 = a.m[i]; v0 = a.v[i]; p0 = a.params[i];
+    const int64_t step = a.step_in[0] + 1;
+    const float bc1 = 1.0f - powf(a.b1, (float)step);
+    const float bc2 = 1.0f - powf(a.b2, (float)step);
+    lr_t = a.lr * sqrtf(bc2) / bc1;
   }
-  red[g][lc] = s;
-  __syncthreads();
-  if (g == 0 && si >= 0) {
-    const RedSeg& sg = a.seg[si];
-    float t = red[0][lc];
+  float s = 0.f;
+  if (col_ok) {
+    const float* p = sg.part + cc;
+    // every row of this thread (g, g+G, ...) is loaded before the first add (one memory round
+    // trip), then summed in row order (fixed order: deterministic)
+    constexpr int MAXR = 16;
+    for (int r = g; r < sg.nrows; r += MAXR * G) {
+      float v[MAXR];
 #pragma unroll
-    for (int k = 1; k < G; ++k) t += red[k][lc];
-    t *= sg.scale;
+      for (int u = 0; u < MAXR; ++u) {
+        const int rr = r + u * G;
+        v[u] = rr < sg.nrows ? p[(int64_t)rr * sg.ld] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < MAXR; ++u) s += v[u];
+    }
+  }
+  red[threadIdx.x] = s;  // [g][lc]
+  __syncthreads();
+  for (int o = G >> 1; o > 0; o >>= 1) {  // fixed pairing: deterministic
+    if (g < o) red[threadIdx.x] += red[threadIdx.x + o * NC];
+    __syncthreads();
+  }
+  if (g == 0 && col_ok) {
+    const float t = red[lc] * sg.scale;
     sg.out[cc] = t;
-    if (a.adam && sg.adam_off >= 0) {
+    if (do_adam) {
       const int64_t i = sg.adam_off + cc;
-      const int64_t step = a.step_in[0] + 1;
-      const float bc1 = 1.0f - powf(a.b1, (float)step);
-      const float bc2 = 1.0f - powf(a.b2, (float)step);
-      const float lr_t = a.lr * sqrtf(bc2) / bc1;
       const float gi = t * a.grad_scale;
-      const float mi = a.b1 * a.m[i] + (1.0f - a.b1) * gi;
-      const float vi = a.b2 * a.v[i] + (1.0f - a.b2) * gi * gi;
+      const float mi = a.b1 * m0 + (1.0f - a.b1) * gi;
+      const float vi = a.b2 * v0 + (1.0f - a.b2) * gi * gi;
       a.m[i] = mi;
       a.v[i] = vi;
-      a.params[i] -= lr_t * mi / (sqrtf(vi) + a.eps);
+      a.params[i] = p0 - lr_t * mi / (sqrtf(vi) + a.eps);
     }
   }
   if (a.adam && a.step) {
@@ -380,19 +389,21 @@ RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* p
   if (adam && (!params || !m || !v || !step || !done)) return RS_ERR_ARG;
   RedArgs a{};
   a.nseg = nseg;
-  int64_t tot = 0;
+  int64_t nblk = 0;
   for (int k = 0; k < nseg; ++k) {
     if (!parts[k] || !outs[k] || nrows[k] < 0 || ncols[k] < 0 || lds[k] < ncols[k]) return RS_ERR_ARG;
-    a.seg[k] = RedSeg{parts[k], lds[k], nrows[k], ncols[k], outs[k], scales[k], adam_offs[k]};
-    a.col0[k] = tot;
-    tot += ncols[k];
+    int lg = 0;  // G = 2^lg row groups: <= 16 rows per thread, at most 1024 groups
+    while (lg < 10 && ((int64_t)16 << lg) < nrows[k]) ++lg;
+    const int64_t nc = 1024 >> lg;
+    a.seg[k] = RedSeg{parts[k], lds[k], nrows[k], ncols[k], outs[k], scales[k], adam_offs[k], lg,
+                      (int32_t)nblk};
+    nblk += (ncols[k] + nc - 1) / nc;
   }
-  for (int k = nseg; k <= RS_RED_MAXSEG; ++k) a.col0[k] = tot;
+  for (int k = nseg; k < RS_RED_MAXSEG; ++k) a.seg[k].blk0 = (int32_t)nblk;
   a.params = params; a.m = m; a.v = v;
   a.step_in = step; a.step = step; a.done = done;
   a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.grad_scale = grad_scale; a.adam = adam;
-  if (tot == 0) return RS_OK;
-  const unsigned grid = (unsigned)((tot + 31) / 32);
-  partials_reduce_adam_kernel<<<grid, 1024, 0, rs_stream(stream)>>>(a);
+  if (nblk == 0) return RS_OK;
+  partials_reduce_adam_kernel<<<(unsigned)nblk, 1024, 0, rs_stream(stream)>>>(a);
   return rs_status_after_launch();
 }
