@@ -59,7 +59,9 @@ int rs_sequence_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offs
  * gradients to its PS): grad_table[rows[k]] += scale(s) * dout[s] for every id k of segment s.
  * Rows touched for the first time this step are claimed (flag -1 -> -2) and appended to
  * touched[*n_touched++] (capacity touched_cap).  flag[] must be all -1 between steps (the
- * optimizer entry points restore it). */
+ * optimizer entry points restore it).  touched == NULL selects SCAN mode: rows are only marked
+ * (flag = -2, plain stores; no claims, n_touched unused) for rs_sparse_adam_scan /
+ * rs_sparse_adagrad_scan / rs_sparse_compact_scan. */
 int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
                               int64_t B, int F, const float* dout, int64_t dout_ld,
                               int64_t dout_fstride, int dim, int combiner, float* grad_table,
@@ -79,6 +81,24 @@ int rs_sparse_adam(void* stream, float* table, float* m, float* v, float* grad_t
 int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* grad_table, int32_t* flag,
                       const int32_t* touched, int32_t* n_touched, int dim, int32_t max_rows,
                       float lr, float grad_scale);
+
+/* Scan-mode sparse optimizers (same update forms): sweep flag[0 .. table_rows) and update every
+ * row marked by a scan-mode push (rs_sparse_grad_accumulate with touched == NULL,
+ * rs_il_bwd_push, rs_sparse_merge_rows with touched == NULL); zero its gradient row, clear its
+ * flag.  dim % 4 == 0. */
+int rs_sparse_adam_scan(void* stream, float* table, float* m, float* v, float* grad_table,
+                        int32_t* flag, int64_t table_rows, int dim, float lr, float beta1,
+                        float beta2, float eps, float grad_scale);
+int rs_sparse_adagrad_scan(void* stream, float* table, float* g2sum, float* grad_table,
+                           int32_t* flag, int64_t table_rows, int dim, float lr,
+                           float grad_scale);
+
+/* Scan-mode compaction for the DP exchange: move every marked row into (rows_out, grads_out)
+ * (gradient row zeroed, flag cleared), *n_out = count (slots past cap are dropped),
+ * rows_out[count .. cap) = -1. */
+int rs_sparse_compact_scan(void* stream, float* grad_table, int32_t* flag, int64_t table_rows,
+                           int dim, int32_t* rows_out, float* grads_out, int32_t* n_out,
+                           int32_t cap);
 
 /* Data-parallel sparse exchange (replaces tensornet's PS push across workers):
  * compact moves this rank's touched rows into (rows_out, grads_out) (padding rows = -1) and
@@ -329,6 +349,18 @@ int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
                             float* params, float* m, float* v, int64_t* step, int32_t* done,
                             float lr, float beta1, float beta2, float eps, float grad_scale,
                             int adam);
+
+/* rs_il_bwd with the sparse push fused into its last pass (F <= 64): dL/dx of the layer input
+ * is not stored; instead grad_table[rows[b * F + f]] += dL/dx[b, f] (+ dx_base[b, f] when
+ * dx_base != NULL, e.g. the deep tower's share of dL/dx0) with float atomics and the rows are
+ * marked scan-mode (flag = -2).  Replaces rs_il_bwd(dx_accumulate = 1) followed by
+ * rs_sparse_grad_accumulate(touched = NULL) for single-id fields (rows = lookup rows_out). */
+int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,
+                   int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L, const float* W,
+                   const float* bias, const float* gamma, const float* beta, float eps,
+                   int use_res, float drop_rate, uint64_t seed, const float* dx_base,
+                   const int32_t* rows, float* grad_table, int32_t* flag, float* dparams,
+                   int dparams_accumulate, float* workspace, int64_t workspace_floats);
 
 /* Grid (= number of per-block partial rows) rs_il_bwd uses for a given batch and workspace. */
 int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats);

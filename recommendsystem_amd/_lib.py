@@ -102,6 +102,13 @@ SIGNATURES: dict[str, tuple] = {
     "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
     "rs_il_bwd_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i64]),
+    "rs_sparse_adam_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
+                                   _f32, _f32]),
+    "rs_sparse_adagrad_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),
+    "rs_sparse_compact_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i32]),
+    "rs_il_bwd_push": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
+                              _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp,
+                              _i32, _vp, _i64]),
 }
 
 _LIB = None

@@ -175,10 +175,15 @@ class AutoIntTrainer:
                                   il.kernel.numel() + il.bias.numel() + il.gamma.numel() + il.beta.numel()]
         self.graph = None
         self.head = self._plan_head()
+        # fused path: the IL backward pushes dL/dx0 straight into the table (scan-mode marks)
+        self.push = self.head is not None and self.F <= 64
+        if self.push:
+            m.table.mode = "scan"
         if self.world > 1:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
             self.x_grads = torch.empty(cap, E, **f32)
+            self.x_count = torch.zeros(1, device=dev, dtype=torch.int32)
 
     def _offset(self, p: torch.Tensor) -> int:
         return (p.data_ptr() - self.model.arena.data.data_ptr()) // 4
@@ -253,6 +258,14 @@ class AutoIntTrainer:
              ptr(lg.kernel), ptr(lg.bias), ptr(self.labels), 1e-6, 1.0, 1e-6, ptr(self.p),
              self.dcat.data_ptr() + 4 * D, CW, ptr(self.dx0), F * E, 0, ptr(hd["ws"]),
              hd["ws"].numel())
+        if self.push:
+            # dL/dx0 = head share (dx0) + IL share, added straight into the table rows
+            call("rs_il_bwd_push", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+                 self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+                 ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
+                 ptr(self.dx0), ptr(self.rows), ptr(t.grad), ptr(t.flag), None, 0,
+                 ptr(self.il_ws), self.il_ws_n)
+            return
         call("rs_il_bwd", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
              self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
              ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed, ptr(self.dx0),
@@ -351,14 +364,21 @@ class AutoIntTrainer:
         from .dist import allreduce_flat, gather_sparse_lists
         m, t = self.model, self.model.table
         allreduce_flat(m.arena.grad, self.pg)
-        cnt = t.n_touched[:1].clone()
-        call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
-             ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
-        t.n_touched.zero_()
+        scan = t.mode == "scan"
+        if scan:
+            call("rs_sparse_compact_scan", stream_handle(), ptr(t.grad), ptr(t.flag), t.rows, t.dim,
+                 ptr(self.x_rows), ptr(self.x_grads), ptr(self.x_count), t.touched_cap)
+            cnt = self.x_count
+        else:
+            cnt = t.n_touched[:1].clone()
+            call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
+                 ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
+            t.n_touched.zero_()
         rows_all, grads_all, n = gather_sparse_lists(self.x_rows, self.x_grads, cnt, self.pg)
         for r in range(self.world if n else 0):  # rank order -> identical sums on every replica
             call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,
-                 t.dim, ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched), t.touched_cap)
+                 t.dim, ptr(t.grad), ptr(t.flag), None if scan else ptr(t.touched),
+                 None if scan else ptr(t.n_touched), t.touched_cap)
 
     def _optimize(self):
         m, cfg = self.model, self.model.cfg

@@ -169,3 +169,11 @@ __device__ __forceinline__ bool rs_last_block(int32_t* ctr) {
   atomicExch(top, 0);
   return true;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Scan-mode row mark: flag[row] = -2 with a plain store (idempotent: the hot rows of a Zipf
+// batch receive thousands of marks, which coalesce in L2; an atomic bitmap update serialised
+// them at the memory side and cost the InteractingLayer backward ~10 us).  Clean state is -1,
+// shared with list mode.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void scan_mark(int32_t* flag, int64_t row) { flag[row] = -2; }

@@ -242,7 +242,10 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
       if (src) for (int e = l; e < dim; e += G) atomicAdd(&vals[slot * dim + e], src[e] * sc);
       else if (l < dim) atomicAdd(&vals[slot * dim + l], v0);
     } else {  // LDS table full: direct global path
-      if (l == 0) claim_row(row, flag, touched, n_touched, touched_cap);
+      if (l == 0) {
+        if (touched) claim_row(row, flag, touched, n_touched, touched_cap);
+        else scan_mark(flag, row);
+      }
       if (src) for (int e = l; e < dim; e += G) atomicAdd(grad_table + (int64_t)row * dim + e, src[e] * sc);
       else if (l < dim) atomicAdd(grad_table + (int64_t)row * dim + l, v0);
     }
@@ -286,6 +289,18 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
     }
   }
   __syncthreads();
+  if (!touched) {
+    // scan mode (touched == NULL): mark rows with a plain store (idempotent; no claims, no shared
+    // counter); the scan-mode optimizer finds them by sweeping flag[]
+    for (int slot = gsub; slot < cap; slot += per_pass) {
+      const int32_t row = keys[slot];
+      if (row < 0) continue;
+      if (l == 0) scan_mark(flag, row);
+      float* dst = grad_table + (int64_t)row * dim;
+      for (int e = l; e < dim; e += G) atomicAdd(dst + e, vals[slot * dim + e]);
+    }
+    return;
+  }
   // ---- phase 2: claim each distinct row once (flag CAS); the claims of the whole block take ONE
   //      global atomic on n_touched (a single counter word serialises ~11 ns per atomic at the
   //      memory side: 30k per-row increments would cost ~0.3 ms) ----
@@ -330,8 +345,8 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
                                      int64_t dout_fstride, int dim, int combiner,
                                      float* grad_table, int32_t* flag, int32_t* touched,
                                      int32_t* n_touched, int32_t touched_cap) {
-  if (!rows || !dout || !grad_table || !flag || !touched || !n_touched || F <= 0 || dim <= 0)
-    return RS_ERR_ARG;
+  if (!rows || !dout || !grad_table || !flag || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
   if (B * (int64_t)F == 0) return RS_OK;
   int G = 1;
   while (G < dim && G < 64) G <<= 1;

@@ -61,6 +61,12 @@ struct BwdReq {
   int dparams_accumulate;
   float* workspace;
   int64_t workspace_floats;
+  // fused sparse push (rs_il_bwd_push): dL/dx of the first iteration is added (with dx's
+  // current contents when dx_accumulate) straight into push_table rows push_rows[b * F + f],
+  // marking push_flag[row] = -2 (scan mode) instead of being stored to dx
+  const int32_t* push_rows = nullptr;
+  float* push_table = nullptr;
+  int32_t* push_flag = nullptr;
 };
 
 constexpr int kMaxFwdWaves = 4;
@@ -124,6 +130,9 @@ struct Args {
   uint64_t seed;
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
   unsigned long long* stamps;  // diagnostic build only
+  const int32_t* push_rows;    // fused sparse push (see BwdReq)
+  float* push_table;
+  int32_t* push_flag;
 };
 
 static inline int r4(int v) { return (v + 3) & ~3; }
@@ -159,6 +168,9 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
 #else
   a.stamps = nullptr;
 #endif
+  a.push_rows = nullptr;
+  a.push_table = nullptr;
+  a.push_flag = nullptr;
   return a;
 }
 
@@ -364,6 +376,54 @@ __device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const Mfm
       if (f < F && e < C::E) {
         float* d = out + f * ld + e;
         *d = accumulate ? (*d + acc[et][r]) : acc[et][r];
+      }
+    }
+  }
+}
+
+// dx of row tile rt as in mfma_dx, but pushed into the sparse gradient table: for each row f,
+// grad_table[rows[f]][e] += dx[f][e] (+ base[f * E + e] when base != NULL: the deep tower's share
+// of dL/dx0 written earlier) with float atomics, and flag[rows[f]] = -2 (scan-mode mark).
+// This replaces the store of dx0 and the separate push kernel that re-read it.
+template <class C>
+__device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, const MfmaW<C>& w,
+                                             const float* base, const int32_t* rows,
+                                             float* table, int32_t* flag) {
+  using M = MfmaW<C>;
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  f32x4 acc[M::ET];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = 16 * rt + j;
+#pragma unroll
+  for (int cs = 0; cs < M::CS; ++cs) {
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (arow < F) {
+      const float4 v = *reinterpret_cast<const float4*>(G + arow * C::PRS + 16 * cs + 4 * q);
+      a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int f = 16 * rt + 4 * q + r;
+    if (f < F) {
+      const int32_t row = rows[f];
+      if (row >= 0) {
+        if (j == 0) scan_mark(flag, row);
+        float* dst = table + (int64_t)row * C::E;
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et) {
+          const int e = 16 * et + j;
+          if (e < C::E) {
+            float v = acc[et][r];
+            if (base) v += base[f * C::E + e];
+            atomicAdd(dst + e, v);
+          }
+        }
       }
     }
   }
@@ -804,6 +864,9 @@ __global__ void __launch_bounds__(128) bwd_kernel(
       for (int rt = w; rt < nrt; rt += 2) {
         mfma_dw<C>(X, GPR, F, rt, dwacc, dbp);
         if (it > 0) mfma_dx<C>(GPR, F, rt, mw, DY, C::U, false);  // dL/d(previous output)
+        else if (a.push_table)
+          mfma_dx_push<C>(GPR, F, rt, mw, dx_accumulate ? dx + b * F * C::E : nullptr,
+                          a.push_rows + b * F, a.push_table, a.push_flag);
         else mfma_dx<C>(GPR, F, rt, mw, dx + b * F * C::E, C::E, dx_accumulate != 0);
       }
       __syncthreads();
@@ -888,6 +951,9 @@ template <class C, bool DROP>
 int bwd_launch(const BwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
   Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
+  a.push_rows = q.push_rows;
+  a.push_table = q.push_table;
+  a.push_flag = q.push_flag;
   // exchange scratch fits: fwd partials (4 + 2*DH per row) in GPR, D partials in ST
   if (C::H * q.F * (5 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
   const size_t lds = (size_t)a.per_wave * sizeof(float);

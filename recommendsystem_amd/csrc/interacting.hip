@@ -47,6 +47,13 @@ RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int 
   return r;
 }
 
+static int bwd_small(const rs_il::BwdReq& q) {
+  int r = rs_il::il_unit_a_bwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
+  return r;
+}
+
 RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
                      int64_t dy_ld, int64_t B,
                      int F, int E, int U, int H, int L, const float* W, const float* bias,
@@ -62,10 +69,29 @@ RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const flo
                   use_res, eps, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
                   workspace, workspace_floats};
   if (F > 64) return rs_il::il_large_bwd(q);
-  int r = rs_il::il_unit_a_bwd(q);
-  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
-  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
-  return r;
+  return bwd_small(q);
+}
+
+RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,
+                          int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                          const float* W, const float* bias, const float* gamma,
+                          const float* beta, float eps, int use_res, float drop_rate,
+                          uint64_t seed, const float* dx_base, const int32_t* rows,
+                          float* grad_table, int32_t* flag, float* dparams,
+                          int dparams_accumulate, float* workspace, int64_t workspace_floats) {
+  if (!x || !dy || !W || !bias || !gamma || !beta || !rows || !grad_table || !flag || !workspace)
+    return RS_ERR_ARG;
+  if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
+    return RS_ERR_ARG;
+  if (drop_rate < 0.f || drop_rate >= 1.f || dy_ld < (int64_t)F * U) return RS_ERR_ARG;
+  if (F > 64) return RS_ERR_UNSUPPORTED;  // the many-field kernels have no fused push
+  rs_il::BwdReq q{rs_stream(stream), x, xsave, dy, W, bias, gamma, beta, dy_ld, B, F, E, U, H, L,
+                  use_res, eps, drop_rate, seed, const_cast<float*>(dx_base), dx_base != nullptr,
+                  dparams, dparams_accumulate, workspace, workspace_floats};
+  q.push_rows = rows;
+  q.push_table = grad_table;
+  q.push_flag = flag;
+  return bwd_small(q);
 }
 
 RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats) {

@@ -164,6 +164,189 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
 }
 
 // ---------------------------------------------------------------------------------------------
+// Scan-mode sparse optimizers: no touched list.  The push marked every touched row with
+// flag = -2 (plain stores).  The table is swept in 64-row chunks; wave w takes chunks
+// w, w + W, w + 2W, ... (W = waves in the grid, one chip-full round), so the dense chunks at the
+// head of each field's Zipf range are spread over many waves while every flag load stays one
+// coalesced 256-B read.  Per chunk: one flag load per lane (the next chunk's is issued before
+// the current one is processed), a ballot, the marked rows compacted into a wave-local LDS list
+// (mbcnt rank), then processed 64 / (dim / 4) rows per pass with dim / 4 lanes per row, each
+// lane moving one float4 of grad / param / m / v (one memory round trip per pass).
+// ---------------------------------------------------------------------------------------------
+constexpr int kScanBlock = 256;
+
+template <bool ADAM>
+__device__ __forceinline__ void scan_update4(float* __restrict__ table, float* __restrict__ m,
+                                             float* __restrict__ v,
+                                             float* __restrict__ grad_table, int64_t o, float lr,
+                                             float b1, float b2, float eps, float grad_scale) {
+  float4 g = *reinterpret_cast<const float4*>(grad_table + o);
+  float4 w = *reinterpret_cast<const float4*>(table + o);
+  float4 mm = *reinterpret_cast<const float4*>(m + o);
+  float4 vv = ADAM ? *reinterpret_cast<const float4*>(v + o) : mm;
+  float* gp = &g.x; float* wp = &w.x; float* mp = &mm.x; float* vp = &vv.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gk = gp[k] * grad_scale;
+    if (ADAM) {
+      mp[k] = b1 * mp[k] + (1.0f - b1) * gk;
+      vp[k] = b2 * vp[k] + (1.0f - b2) * gk * gk;
+      wp[k] -= lr * mp[k] / (eps + sqrtf(vp[k]));
+    } else {  // AdaGrad: m holds g2sum
+      mp[k] += gk * gk;
+      wp[k] -= lr * gk / sqrtf(mp[k]);
+    }
+  }
+  *reinterpret_cast<float4*>(table + o) = w;
+  *reinterpret_cast<float4*>(m + o) = mm;
+  if (ADAM) *reinterpret_cast<float4*>(v + o) = vv;
+  *reinterpret_cast<float4*>(grad_table + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <bool ADAM>
+__global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
+    float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
+    float lr, float b1, float b2, float eps, float grad_scale) {
+  __shared__ int32_t lists[kScanBlock];  // 64 row slots per wave
+  int32_t* list = lists + (threadIdx.x & ~63);
+  const int lane = threadIdx.x & 63;
+  const int64_t nchunks = (nrows + 63) / 64;
+  const int64_t nwaves = (int64_t)gridDim.x * (kScanBlock / 64);
+  const int64_t gw = (int64_t)blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6);
+  const int nv = dim >> 2;             // float4 per row
+  const int lpr = nv < 64 ? nv : 64;   // lanes per row
+  const int rpp = 64 / lpr;            // rows per pass
+  const int sub = lane % lpr, slot = lane / lpr;
+  int64_t c = gw;
+  int32_t fl = -1;
+  if (c < nchunks && c * 64 + lane < nrows) fl = flag[c * 64 + lane];
+  while (c < nchunks) {
+    const int64_t row0 = c * 64;
+    // prefetch the next chunk's flags
+    const int64_t cn = c + nwaves;
+    int32_t fn = -1;
+    if (cn < nchunks && cn * 64 + lane < nrows) fn = flag[cn * 64 + lane];
+    const bool hit = fl != -1;
+    const uint64_t mask = __ballot(hit);
+    if (mask) {
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+      if (hit) {
+        list[rank] = lane;
+        flag[row0 + lane] = -1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int n = __popcll(mask);
+      for (int p0 = 0; p0 < n; p0 += rpp) {
+        const int k = p0 + slot;
+        if (slot < rpp && k < n) {
+          const int64_t row = row0 + list[k];
+          for (int e4 = sub; e4 < nv; e4 += lpr)
+            scan_update4<ADAM>(table, m, v, grad_table, row * dim + 4 * e4, lr, b1, b2, eps,
+                               grad_scale);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // list reuse by the next chunk
+    }
+    fl = fn;
+    c = cn;
+  }
+}
+
+static int64_t scan_grid(int64_t nrows) {
+  // one chip-full round of waves (256 CUs x 32), fewer for small tables
+  const int64_t chunks = (nrows + 63) / 64;
+  int64_t grid = (chunks + kScanBlock / 64 - 1) / (kScanBlock / 64);
+  return grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
+}
+
+template <bool ADAM>
+static void launch_scan_opt(hipStream_t s, unsigned grid, float* table, float* m, float* v,
+                            float* grad, int32_t* flag, int64_t nrows, int dim, float lr, float b1,
+                            float b2, float eps, float gs) {
+  sparse_scan_opt_kernel<ADAM><<<grid, kScanBlock, 0, s>>>(table, m, v, grad, flag, nrows, dim, lr,
+                                                           b1, b2, eps, gs);
+}
+
+RS_API int rs_sparse_adam_scan(void* stream, float* table, float* m, float* v, float* grad_table,
+                               int32_t* flag, int64_t table_rows, int dim, float lr, float beta1,
+                               float beta2, float eps, float grad_scale) {
+  if (!table || !m || !v || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0)
+    return RS_ERR_ARG;
+  if (table_rows == 0) return RS_OK;
+  launch_scan_opt<true>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, m, v,
+                        grad_table, flag, table_rows, dim, lr, beta1, beta2, eps, grad_scale);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_adagrad_scan(void* stream, float* table, float* g2sum, float* grad_table,
+                                  int32_t* flag, int64_t table_rows, int dim, float lr,
+                                  float grad_scale) {
+  if (!table || !g2sum || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0)
+    return RS_ERR_ARG;
+  if (table_rows == 0) return RS_OK;
+  launch_scan_opt<false>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, g2sum,
+                         nullptr, grad_table, flag, table_rows, dim, lr, 0.f, 0.f, 0.f,
+                         grad_scale);
+  return rs_status_after_launch();
+}
+
+// Scan-mode compaction for the data-parallel exchange: every marked row is moved out of the
+// gradient table into (rows_out, grads_out) (gradient row zeroed, flag cleared); the slots are
+// allocated with one counter atomic per block (n_out[0]; rows past `cap` are dropped and
+// counted).  The list order is allocation order; the rank-ordered merge does not depend on it.
+__global__ void __launch_bounds__(256) sparse_compact_scan_kernel(
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
+    int32_t* __restrict__ rows_out, float* __restrict__ grads_out, int32_t* __restrict__ n_out,
+    int32_t cap) {
+  __shared__ int32_t cnt, base;
+  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < nrows;
+       r0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = r0 + threadIdx.x;
+    const bool hit = row < nrows && flag[row] != -1;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const int li = hit ? atomicAdd(&cnt, 1) : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) base = cnt > 0 ? atomicAdd(n_out, cnt) : 0;
+    __syncthreads();
+    if (hit) {
+      const int32_t u = base + li;
+      for (int e = 0; e < dim; e += 4) {
+        if (u < cap)
+          *reinterpret_cast<float4*>(grads_out + (int64_t)u * dim + e) =
+              *reinterpret_cast<const float4*>(grad_table + row * dim + e);
+        // over capacity the row's gradient is dropped (never left stale)
+        *reinterpret_cast<float4*>(grad_table + row * dim + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (u < cap) rows_out[u] = (int32_t)row;
+      flag[row] = -1;
+    }
+    __syncthreads();
+  }
+}
+
+RS_API int rs_sparse_compact_scan(void* stream, float* grad_table, int32_t* flag,
+                                  int64_t table_rows, int dim, int32_t* rows_out,
+                                  float* grads_out, int32_t* n_out, int32_t cap) {
+  if (!grad_table || !flag || !rows_out || !grads_out || !n_out || dim <= 0 || dim % 4)
+    return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  (void)hipMemsetAsync(n_out, 0, sizeof(int32_t), s);
+  // rows past the count read -1 (the padding the rank-ordered merge skips)
+  if (cap > 0) (void)hipMemsetAsync(rows_out, 0xFF, (size_t)cap * sizeof(int32_t), s);
+  if (table_rows == 0) return rs_status_after_launch();
+  int64_t grid = (table_rows + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  sparse_compact_scan_kernel<<<(int)grid, 256, 0, s>>>(grad_table, flag, table_rows, dim,
+                                                       rows_out, grads_out, n_out, cap);
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Data-parallel sparse exchange helpers.
 //   compact: move this rank's touched rows out of the gradient table into a dense list
 //            (rows_out[u], grads_out[u, :]), zero the slots and release the flags, so the
@@ -209,12 +392,16 @@ __global__ void __launch_bounds__(256) sparse_merge_kernel(
     const int32_t row = u < count ? rows[u] : -1;
     if (threadIdx.x == 0) nclaim = 0;
     __syncthreads();
-    if (l == 0) lidx[gi] = (row >= 0 && atomicCAS(&flag[row], -1, -2) == -1) ? atomicAdd(&nclaim, 1) : -1;
-    __syncthreads();
-    if (threadIdx.x == 0) base = nclaim > 0 ? atomicAdd(n_touched, nclaim) : 0;
+    if (touched) {
+      if (l == 0) lidx[gi] = (row >= 0 && atomicCAS(&flag[row], -1, -2) == -1) ? atomicAdd(&nclaim, 1) : -1;
+      __syncthreads();
+      if (threadIdx.x == 0) base = nclaim > 0 ? atomicAdd(n_touched, nclaim) : 0;
+    } else if (l == 0 && row >= 0) {
+      scan_mark(flag, row);  // scan mode
+    }
     __syncthreads();
     if (row >= 0) {
-      if (l == 0 && lidx[gi] >= 0 && base + lidx[gi] < touched_cap) touched[base + lidx[gi]] = row;
+      if (touched && l == 0 && lidx[gi] >= 0 && base + lidx[gi] < touched_cap) touched[base + lidx[gi]] = row;
       for (int e = l; e < dim; e += lps)
         grad_table[(int64_t)row * dim + e] += grads[(int64_t)u * dim + e];
     }
@@ -241,8 +428,8 @@ RS_API int rs_sparse_compact(void* stream, float* grad_table, int32_t* flag,
 RS_API int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* grads,
                                 int32_t count, int dim, float* grad_table, int32_t* flag,
                                 int32_t* touched, int32_t* n_touched, int32_t touched_cap) {
-  if (!rows || !grads || !grad_table || !flag || !touched || !n_touched || dim <= 0)
-    return RS_ERR_ARG;
+  if (!rows || !grads || !grad_table || !flag || dim <= 0) return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
   if (count <= 0) return RS_OK;
   const int lps = lanes_for_dim(dim);
   int64_t grid = ((int64_t)count * lps + 255) / 256;

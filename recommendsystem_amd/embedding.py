@@ -80,20 +80,35 @@ class SparseTable:
             self.v = torch.zeros_like(self.weight)
         else:
             self.g2sum = torch.full_like(self.weight, self.optimizer.initial_g2sum)
+        # "list": pushes claim rows into `touched` (grid sized by touched_cap); "scan": pushes only
+        # mark flag[] and the optimizer sweeps it (no returning atomics in the push; best when
+        # the table is not much larger than ~100x the rows a step touches)
+        self.mode = "list"
         # autograd anchor: lets the lookup's backward run (it returns no dense gradient)
         self.anchor = torch.zeros((), device=device, dtype=torch.float32, requires_grad=True)
 
     # ---- push / update -----------------------------------------------------------------
     def accumulate(self, rows: torch.Tensor, offsets: torch.Tensor | None, B: int, F: int,
                    dout: torch.Tensor, dout_ld: int, dout_fstride: int, combiner: int) -> None:
+        scan = self.mode == "scan"
         call("rs_sparse_grad_accumulate", stream_handle(), ptr(rows), ptr(offsets), B, F, ptr(dout),
              dout_ld, dout_fstride, self.dim, combiner, ptr(self.grad), ptr(self.flag),
-             ptr(self.touched), ptr(self.n_touched), self.touched_cap)
+             None if scan else ptr(self.touched), None if scan else ptr(self.n_touched),
+             self.touched_cap)
 
     def step(self, grad_scale: float = 1.0) -> None:
         """Apply the sparse optimizer to the rows touched since the last step."""
         o = self.optimizer
         s = stream_handle()
+        if self.mode == "scan":
+            if isinstance(o, SparseAdam):
+                call("rs_sparse_adam_scan", s, ptr(self.weight), ptr(self.m), ptr(self.v),
+                     ptr(self.grad), ptr(self.flag), self.rows, self.dim, o.learning_rate, o.beta1,
+                     o.beta2, o.epsilon, grad_scale)
+            else:
+                call("rs_sparse_adagrad_scan", s, ptr(self.weight), ptr(self.g2sum), ptr(self.grad),
+                     ptr(self.flag), self.rows, self.dim, o.learning_rate, grad_scale)
+            return
         if isinstance(o, SparseAdam):
             call("rs_sparse_adam", s, ptr(self.weight), ptr(self.m), ptr(self.v), ptr(self.grad),
                  ptr(self.flag), ptr(self.touched), ptr(self.n_touched), self.dim,

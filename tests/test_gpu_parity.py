@@ -112,6 +112,88 @@ def test_sparse_push_and_adam():
     assert float(table.grad.abs().max()) == 0.0
 
 
+def _scan_marked(flag, nrows):
+    """Rows marked by a scan-mode push (flag = -2; clean = -1)."""
+    f = flag.cpu().numpy()
+    assert np.all((f == -1) | (f == -2))
+    return set(np.nonzero(f[:nrows] == -2)[0].tolist())
+
+
+def _scan_mark(flag, rows):
+    flag[torch.from_numpy(np.asarray(rows)).to(flag.device)] = -2
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "adagrad"])
+def test_sparse_push_scan_mode_matches_oracle(optimizer):
+    """Scan mode (touched == NULL): the push only marks flag[]; the scan optimizers sweep it."""
+    from recommendsystem_amd.embedding import EmbeddingFeatures, SparseAdaGrad, SparseAdam, SparseTable
+    rng = np.random.default_rng(7)
+    B, F, dim, vocab = 96, 5, 16, 11
+    opt = SparseAdam(learning_rate=1e-2) if optimizer == "adam" else SparseAdaGrad(learning_rate=5e-3)
+    table = SparseTable(F * vocab, dim, opt, device=DEV, seed=8)
+    table.mode = "scan"
+    emb = EmbeddingFeatures(table, [vocab] * F, combiner="mean")
+    lens = rng.integers(0, 3, size=B * F)
+    offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ids = rng.integers(0, 1000, size=int(offsets[-1]), dtype=np.int64)
+    W0 = table.weight.cpu().numpy().astype(np.float64)
+    G0 = table.g2sum.cpu().numpy().astype(np.float64) if optimizer == "adagrad" else None
+    out = emb(torch.from_numpy(ids).to(DEV), torch.from_numpy(offsets).to(DEV))
+    dout = torch.randn(B, F, dim, device=DEV)
+    out.backward(dout)
+    torch.cuda.synchronize()
+    _, rows = npo.embedding_lookup(ids, offsets, B, F, emb.row_base.cpu().numpy(),
+                                   emb.bucket.cpu().numpy(), W0, "mod", "mean")
+    gref = npo.sparse_grad_sum(rows, offsets, B, F, _np(dout), "mean")
+    assert _scan_marked(table.flag, table.rows) == set(gref.keys())  # bit-exact row set
+    table.step()
+    torch.cuda.synchronize()
+    W1 = table.weight.cpu().numpy()
+    for r, g in gref.items():
+        if optimizer == "adam":
+            w, _, _ = npo.adam_sparse(W0[r], g, np.zeros(dim), np.zeros(dim), 1e-2)
+        else:
+            g2 = G0[r] + g * g
+            w = W0[r] - 5e-3 * g / np.sqrt(g2)
+        assert_close(W1[r], w, 1e-5, 1e-4, what=f"{optimizer} row {r}")
+    untouched = np.setdiff1d(np.arange(table.rows), list(gref.keys()))
+    assert np.array_equal(W1[untouched], W0[untouched].astype(np.float32))
+    assert bool((table.flag == -1).all()) and float(table.grad.abs().max()) == 0.0
+
+
+def test_sparse_compact_scan_and_merge():
+    """DP exchange in scan mode: compact every marked row, merge lists back (touched == NULL)."""
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rows_n, dim, cap = 5000, 16, 512
+    rng = np.random.default_rng(11)
+    grad = torch.zeros(rows_n, dim, device=DEV)
+    flag = torch.full((rows_n,), -1, dtype=torch.int32, device=DEV)
+    hit = np.sort(rng.choice(rows_n, size=300, replace=False))
+    gv = torch.randn(len(hit), dim, device=DEV)
+    grad[torch.from_numpy(hit).to(DEV)] = gv
+    _scan_mark(flag, hit)
+    r_out = torch.empty(cap, dtype=torch.int32, device=DEV)
+    g_out = torch.empty(cap, dim, device=DEV)
+    n_out = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = stream_handle()
+    call("rs_sparse_compact_scan", s, ptr(grad), ptr(flag), rows_n, dim, ptr(r_out), ptr(g_out),
+         ptr(n_out), cap)
+    torch.cuda.synchronize()
+    n = int(n_out.item())
+    assert n == len(hit) and bool((flag == -1).all()) and float(grad.abs().max()) == 0.0
+    got = r_out[:n].cpu().numpy()
+    assert sorted(got.tolist()) == hit.tolist() and bool((r_out[n:] == -1).all())
+    order = np.argsort(got)
+    assert torch.equal(g_out[:n][torch.from_numpy(order).to(DEV)], gv)
+    # merge the list back twice (two "ranks"), scan-mode marking
+    for _ in range(2):
+        call("rs_sparse_merge_rows", s, ptr(r_out), ptr(g_out), cap, dim, ptr(grad), ptr(flag),
+             None, None, cap)
+    torch.cuda.synchronize()
+    assert torch.equal(grad[torch.from_numpy(hit).to(DEV)], 2 * gv)
+    assert _scan_marked(flag, rows_n) == set(hit.tolist())
+
+
 # ------------------------------------------------------------------------------------------
 # H3 InteractingLayer
 # ------------------------------------------------------------------------------------------
@@ -179,6 +261,52 @@ def test_interacting_backward(case):
     assert_grad_close(_np(il.bias.grad), b.grad.numpy(), what="db")
     assert_grad_close(_np(il.gamma.grad), g.grad.numpy(), what="dgamma")
     assert_grad_close(_np(il.beta.grad), be.grad.numpy(), what="dbeta")
+
+
+@pytest.mark.parametrize("with_base", [True, False])
+def test_interacting_backward_fused_push(with_base):
+    """rs_il_bwd_push == rs_il_bwd's dx (+ dx_base) scattered into the table rows (collisions,
+    skipped -1 rows), rows marked scan-mode; weight partials identical to rs_il_bwd's."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    B, F, E, U, H, L = 64, 26, 16, 16, 2, 3
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = torch.rand(B, F, E, device=DEV, generator=g) - 0.5
+    xs = torch.empty(L - 1, B, F, U, device=DEV)
+    W = (torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.5
+    bias = (torch.rand(4 * U, device=DEV, generator=g) - 0.5) * 0.1
+    gam = torch.rand(U, device=DEV, generator=g) + 0.5
+    bet = (torch.rand(U, device=DEV, generator=g) - 0.5) * 0.2
+    y = torch.empty(B, F * U, device=DEV)
+    dy = torch.randn(B, F * U, device=DEV, generator=g)
+    base = torch.randn(B, F * E, device=DEV, generator=g)
+    rows = torch.randint(-1, 50, (B * F,), device=DEV, dtype=torch.int32, generator=g)
+    lib = _lib.load()
+    wsn = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+    ws1, ws2 = torch.empty(wsn, device=DEV), torch.empty(wsn, device=DEV)
+    s = stream_handle()
+    call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gam), ptr(bet), 1e-14, 1,
+         0.0, 0, ptr(y), F * U, ptr(xs))
+    dx = base.clone() if with_base else torch.zeros(B, F * E, device=DEV)
+    call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias),
+         ptr(gam), ptr(bet), 1e-14, 1, 0.0, 0, ptr(dx), 1, None, 0, ptr(ws1), wsn)
+    table = torch.zeros(50, E, device=DEV)
+    flag = torch.full((50,), -1, dtype=torch.int32, device=DEV)
+    call("rs_il_bwd_push", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias),
+         ptr(gam), ptr(bet), 1e-14, 1, 0.0, 0, ptr(base) if with_base else None, ptr(rows),
+         ptr(table), ptr(flag), None, 0, ptr(ws2), wsn)
+    torch.cuda.synchronize()
+    r = rows.cpu().numpy()
+    want = np.zeros((50, E))
+    dxn = _np(dx).reshape(B * F, E)
+    for k in range(B * F):
+        if r[k] >= 0:
+            want[r[k]] += dxn[k]
+    assert_grad_close(_np(table), want, what="pushed rows")
+    assert _scan_marked(flag, 50) == set(r[r >= 0].tolist())
+    nb = int(lib.rs_il_bwd_partial_blocks(B, F, E, U, wsn))
+    npar = int(lib.rs_il_param_count(E, U))
+    assert torch.equal(ws1[:nb * npar], ws2[:nb * npar])
 
 
 def test_interacting_dropout_mask_matches_oracle():
