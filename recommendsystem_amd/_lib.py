@@ -118,11 +118,13 @@ class RecsysKernelError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load (once) and type the shared library.  Raises if it has not been built."""
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and type the shared library.  Raises if it has not been built.
+    RS_LIB_PATH overrides the in-tree library (kernel-variant experiments only)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("RS_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise RecsysKernelError(
             f"{path} not found: build the HIP extension first (python -c "

@@ -71,7 +71,10 @@ struct BwdReq {
 
 constexpr int kMaxFwdWaves = 4;
 constexpr int kMaxBwdWaves = 2;
-constexpr int kMaxBwdGrid = 1024;
+#ifndef RS_IL_BWD_GRID
+#define RS_IL_BWD_GRID 1536
+#endif
+constexpr int kMaxBwdGrid = RS_IL_BWD_GRID;
 constexpr size_t kLdsBytes = 160 * 1024;
 
 template <int E_, int U_, int H_, int FMAX_, bool EXACT_ = false>
@@ -129,6 +132,7 @@ struct Args {
   float sc2;        // log2(e) / sqrt(dh): scores go straight to the exp2 domain
   uint64_t seed;
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
+  int l_tmp;                   // bwd2 only: partial-row exchange / dV buffer
   unsigned long long* stamps;  // diagnostic build only
   const int32_t* push_rows;    // fused sparse push (see BwdReq)
   float* push_table;
@@ -153,15 +157,17 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   int off = 0;
   a.l_x = off; off += r4(F * C::E);
   a.l_pr = off; off += r4(C::FMAX * C::PRS);  // FMAX rows: padded key/value rows stay zero
-  a.l_o = off; off += r4(F * C::OS);
+  a.l_o = 0;  // forward: the attention output aliases the Q columns of PR
   a.l_gpr = a.l_dy = a.l_pm = a.l_st = 0;
   if (bwd) {
+    a.l_o = off; off += r4(F * C::OS);
     a.l_gpr = off; off += r4(F * C::PRS);
     a.l_dy = off; off += r4(F * C::U);
     a.l_pm = off; off += r4(C::H * F * C::PMS);
     a.l_st = off; off += r4(2 * C::H * F);   // LN stats / the split-j D partials
   }
   a.per_wave = off;
+  a.l_tmp = 0;
 #ifdef RS_IL_STAMPS
   extern unsigned long long* g_il_stamps;
   a.stamps = g_il_stamps;
@@ -171,6 +177,25 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.push_rows = nullptr;
   a.push_table = nullptr;
   a.push_flag = nullptr;
+  return a;
+}
+
+// bwd2 carve-up (one block = one sample at a time, two waves): no separate gradient region (the
+// projection gradients overwrite Q/K/V/R in place once each is dead), a TMP region for partial
+// rows / dV, and ST holding [m0 | m1 | l0 | l1] (forward recompute) then the D partials.
+template <class C>
+Args make_args2(int64_t B, int F, int L, int use_res, float eps, float drop_rate, uint64_t seed) {
+  Args a = make_args<C>(B, F, L, use_res, eps, drop_rate, seed, false);
+  int off = 0;
+  a.l_x = off; off += r4(F * C::E);
+  a.l_pr = off; off += r4(C::FMAX * C::PRS);
+  a.l_o = off; off += r4(F * C::OS);
+  a.l_dy = off; off += r4(F * C::U);
+  a.l_tmp = off; off += r4(F * C::U);           // == DH * H * F
+  a.l_pm = off; off += r4(C::H * F * C::PMS);
+  a.l_st = off; off += r4(4 * C::H * F);
+  a.l_gpr = 0;
+  a.per_wave = off;
   return a;
 }
 
@@ -253,6 +278,12 @@ struct MfmaW {
   float bp[NT];         // bias[16nt + j] (loop-invariant: kept out of the per-row loops)
 
   __device__ __forceinline__ void load(const float* __restrict__ W, const float* __restrict__ bias) {
+    load_proj(W, bias);
+    load_dx(W);
+  }
+  // projection B operand + bias only
+  __device__ __forceinline__ void load_proj(const float* __restrict__ W,
+                                            const float* __restrict__ bias) {
     const int q = lane_id() >> 4, j = lane_id() & 15;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) bp[nt] = bias[16 * nt + j];
@@ -265,6 +296,10 @@ struct MfmaW {
           const int k = 16 * ks + 4 * q + t;
           wp[ks][t][nt] = k < C::E ? W[k * C::NC + 16 * nt + j] : 0.f;
         }
+  }
+  // dx B operand only
+  __device__ __forceinline__ void load_dx(const float* __restrict__ W) {
+    const int q = lane_id() >> 4, j = lane_id() & 15;
 #pragma unroll
     for (int cs = 0; cs < CS; ++cs)
 #pragma unroll
@@ -430,7 +465,7 @@ __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, cons
 }
 
 // ---- phase: attention forward; optionally keeps P (pre-dropout) for backward ----------------
-template <class C, bool STORE_P, bool DROP>
+template <class C, bool STORE_P, bool DROP, int OSTR = C::OS>
 __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* PM,
                                               const Args& a, int64_t b, uint64_t lseed) {
   const int lane = lane_id();
@@ -469,7 +504,7 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
       axpy_row(o, p, vb + j * C::PRS);
     }
     if (act) {
-      float4* orow = reinterpret_cast<float4*>(O + i * C::OS + h * C::DH);
+      float4* orow = reinterpret_cast<float4*>(O + i * OSTR + h * C::DH);
 #pragma unroll
       for (int d4 = 0; d4 < C::DH / 4; ++d4)
         orow[d4] = make_float4(o[4 * d4], o[4 * d4 + 1], o[4 * d4 + 2], o[4 * d4 + 3]);
@@ -479,7 +514,7 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
 
 // ---- phase: z = relu(O + R); y = LN(z).  MODE 0: write y (to LDS X or to global).
 //      MODE 1 (backward recompute): keep z in O, (mean, std) per row in ST. -----------------
-template <class C, int MODE>
+template <class C, int MODE, int OSTR = C::OS>
 __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, float* Y,
                                          int y_stride, const Args& a, const float (&gam)[C::CPLN],
                                          const float (&bet)[C::CPLN]) {
@@ -493,7 +528,7 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
 #pragma unroll
     for (int c = 0; c < C::CPLN; ++c) {
       const int u = u0 + c * C::LPR;
-      float t = act ? O[f * C::OS + u] : 0.f;
+      float t = act ? O[f * OSTR + u] : 0.f;
       if (a.use_res && act) t += PR[f * C::PRS + 3 * C::U + u];
       z[c] = fmaxf(t, 0.f);
       sum += z[c];
@@ -509,7 +544,7 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
       for (int c = 0; c < C::CPLN; ++c) {
         const int u = u0 + c * C::LPR;
         if (MODE == 0) Y[f * y_stride + u] = (z[c] - mean) * rstd * gam[c] + bet[c];
-        else O[f * C::OS + u] = z[c];
+        else O[f * OSTR + u] = z[c];
       }
       if (MODE == 1 && u0 == 0) { ST[2 * f] = mean; ST[2 * f + 1] = rstd; }
     }
@@ -518,7 +553,7 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
 
 // ============================== forward kernel ===============================================
 template <class C, bool DROP>
-__global__ void __launch_bounds__(256, 3) fwd_kernel(
+__global__ void __launch_bounds__(256, 4) fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y,
     int64_t y_ld, float* __restrict__ xsave, Args a) {
@@ -526,7 +561,6 @@ __global__ void __launch_bounds__(256, 3) fwd_kernel(
   float* base = smem + wave_id() * a.per_wave;
   float* X = base + a.l_x;
   float* PR = base + a.l_pr;
-  float* O = base + a.l_o;
   const int lane = lane_id();
   const int wpb = blockDim.x >> 6;
   const int F = a.F;
@@ -547,12 +581,13 @@ __global__ void __launch_bounds__(256, 3) fwd_kernel(
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
       for (int rt = 0; rt * 16 < F; ++rt) mfma_project<C>(X, PR, F, rt, mw);
       wave_lds_sync();
-      attention_fwd<C, false, DROP>(PR, O, nullptr, a, b, lseed);
+      // O_i overwrites Q_i in place (only lane (h, i) ever reads Q_i, before writing O_i)
+      attention_fwd<C, false, DROP, C::PRS>(PR, PR, nullptr, a, b, lseed);
       wave_lds_sync();
       if (it == a.L - 1) {
-        epilogue<C, 0>(O, PR, nullptr, y + b * y_ld, C::U, a, gam, bet);
+        epilogue<C, 0, C::PRS>(PR, PR, nullptr, y + b * y_ld, C::U, a, gam, bet);
       } else {
-        epilogue<C, 0>(O, PR, nullptr, X, C::E, a, gam, bet);  // E == U when L > 1
+        epilogue<C, 0, C::PRS>(PR, PR, nullptr, X, C::E, a, gam, bet);  // E == U when L > 1
         wave_lds_sync();
         if (xsave) {
           float4* dst = reinterpret_cast<float4*>(xsave + ((int64_t)it * a.B + b) * F * C::U);
@@ -575,7 +610,10 @@ __global__ void __launch_bounds__(256, 3) fwd_kernel(
 //   dV / dQ / dK  : DY region holds the second wave's partial row vector, ST the partial D_i.
 // Every sum combines the partials in a fixed order (wave 0 + wave 1): deterministic.
 template <class C, bool DROP>
-__global__ void __launch_bounds__(128) bwd_kernel(
+#ifndef RS_IL_BWD_OCC
+#define RS_IL_BWD_OCC 2
+#endif
+__global__ void __launch_bounds__(128, RS_IL_BWD_OCC) bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
     int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
@@ -926,6 +964,387 @@ __global__ void __launch_bounds__(128) bwd_kernel(
     partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
 }
 
+// ============================== backward kernel, v2 ===========================================
+// Same math and the same two-waves-per-sample split as bwd_kernel, re-laid out for occupancy:
+//   * no gradient region: the projection gradients overwrite Q, K, V, R in place as each input
+//     dies (R after the LN backward; V after dS; K after dQ; Q after dK), dV / dQ wait in
+//     TMP / DY / O meanwhile -> ~20 KB of LDS per sample instead of ~26 KB;
+//   * W is not held in VGPRs across the kernel: its MFMA fragments are loaded (L1/L2 hits) in
+//     the two phases that use them -> <= 128 VGPRs (4 waves per SIMD instead of 2);
+//   * the forward-recompute partials exchange through ST (m, l) and TMP (o of wave 1).
+// Phases per sample and iteration (barriers between them):
+//   P1 projection recompute (MFMA)      P2 attention recompute (keys split), P, O
+//   P3 LN + ReLU backward: O <- dt, R <- gR
+//   P4 dV (queries split) -> DY         P5 dS (in place of P), dQ (keys split) -> O
+//   P6 dK (queries split) -> K <- gK;  V <- gV (DY), Q <- gQ (O)
+//   P7 dW, db += X^T G; dx = G W^T -> DY (next iteration's dy) or the input gradient / push
+#ifndef RS_IL_BWD2_OCC
+#define RS_IL_BWD2_OCC 3
+#endif
+template <class C, bool DROP>
+__global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
+    const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
+    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
+    int dx_accumulate, float* __restrict__ partials, Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int JH = (C::FMAX + 1) / 2;  // keys (or queries) per wave in the split passes
+  float* X = smem + a.l_x;
+  float* PR = smem + a.l_pr;
+  float* O = smem + a.l_o;
+  float* DY = smem + a.l_dy;
+  float* TMP = smem + a.l_tmp;
+  float* PM = smem + a.l_pm;
+  float* ST = smem + a.l_st;
+  const int lane = lane_id();
+  const int w = wave_id();  // 0 or 1
+  const int F = a.F;
+  const int HF = C::H * F;
+  const int j0 = w * JH;
+
+  for (int k = F * C::PRS + threadIdx.x; k < C::FMAX * C::PRS; k += blockDim.x) PR[k] = 0.f;
+  __syncthreads();
+
+  using M = MfmaW<C>;
+  f32x4 dwacc[M::ET][M::NT];
+  float dbp[M::NT];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
+  float dg[C::CPLN], dbt[C::CPLN];
+  const int u0 = lane % C::LPR;
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; }
+  const int nrt = (F + 15) / 16;
+
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    {
+      const float* src = dy + b * dy_ld;
+      for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
+    }
+    for (int it = a.L - 1; it >= 0; --it) {
+      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      {
+        const float* xin = (it == 0) ? (x + b * F * C::E)
+                                     : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
+        const float4* src = reinterpret_cast<const float4*>(xin);
+        for (int k = threadIdx.x; k < F * C::E / 4; k += blockDim.x)
+          reinterpret_cast<float4*>(X)[k] = src[k];
+      }
+      __syncthreads();
+      // ---- P1: projections (row tiles split between the waves) ----
+      {
+        // launder W / bias so the fragment loads are NOT hoisted out of the sample loop (they
+        // would then stay live in 36 VGPRs across every phase): reloading them costs a few
+        // L1 hits per iteration, keeping them costs two waves per SIMD
+        const float* Wl = W;
+        const float* bl = bias;
+        asm volatile("" : "+s"(Wl), "+s"(bl));
+        MfmaW<C> mw;
+        mw.load_proj(Wl, bl);
+        for (int rt = w; rt < nrt; rt += 2) mfma_project<C>(X, PR, F, rt, mw);
+      }
+      __syncthreads();
+      // ---- P2: attention recompute, keys split; m / l through ST, wave 1's o through TMP ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, i = act ? r % F : 0;
+        float q[C::DH];
+        load_row(q, PR + i * C::PRS + h * C::DH);
+        const float* kb = PR + C::U + h * C::DH;
+        float s[JH];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          const float acc = (j < C::FMAX) ? dot_row(q, kb + j * C::PRS) : 0.f;
+          s[jj] = (j < F) ? acc * a.sc2 : -INFINITY;
+          mx = fmaxf(mx, s[jj]);
+        }
+        if (act) ST[w * HF + r] = mx;
+        __syncthreads();
+        const float m = act ? fmaxf(ST[r], ST[HF + r]) : 0.f;
+        float l = 0.f;
+        float o[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
+        const float* vb = PR + 2 * C::U + h * C::DH;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          s[jj] = __builtin_amdgcn_exp2f(s[jj] - m);
+          l += s[jj];
+          float e = s[jj];
+          if (DROP && j < F) e = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? e * a.drop_scale : 0.f;
+          if (j < C::FMAX) axpy_row(o, e, vb + j * C::PRS);
+        }
+        if (act) {
+          ST[(2 + w) * HF + r] = l;
+          if (w == 1) {
+#pragma unroll
+            for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = o[d];
+          }
+        }
+        __syncthreads();
+        if (act) {
+          const float inv = 1.0f / (ST[2 * HF + r] + ST[3 * HF + r]);
+          float* pm_row = PM + (h * F + i) * C::PMS;
+#pragma unroll
+          for (int jj = 0; jj < JH; ++jj)
+            if (j0 + jj < C::FMAX) pm_row[j0 + jj] = s[jj] * inv;
+          if (w == 0) {
+            float ov[C::DH];
+#pragma unroll
+            for (int d = 0; d < C::DH; ++d) ov[d] = (o[d] + TMP[d * HF + r]) * inv;
+            store_row(O + i * C::OS + h * C::DH, ov);
+          }
+        }
+        __syncthreads();
+      }
+      // ---- P3: z = relu(O + R), LN stats, LN + ReLU backward (rows split):
+      //      O <- dt; R <- gR = dt * (R > 0) (R dies here) ----
+      {
+        float gam[C::CPLN];
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) gam[c] = gamma[u0 + c * C::LPR];
+        for (int f0 = w * C::RG; f0 < F; f0 += 2 * C::RG) {
+          const int f = f0 + lane / C::LPR;
+          const bool act = f < F;
+          float z[C::CPLN], rr[C::CPLN];
+          float sum = 0.f;
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            float t = act ? O[f * C::OS + u] : 0.f;
+            rr[c] = (a.use_res && act) ? PR[f * C::PRS + 3 * C::U + u] : 0.f;
+            t += rr[c];
+            z[c] = fmaxf(t, 0.f);
+            sum += z[c];
+          }
+          const float mean = group_sum<C::LPR>(sum) * (1.0f / (float)C::U);
+          float sq = 0.f;
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
+          const float var = group_sum<C::LPR>(sq) * (1.0f / (float)C::U);
+          const float rstd = 1.0f / sqrtf(var + a.eps);
+          float zh[C::CPLN], g[C::CPLN];
+          float sg = 0.f, sgz = 0.f;
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            zh[c] = (z[c] - mean) * rstd;
+            const float dyv = act ? DY[f * C::U + u] : 0.f;
+            dg[c] = fmaf(dyv, zh[c], dg[c]);
+            dbt[c] += dyv;
+            g[c] = dyv * gam[c];
+            sg += g[c];
+            sgz += g[c] * zh[c];
+          }
+          sg = group_sum<C::LPR>(sg) * (1.0f / (float)C::U);
+          sgz = group_sum<C::LPR>(sgz) * (1.0f / (float)C::U);
+          if (act) {
+#pragma unroll
+            for (int c = 0; c < C::CPLN; ++c) {
+              const int u = u0 + c * C::LPR;
+              const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
+              const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+              O[f * C::OS + u] = dt;
+              // without use_res the R columns carry no gradient (their dW / db must be zero)
+              PR[f * C::PRS + 3 * C::U + u] = (a.use_res && rr[c] > 0.f) ? dt : 0.f;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // ---- P4: dV_j = sum_i Pd_ij dO_i (lane = (h, j); queries split) -> DY[j][h dh + d] ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dv[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
+#pragma unroll 2
+        for (int ii = 0; ii < JH; ++ii) {
+          const int i = j0 + ii;
+          if (C::EXACT ? (i < C::FMAX) : (i < F)) {
+            float p = PM[(h * F + i) * C::PMS + j];
+            if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+            axpy_row(dv, p, O + i * C::OS + h * C::DH);
+          }
+        }
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dv[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) dv[d] += TMP[d * HF + r];
+          store_row(DY + j * C::U + h * C::DH, dv);
+        }
+        __syncthreads();
+      }
+      // ---- P5: dS (in place of P) and dQ (lane = (h, i); keys split) -> O (dO dies here) ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, i = act ? r % F : 0;
+        float dO[C::DH];
+        load_row(dO, O + i * C::OS + h * C::DH);
+        const float* vb = PR + 2 * C::U + h * C::DH;
+        const float* kb = PR + C::U + h * C::DH;
+        float* pm_row = PM + (h * F + i) * C::PMS;
+        float s[JH];
+        float Dw = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          float dp = (j < C::FMAX) ? dot_row(dO, vb + j * C::PRS) : 0.f;
+          if (DROP && j < F) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          const float p = (j < C::FMAX) ? pm_row[j] : 0.f;
+          Dw = fmaf(p, dp, Dw);
+          s[jj] = dp;
+        }
+        if (act) ST[w * HF + r] = Dw;
+        __syncthreads();
+        const float D = act ? ST[r] + ST[HF + r] : 0.f;
+        float dq[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < JH; ++jj) {
+          const int j = j0 + jj;
+          if (j < C::FMAX) {
+            const float ds = pm_row[j] * (s[jj] - D) * a.inv_sdh;
+            axpy_row(dq, ds, kb + j * C::PRS);
+            if (act) pm_row[j] = ds;
+          }
+        }
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dq[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) dq[d] += TMP[d * HF + r];
+          store_row(O + i * C::OS + h * C::DH, dq);
+        }
+        __syncthreads();
+      }
+      // ---- P6: dK_j = sum_i dS_ij Q_i (lane = (h, j); queries split); then K <- gK (wave 0),
+      //      V <- gV from DY and Q <- gQ from O (wave 1) ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dk[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
+#pragma unroll 2
+        for (int ii = 0; ii < JH; ++ii) {
+          const int i = j0 + ii;
+          if (C::EXACT ? (i < C::FMAX) : (i < F))
+            axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+        }
+        if (act && w == 1) {
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dk[d];
+        }
+        __syncthreads();
+        if (act && w == 0) {
+          float kr[C::DH];
+          load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] + TMP[d * HF + r] : 0.f;
+          store_row(PR + j * C::PRS + C::U + h * C::DH, kr);
+        }
+        if (w == 1 && r0 + 64 >= HF) {  // once, after the last row chunk's dK reads of Q
+          for (int k = lane; k < F * C::U; k += 64) {
+            const int f = k / C::U, c = k % C::U;
+            float* vq = PR + f * C::PRS + 2 * C::U + c;
+            *vq = *vq > 0.f ? DY[k] : 0.f;
+            float* qq = PR + f * C::PRS + c;
+            *qq = *qq > 0.f ? O[f * C::OS + c] : 0.f;
+          }
+        }
+        __syncthreads();
+      }
+      // ---- P7: dW += X^T G, db += colsum G; dx = G W^T (row tiles split; MFMA) ----
+      for (int rt = w; rt < nrt; rt += 2) mfma_dw<C>(X, PR, F, rt, dwacc, dbp);
+      __builtin_amdgcn_sched_barrier(0);  // keep the dx pass's loads out of the dW pass
+      {
+        const float* Wl = W;
+        asm volatile("" : "+s"(Wl));
+        MfmaW<C> mw;
+        mw.load_dx(Wl);
+        for (int rt = w; rt < nrt; rt += 2) {
+          if (it > 0) mfma_dx<C>(PR, F, rt, mw, DY, C::U, false);  // dL/d(previous output)
+          else if (a.push_table)
+            mfma_dx_push<C>(PR, F, rt, mw, dx_accumulate ? dx + b * F * C::E : nullptr,
+                            a.push_rows + b * F, a.push_table, a.push_flag);
+          else mfma_dx<C>(PR, F, rt, mw, dx + b * F * C::E, C::E, dx_accumulate != 0);
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- lanes -> wave -> block (wave order), as bwd_kernel ----
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) {
+    dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
+    dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
+  }
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) {
+#pragma unroll
+    for (int o = C::LPR; o < 64; o <<= 1) {
+      dg[c] += __shfl_xor(dg[c], o, 64);
+      dbt[c] += __shfl_xor(dbt[c], o, 64);
+    }
+  }
+  float* RED = smem;
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
+  __syncthreads();
+  {
+    const int q = lane >> 4, jx = lane & 15;
+    for (int ww = 0; ww < 2; ++ww) {
+      if (w == ww) {
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int e = 16 * et + 4 * q + r;
+              if (e < C::E) RED[e * C::NC + 16 * nt + jx] += dwacc[et][nt][r];
+            }
+        if (q == 0) {
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + jx] += dbp[nt];
+        }
+        if (lane < C::LPR) {
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            RED[C::E * C::NC + C::NC + u] += dg[c];
+            RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
+    partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
+}
+
 // grid-level reduction of the per-block partials, fixed order (deterministic); interacting.hip
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
                    int accumulate);
@@ -947,6 +1366,33 @@ int fwd_launch(const FwdReq& q) {
   return rs_status_after_launch();
 }
 
+#ifndef RS_IL_BWD_V1
+template <class C, bool DROP>
+int bwd_launch(const BwdReq& q) {
+  if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
+  Args a = make_args2<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed);
+  a.push_rows = q.push_rows;
+  a.push_table = q.push_table;
+  a.push_flag = q.push_flag;
+  const size_t lds = (size_t)a.per_wave * sizeof(float);
+  if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
+  // kMaxBwdGrid = one resident round of this kernel on MI355X (6 blocks per CU x 256 CUs at
+  // config 2), so no block waits for a second round while others idle.  A fixed rule (not an
+  // occupancy query) because callers size the partial-row reduction with
+  // rs_il_bwd_partial_blocks.
+  int64_t grid = q.B;
+  const int64_t max_grid = q.workspace_floats / C::NPARAM;
+  if (grid > kMaxBwdGrid) grid = kMaxBwdGrid;
+  if (grid > max_grid) grid = max_grid;
+  if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
+  bwd2_kernel<C, DROP><<<(int)grid, 128, lds, q.stream>>>(
+      q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
+      q.workspace, a);
+  if (q.dparams)  // NULL: leave the per-block partials in the workspace
+    reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+  return rs_status_after_launch();
+}
+#else
 template <class C, bool DROP>
 int bwd_launch(const BwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
@@ -970,6 +1416,7 @@ int bwd_launch(const BwdReq& q) {
     reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
   return rs_status_after_launch();
 }
+#endif
 
 // EXACT instantiations (F == FMAX) drop the padded-key mask entirely.
 template <int E, int U, int H, int FMAX, bool EXACT = false>
