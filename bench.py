@@ -34,6 +34,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only "
+                         "to rehearse the DP path with several ranks on one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (config 2: 4096)")
@@ -169,13 +172,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())  # (rehearsal: several ranks per GPU)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
         pg = dist.group.WORLD
 
     from recommendsystem_amd import _lib
@@ -267,7 +274,7 @@ def main():
                                "26 fields x emb 16, per-GPU batch 4096",
                    "global_batch": B * world, "fields": F, "emb_dim": E, "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd_kernel (InteractingLayer backward)",
+        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd2_kernel (InteractingLayer backward)",
                      "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                      "launch_us": round(t_bwd * 1e6, 2),
