@@ -33,7 +33,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// readfirstlane: the wave index is uniform, and saying so lets `if (wave_id() == k)` compile to a
+// scalar branch instead of exec-mask save/restore around every guarded instruction
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
 
 // Sum over aligned groups of `W` lanes (W power of two, <= 64), result in every lane of the group.
 // W <= 16 uses DPP row operations only (VALU, no LDS round trip): quad_perm xor-1 / xor-2, then

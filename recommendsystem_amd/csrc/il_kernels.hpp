@@ -520,9 +520,10 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
                                          const float (&bet)[C::CPLN]) {
   const int lane = lane_id();
   const int u0 = lane % C::LPR;
-  for (int f0 = 0; f0 < a.F; f0 += C::RG) {
+  const int F = a.F;
+  for (int f0 = 0; f0 < F; f0 += C::RG) {
     const int f = f0 + lane / C::LPR;
-    const bool act = f < a.F;
+    const bool act = f < F;
     float z[C::CPLN];
     float sum = 0.f;
 #pragma unroll
@@ -998,7 +999,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
   float* ST = smem + a.l_st;
   const int lane = lane_id();
   const int w = wave_id();  // 0 or 1
-  const int F = a.F;
+  const int F = C::EXACT ? C::FMAX : a.F;  // compile-time for exact-F shapes
   const int HF = C::H * F;
   const int j0 = w * JH;
 
@@ -1258,19 +1259,23 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
         }
         __syncthreads();
         if (act && w == 0) {
-          float kr[C::DH];
+          float kr[C::DH], pt[C::DH];
           load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] + TMP[d * HF + r] : 0.f;
+          for (int d = 0; d < C::DH; ++d) pt[d] = TMP[d * HF + r];  // unconditional: no branches
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] + pt[d] : 0.f;
           store_row(PR + j * C::PRS + C::U + h * C::DH, kr);
         }
         if (w == 1 && r0 + 64 >= HF) {  // once, after the last row chunk's dK reads of Q
           for (int k = lane; k < F * C::U; k += 64) {
             const int f = k / C::U, c = k % C::U;
             float* vq = PR + f * C::PRS + 2 * C::U + c;
-            *vq = *vq > 0.f ? DY[k] : 0.f;
             float* qq = PR + f * C::PRS + c;
-            *qq = *qq > 0.f ? O[f * C::OS + c] : 0.f;
+            const float gv = DY[k], gq = O[f * C::OS + c];  // unconditional loads, then select
+            const float v0 = *vq, q0 = *qq;
+            *vq = v0 > 0.f ? gv : 0.f;
+            *qq = q0 > 0.f ? gq : 0.f;
           }
         }
         __syncthreads();
