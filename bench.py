@@ -52,6 +52,11 @@ def parse():
     return ap.parse_args()
 
 
+def trace(msg):
+    if os.environ.get("RS_BENCH_TRACE"):
+        print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
 def zipf_ids(rng, B, F, vocab, a=1.2):
     z = rng.zipf(a, size=(B, F)) - 1
     return np.minimum(z, vocab - 1).astype(np.int64)
@@ -207,7 +212,9 @@ def main():
     pool = [(i.to(dev), l.to(dev)) for i, l in pool_cpu]
 
     # one HIP graph per resident batch (the step reads its batch in place: no input copy)
+    trace("capturing")
     trainer.capture_pool(pool, warmup=max(1, min(args.warmup, 3)))
+    trace("captured")
     for i in range(args.warmup):
         trainer.step_pool(i)
     torch.cuda.synchronize()
@@ -229,6 +236,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     loss = float(trainer.loss.item())
+    trace(f"timed loop done, loss {loss}")
 
     # ---- roofline of the dominant kernel (IL backward), HIP events on its stream ----
     from recommendsystem_amd._lib import call, ptr, stream_handle
@@ -236,16 +244,21 @@ def main():
     E, U, H, L = cfg.embed_dim, cfg.unit_num, cfg.head_num, cfg.layer_num
 
     def il_bwd_once():
-        call("rs_il_bwd", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
-             trainer.dcat.data_ptr() + 4 * trainer.D, trainer.CW, B, F, E, U, H, L, ptr(il.kernel),
-             ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0, ptr(trainer.dx0), 0,
-             None, 0, ptr(trainer.il_ws), trainer.il_ws_n)
+        # the exact launch the step makes: backward + fused sparse push into the gradient table
+        # (scan-mode marks); it adds into table.grad, which only matters after the timed region
+        t = model.table
+        call("rs_il_bwd_push", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
+             trainer.dcat.data_ptr() + 4 * trainer.D, trainer.CW, B, F, E, U, H, L,
+             ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
+             ptr(trainer.dx0), ptr(trainer.rows), ptr(t.grad), ptr(t.flag), None, 0,
+             ptr(trainer.il_ws), trainer.il_ws_n)
 
     def il_fwd_once():
         call("rs_il_fwd", stream_handle(), ptr(trainer.x0), B, F, E, U, H, L, ptr(il.kernel),
              ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
              trainer.cat.data_ptr() + 4 * trainer.D, trainer.CW, ptr(trainer.xsave))
 
+    trace("kernel timing")
     t_bwd = time_kernel(il_bwd_once, args.kernel_reps)
     t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
     bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
@@ -274,7 +287,7 @@ def main():
                                "26 fields x emb 16, per-GPU batch 4096",
                    "global_batch": B * world, "fields": F, "emb_dim": E, "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd2_kernel (InteractingLayer backward)",
+        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd2_kernel (InteractingLayer backward + fused sparse push)",
                      "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                      "launch_us": round(t_bwd * 1e6, 2),

@@ -111,6 +111,23 @@ int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* grads, 
                          int dim, float* grad_table, int32_t* flag, int32_t* touched,
                          int32_t* n_touched, int32_t touched_cap);
 
+/* Packed scan-mode exchange (the graph-captured DP step of the AutoInt trainer; same role as
+ * compact/merge above).  pack: every marked row becomes one record [row (int32 bits) | grad[dim]]
+ * of dim + 1 floats at records[u * (dim + 1)], u < *count_out (records past cap are dropped;
+ * cap >= the rows one rank can touch makes that impossible); the gradient row is zeroed and the
+ * flag cleared.  One all-gather then moves every rank's records as one contiguous prefix of
+ * nmax = max_r count_r records.  merge_packed adds rank `rank`'s records (at
+ * records + rank * nmax * (dim + 1); counts[r * counts_stride] is rank r's count, nmax is
+ * recomputed on the device, so the launch needs no host-side count and is graph-capturable) and
+ * scan-marks the rows.  Launching it for rank 0 .. world-1 in order gives bitwise-identical sums
+ * on every replica.  Record rows outside [0, table_rows) are skipped; counts are clamped to cap
+ * (each rank's record capacity). */
+int rs_sparse_pack_scan(void* stream, float* grad_table, int32_t* flag, int64_t table_rows,
+                        int dim, float* records, int32_t* count_out, int32_t cap);
+int rs_sparse_merge_packed(void* stream, const float* records, const int32_t* counts,
+                           int64_t counts_stride, int world, int rank, int dim, float* grad_table,
+                           int32_t* flag, int64_t table_rows, int32_t cap);
+
 /* ---------------------------------------------------------------------------------------
  * H3  InteractingLayer (InteractingLayer.py:7-61; rank/multi_head/interacting_layer.py:7-61).
  * x [B, F, E]; W [E, 4U] = [Wq | Wk | Wv | Wr] (Keras Dense kernels), bias [4U],

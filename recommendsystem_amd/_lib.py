@@ -106,6 +106,8 @@ SIGNATURES: dict[str, tuple] = {
                                    _f32, _f32]),
     "rs_sparse_adagrad_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),
     "rs_sparse_compact_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i32]),
+    "rs_sparse_pack_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32]),
+    "rs_sparse_merge_packed": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i64, _i32]),
     "rs_il_bwd_push": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                               _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64]),
@@ -138,8 +140,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+_TRACE = bool(os.environ.get("RS_TRACE_CALLS"))  # debugging: sync + name after every launch
+
+
 def call(name: str, *args) -> int:
     rc = getattr(load(), name)(*args)
+    if _TRACE and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.synchronize()
+        print(f"[rs] {name} ok", flush=True)
     if SIGNATURES[name][0] is _i32 and rc != RS_OK and not name.endswith(("_count", "_blocks")):
         raise RecsysKernelError(f"{name} returned {rc} ({_ERRS.get(rc, 'hip error')})")
     return rc

@@ -179,7 +179,23 @@ class AutoIntTrainer:
         self.push = self.head is not None and self.F <= 64
         if self.push:
             m.table.mode = "scan"
-        if self.world > 1:
+        # data parallel, fused path: packed exchange (dist.exchange_packed) -- the dense partials
+        # reduce into a send bucket that also carries the sparse record count, the touched rows
+        # are packed into [row | grad] records; two all-gathers, then graph-captured rank-ordered
+        # merges and a rank-ordered dense sum fused with Adam
+        self.packed_dp = self.world > 1 and self.push
+        if self.packed_dp:
+            n = m.arena.n
+            self.dp_n = n
+            self.dp_ld = ld = (n + 1 + 3) // 4 * 4
+            self.dp_send = torch.zeros(ld, **f32)
+            self.dp_recv = torch.zeros(self.world * ld, **f32)
+            self.dp_rs = E + 1
+            self.dp_cap = B * F  # one rank touches at most B * F rows per step
+            self.dp_recs = torch.empty(self.dp_cap * self.dp_rs, **f32)
+            self.dp_recs_all = torch.empty(self.world * self.dp_cap * self.dp_rs, **f32)
+            self.dp_nmax = 0
+        elif self.world > 1:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
             self.x_grads = torch.empty(cap, E, **f32)
@@ -277,7 +293,8 @@ class AutoIntTrainer:
         adam, apply the dense Adam in the same launch."""
         m, hd, cfg = self.model, self.head, self.model.cfg
         ar = m.arena
-        g0 = ar.grad.data_ptr()
+        # data parallel: the local gradient goes to the exchange bucket, not the arena
+        g0 = self.dp_send.data_ptr() if self.packed_dp else ar.grad.data_ptr()
         npl = hd["npar"] + 1
         segs = [
             (self.il_ws.data_ptr(), hd["il_n"], hd["il_blocks"], hd["il_n"], g0 + 4 * hd["il_off"],
@@ -295,6 +312,11 @@ class AutoIntTrainer:
             self._forward_backward_fused()
             if self.world > 1:
                 self._reduce_dense(adam=False)
+            if self.packed_dp:
+                t = self.model.table
+                call("rs_sparse_pack_scan", stream_handle(), ptr(t.grad), ptr(t.flag), t.rows,
+                     t.dim, ptr(self.dp_recs), self.dp_send.data_ptr() + 4 * self.dp_n,
+                     self.dp_cap)
             return
         m, cfg = self.model, self.model.cfg
         B, F, E, U, L, H, D, CW = self.B, self.F, self.E, self.U, self.L, self.H, self.D, self.CW
@@ -361,8 +383,14 @@ class AutoIntTrainer:
 
     def _exchange(self):
         """Data-parallel gradient exchange (recommendsystem_amd/dist.py)."""
-        from .dist import allreduce_flat, gather_sparse_lists
+        from .dist import allreduce_flat, exchange_packed, gather_sparse_lists
         m, t = self.model, self.model.table
+        if self.packed_dp:
+            self.dp_nmax = exchange_packed(self.dp_send, self.dp_recv, self.dp_n, self.dp_recs,
+                                           self.dp_recs_all, self.dp_rs, self.pg)
+            if self.dp_nmax > self.dp_cap:
+                raise RuntimeError(f"sparse exchange: {self.dp_nmax} records > capacity {self.dp_cap}")
+            return
         allreduce_flat(m.arena.grad, self.pg)
         scan = t.mode == "scan"
         if scan:
@@ -388,6 +416,19 @@ class AutoIntTrainer:
             m.table.step(grad_scale=1.0)
             return
         scale = 1.0 / self.world
+        if self.packed_dp:
+            s, t = stream_handle(), m.table
+            counts = self.dp_recv.data_ptr() + 4 * self.dp_n
+            for r in range(self.world):  # rank order: identical sums on every replica
+                call("rs_sparse_merge_packed", s, ptr(self.dp_recs_all), counts, self.dp_ld,
+                     self.world, r, t.dim, ptr(t.grad), ptr(t.flag), t.rows, self.dp_cap)
+            # dense: rank-ordered sum of the gathered buckets -> arena grad -> Adam, one launch
+            _lib.partials_reduce_adam(s, [(ptr(self.dp_recv), self.dp_ld, self.world, self.dp_n,
+                                           ptr(ar.grad), 1.0, 0)], ar.data, self.adam_m,
+                                      self.adam_v, self.step_count, self.head["done"],
+                                      cfg.lr_dense, 0.9, 0.999, 1e-8, scale, True)
+            t.step(grad_scale=scale)
+            return
         call("rs_dense_adam", stream_handle(), ptr(ar.data), ptr(ar.grad), ptr(self.adam_m),
              ptr(self.adam_v), ar.n, ptr(self.step_count), cfg.lr_dense, 0.9, 0.999, 1e-8, scale, 0)
         m.table.step(grad_scale=scale)

@@ -17,7 +17,8 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 BUILD_DIR = os.path.join(PKG_DIR, "_build")
-LIB_PATH = os.path.join(PKG_DIR, "librecsys_amd.so")
+# RS_LIB_OUT: build a kernel variant (extra -D flags) to another path, loaded with RS_LIB_PATH
+LIB_PATH = os.environ.get("RS_LIB_OUT") or os.path.join(PKG_DIR, "librecsys_amd.so")
 ARCH = os.environ.get("RS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -44,6 +44,57 @@ def gather_sparse_lists(rows: torch.Tensor, grads: torch.Tensor, count: torch.Te
     return rows_all, grads_all, n
 
 
+def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """out[r * inp.numel():(r + 1) * inp.numel()] = rank r's inp (one contiguous receive buffer).
+    RCCL moves it with one all-gather; backends without the flat form get per-rank views."""
+    try:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    except (RuntimeError, NotImplementedError):
+        world = dist.get_world_size(group)
+        dist.all_gather(list(out.view(world, -1).unbind(0)), inp, group=group)
+
+
+def exchange_packed(send: torch.Tensor, recv: torch.Tensor, n_dense: int, recs: torch.Tensor,
+                    recs_all: torch.Tensor, rec_floats: int, group=None) -> int:
+    """The AutoInt trainer's data-parallel exchange: TWO all-gathers per step.
+
+    send  [ld] fp32 : this rank's dense gradient (n_dense floats) + its record count (int32 bits
+                      at index n_dense), ld >= n_dense + 1;
+    recv  [world * ld] : every rank's send buffer (a deterministic rank-ordered sum of the dense
+                      part replaces the all-reduce, so replicas stay bitwise identical);
+    recs  [cap * rec_floats] : this rank's packed sparse records (rs_sparse_pack_scan);
+    recs_all [world * cap * rec_floats] : receives nmax records per rank, rank r's at
+                      r * nmax * rec_floats (rs_sparse_merge_packed recomputes nmax on the device).
+    Returns nmax = the largest count (the only host synchronisation of the step).
+    """
+    world = dist.get_world_size(group)
+    ld = send.numel()
+    _all_gather_flat(recv, send, group)
+    counts = recv.view(torch.int32).view(world, ld)[:, n_dense]
+    nmax = int(counts.max().item())
+    if nmax > 0:
+        k = nmax * rec_floats
+        _all_gather_flat(recs_all[:world * k], recs[:k], group)
+    return nmax
+
+
+def merge_packed_reference(recv, ld, n_dense, recs_all, rec_floats, table_grad):
+    """Host restatement of rs_sparse_merge_packed over every rank in order (CPU tests)."""
+    world = recv.numel() // ld
+    counts = recv.view(torch.int32).view(world, ld)[:, n_dense].tolist()
+    nmax = max(counts)
+    touched = []
+    for r in range(world):
+        base = r * nmax * rec_floats
+        for u in range(counts[r]):
+            rec = recs_all[base + u * rec_floats: base + (u + 1) * rec_floats]
+            row = int(rec[:1].view(torch.int32)[0])
+            if row not in touched:
+                touched.append(row)
+            table_grad[row] += rec[1:].numpy()
+    return touched
+
+
 def merge_reference(rows_all, grads_all, table_grad):
     """Host restatement of the rank-ordered merge (what rs_sparse_merge_rows does per rank),
     used by the CPU tests: table_grad[row] += grads in rank order, skipping -1 padding."""

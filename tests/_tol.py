@@ -17,7 +17,8 @@ def assert_close(got, ref, atol, rtol=0.0, what=""):
     assert worst <= 0, f"{what}: max|err|={err.max():.3e} (atol={atol}, rtol={rtol})"
 
 
-def assert_grad_close(got, ref, what=""):
-    """Gradients: |err| <= 1e-4 |ref| + max(1e-4, 2e-6 max|ref|) (fp32 sums over many terms)."""
+def assert_grad_close(got, ref, what="", scale=2e-6):
+    """Gradients: |err| <= 1e-4 |ref| + max(1e-4, scale max|ref|) (fp32 sums over many terms;
+    scale grows with the length of the cancelling sums, e.g. 1e-5 for F > 64 fields)."""
     ref = np.asarray(ref, dtype=np.float64)
-    assert_close(got, ref, max(1e-4, 2e-6 * float(np.abs(ref).max(initial=0.0))), 1e-4, what)
+    assert_close(got, ref, max(1e-4, scale * float(np.abs(ref).max(initial=0.0))), 1e-4, what)

@@ -20,3 +20,11 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _seed_torch():
+    """Every test sees the same torch RNG stream (CPU and device) whatever ran before it."""
+    import torch
+    torch.manual_seed(1234)
+    yield

@@ -67,3 +67,59 @@ def test_dp_exchange_two_ranks():
             ref[r[k]] += g[k]
     assert np.allclose(t0, ref, atol=1e-6)
     assert tc0 == sorted(set(int(v) for rank in range(world) for v in _local_lists(rank)[0] if v >= 0))
+
+
+# ---- packed exchange (the AutoInt trainer's DP step: dist.exchange_packed) -------------------
+N_DENSE, REC = 10, DIM + 1
+
+
+def _packed_local(rank):
+    """What the fused step leaves on rank `rank`: the dense bucket [grad | count | pad] and the
+    packed records [row | grad] (rs_sparse_pack_scan's layout)."""
+    r, g, n = _local_lists(rank)
+    ld = (N_DENSE + 1 + 3) // 4 * 4
+    send = torch.zeros(ld)
+    send[:N_DENSE] = torch.arange(N_DENSE, dtype=torch.float32) * (rank + 1)
+    send.view(torch.int32)[N_DENSE] = n
+    recs = torch.zeros(CAP * REC)
+    for u in range(n):
+        recs[u * REC:(u + 1) * REC].view(torch.int32)[0] = int(r[u])
+        recs[u * REC + 1:(u + 1) * REC] = torch.from_numpy(g[u])
+    return send, recs, ld
+
+
+def _packed_worker(rank, world, port, out):
+    from recommendsystem_amd.dist import exchange_packed, merge_packed_reference
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    send, recs, ld = _packed_local(rank)
+    recv = torch.zeros(world * ld)
+    recs_all = torch.full((world * CAP * REC,), float("nan"))
+    nmax = exchange_packed(send, recv, N_DENSE, recs, recs_all, REC)
+    # the rank-ordered dense sum (what rs_partials_reduce_adam does over the gathered buckets)
+    dense = recv.view(world, ld)[:, :N_DENSE].sum(0)
+    table = np.zeros((ROWS, DIM), np.float32)
+    touched = merge_packed_reference(recv, ld, N_DENSE, recs_all, REC, table)
+    out[rank] = (dense.numpy().copy(), table.copy(), sorted(touched), nmax)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_packed_exchange_two_ranks():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_packed_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    d0, t0, tc0, n0 = out[0]
+    d1, t1, tc1, n1 = out[1]
+    assert np.array_equal(d0, d1) and np.array_equal(d0, np.arange(N_DENSE) * 3.0)
+    assert np.array_equal(t0, t1) and tc0 == tc1  # replicas bitwise identical
+    assert n0 == n1 == 12  # max(7, 12)
+    ref = np.zeros((ROWS, DIM), np.float64)
+    for rank in range(world):
+        r, g, n = _local_lists(rank)
+        for k in range(n):
+            ref[r[k]] += g[k]
+    assert np.allclose(t0, ref, atol=1e-6)
+    assert tc0 == sorted(set(int(v) for rank in range(world) for v in _local_lists(rank)[0] if v >= 0))

@@ -1,0 +1,126 @@
+"""GPU, world size 2 on one device (gloo transport; RCCL on the 8-GPU node runs the same code):
+the data-parallel AutoInt step (dist.exchange_packed: dense bucket + packed sparse records, two
+all-gathers, rank-ordered merges and dense sum) after 3 steps
+
+  * leaves bitwise-identical replicas (dense parameters and the embedding table), and
+  * matches the CPU oracle's single-process train step on the union of the ranks' batches
+    (same tolerances as test_gpu_parity::test_autoint_train_steps_match_oracle).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _tol import assert_close
+
+pytestmark = pytest.mark.gpu
+
+B_LOCAL, WORLD, STEPS = 128, 2, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(max_batch, world):
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig
+    cfg = AutoIntConfig(vocab_per_field=50, layer_num=3, lr_dense=1e-3, lr_sparse=1e-3)
+    return cfg, AutoInt(cfg, device=torch.device("cuda", 0), seed=21, max_batch=max_batch,
+                        world_size=world)
+
+
+def _worker(rank, world, port, ids, labels, graph, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from recommendsystem_amd.autoint import AutoIntTrainer
+    cfg, model = _model(B_LOCAL, world)
+    trn = AutoIntTrainer(model, B_LOCAL, process_group=dist.group.WORLD)
+    assert trn.packed_dp
+    sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
+    idt = torch.from_numpy(ids[sl]).cuda()
+    lbt = torch.from_numpy(labels[sl]).cuda()
+    if graph:
+        trn.capture_pool([(idt, lbt)], warmup=0)
+        for _ in range(STEPS):
+            trn.step_pool(0)
+    else:
+        for _ in range(STEPS):
+            trn.step(idt, lbt)
+    torch.cuda.synchronize()
+    params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).numpy()
+    out[rank] = (params, model.table.weight.cpu().numpy(), float(trn.loss))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_dp_two_ranks_match_oracle(graph):
+    from test_gpu_parity import _oracle_from_model
+    B = B_LOCAL * WORLD
+    cfg, model = _model(B, 1)
+    rng = np.random.default_rng(21)
+    ids = rng.integers(0, 10 * cfg.vocab_per_field, size=(B, cfg.num_fields), dtype=np.int64)
+    labels = (rng.uniform(size=(B, 1)) < 0.25).astype(np.float32)
+    ref, *_ = _oracle_from_model(model, cfg)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(WORLD, _free_port(), ids, labels, graph, out), nprocs=WORLD, join=True)
+    p0, t0, l0 = out[0]
+    p1, t1, l1 = out[1]
+    assert np.array_equal(p0, p1), "dense replicas diverged"
+    assert np.array_equal(t0, t1), "embedding-table replicas diverged"
+    for _ in range(STEPS):
+        loss_ref = ref.step(torch.from_numpy(ids), torch.from_numpy(labels))
+    # each rank's loss is its half-batch mean: their average is the global-batch loss
+    assert abs(0.5 * (l0 + l1) - loss_ref) < 1e-5
+    want = torch.cat([p.detach().reshape(-1) for p in ref.dense_list]).numpy()
+    assert_close(p0.astype(np.float64), want, 2e-6, 1e-4, what="dense params after DP steps")
+    assert_close(t0, ref.table.numpy(), 2e-6, 1e-4, what="table after DP steps")
+
+
+def _worker_full(rank, world, port, out):
+    """Config-2 size (B = 4096 per rank, 26 x 100k table), graph-captured steps like bench.py."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
+    B = 4096
+    cfg = AutoIntConfig()
+    model = AutoInt(cfg, device=torch.device("cuda", 0), seed=0, max_batch=B, world_size=world)
+    trn = AutoIntTrainer(model, B, process_group=dist.group.WORLD)
+    rng = np.random.default_rng(2 + 1000 * rank)
+    z = np.minimum(rng.zipf(1.2, size=(B, cfg.num_fields)) - 1, cfg.vocab_per_field - 1)
+    ids = torch.from_numpy(z.astype(np.int64)).cuda()
+    labels = (torch.rand(B, 1, generator=torch.Generator().manual_seed(rank)) < 0.25).float().cuda()
+    trn.capture_pool([(ids, labels)], warmup=1)
+    for _ in range(STEPS):
+        trn.step_pool(0)
+    torch.cuda.synchronize()
+    params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).numpy()
+    h = model.table.weight.double().sum(1).cpu().numpy()  # per-row checksum of the table
+    out[rank] = (params, h, float(trn.loss), trn.dp_nmax)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_two_ranks_config2_size():
+    """The full-size exchange (tens of thousands of records per rank): replicas stay identical."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_full, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    p0, h0, l0, n0 = out[0]
+    p1, h1, l1, n1 = out[1]
+    assert n0 == n1 > 10_000
+    assert np.isfinite(l0) and np.isfinite(l1)
+    assert np.array_equal(p0, p1) and np.array_equal(h0, h1)

@@ -226,10 +226,11 @@ def test_interacting_forward(case):
     x = rng.uniform(-0.5, 0.5, size=(B, F, E))
     il = InteractingLayer(L, U, H, use_res=res, seed=7, device=DEV)
     il.build((B, F, E), device=DEV)
-    with torch.no_grad():  # non-trivial LN affine + biases
-        il.bias.uniform_(-0.1, 0.1)
-        il.gamma.uniform_(0.5, 1.5)
-        il.beta.uniform_(-0.2, 0.2)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    with torch.no_grad():  # non-trivial LN affine + biases (seeded)
+        il.bias.uniform_(-0.1, 0.1, generator=gen)
+        il.gamma.uniform_(0.5, 1.5, generator=gen)
+        il.beta.uniform_(-0.2, 0.2, generator=gen)
     y = il(torch.from_numpy(x).float().to(DEV))
     W, b, g, be = _il_ref_params(il)
     ref = npo.interacting_layer(x.astype(np.float32).astype(np.float64), W, b, g, be, L, H, res)
@@ -245,10 +246,11 @@ def test_interacting_backward(case):
     dy = rng.normal(size=(B, F, U)).astype(np.float32)
     il = InteractingLayer(L, U, H, use_res=res, seed=8, device=DEV)
     il.build((B, F, E), device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(9)  # seeded: the case is the same every run
     with torch.no_grad():
-        il.bias.uniform_(-0.1, 0.1)
-        il.gamma.uniform_(0.5, 1.5)
-        il.beta.uniform_(-0.2, 0.2)
+        il.bias.uniform_(-0.1, 0.1, generator=gen)
+        il.gamma.uniform_(0.5, 1.5, generator=gen)
+        il.beta.uniform_(-0.2, 0.2, generator=gen)
     xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
     il(xd).backward(torch.from_numpy(dy).to(DEV))
     torch.cuda.synchronize()
@@ -256,11 +258,12 @@ def test_interacting_backward(case):
     xr = torch.from_numpy(x).double().requires_grad_(True)
     yr = tr.interacting_layer(xr, W, b, g, be, L, H, res)
     yr.backward(torch.from_numpy(dy).double())
-    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dx")
-    assert_grad_close(_np(il.kernel.grad), W.grad.numpy(), what="dW")
-    assert_grad_close(_np(il.bias.grad), b.grad.numpy(), what="db")
-    assert_grad_close(_np(il.gamma.grad), g.grad.numpy(), what="dgamma")
-    assert_grad_close(_np(il.beta.grad), be.grad.numpy(), what="dbeta")
+    sc = 2e-6 if F <= 64 else 1e-5  # F > 64: sums of F * B * L cancelling fp32 terms
+    assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dx", scale=sc)
+    assert_grad_close(_np(il.kernel.grad), W.grad.numpy(), what="dW", scale=sc)
+    assert_grad_close(_np(il.bias.grad), b.grad.numpy(), what="db", scale=sc)
+    assert_grad_close(_np(il.gamma.grad), g.grad.numpy(), what="dgamma", scale=sc)
+    assert_grad_close(_np(il.beta.grad), be.grad.numpy(), what="dbeta", scale=sc)
 
 
 @pytest.mark.parametrize("with_base", [True, False])
