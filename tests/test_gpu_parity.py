@@ -16,26 +16,14 @@ import torch
 from oracle import ctr_oracle as npo
 from oracle import torch_ref as tr
 
+from _tol import assert_close, assert_grad_close
+
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
 def _np(t):
     return t.detach().double().cpu().numpy()
-
-
-def assert_grad_close(got, ref, what=""):
-    ref = np.asarray(ref, dtype=np.float64)
-    assert_close(got, ref, max(1e-4, 2e-6 * float(np.abs(ref).max(initial=0.0))), 1e-4, what)
-
-
-def assert_close(got, ref, atol, rtol=0.0, what=""):
-    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
-    assert got.shape == ref.shape, (what, got.shape, ref.shape)
-    err = np.abs(got - ref)
-    bound = atol + rtol * np.abs(ref)
-    worst = np.max(err - bound) if err.size else -1
-    assert worst <= 0, f"{what}: max|err|={err.max():.3e} (atol={atol}, rtol={rtol})"
 
 
 # ------------------------------------------------------------------------------------------
