@@ -153,6 +153,14 @@ def call(name: str, *args) -> int:
     return rc
 
 
+def trace_point(what: str) -> None:
+    """RS_TRACE_CALLS debugging: synchronise and name the step section that just completed
+    (graph replays are not visible to `call`)."""
+    if _TRACE and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.synchronize()
+        print(f"[rs] {what} ok", flush=True)
+
+
 def ptr(t) -> int | None:
     """Device pointer of a tensor (None -> NULL)."""
     if t is None:

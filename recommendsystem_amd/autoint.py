@@ -470,11 +470,26 @@ class AutoIntTrainer:
     def capture_pool(self, batches, warmup: int = 2) -> None:
         """One graph per device-resident batch [(ids, labels), ...]: each graph's lookup and loss
         read that batch's own buffers, so replaying batch i needs no copy into a static input
-        (what a double-buffered loader hands over).  ``step_pool(i)`` replays batch i."""
-        self.pool_graphs = []
-        for k, (ids, labels) in enumerate(batches):
+        (what a double-buffered loader hands over).  ``step_pool(i)`` replays batch i.
+
+        Data parallel (world > 1): ONE forward/backward graph over the static input buffers, and
+        step_pool(i) copies batch i into them (0.85 MB device-to-device at config 2).  A second
+        forward/backward graph captured after the first pair (graph_fb, graph_opt) faulted on
+        its first replay in the 2-rank rehearsal (bench.py --backend gloo, pool of 8), while one
+        graph replayed many times is the configuration tests/test_gpu_dp.py pins."""
+        for ids, labels in batches:
             if ids.shape != (self.B, self.F) or ids.dtype != torch.int64 or not ids.is_contiguous():
                 raise ValueError("pool ids must be contiguous int64 [B, F]")
+        if self.world > 1:
+            self.pool_batches = [(ids, labels.reshape(self.B, self.T).float().contiguous())
+                                 for ids, labels in batches]
+            self.load_batch(*self.pool_batches[0])
+            self.graph = None
+            self.capture(warmup=warmup)
+            self.pool_graphs = [(self.graph, self.graph_fb)]
+            return
+        self.pool_graphs = []
+        for k, (ids, labels) in enumerate(batches):
             self.ids = ids
             self.labels = labels.reshape(self.B, self.T).float().contiguous()
             self.graph = None
@@ -482,13 +497,17 @@ class AutoIntTrainer:
             self.pool_graphs.append((self.graph, getattr(self, "graph_fb", None)))
 
     def step_pool(self, i: int) -> torch.Tensor:
-        g, gfb = self.pool_graphs[i % len(self.pool_graphs)]
         if self.world == 1:
+            g, _ = self.pool_graphs[i % len(self.pool_graphs)]
             g.replay()
-        else:
-            gfb.replay()
-            self._exchange()
-            self.graph_opt.replay()
+            return self.loss
+        self.load_batch(*self.pool_batches[i % len(self.pool_batches)])
+        self.graph_fb.replay()
+        _lib.trace_point("graph_fb")
+        self._exchange()
+        _lib.trace_point("exchange")
+        self.graph_opt.replay()
+        _lib.trace_point("graph_opt")
         return self.loss
 
     def step(self, ids: torch.Tensor | None = None, labels: torch.Tensor | None = None) -> torch.Tensor:

@@ -28,6 +28,9 @@ enum { RS_COMBINER_SUM = 0, RS_COMBINER_MEAN = 1, RS_COMBINER_SQRTN = 2 };
 __device__ __forceinline__ int64_t hash_row(int64_t id, int64_t base, int64_t bucket, int mode) {
   uint64_t u = (uint64_t)id;
   if (mode == RS_HASH_SPLITMIX) u = splitmix64(u);
+  // same value either way; a 64-bit remainder is a long emulated sequence on the GPU, the 32-bit
+  // one a few VALU ops (Criteo-style ids and per-field buckets fit in 32 bits)
+  if (((u | (uint64_t)bucket) >> 32) == 0) return base + (int64_t)((uint32_t)u % (uint32_t)bucket);
   return base + (int64_t)(u % (uint64_t)bucket);
 }
 
@@ -51,8 +54,17 @@ __global__ void __launch_bounds__(256) embed_lookup_fwd_kernel(
   const int nvec = dim >> 2;
   for (int64_t s = (int64_t)blockIdx.x * groups_per_block + g; s < nseg;
        s += (int64_t)gridDim.x * groups_per_block) {
-    const int f = (int)(s % F);
-    const int64_t b = s / F;
+    // segment -> (b, f) in 32 bits when it fits (launch sizes here are far below 2^31)
+    int f;
+    int64_t b;
+    if (nseg <= INT32_MAX) {
+      const uint32_t s32 = (uint32_t)s, b32 = s32 / (uint32_t)F;
+      b = b32;
+      f = (int)(s32 - b32 * (uint32_t)F);
+    } else {
+      f = (int)(s % F);
+      b = s / F;
+    }
     const int64_t beg = offsets ? offsets[s] : s;
     const int64_t end = offsets ? offsets[s + 1] : s + 1;
     const int64_t base = row_base[f], bk = bucket[f];

@@ -89,7 +89,8 @@ def test_dp_two_ranks_match_oracle(graph):
 
 
 def _worker_full(rank, world, port, out):
-    """Config-2 size (B = 4096 per rank, 26 x 100k table), graph-captured steps like bench.py."""
+    """Config-2 size (B = 4096 per rank, 26 x 100k table), a 2-batch pool, graph-captured steps
+    like bench.py (3 eager warm-up steps, then alternating batches)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -100,12 +101,15 @@ def _worker_full(rank, world, port, out):
     model = AutoInt(cfg, device=torch.device("cuda", 0), seed=0, max_batch=B, world_size=world)
     trn = AutoIntTrainer(model, B, process_group=dist.group.WORLD)
     rng = np.random.default_rng(2 + 1000 * rank)
-    z = np.minimum(rng.zipf(1.2, size=(B, cfg.num_fields)) - 1, cfg.vocab_per_field - 1)
-    ids = torch.from_numpy(z.astype(np.int64)).cuda()
-    labels = (torch.rand(B, 1, generator=torch.Generator().manual_seed(rank)) < 0.25).float().cuda()
-    trn.capture_pool([(ids, labels)], warmup=1)
-    for _ in range(STEPS):
-        trn.step_pool(0)
+    pool = []
+    for k in range(2):  # a batch pool, as bench.py runs it (steps alternate between batches)
+        z = np.minimum(rng.zipf(1.2, size=(B, cfg.num_fields)) - 1, cfg.vocab_per_field - 1)
+        ids = torch.from_numpy(z.astype(np.int64)).cuda()
+        g = torch.Generator().manual_seed(10 * rank + k)
+        pool.append((ids, (torch.rand(B, 1, generator=g) < 0.25).float().cuda()))
+    trn.capture_pool(pool, warmup=3)
+    for i in range(2 * STEPS):
+        trn.step_pool(i)
     torch.cuda.synchronize()
     params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).numpy()
     h = model.table.weight.double().sum(1).cpu().numpy()  # per-row checksum of the table
