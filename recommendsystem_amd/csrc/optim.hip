@@ -175,13 +175,15 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
 // ---------------------------------------------------------------------------------------------
 constexpr int kScanBlock = 256;
 
-// update one float4 of a row from its loaded (grad, param, m, v) and store param, m, v, grad = 0
 template <bool ADAM>
-__device__ __forceinline__ void scan_apply4(float* __restrict__ table, float* __restrict__ m,
-                                            float* __restrict__ v, float* __restrict__ grad_table,
-                                            int64_t o, float4 g, float4 w, float4 mm, float4 vv,
-                                            float lr, float b1, float b2, float eps,
-                                            float grad_scale) {
+__device__ __forceinline__ void scan_update4(float* __restrict__ table, float* __restrict__ m,
+                                             float* __restrict__ v,
+                                             float* __restrict__ grad_table, int64_t o, float lr,
+                                             float b1, float b2, float eps, float grad_scale) {
+  float4 g = *reinterpret_cast<const float4*>(grad_table + o);
+  float4 w = *reinterpret_cast<const float4*>(table + o);
+  float4 mm = *reinterpret_cast<const float4*>(m + o);
+  float4 vv = ADAM ? *reinterpret_cast<const float4*>(v + o) : mm;
   float* gp = &g.x; float* wp = &w.x; float* mp = &mm.x; float* vp = &vv.x;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -199,18 +201,6 @@ __device__ __forceinline__ void scan_apply4(float* __restrict__ table, float* __
   *reinterpret_cast<float4*>(m + o) = mm;
   if (ADAM) *reinterpret_cast<float4*>(v + o) = vv;
   *reinterpret_cast<float4*>(grad_table + o) = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-template <bool ADAM>
-__device__ __forceinline__ void scan_update4(float* __restrict__ table, float* __restrict__ m,
-                                             float* __restrict__ v,
-                                             float* __restrict__ grad_table, int64_t o, float lr,
-                                             float b1, float b2, float eps, float grad_scale) {
-  const float4 g = *reinterpret_cast<const float4*>(grad_table + o);
-  const float4 w = *reinterpret_cast<const float4*>(table + o);
-  const float4 mm = *reinterpret_cast<const float4*>(m + o);
-  const float4 vv = ADAM ? *reinterpret_cast<const float4*>(v + o) : mm;
-  scan_apply4<ADAM>(table, m, v, grad_table, o, g, w, mm, vv, lr, b1, b2, eps, grad_scale);
 }
 
 template <bool ADAM>
@@ -250,39 +240,13 @@ __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const int n = __popcll(mask);
-      if (nv <= 64) {
-        // one float4 per lane per row: UN passes' loads are issued before any update, so a
-        // dense chunk (64 hits = 4 passes at dim 16) costs one memory round trip, not four.
-        // Lanes past the hit count load row list[0] (always a hit here) and store nothing.
-        constexpr int UN = 4;
-        for (int p0 = 0; p0 < n; p0 += UN * rpp) {
-          float4 g[UN], w[UN], mm[UN], vv[UN];
-          int64_t o[UN];
-          bool ok[UN];
-#pragma unroll
-          for (int u = 0; u < UN; ++u) {
-            const int k = p0 + u * rpp + slot;
-            ok[u] = slot < rpp && k < n;
-            o[u] = (row0 + list[ok[u] ? k : 0]) * dim + 4 * sub;
-            g[u] = *reinterpret_cast<const float4*>(grad_table + o[u]);
-            w[u] = *reinterpret_cast<const float4*>(table + o[u]);
-            mm[u] = *reinterpret_cast<const float4*>(m + o[u]);
-            vv[u] = ADAM ? *reinterpret_cast<const float4*>(v + o[u]) : mm[u];
-          }
-#pragma unroll
-          for (int u = 0; u < UN; ++u)
-            if (ok[u]) scan_apply4<ADAM>(table, m, v, grad_table, o[u], g[u], w[u], mm[u], vv[u],
-                                         lr, b1, b2, eps, grad_scale);
-        }
-      } else {
-        for (int p0 = 0; p0 < n; p0 += rpp) {
-          const int k = p0 + slot;
-          if (slot < rpp && k < n) {
-            const int64_t row = row0 + list[k];
-            for (int e4 = sub; e4 < nv; e4 += lpr)
-              scan_update4<ADAM>(table, m, v, grad_table, row * dim + 4 * e4, lr, b1, b2, eps,
-                                 grad_scale);
-          }
+      for (int p0 = 0; p0 < n; p0 += rpp) {
+        const int k = p0 + slot;
+        if (slot < rpp && k < n) {
+          const int64_t row = row0 + list[k];
+          for (int e4 = sub; e4 < nv; e4 += lpr)
+            scan_update4<ADAM>(table, m, v, grad_table, row * dim + 4 * e4, lr, b1, b2, eps,
+                               grad_scale);
         }
       }
       __builtin_amdgcn_wave_barrier();  // list reuse by the next chunk
