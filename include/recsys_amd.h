@@ -141,6 +141,19 @@ int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int U, int 
               const float* W, const float* bias, const float* gamma, const float* beta,
               float eps, int use_res, float drop_rate, uint64_t seed, float* y, int64_t y_ld,
               float* xsave);
+/* Forward with the embedding front end fused in (single-hot fields, F <= 64): replaces
+ * rs_embedding_lookup_fwd(ids, offsets = NULL, ...) + rs_il_fwd(x, ...) -- the
+ * EmbeddingFeatures lookup + expand/Concatenate of autoint:22-26 (rank/ctr/base_model.py:203-217)
+ * followed by InteractingLayer.call (InteractingLayer.py:37-61).  x[b, f, :] =
+ * table[row_base[f] + H(ids[b, f]) mod bucket[f]] is read straight into the kernel's LDS and ALSO
+ * stored to x [B, F, E] (the MLP head's and the backward's input) and rows_out [B*F] (nullable;
+ * the sparse push's rows).  Bit-identical to the two separate calls. */
+int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row_base,
+                     const int64_t* bucket, int hash_mode, const float* table, int64_t table_rows,
+                     float* x, int32_t* rows_out, int64_t B, int F, int E, int U, int H, int L,
+                     const float* W, const float* bias, const float* gamma, const float* beta,
+                     float eps, int use_res, float drop_rate, uint64_t seed, float* y,
+                     int64_t y_ld, float* xsave);
 /* Backward (TF autograd of the graph above).  dx [B, F, E] written (or accumulated).
  * dparams = [dW (E*4U) | dbias (4U) | dgamma (U) | dbeta (U)] written (or accumulated);
  * dparams == NULL skips the grid reduction (per-block partials stay in the workspace).

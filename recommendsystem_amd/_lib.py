@@ -39,6 +39,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_il_param_count": (_i32, [_i32, _i32]),
     "rs_il_fwd": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32,
                          _i32, _f32, _u64, _vp, _i64, _vp]),
+    "rs_il_fwd_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _i32, _i32,
+                                _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp,
+                                _i64, _vp]),
     "rs_il_bwd_workspace_floats": (_i64, [_i64, _i32, _i32]),
     "rs_il_bwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                          _vp, _vp, _f32, _i32, _f32, _u64, _vp, _i32, _vp, _i32, _vp, _i64]),

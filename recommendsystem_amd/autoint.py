@@ -251,19 +251,28 @@ class AutoIntTrainer:
                     done=torch.zeros(288, device=dev, dtype=torch.int32))
 
     def _forward_backward_fused(self):
-        """lookup -> IL fwd -> fused head (MLP fwd, clip+BCE, MLP bwd) -> IL bwd -> sparse push:
-        five launches; dense gradients stay as per-block partials until _reduce_dense."""
+        """lookup + IL fwd (one launch for F <= 64) -> fused head (MLP fwd, clip+BCE, MLP bwd) ->
+        IL bwd + sparse push: three launches; dense gradients stay as per-block partials until
+        _reduce_dense."""
         m, hd = self.model, self.head
         B, F, E, U, L, H, D, CW = self.B, self.F, self.E, self.U, self.L, self.H, self.D, self.CW
         s = stream_handle()
         il, emb, t = m.interact, m.embedding, m.table
-        call("rs_embedding_lookup_fwd", s, ptr(self.ids), None, B, F, ptr(emb.row_base),
-             ptr(emb.bucket), emb.hash_mode, emb.combiner, ptr(t.weight), t.rows, E, ptr(self.x0),
-             F * E, E, ptr(self.rows))
         drop = il.dropout_rate if il.use_dropout else 0.0
-        call("rs_il_fwd", s, ptr(self.x0), B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
-             ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
-             self.cat.data_ptr() + 4 * D, CW, ptr(self.xsave) if L > 1 else None)
+        if F > 64:  # the many-field IL kernels read x0 from the lookup
+            call("rs_embedding_lookup_fwd", s, ptr(self.ids), None, B, F, ptr(emb.row_base),
+                 ptr(emb.bucket), emb.hash_mode, emb.combiner, ptr(t.weight), t.rows, E,
+                 ptr(self.x0), F * E, E, ptr(self.rows))
+            call("rs_il_fwd", s, ptr(self.x0), B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
+                 ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
+                 self.cat.data_ptr() + 4 * D, CW, ptr(self.xsave) if L > 1 else None)
+        else:  # single-hot lookup + concat + IL forward in one launch (x0 and the hashed rows
+            # are by-products for the head and the push)
+            call("rs_il_fwd_gather", s, ptr(self.ids), ptr(emb.row_base), ptr(emb.bucket),
+                 emb.hash_mode, ptr(t.weight), t.rows, ptr(self.x0), ptr(self.rows), B, F, E, U,
+                 H, L, ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon,
+                 int(il.use_res), drop, il.seed, self.cat.data_ptr() + 4 * D, CW,
+                 ptr(self.xsave) if L > 1 else None)
         d = self.deep_layers
         lg = self.logit_layers[0]
         d2 = d[1] if hd["N2"] else None

@@ -157,6 +157,20 @@ static inline void launch_column_reduce(hipStream_t s, const float* part, int nr
 // in thread 0 of the last block only.  No memory fence: callers use it only to order their own
 // earlier LOADS (consumed values) before a reset done by the last block.
 // ---------------------------------------------------------------------------------------------
+// id -> table row (embedding.hip header): row = base + H(id) mod bucket, H = identity or SplitMix64
+// ---------------------------------------------------------------------------------------------
+enum { RS_HASH_MOD = 0, RS_HASH_SPLITMIX = 1 };
+
+__device__ __forceinline__ int64_t hash_row(int64_t id, int64_t base, int64_t bucket, int mode) {
+  uint64_t u = (uint64_t)id;
+  if (mode == RS_HASH_SPLITMIX) u = splitmix64(u);
+  // same value either way; a 64-bit remainder is a long emulated sequence on the GPU, the 32-bit
+  // one a few VALU ops (Criteo-style ids and per-field buckets fit in 32 bits)
+  if (((u | (uint64_t)bucket) >> 32) == 0) return base + (int64_t)((uint32_t)u % (uint32_t)bucket);
+  return base + (int64_t)(u % (uint64_t)bucket);
+}
+
+// ---------------------------------------------------------------------------------------------
 #define RS_DONE_STRIDE 32
 #define RS_DONE_WORDS (9 * RS_DONE_STRIDE)
 __device__ __forceinline__ bool rs_last_block(int32_t* ctr) {

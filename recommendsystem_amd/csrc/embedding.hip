@@ -22,17 +22,8 @@
 // and writes 1 KiB of contiguous [B, F, 16] output per step at config 2).
 #include "common.hpp"
 
-enum { RS_HASH_MOD = 0, RS_HASH_SPLITMIX = 1 };
+// RS_HASH_* and hash_row live in common.hpp (shared with the InteractingLayer's fused gather)
 enum { RS_COMBINER_SUM = 0, RS_COMBINER_MEAN = 1, RS_COMBINER_SQRTN = 2 };
-
-__device__ __forceinline__ int64_t hash_row(int64_t id, int64_t base, int64_t bucket, int mode) {
-  uint64_t u = (uint64_t)id;
-  if (mode == RS_HASH_SPLITMIX) u = splitmix64(u);
-  // same value either way; a 64-bit remainder is a long emulated sequence on the GPU, the 32-bit
-  // one a few VALU ops (Criteo-style ids and per-field buckets fit in 32 bits)
-  if (((u | (uint64_t)bucket) >> 32) == 0) return base + (int64_t)((uint32_t)u % (uint32_t)bucket);
-  return base + (int64_t)(u % (uint64_t)bucket);
-}
 
 __device__ __forceinline__ float combiner_scale(int n, int combiner) {
   if (n <= 0) return 0.f;

@@ -45,6 +45,15 @@ struct FwdReq {
   uint64_t seed;
   float *y, *xsave;
   int64_t y_ld;  // row stride of y (>= F*U): lets the layer write into a concat buffer
+  // fused single-hot gather (rs_il_fwd_gather): x[b, f, :] = table[hash(ids[b, f])] is read
+  // straight into LDS, stored to x (the head's and the backward's input) and the hashed rows to
+  // gather_rows -- replaces the rs_embedding_lookup_fwd launch and the re-read of x
+  const int64_t* gather_ids = nullptr;
+  const int64_t* gather_base = nullptr;
+  const int64_t* gather_bucket = nullptr;
+  const float* gather_table = nullptr;
+  int32_t* gather_rows = nullptr;
+  int gather_hash = 0;
 };
 
 struct BwdReq {
@@ -137,6 +146,12 @@ struct Args {
   const int32_t* push_rows;    // fused sparse push (see BwdReq)
   float* push_table;
   int32_t* push_flag;
+  const int64_t* g_ids;        // fused gather (see FwdReq); g_table == nullptr: read x
+  const int64_t* g_base;
+  const int64_t* g_bucket;
+  const float* g_table;
+  int32_t* g_rows;
+  int g_hash;
 };
 
 static inline int r4(int v) { return (v + 3) & ~3; }
@@ -177,6 +192,10 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.push_rows = nullptr;
   a.push_table = nullptr;
   a.push_flag = nullptr;
+  a.g_ids = a.g_base = a.g_bucket = nullptr;
+  a.g_table = nullptr;
+  a.g_rows = nullptr;
+  a.g_hash = 0;
   return a;
 }
 
@@ -575,8 +594,23 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
     bet[c] = beta[lane % C::LPR + c * C::LPR];
   }
   for (int64_t b = (int64_t)blockIdx.x * wpb + wave_id(); b < a.B; b += (int64_t)gridDim.x * wpb) {
-    const float4* src = reinterpret_cast<const float4*>(x + b * F * C::E);
-    for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
+    if (a.g_table) {
+      // fused gather: float4 k of the sample is quarter k % (E/4) of field k / (E/4)'s row; the
+      // E/4 lanes of a field hash the same id (one cached 8-B load), lane q == 0 records the row
+      constexpr int QV = C::E / 4;
+      float4* xo = reinterpret_cast<float4*>(const_cast<float*>(x) + b * F * C::E);
+      for (int k = lane; k < F * QV; k += 64) {
+        const int f = k / QV, q = k - f * QV;
+        const int64_t row = hash_row(a.g_ids[b * F + f], a.g_base[f], a.g_bucket[f], a.g_hash);
+        const float4 v = reinterpret_cast<const float4*>(a.g_table + row * C::E)[q];
+        reinterpret_cast<float4*>(X)[k] = v;
+        xo[k] = v;
+        if (q == 0 && a.g_rows) a.g_rows[b * F + f] = (int32_t)row;
+      }
+    } else {
+      const float4* src = reinterpret_cast<const float4*>(x + b * F * C::E);
+      for (int k = lane; k < F * C::E / 4; k += 64) reinterpret_cast<float4*>(X)[k] = src[k];
+    }
     wave_lds_sync();
     for (int it = 0; it < a.L; ++it) {
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
@@ -1359,6 +1393,12 @@ template <class C, bool DROP>
 int fwd_launch(const FwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
   Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, false);
+  a.g_ids = q.gather_ids;
+  a.g_base = q.gather_base;
+  a.g_bucket = q.gather_bucket;
+  a.g_table = q.gather_table;
+  a.g_rows = q.gather_rows;
+  a.g_hash = q.gather_hash;
   const size_t per_wave = (size_t)a.per_wave * sizeof(float);
   int wpb = (int)(kLdsBytes / per_wave);
   if (wpb > kMaxFwdWaves) wpb = kMaxFwdWaves;

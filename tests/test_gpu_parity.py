@@ -225,6 +225,49 @@ def test_interacting_forward(case):
     assert_close(_np(y), ref, 2e-5, what=f"IL fwd {case}")
 
 
+@pytest.mark.parametrize("F", [26, 20])          # exact-F instantiation and a padded one (FMAX 32)
+@pytest.mark.parametrize("hash_mode", ["mod", "splitmix"])
+@pytest.mark.parametrize("id_bits", [20, 62])     # 32-bit remainder fast path and the 64-bit path
+def test_il_fwd_gather_matches_lookup_then_fwd(F, hash_mode, id_bits):
+    """rs_il_fwd_gather (lookup + concat fused into the IL forward) is bit-identical to
+    rs_embedding_lookup_fwd followed by rs_il_fwd: x0, hashed rows (== the oracle's), xsave, y."""
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    from recommendsystem_amd.embedding import EmbeddingFeatures, SparseAdam, SparseTable
+    from recommendsystem_amd.layers import InteractingLayer
+    B, E, U, H, L, vocab = 300, 16, 16, 2, 3, 997
+    rng = np.random.default_rng(41)
+    table = SparseTable(F * vocab, E, SparseAdam(), device=DEV, seed=5)
+    emb = EmbeddingFeatures(table, [vocab] * F, combiner="mean", hash_mode=hash_mode)
+    ids = rng.integers(0, 1 << id_bits, size=(B, F), dtype=np.int64)
+    idt = torch.from_numpy(ids).to(DEV)
+    il = InteractingLayer(L, U, H, use_res=True, seed=7, device=DEV)
+    il.build((B, F, E), device=DEV)
+    s = stream_handle()
+    args = (ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0)
+    x_a = torch.empty(B, F * E, device=DEV)
+    rows_a = torch.empty(B * F, device=DEV, dtype=torch.int32)
+    y_a, xs_a = torch.empty(B, F * U, device=DEV), torch.empty(L - 1, B, F, U, device=DEV)
+    call("rs_embedding_lookup_fwd", s, ptr(idt), None, B, F, ptr(emb.row_base), ptr(emb.bucket),
+         emb.hash_mode, emb.combiner, ptr(table.weight), table.rows, E, ptr(x_a), F * E, E,
+         ptr(rows_a))
+    call("rs_il_fwd", s, ptr(x_a), B, F, E, U, H, L, *args, ptr(y_a), F * U, ptr(xs_a))
+    x_b = torch.full((B, F * E), float("nan"), device=DEV)
+    rows_b = torch.full((B * F,), -7, device=DEV, dtype=torch.int32)
+    y_b, xs_b = torch.empty(B, F * U, device=DEV), torch.empty(L - 1, B, F, U, device=DEV)
+    call("rs_il_fwd_gather", s, ptr(idt), ptr(emb.row_base), ptr(emb.bucket), emb.hash_mode,
+         ptr(table.weight), table.rows, ptr(x_b), ptr(rows_b), B, F, E, U, H, L, *args,
+         ptr(y_b), F * U, ptr(xs_b))
+    torch.cuda.synchronize()
+    fields = np.tile(np.arange(F), B)
+    want_rows = npo.hash_rows(ids.reshape(-1), fields, emb.row_base.cpu().numpy(),
+                              emb.bucket.cpu().numpy(), hash_mode)
+    assert np.array_equal(rows_b.cpu().numpy().astype(np.int64), want_rows)
+    assert torch.equal(rows_a, rows_b)
+    assert torch.equal(x_a, x_b)
+    assert torch.equal(xs_a, xs_b)
+    assert torch.equal(y_a, y_b)
+
+
 @pytest.mark.parametrize("case", [c for c in IL_CASES if c[3] <= 32])
 def test_interacting_backward(case):
     from recommendsystem_amd.layers import InteractingLayer
