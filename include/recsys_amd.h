@@ -312,6 +312,17 @@ int rs_row_select(void* stream, const float* mask, const float* A, int64_t lda, 
 int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, int T, float lo, float hi,
                 float log_eps, const float* W, float gscale, float* loss_rows, float* dP);
 
+/* N1  staytime parse_input_func labels (staytime/parse.py:16-71) for a batch of B samples:
+ * label [B, ld] rows = nbins Gaussian soft-label bins (sigma, width = (right - left)/(nbins - 1))
+ * then the clipped watch time in seconds; short/long = watch_ms > 7000 / > 18000 (fp32 0/1);
+ * weight = 5 where landing[b] != 0 (the host's regex match of extra_info against
+ * ".*video_homepage_landing.*", parse.py:64), else 1.  landing, short_label, long_label and
+ * weight may be NULL.  Requires ld >= nbins + 1, nbins >= 2, sigma > 0. */
+int rs_staytime_labels(void* stream, const int64_t* watch_ms, const uint8_t* landing, int64_t B,
+                       const float* bins, int nbins, float sigma, float left, float right,
+                       float* label, int64_t ld, float* short_label, float* long_label,
+                       float* weight);
+
 /* Elementwise activation of a contiguous [n] tensor (tf.sigmoid of the rough_rank logits,
  * rough_rank/model.py:80,146): Y = act(X); backward dX = dY * act'(Y). */
 int rs_act_fwd(void* stream, const float* X, int64_t n, int act, float* Y);

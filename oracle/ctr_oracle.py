@@ -355,3 +355,36 @@ def din_softmax_pool(query, facts, mask, W1, b1, W2, b2, return_probs=False):
     if return_probs:
         return out, probs[:, 0, :]
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# N1  staytime parse_input_func labels (staytime/parse.py:16-71), fp32 in the TF graph's op order
+# ------------------------------------------------------------------------------------------
+STAYTIME_LANDING_RE = r".*video_homepage_landing.*"                       # parse.py:64
+
+
+def staytime_parse_labels(watch_ms, extra_info, bins, sigma=4, left=-19, right=180.5):
+    """watch_ms int64 [B], extra_info list of str [B], bins [nbins] (config.py:18 bin_list) ->
+    (staytime_label [B, nbins + 1] f32, short [B] f32, long [B] f32, sample_weight [B] f32).
+    Each step is one fp32 TF op, in order; the Python-float constants become fp32 tensors."""
+    import math
+    import re
+    f32 = np.float32
+    wt_i = np.asarray(watch_ms, dtype=np.int64)
+    short = np.where(wt_i > 7000, 1, 0).astype(f32)                      # :31-34
+    long_ = np.where(wt_i > 18000, 1, 0).astype(f32)                     # :37-38
+    wt = wt_i.astype(f32)                                                 # :40
+    wt = np.divide(wt, f32(1000.0))                                       # :41
+    wt = np.where(wt > f32(160.0), f32(160.0), wt).astype(f32)            # :42
+    b = np.asarray(bins, dtype=f32)[None, :]                              # :45-46
+    dist = np.subtract(b, wt[:, None])                                    # :48-52
+    sq = np.square(np.abs(dist))                                          # :53
+    nb = b.shape[1]
+    width = (right - left) / (nb - 1)                                     # :55-57
+    div_num = f32(math.sqrt(2 * math.pi) * sigma)                         # :59
+    label = np.divide(np.exp(np.divide(sq, f32(-2 * math.pow(sigma, 2)))), div_num)  # :60
+    label = np.multiply(label, f32(width))                                # :61
+    stay = np.concatenate([label, wt[:, None]], -1).astype(f32)           # :62
+    pat = re.compile(STAYTIME_LANDING_RE)
+    sw = np.array([5.0 if pat.fullmatch(s) else 1.0 for s in extra_info], dtype=f32)  # :64
+    return stay, short, long_, sw

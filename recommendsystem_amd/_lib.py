@@ -96,6 +96,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_act_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "rs_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "rs_bce_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _f32, _vp, _vp]),
+    "rs_staytime_labels": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _f32, _vp, _i64,
+                                  _vp, _vp, _vp]),
     "rs_mlp_head_param_floats": (_i64, [_i32, _i32, _i32, _i32, _i32]),
     "rs_mlp_head_workspace_floats": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32]),
     "rs_mlp_head_partial_blocks": (_i32, [_i64]),

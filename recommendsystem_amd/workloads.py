@@ -26,6 +26,7 @@ from .embedding import (EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, Spa
 from .layers import Dense
 from .models import (DSSM, STAYTIME_BINS, DSSMConfig, MultiHeadConfig, MultiHeadRanker,
                      StaytimeConfig, StaytimeMTL)
+from .parse import staytime_labels as device_staytime_labels
 from .towers import cross_entropy_sum
 
 
@@ -159,8 +160,10 @@ def staytime_batch(rng, B, model: StaytimeRoughRank, device, id_space=1 << 40):
         seq_ids.append(t(zipf_ids(rng, (int(offs[-1]),), id_space, 1.2)))
         seq_offs.append(t(offs))
     rr_ids = zipf_ids(rng, (B, rr.user_fields + rr.item_fields), id_space, 1.2)
-    stay, short, long_, sw = staytime_labels(rng, B)
+    # labels built on the device from raw watch times (parse_input_func, staytime/parse.py:30-64)
+    wt_ms = np.exp(rng.normal(9.5, 1.0, size=B)).astype(np.int64)
+    landing = (rng.uniform(size=B) < 0.1).astype(np.uint8)
+    stay, short, long_, sw = device_staytime_labels(t(wt_ms), t(landing))
     click = (rng.uniform(size=(B, 1)) < 0.1).astype(np.float32)
     mask = (rng.uniform(size=(B, 1)) < 0.5).astype(np.float32)
-    return (t(st_ids), seq_ids, seq_offs, t(rr_ids), t(stay), t(short), t(long_), t(sw), t(click),
-            t(mask))
+    return (t(st_ids), seq_ids, seq_offs, t(rr_ids), stay, short, long_, sw, t(click), t(mask))
