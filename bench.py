@@ -172,9 +172,32 @@ def run_workload(args, world, rank, dev, pg):
         print(json.dumps(out), flush=True)
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N fresh rank processes through
+    torch.distributed.run and return its exit code.  The parent never touches the GPU (no HIP
+    call before the children exist), so every rank initialises its own device cleanly."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per "
+                         "GPU (torch.distributed.run --nproc-per-node N) or let bench.py do it")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())  # (rehearsal: several ranks per GPU)
@@ -189,6 +212,10 @@ def main():
         else:
             dist.init_process_group(args.backend)
         pg = dist.group.WORLD
+        if rank == 0:
+            print(f"[bench] {dist.get_backend(pg)} world size {dist.get_world_size(pg)}",
+                  file=sys.stderr, flush=True)
+        assert dist.get_world_size(pg) == args.gpus
 
     from recommendsystem_amd import _lib
     from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer

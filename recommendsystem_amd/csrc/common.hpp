@@ -32,6 +32,47 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LDS-only workgroup barrier: makes every wave's earlier LDS writes visible to the block and
+// waits only for the wave's own LDS traffic (lgkmcnt).  __syncthreads()'s fence also drains vmcnt,
+// i.e. it stalls each wave at every phase boundary until its outstanding global loads, stores and
+// atomics (prefetches, a fused push) have completed.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// wait for this wave's outstanding vector-memory operations (global loads incl. the async
+// global->LDS copies below, stores, atomics); follow with lds_barrier() to publish LDS-DMA data
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Asynchronous copy of n4 float4 from global `src` to LDS `dst` by the whole block
+// (global_load_lds_dwordx4: no VGPR round trip; each wave instruction writes 64 consecutive
+// 16-B slots from the wave-uniform base in M0).  Complete after vm_wait_all() + lds_barrier().
+// Issued from inline asm ON PURPOSE: through __builtin_amdgcn_global_load_lds the compiler
+// cannot tell the DMA's LDS bytes from the kernel's other LDS data (one dynamic array) and puts
+// an s_waitcnt vmcnt(0) in front of the next LDS read -- the prefetch would complete
+// synchronously.  The compiler does not see these loads at all, so every vmcnt wait it emits
+// for its own global loads is still correct (in-order return: it may only wait longer).
+__device__ __forceinline__ void glds_copy(float* dst, const float* src, int n4) {
+  for (int k = threadIdx.x; k < n4; k += blockDim.x) {
+    const int wbase = k - (int)(threadIdx.x & 63);  // wave-uniform
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(dst + 4 * wbase));  // generic -> LDS offset (low 32 bits)
+    const float* g = src + 4 * k;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds)
+        : "memory");
+  }
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // readfirstlane: the wave index is uniform, and saying so lets `if (wave_id() == k)` compile to a
 // scalar branch instead of exec-mask save/restore around every guarded instruction

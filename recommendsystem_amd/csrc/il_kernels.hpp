@@ -142,6 +142,8 @@ struct Args {
   uint64_t seed;
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
   int l_tmp;                   // bwd2 only: partial-row exchange / dV buffer
+  int l_x2, l_w, l_b;          // bwd2 only: second X buffer (prefetch), W and bias in LDS
+  int dy_vec;                  // bwd2 only: dy rows 16-B aligned (async LDS copy)
   unsigned long long* stamps;  // diagnostic build only
   const int32_t* push_rows;    // fused sparse push (see BwdReq)
   float* push_table;
@@ -183,6 +185,8 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   }
   a.per_wave = off;
   a.l_tmp = 0;
+  a.l_x2 = a.l_w = a.l_b = 0;
+  a.dy_vec = 0;
 #ifdef RS_IL_STAMPS
   extern unsigned long long* g_il_stamps;
   a.stamps = g_il_stamps;
@@ -199,14 +203,18 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   return a;
 }
 
-// bwd2 carve-up (one block = one sample at a time, two waves): no separate gradient region (the
-// projection gradients overwrite Q/K/V/R in place once each is dead), a TMP region for partial
-// rows / dV, and ST holding [m0 | m1 | l0 | l1] (forward recompute) then the D partials.
+// bwd2 carve-up (one block = one sample at a time, two waves): W and bias resident for the whole
+// kernel, two X buffers, no separate gradient region (the projection gradients overwrite Q/K/V/R
+// in place once each is dead), a TMP region for partial rows / dV, and ST holding
+// [m0 | m1 | l0 | l1] (forward recompute) then the D partials.
 template <class C>
 Args make_args2(int64_t B, int F, int L, int use_res, float eps, float drop_rate, uint64_t seed) {
   Args a = make_args<C>(B, F, L, use_res, eps, drop_rate, seed, false);
   int off = 0;
-  a.l_x = off; off += r4(F * C::E);
+  a.l_w = off; off += r4(C::E * C::WPS);        // W [E][NC] (row stride WPS), block-resident
+  a.l_b = off; off += r4(C::NC);                // bias
+  a.l_x = off; off += r4(F * C::E);             // X, double-buffered: the next iteration's
+  a.l_x2 = off; off += r4(F * C::E);            // input streams in while this one runs
   a.l_pr = off; off += r4(C::FMAX * C::PRS);
   a.l_o = off; off += r4(F * C::OS);
   a.l_dy = off; off += r4(F * C::U);
@@ -316,6 +324,34 @@ struct MfmaW {
           wp[ks][t][nt] = k < C::E ? W[k * C::NC + 16 * nt + j] : 0.f;
         }
   }
+  // the same fragments from a block-resident LDS copy of W ([E][NC], row stride C::WPS) and bias
+  __device__ __forceinline__ void load_proj_lds(const float* WL, const float* BL) {
+    const int q = lane_id() >> 4, j = lane_id() & 15;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bp[nt] = BL[16 * nt + j];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int k = 16 * ks + 4 * q + t;
+          wp[ks][t][nt] = k < C::E ? WL[k * C::WPS + 16 * nt + j] : 0.f;
+        }
+  }
+  __device__ __forceinline__ void load_dx_lds(const float* WL) {
+    const int q = lane_id() >> 4, j = lane_id() & 15;
+#pragma unroll
+    for (int cs = 0; cs < CS; ++cs)
+#pragma unroll
+      for (int et = 0; et < ET; ++et) {
+        const int e = 16 * et + j;
+        // the 4 t-values are consecutive columns: one ds_read_b128
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < C::E) v = *reinterpret_cast<const float4*>(WL + e * C::WPS + 16 * cs + 4 * q);
+        wx[cs][0][et] = v.x; wx[cs][1][et] = v.y; wx[cs][2][et] = v.z; wx[cs][3][et] = v.w;
+      }
+  }
   // dx B operand only
   __device__ __forceinline__ void load_dx(const float* __restrict__ W) {
     const int q = lane_id() >> 4, j = lane_id() & 15;
@@ -400,11 +436,21 @@ __device__ __forceinline__ void mfma_dw(const float* X, const float* G, int F, i
 }
 
 // dx[f][e] = sum_c G[f][c] W[e][c] for row tile rt; writes rows < F to out[f * ld + e]
+// (accumulate: adds to out's contents, whose loads are issued before the MFMAs so that one
+// memory round trip overlaps them instead of one per row)
 template <class C>
 __device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const MfmaW<C>& w,
                                         float* out, int ld, bool accumulate) {
   using M = MfmaW<C>;
   const int q = lane_id() >> 4, j = lane_id() & 15;
+  float prev[M::ET][4];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * rt + 4 * q + r, e = 16 * et + j;
+      prev[et][r] = (accumulate && f < F && e < C::E) ? out[f * ld + e] : 0.f;
+    }
   f32x4 acc[M::ET];
 #pragma unroll
   for (int et = 0; et < M::ET; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -427,10 +473,7 @@ __device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const Mfm
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 16 * rt + 4 * q + r;
-      if (f < F && e < C::E) {
-        float* d = out + f * ld + e;
-        *d = accumulate ? (*d + acc[et][r]) : acc[et][r];
-      }
+      if (f < F && e < C::E) out[f * ld + e] = acc[et][r] + prev[et][r];
     }
   }
 }
@@ -438,13 +481,26 @@ __device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const Mfm
 // dx of row tile rt as in mfma_dx, but pushed into the sparse gradient table: for each row f,
 // grad_table[rows[f]][e] += dx[f][e] (+ base[f * E + e] when base != NULL: the deep tower's share
 // of dL/dx0 written earlier) with float atomics, and flag[rows[f]] = -2 (scan-mode mark).
-// This replaces the store of dx0 and the separate push kernel that re-read it.
+// This replaces the store of dx0 and the separate push kernel that re-read it.  The row indices
+// and base values are loaded before the MFMAs (one overlapped round trip, not two per row).
 template <class C>
 __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, const MfmaW<C>& w,
                                              const float* base, const int32_t* rows,
                                              float* table, int32_t* flag) {
   using M = MfmaW<C>;
   const int q = lane_id() >> 4, j = lane_id() & 15;
+  int32_t rw[4];
+  float bv[M::ET][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int f = 16 * rt + 4 * q + r;
+    rw[r] = f < F ? rows[f] : -1;
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et) {
+      const int e = 16 * et + j;
+      bv[et][r] = (base && f < F && e < C::E) ? base[f * C::E + e] : 0.f;
+    }
+  }
   f32x4 acc[M::ET];
 #pragma unroll
   for (int et = 0; et < M::ET; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -463,21 +519,14 @@ __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, cons
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int f = 16 * rt + 4 * q + r;
-    if (f < F) {
-      const int32_t row = rows[f];
-      if (row >= 0) {
-        if (j == 0) scan_mark(flag, row);
-        float* dst = table + (int64_t)row * C::E;
+    const int32_t row = rw[r];
+    if (row >= 0) {  // f >= F and rows < 0 (invalid ids) push nothing
+      if (j == 0) scan_mark(flag, row);
+      float* dst = table + (int64_t)row * C::E;
 #pragma unroll
-        for (int et = 0; et < M::ET; ++et) {
-          const int e = 16 * et + j;
-          if (e < C::E) {
-            float v = acc[et][r];
-            if (base) v += base[f * C::E + e];
-            atomicAdd(dst + e, v);
-          }
-        }
+      for (int et = 0; et < M::ET; ++et) {
+        const int e = 16 * et + j;
+        if (e < C::E) atomicAdd(dst + e, acc[et][r] + bv[et][r]);
       }
     }
   }
@@ -1024,7 +1073,10 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int JH = (C::FMAX + 1) / 2;  // keys (or queries) per wave in the split passes
-  float* X = smem + a.l_x;
+  float* const X0 = smem + a.l_x;
+  float* const X1 = smem + a.l_x2;
+  float* const WL = smem + a.l_w;
+  float* const BL = smem + a.l_b;
   float* PR = smem + a.l_pr;
   float* O = smem + a.l_o;
   float* DY = smem + a.l_dy;
@@ -1038,7 +1090,26 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
   const int j0 = w * JH;
 
   for (int k = F * C::PRS + threadIdx.x; k < C::FMAX * C::PRS; k += blockDim.x) PR[k] = 0.f;
-  __syncthreads();
+  // W and bias stay in LDS for the whole kernel (the MFMA fragments are re-read per phase from
+  // there instead of from L1/L2: a global round trip at the head of two phases per iteration)
+  for (int k = threadIdx.x; k < C::E * C::NC; k += blockDim.x)
+    WL[(k / C::NC) * C::WPS + k % C::NC] = W[k];
+  for (int k = threadIdx.x; k < C::NC; k += blockDim.x) BL[k] = bias[k];
+  // iteration inputs stream in asynchronously one iteration ahead (X double buffer; dy of the
+  // next sample during the last iteration's dW/dx phase)
+  auto x_src = [&](int64_t bb, int itx) -> const float* {
+    return itx == 0 ? x + bb * F * C::E : xsave + ((int64_t)(itx - 1) * a.B + bb) * F * C::U;
+  };
+  auto load_dy = [&](int64_t bb) {
+    const float* src = dy + bb * dy_ld;
+    if (a.dy_vec) glds_copy(DY, src, F * C::U / 4);
+    else for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
+  };
+  if ((int64_t)blockIdx.x < a.B) {
+    glds_copy(X0, x_src(blockIdx.x, a.L - 1), F * C::E / 4);
+    load_dy(blockIdx.x);
+  }
+  int par = 0;
 
   using M = MfmaW<C>;
   f32x4 dwacc[M::ET][M::NT];
@@ -1049,40 +1120,36 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
     for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
-  float dg[C::CPLN], dbt[C::CPLN];
+  float dg[C::CPLN], dbt[C::CPLN], gam[C::CPLN];
   const int u0 = lane % C::LPR;
 #pragma unroll
-  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; }
+  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
   const int nrt = (F + 15) / 16;
 
+  IL_STAMP_DECL
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    {
-      const float* src = dy + b * dy_ld;
-      for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
-    }
     for (int it = a.L - 1; it >= 0; --it) {
+      IL_STAMP(0)
       const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
-      {
-        const float* xin = (it == 0) ? (x + b * F * C::E)
-                                     : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
-        const float4* src = reinterpret_cast<const float4*>(xin);
-        for (int k = threadIdx.x; k < F * C::E / 4; k += blockDim.x)
-          reinterpret_cast<float4*>(X)[k] = src[k];
+      float* const X = par ? X1 : X0;
+      vm_wait_all();  // this wave's share of X (and of dy at it == L-1) has landed
+      lds_barrier();
+      {  // prefetch the next iteration's input into the other buffer
+        const int64_t bn = it > 0 ? b : b + gridDim.x;
+        if (bn < a.B) glds_copy(par ? X0 : X1, x_src(bn, it > 0 ? it - 1 : a.L - 1), F * C::E / 4);
       }
-      __syncthreads();
+      IL_STAMP(1)
       // ---- P1: projections (row tiles split between the waves) ----
       {
         // launder W / bias so the fragment loads are NOT hoisted out of the sample loop (they
         // would then stay live in 36 VGPRs across every phase): reloading them costs a few
         // L1 hits per iteration, keeping them costs two waves per SIMD
-        const float* Wl = W;
-        const float* bl = bias;
-        asm volatile("" : "+s"(Wl), "+s"(bl));
         MfmaW<C> mw;
-        mw.load_proj(Wl, bl);
+        mw.load_proj_lds(WL, BL);
         for (int rt = w; rt < nrt; rt += 2) mfma_project<C>(X, PR, F, rt, mw);
       }
-      __syncthreads();
+      lds_barrier();
+      IL_STAMP(2)
       // ---- P2: attention recompute, keys split; m / l through ST, wave 1's o through TMP ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -1101,7 +1168,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
           mx = fmaxf(mx, s[jj]);
         }
         if (act) ST[w * HF + r] = mx;
-        __syncthreads();
+        lds_barrier();
         const float m = act ? fmaxf(ST[r], ST[HF + r]) : 0.f;
         float l = 0.f;
         float o[C::DH];
@@ -1124,7 +1191,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
             for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = o[d];
           }
         }
-        __syncthreads();
+        lds_barrier();
         if (act) {
           const float inv = 1.0f / (ST[2 * HF + r] + ST[3 * HF + r]);
           float* pm_row = PM + (h * F + i) * C::PMS;
@@ -1138,14 +1205,12 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
             store_row(O + i * C::OS + h * C::DH, ov);
           }
         }
-        __syncthreads();
+        lds_barrier();
       }
+      IL_STAMP(3)
       // ---- P3: z = relu(O + R), LN stats, LN + ReLU backward (rows split):
       //      O <- dt; R <- gR = dt * (R > 0) (R dies here) ----
       {
-        float gam[C::CPLN];
-#pragma unroll
-        for (int c = 0; c < C::CPLN; ++c) gam[c] = gamma[u0 + c * C::LPR];
         for (int f0 = w * C::RG; f0 < F; f0 += 2 * C::RG) {
           const int f = f0 + lane / C::LPR;
           const bool act = f < F;
@@ -1194,7 +1259,8 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
+      IL_STAMP(4)
       // ---- P4: dV_j = sum_i Pd_ij dO_i (lane = (h, j); queries split) -> DY[j][h dh + d] ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -1216,14 +1282,15 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
 #pragma unroll
           for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dv[d];
         }
-        __syncthreads();
+        lds_barrier();
         if (act && w == 0) {
 #pragma unroll
           for (int d = 0; d < C::DH; ++d) dv[d] += TMP[d * HF + r];
           store_row(DY + j * C::U + h * C::DH, dv);
         }
-        __syncthreads();
+        lds_barrier();
       }
+      IL_STAMP(5)
       // ---- P5: dS (in place of P) and dQ (lane = (h, i); keys split) -> O (dO dies here) ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
         const int r = r0 + lane;
@@ -1246,7 +1313,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
           s[jj] = dp;
         }
         if (act) ST[w * HF + r] = Dw;
-        __syncthreads();
+        lds_barrier();
         const float D = act ? ST[r] + ST[HF + r] : 0.f;
         float dq[C::DH];
 #pragma unroll
@@ -1264,14 +1331,15 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
 #pragma unroll
           for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dq[d];
         }
-        __syncthreads();
+        lds_barrier();
         if (act && w == 0) {
 #pragma unroll
           for (int d = 0; d < C::DH; ++d) dq[d] += TMP[d * HF + r];
           store_row(O + i * C::OS + h * C::DH, dq);
         }
-        __syncthreads();
+        lds_barrier();
       }
+      IL_STAMP(6)
       // ---- P6: dK_j = sum_i dS_ij Q_i (lane = (h, j); queries split); then K <- gK (wave 0),
       //      V <- gV from DY and Q <- gQ from O (wave 1) ----
       for (int r0 = 0; r0 < HF; r0 += 64) {
@@ -1291,7 +1359,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
 #pragma unroll
           for (int d = 0; d < C::DH; ++d) TMP[d * HF + r] = dk[d];
         }
-        __syncthreads();
+        lds_barrier();
         if (act && w == 0) {
           float kr[C::DH], pt[C::DH];
           load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
@@ -1312,16 +1380,15 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
             *qq = q0 > 0.f ? gq : 0.f;
           }
         }
-        __syncthreads();
+        lds_barrier();
       }
+      IL_STAMP(7)
       // ---- P7: dW += X^T G, db += colsum G; dx = G W^T (row tiles split; MFMA) ----
       for (int rt = w; rt < nrt; rt += 2) mfma_dw<C>(X, PR, F, rt, dwacc, dbp);
       __builtin_amdgcn_sched_barrier(0);  // keep the dx pass's loads out of the dW pass
       {
-        const float* Wl = W;
-        asm volatile("" : "+s"(Wl));
         MfmaW<C> mw;
-        mw.load_dx(Wl);
+        mw.load_dx_lds(WL);
         for (int rt = w; rt < nrt; rt += 2) {
           if (it > 0) mfma_dx<C>(PR, F, rt, mw, DY, C::U, false);  // dL/d(previous output)
           else if (a.push_table)
@@ -1330,9 +1397,16 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
           else mfma_dx<C>(PR, F, rt, mw, dx + b * F * C::E, C::E, dx_accumulate != 0);
         }
       }
-      __syncthreads();
+      // the next sample's dy (DY is dead after P6 at it == 0); issued after the push's own
+      // loads so that their waits do not also wait for this copy
+      if (it == 0 && b + gridDim.x < a.B) load_dy(b + gridDim.x);
+      lds_barrier();
+      IL_STAMP(8)
+      par ^= 1;
     }
   }
+  vm_wait_all();
+  IL_STAMP_FLUSH(a.stamps)
 
   // ---- lanes -> wave -> block (wave order), as bwd_kernel ----
 #pragma unroll
@@ -1419,8 +1493,11 @@ int bwd_launch(const BwdReq& q) {
   a.push_rows = q.push_rows;
   a.push_table = q.push_table;
   a.push_flag = q.push_flag;
+  a.dy_vec = (q.dy_ld % 4 == 0) && ((uintptr_t)q.dy % 16 == 0);
   const size_t lds = (size_t)a.per_wave * sizeof(float);
   if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
+  // x / xsave rows are copied to LDS 16 B at a time
+  if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
   // kMaxBwdGrid = one resident round of this kernel on MI355X (6 blocks per CU x 256 CUs at
   // config 2), so no block waits for a second round while others idle.  A fixed rule (not an
   // occupancy query) because callers size the partial-row reduction with

@@ -66,16 +66,25 @@ RS_API int rs_dense_adam(void* stream, float* params, float* grads, float* m, fl
 // n_touched = int32[1 + RS_DONE_WORDS]: {count, completion counters}.  Every block of a sparse
 // optimizer launch reads count first; the last block to finish resets it (rs_last_block), so the
 // next step's accumulate starts from zero without a separate memset launch.
-__device__ __forceinline__ void release_touched_count(int32_t* n_touched) {
-  if (rs_last_block(n_touched + 1)) atomicExch(n_touched, 0);
+// A push that claimed more rows than the touched list holds (count > cap) is an overflow: the
+// optimizer updates only the first cap rows, and the last block records the count in the sticky
+// word n_touched[RS_TOUCHED_OVERFLOW] (SparseTable.check_overflow raises on it).
+#define RS_TOUCHED_OVERFLOW RS_DONE_WORDS
+__device__ __forceinline__ void release_touched_count(int32_t* n_touched, int32_t count,
+                                                      int32_t cap) {
+  if (rs_last_block(n_touched + 1)) {
+    if (count > cap) atomicMax(n_touched + RS_TOUCHED_OVERFLOW, count);
+    atomicExch(n_touched, 0);
+  }
 }
 
 __global__ void __launch_bounds__(256) sparse_adam_kernel(
     float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ grad_table, int32_t* __restrict__ flag,
     const int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int dim,
-    int lps, float lr, float b1, float b2, float eps, float grad_scale) {
-  const int nrows = *n_touched;
+    int32_t cap, int lps, float lr, float b1, float b2, float eps, float grad_scale) {
+  const int count = *n_touched;
+  const int nrows = min(count, cap);
   const int per_block = blockDim.x / lps;
   const int gi = threadIdx.x / lps;
   const int l = threadIdx.x % lps;
@@ -93,14 +102,15 @@ __global__ void __launch_bounds__(256) sparse_adam_kernel(
     }
     if (l == 0) flag[row] = -1;
   }
-  release_touched_count(n_touched);
+  release_touched_count(n_touched, count, cap);
 }
 
 __global__ void __launch_bounds__(256) sparse_adagrad_kernel(
     float* __restrict__ table, float* __restrict__ g2sum, float* __restrict__ grad_table,
     int32_t* __restrict__ flag, const int32_t* __restrict__ touched,
-    int32_t* __restrict__ n_touched, int dim, int lps, float lr, float grad_scale) {
-  const int nrows = *n_touched;
+    int32_t* __restrict__ n_touched, int dim, int32_t cap, int lps, float lr, float grad_scale) {
+  const int count = *n_touched;
+  const int nrows = min(count, cap);
   const int per_block = blockDim.x / lps;
   const int gi = threadIdx.x / lps;
   const int l = threadIdx.x % lps;
@@ -116,7 +126,7 @@ __global__ void __launch_bounds__(256) sparse_adagrad_kernel(
     }
     if (l == 0) flag[row] = -1;
   }
-  release_touched_count(n_touched);
+  release_touched_count(n_touched, count, cap);
 }
 
 static int lanes_for_dim(int dim) {
@@ -137,7 +147,7 @@ RS_API int rs_sparse_adam(void* stream, float* table, float* m, float* v, float*
     int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
     if (grid > 1024) grid = 1024;
     sparse_adam_kernel<<<(int)grid, 256, 0, s>>>(table, m, v, grad_table, flag, touched,
-                                                 n_touched, dim, lps, lr, beta1, beta2, eps,
+                                                 n_touched, dim, max_rows, lps, lr, beta1, beta2, eps,
                                                  grad_scale);
   }
   else
@@ -156,7 +166,7 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
     int64_t grid = ((int64_t)max_rows * lps + 255) / 256;
     if (grid > 1024) grid = 1024;
     sparse_adagrad_kernel<<<(int)grid, 256, 0, s>>>(table, g2sum, grad_table, flag, touched,
-                                                    n_touched, dim, lps, lr, grad_scale);
+                                                    n_touched, dim, max_rows, lps, lr, grad_scale);
   }
   else
     (void)hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);

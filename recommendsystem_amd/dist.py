@@ -46,12 +46,19 @@ def gather_sparse_lists(rows: torch.Tensor, grads: torch.Tensor, count: torch.Te
 
 def _all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     """out[r * inp.numel():(r + 1) * inp.numel()] = rank r's inp (one contiguous receive buffer).
-    RCCL moves it with one all-gather; backends without the flat form get per-rank views."""
-    try:
+    RCCL ('nccl') moves it with one all_gather_into_tensor; gloo gets per-rank views.  The path
+    is chosen by backend, never by catching a failure (a failed collective on one rank must not
+    turn into a different collective on it while the others wait in the first)."""
+    if uses_flat_all_gather(group):
         dist.all_gather_into_tensor(out, inp, group=group)
-    except (RuntimeError, NotImplementedError):
+    else:
         world = dist.get_world_size(group)
         dist.all_gather(list(out.view(world, -1).unbind(0)), inp, group=group)
+
+
+def uses_flat_all_gather(group=None) -> bool:
+    """True for RCCL ('nccl' on ROCm), the backend with a flat all_gather_into_tensor."""
+    return dist.get_backend(group) == "nccl"
 
 
 def exchange_packed(send: torch.Tensor, recv: torch.Tensor, n_dense: int, recs: torch.Tensor,
