@@ -174,6 +174,8 @@ class AutoIntTrainer:
         self.il_dparams = ar.grad[self._offset(il.kernel):self._offset(il.kernel) +
                                   il.kernel.numel() + il.bias.numel() + il.gamma.numel() + il.beta.numel()]
         self.graph = None
+        self.graph_opt = None
+        self.pool_graphs = []
         self.head = self._plan_head()
         # fused path: the IL backward pushes dL/dx0 straight into the table (scan-mode marks)
         self.push = self.head is not None and self.F <= 64
@@ -453,70 +455,103 @@ class AutoIntTrainer:
         self.ids.copy_(ids, non_blocking=True)
         self.labels.copy_(labels.reshape(self.B, self.T), non_blocking=True)
 
-    def capture(self, warmup: int = 2) -> None:
-        """Capture the single-GPU step into a HIP graph (N > 1 keeps collectives eager and
-        captures the compute-only halves)."""
-        if warmup > 0:
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(warmup):
-                    self._step_eager()
-            torch.cuda.current_stream().wait_stream(side)
-        if self.world == 1:
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+    def _state(self):
+        """Every tensor a training step mutates (dense arena + Adam moments + step counter, the
+        table with its optimizer slots, gradient rows, flags and counters, the loss)."""
+        m, t = self.model, self.model.table
+        out = [m.arena.data, m.arena.grad, self.adam_m, self.adam_v, self.step_count, self.loss,
+               t.weight, t.grad, t.flag, t.n_touched, t.touched]
+        out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]
+        if self.head is not None:
+            out.append(self.head["done"])
+        return out
+
+    def _warmup(self, steps: int) -> None:
+        """Run `steps` eager steps on a side stream (first-launch initialisation before a capture)
+        and then restore the training state: warm-up leaves parameters, optimizer state and the
+        table exactly as they were."""
+        if steps <= 0:
+            return
+        saved = [t.clone() for t in self._state()]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(steps):
                 self._step_eager()
-        else:
-            self.graph_fb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_fb):
+        torch.cuda.current_stream().wait_stream(side)
+        for t, s in zip(self._state(), saved):
+            t.copy_(s)
+        torch.cuda.synchronize()
+
+    def _record(self):
+        """Record the step over the CURRENT self.ids / self.labels: one graph for the whole step
+        (N = 1), or the forward/backward half only (N > 1: the collectives stay eager and the
+        optimizer half is recorded once by _record_opt)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            if self.world == 1:
+                self._step_eager()
+            else:
                 self._forward_backward()
+        return g
+
+    def _record_opt(self):
+        if getattr(self, "graph_opt", None) is None:
             self.graph_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_opt):
                 self._optimize()
+
+    def capture(self, warmup: int = 2) -> None:
+        """Capture the step over the trainer's own static ids / labels buffers (``step()``
+        replays it).  ``warmup`` eager steps run first and are rolled back (see _warmup)."""
+        self._warmup(warmup)
+        if self.world == 1:
+            self.graph = self._record()
+        else:
+            self.graph_fb = self._record()
+            self._record_opt()
             self.graph = True
 
     def capture_pool(self, batches, warmup: int = 2) -> None:
         """One graph per device-resident batch [(ids, labels), ...]: each graph's lookup and loss
         read that batch's own buffers, so replaying batch i needs no copy into a static input
         (what a double-buffered loader hands over).  ``step_pool(i)`` replays batch i.
+        Data parallel (N > 1): one forward/backward graph per batch plus ONE optimizer graph
+        (it does not depend on the batch), the exchange between them eager.
 
-        Data parallel (world > 1): ONE forward/backward graph over the static input buffers, and
-        step_pool(i) copies batch i into them (0.85 MB device-to-device at config 2).  A second
-        forward/backward graph captured after the first pair (graph_fb, graph_opt) faulted on
-        its first replay in the 2-rank rehearsal (bench.py --backend gloo, pool of 8), while one
-        graph replayed many times is the configuration tests/test_gpu_dp.py pins."""
+        Every graph object is kept for the trainer's lifetime (self.pool_graphs; a graph owns a
+        private memory pool).  Round 1's version re-ran capture() per batch, which replaced
+        graph_opt each time and dropped the earlier ones while the forward/backward graphs
+        recorded beside them stayed in use; that configuration faulted on its first replay in a
+        2-rank rehearsal and was replaced by a single graph.  tests/test_gpu_dp.py replays
+        several pairs of this layout alternately.  The trainer's own static buffers and its
+        step() graph are untouched: step(ids, labels) still copies into them."""
+        self.pool_batches = []
         for ids, labels in batches:
             if ids.shape != (self.B, self.F) or ids.dtype != torch.int64 or not ids.is_contiguous():
                 raise ValueError("pool ids must be contiguous int64 [B, F]")
-        if self.world > 1:
-            self.pool_batches = [(ids, labels.reshape(self.B, self.T).float().contiguous())
-                                 for ids, labels in batches]
-            self.load_batch(*self.pool_batches[0])
-            self.graph = None
-            self.capture(warmup=warmup)
-            self.pool_graphs = [(self.graph, self.graph_fb)]
-            return
+            self.pool_batches.append((ids, labels.reshape(self.B, self.T).float().contiguous()))
+        own = (self.ids, self.labels)
+        self._warmup(warmup)
         self.pool_graphs = []
-        for k, (ids, labels) in enumerate(batches):
-            self.ids = ids
-            self.labels = labels.reshape(self.B, self.T).float().contiguous()
-            self.graph = None
-            self.capture(warmup=warmup if k == 0 else 0)
-            self.pool_graphs.append((self.graph, getattr(self, "graph_fb", None)))
+        try:
+            for ids, labels in self.pool_batches:
+                self.ids, self.labels = ids, labels
+                self.pool_graphs.append(self._record())
+        finally:
+            self.ids, self.labels = own
+        if self.world > 1:
+            self._record_opt()
 
     def step_pool(self, i: int) -> torch.Tensor:
-        if self.world == 1:
-            g, _ = self.pool_graphs[i % len(self.pool_graphs)]
-            g.replay()
-            return self.loss
-        self.load_batch(*self.pool_batches[i % len(self.pool_batches)])
-        self.graph_fb.replay()
-        _lib.trace_point("graph_fb")
-        self._exchange()
-        _lib.trace_point("exchange")
-        self.graph_opt.replay()
-        _lib.trace_point("graph_opt")
+        g = self.pool_graphs[i % len(self.pool_graphs)]
+        g.replay()
+        if self.world > 1:
+            _lib.trace_point("graph_fb")
+            self._exchange()
+            _lib.trace_point("exchange")
+            self.graph_opt.replay()
+            _lib.trace_point("graph_opt")
         return self.loss
 
     def step(self, ids: torch.Tensor | None = None, labels: torch.Tensor | None = None) -> torch.Tensor:

@@ -109,6 +109,27 @@ __device__ __forceinline__ float group_max(float v) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fill n 32-bit words with `value` as a kernel node.  Used instead of hipMemsetAsync on every
+// path that callers capture into HIP graphs: a captured memset becomes a runtime-managed memset
+// node, and the data-parallel AutoInt pool (several captured graphs replayed back to back)
+// faulted only while such nodes were in its graphs.
+// ---------------------------------------------------------------------------------------------
+namespace {  // one copy per translation unit
+__global__ void __launch_bounds__(256) rs_fill_u32_kernel(uint32_t* __restrict__ p, uint32_t value,
+                                                         int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    p[i] = value;
+}
+
+static inline void rs_fill_u32(hipStream_t s, void* p, uint32_t value, int64_t n) {
+  if (n <= 0) return;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  rs_fill_u32_kernel<<<(unsigned)grid, 256, 0, s>>>(reinterpret_cast<uint32_t*>(p), value, n);
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
 // Counter-based dropout mask (shared bit-for-bit with oracle/ctr_oracle.py::dropout_keep).
 // TF's stateful RNG cannot be reproduced, so the framework pins its own.  For the 64-bit layer
 // seed s (splitmix64(seed + iteration)) and sample b, a per-sample key

@@ -318,8 +318,8 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
   hipStream_t s = rs_stream(stream);
   if (M == 0) {
     if (!accumulate) {
-      (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)K * N, s);
-      (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)N, s);
+      rs_fill_u32(s, dW, 0u, (int64_t)K * N);
+      rs_fill_u32(s, db, 0u, N);
     }
     return rs_status_after_launch();
   }

@@ -37,8 +37,8 @@ template <int G>
 __global__ void __launch_bounds__(256) embed_lookup_fwd_kernel(
     const int64_t* __restrict__ ids, const int32_t* __restrict__ offsets, int64_t nseg, int F,
     const int64_t* __restrict__ row_base, const int64_t* __restrict__ bucket, int hash_mode,
-    int combiner, const float* __restrict__ table, int dim, float* __restrict__ out,
-    int64_t out_ld, int64_t out_fstride, int32_t* __restrict__ rows_out) {
+    int combiner, const float* __restrict__ table, int64_t table_rows, int dim,
+    float* __restrict__ out, int64_t out_ld, int64_t out_fstride, int32_t* __restrict__ rows_out) {
   const int groups_per_block = blockDim.x / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
@@ -65,8 +65,11 @@ __global__ void __launch_bounds__(256) embed_lookup_fwd_kernel(
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int64_t k = beg; k < end; ++k) {
         const int64_t row = hash_row(ids[k], base, bk, hash_mode);
-        if (v0 == 0 && l == 0 && rows_out) rows_out[k] = (int32_t)row;
-        if (v < nvec) {
+        // a (row_base, bucket) pair outside the table (the C ABI cannot check device arrays on
+        // the host): the id contributes nothing and its row index is -1, which every push skips
+        const bool ok = row >= 0 && row < table_rows;
+        if (v0 == 0 && l == 0 && rows_out) rows_out[k] = ok ? (int32_t)row : -1;
+        if (ok && v < nvec) {
           const float4 t = reinterpret_cast<const float4*>(table + row * dim)[v];
           acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
         }
@@ -85,8 +88,8 @@ RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32
                                    const int64_t* bucket, int hash_mode, int combiner,
                                    const float* table, int64_t table_rows, int dim, float* out,
                                    int64_t out_ld, int64_t out_fstride, int32_t* rows_out) {
-  (void)table_rows;
   if (!ids || !row_base || !bucket || !table || !out || B < 0 || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  if (table_rows <= 0 || table_rows > INT32_MAX) return RS_ERR_ARG;  // rows_out is int32
   if (dim % 4 != 0 || out_ld % 4 != 0 || out_fstride % 4 != 0) return RS_ERR_ARG;
   const int64_t nseg = B * (int64_t)F;
   if (nseg == 0) return RS_OK;
@@ -101,7 +104,8 @@ RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32
   case GG:                                                                                        \
     embed_lookup_fwd_kernel<GG><<<(int)grid, block, 0, s>>>(ids, offsets, nseg, F, row_base,      \
                                                             bucket, hash_mode, combiner, table,  \
-                                                            dim, out, out_ld, out_fstride,        \
+                                                            table_rows, dim, out, out_ld,         \
+                                                            out_fstride,                          \
                                                             rows_out);                            \
     break;
   switch (G) {

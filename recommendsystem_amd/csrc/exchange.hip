@@ -102,7 +102,7 @@ RS_API int rs_sparse_pack_scan(void* stream, float* grad_table, int32_t* flag, i
       table_rows > INT32_MAX || cap < 0)
     return RS_ERR_ARG;
   hipStream_t s = rs_stream(stream);
-  (void)hipMemsetAsync(count_out, 0, sizeof(int32_t), s);
+  rs_fill_u32(s, count_out, 0u, 1);
   if (table_rows == 0) return rs_status_after_launch();
   pack_scan_kernel<<<(unsigned)sweep_grid(table_rows), kBlock, 0, s>>>(
       grad_table, flag, table_rows, dim, records, count_out, cap);

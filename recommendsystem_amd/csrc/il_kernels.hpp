@@ -52,6 +52,7 @@ struct FwdReq {
   const int64_t* gather_base = nullptr;
   const int64_t* gather_bucket = nullptr;
   const float* gather_table = nullptr;
+  int64_t gather_table_rows = 0;
   int32_t* gather_rows = nullptr;
   int gather_hash = 0;
 };
@@ -153,6 +154,7 @@ struct Args {
   const int64_t* g_bucket;
   const float* g_table;
   int32_t* g_rows;
+  int64_t g_table_rows;
   int g_hash;
 };
 
@@ -199,6 +201,7 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.g_ids = a.g_base = a.g_bucket = nullptr;
   a.g_table = nullptr;
   a.g_rows = nullptr;
+  a.g_table_rows = 0;
   a.g_hash = 0;
   return a;
 }
@@ -651,10 +654,13 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
       for (int k = lane; k < F * QV; k += 64) {
         const int f = k / QV, q = k - f * QV;
         const int64_t row = hash_row(a.g_ids[b * F + f], a.g_base[f], a.g_bucket[f], a.g_hash);
-        const float4 v = reinterpret_cast<const float4*>(a.g_table + row * C::E)[q];
+        // rows outside the table (bad row_base / bucket): a zero embedding, row index -1
+        const bool ok = row >= 0 && row < a.g_table_rows;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) v = reinterpret_cast<const float4*>(a.g_table + row * C::E)[q];
         reinterpret_cast<float4*>(X)[k] = v;
         xo[k] = v;
-        if (q == 0 && a.g_rows) a.g_rows[b * F + f] = (int32_t)row;
+        if (q == 0 && a.g_rows) a.g_rows[b * F + f] = ok ? (int32_t)row : -1;
       }
     } else {
       const float4* src = reinterpret_cast<const float4*>(x + b * F * C::E);
@@ -1471,6 +1477,7 @@ int fwd_launch(const FwdReq& q) {
   a.g_base = q.gather_base;
   a.g_bucket = q.gather_bucket;
   a.g_table = q.gather_table;
+  a.g_table_rows = q.gather_table_rows;
   a.g_rows = q.gather_rows;
   a.g_hash = q.gather_hash;
   const size_t per_wave = (size_t)a.per_wave * sizeof(float);

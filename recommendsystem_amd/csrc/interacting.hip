@@ -53,19 +53,20 @@ RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row
                             int E, int U, int H, int L, const float* W, const float* bias,
                             const float* gamma, const float* beta, float eps, int use_res,
                             float drop_rate, uint64_t seed, float* y, int64_t y_ld, float* xsave) {
-  (void)table_rows;
   if (!ids || !row_base || !bucket || !table || !x || !W || !bias || !gamma || !beta || !y ||
       B < 0 || F <= 0 || L <= 0 || H <= 0 || (hash_mode != RS_HASH_MOD && hash_mode != RS_HASH_SPLITMIX))
     return RS_ERR_ARG;
   if (U % H != 0 || (L > 1 && (E != U || !xsave))) return RS_ERR_ARG;
   if (drop_rate < 0.f || drop_rate >= 1.f || y_ld < (int64_t)F * U) return RS_ERR_ARG;
   if (F > 64) return RS_ERR_UNSUPPORTED;  // the many-field kernels read x (rs_embedding_lookup_fwd)
+  if (table_rows <= 0 || table_rows > INT32_MAX) return RS_ERR_ARG;
   rs_il::FwdReq q{rs_stream(stream), x, W, bias, gamma, beta, B, F, E, U, H, L, use_res,
                   eps, drop_rate, seed, y, xsave, y_ld};
   q.gather_ids = ids;
   q.gather_base = row_base;
   q.gather_bucket = bucket;
   q.gather_table = table;
+  q.gather_table_rows = table_rows;
   q.gather_rows = rows_out;
   q.gather_hash = hash_mode;
   int r = rs_il::il_unit_a_fwd(q);

@@ -151,7 +151,7 @@ RS_API int rs_sparse_adam(void* stream, float* table, float* m, float* v, float*
                                                  grad_scale);
   }
   else
-    (void)hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+    rs_fill_u32(s, n_touched, 0u, 1);
   return rs_status_after_launch();
 }
 
@@ -169,7 +169,7 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
                                                     n_touched, dim, max_rows, lps, lr, grad_scale);
   }
   else
-    (void)hipMemsetAsync(n_touched, 0, sizeof(int32_t), s);
+    rs_fill_u32(s, n_touched, 0u, 1);
   return rs_status_after_launch();
 }
 
@@ -345,9 +345,9 @@ RS_API int rs_sparse_compact_scan(void* stream, float* grad_table, int32_t* flag
   if (!grad_table || !flag || !rows_out || !grads_out || !n_out || dim <= 0 || dim % 4)
     return RS_ERR_ARG;
   hipStream_t s = rs_stream(stream);
-  (void)hipMemsetAsync(n_out, 0, sizeof(int32_t), s);
+  rs_fill_u32(s, n_out, 0u, 1);
   // rows past the count read -1 (the padding the rank-ordered merge skips)
-  if (cap > 0) (void)hipMemsetAsync(rows_out, 0xFF, (size_t)cap * sizeof(int32_t), s);
+  rs_fill_u32(s, rows_out, 0xFFFFFFFFu, cap);
   if (table_rows == 0) return rs_status_after_launch();
   int64_t grid = (table_rows + 255) / 256;
   if (grid > 4096) grid = 4096;

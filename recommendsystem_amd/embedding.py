@@ -74,7 +74,8 @@ class SparseTable:
         cap = int(min(self.rows, max_touched)) if max_touched else self.rows
         self.touched_cap = cap
         self.touched = torch.zeros(cap, device=device, dtype=torch.int32)
-        self.n_touched = torch.zeros(1 + 288, device=device, dtype=torch.int32)  # {count, completion counters}
+        # {count, completion counters (csrc/common.hpp RS_DONE_WORDS), overflow word}
+        self.n_touched = torch.zeros(1 + 288, device=device, dtype=torch.int32)
         if isinstance(self.optimizer, SparseAdam):
             self.m = torch.zeros_like(self.weight)
             self.v = torch.zeros_like(self.weight)
@@ -95,6 +96,17 @@ class SparseTable:
              dout_ld, dout_fstride, self.dim, combiner, ptr(self.grad), ptr(self.flag),
              None if scan else ptr(self.touched), None if scan else ptr(self.n_touched),
              self.touched_cap)
+
+    def check_overflow(self) -> None:
+        """Raise if any step since the last check claimed more rows than the touched list holds
+        (list mode; csrc/optim.hip records the largest such count in the sticky word
+        n_touched[288] and updates only the first touched_cap rows).  Reads the device: call it
+        outside the timed / captured region."""
+        n = int(self.n_touched[288].item())
+        if n:
+            self.n_touched[288].zero_()
+            raise RuntimeError(f"sparse table touched-row overflow: a step claimed {n} rows, the "
+                               f"touched list holds {self.touched_cap} (raise max_touched)")
 
     def step(self, grad_scale: float = 1.0) -> None:
         """Apply the sparse optimizer to the rows touched since the last step."""

@@ -1,6 +1,7 @@
 """GPU, world size 2 on one device (gloo transport; RCCL on the 8-GPU node runs the same code):
 the data-parallel AutoInt step (dist.exchange_packed: dense bucket + packed sparse records, two
-all-gathers, rank-ordered merges and dense sum) after 3 steps
+all-gathers, rank-ordered merges and dense sum) after 3 steps over two alternating batches
+(eager, and as one captured forward/backward graph per batch + one optimizer graph)
 
   * leaves bitwise-identical replicas (dense parameters and the embedding table), and
   * matches the CPU oracle's single-process train step on the union of the ranks' batches
@@ -38,6 +39,9 @@ def _model(max_batch, world):
 
 
 def _worker(rank, world, port, ids, labels, graph, out):
+    """ids / labels: [NB, B_global, ...] global batches; step s trains on batch s % NB (rank r
+    takes its slice).  graph: one captured forward/backward graph per batch + one optimizer
+    graph, replayed alternately (capture_pool / step_pool)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -47,15 +51,15 @@ def _worker(rank, world, port, ids, labels, graph, out):
     trn = AutoIntTrainer(model, B_LOCAL, process_group=dist.group.WORLD)
     assert trn.packed_dp
     sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
-    idt = torch.from_numpy(ids[sl]).cuda()
-    lbt = torch.from_numpy(labels[sl]).cuda()
+    pool = [(torch.from_numpy(i[sl]).cuda(), torch.from_numpy(l[sl]).cuda()) for i, l in zip(ids, labels)]
     if graph:
-        trn.capture_pool([(idt, lbt)], warmup=0)
-        for _ in range(STEPS):
-            trn.step_pool(0)
+        trn.capture_pool(pool, warmup=1)  # the warm-up step is rolled back
+        assert len(trn.pool_graphs) == len(pool)
+        for s in range(STEPS):
+            trn.step_pool(s)
     else:
-        for _ in range(STEPS):
-            trn.step(idt, lbt)
+        for s in range(STEPS):
+            trn.step(*pool[s % len(pool)])
     torch.cuda.synchronize()
     params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).numpy()
     out[rank] = (params, model.table.weight.cpu().numpy(), float(trn.loss))
@@ -69,8 +73,9 @@ def test_dp_two_ranks_match_oracle(graph):
     B = B_LOCAL * WORLD
     cfg, model = _model(B, 1)
     rng = np.random.default_rng(21)
-    ids = rng.integers(0, 10 * cfg.vocab_per_field, size=(B, cfg.num_fields), dtype=np.int64)
-    labels = (rng.uniform(size=(B, 1)) < 0.25).astype(np.float32)
+    NB = 2  # two different global batches, alternated
+    ids = rng.integers(0, 10 * cfg.vocab_per_field, size=(NB, B, cfg.num_fields), dtype=np.int64)
+    labels = (rng.uniform(size=(NB, B, 1)) < 0.25).astype(np.float32)
     ref, *_ = _oracle_from_model(model, cfg)
     mgr = mp.Manager()
     out = mgr.dict()
@@ -79,8 +84,8 @@ def test_dp_two_ranks_match_oracle(graph):
     p1, t1, l1 = out[1]
     assert np.array_equal(p0, p1), "dense replicas diverged"
     assert np.array_equal(t0, t1), "embedding-table replicas diverged"
-    for _ in range(STEPS):
-        loss_ref = ref.step(torch.from_numpy(ids), torch.from_numpy(labels))
+    for st in range(STEPS):
+        loss_ref = ref.step(torch.from_numpy(ids[st % NB]), torch.from_numpy(labels[st % NB]))
     # each rank's loss is its half-batch mean: their average is the global-batch loss
     assert abs(0.5 * (l0 + l1) - loss_ref) < 1e-5
     want = torch.cat([p.detach().reshape(-1) for p in ref.dense_list]).numpy()
@@ -128,3 +133,99 @@ def test_dp_two_ranks_config2_size():
     assert n0 == n1 > 10_000
     assert np.isfinite(l0) and np.isfinite(l1)
     assert np.array_equal(p0, p1) and np.array_equal(h0, h1)
+
+
+# ------------------------------------------------------------------------------------------
+# the generic Trainer (configs 3-5: trainer.py's all-reduce + list-mode sparse exchange)
+# ------------------------------------------------------------------------------------------
+B_DIN, T_DIN, V_DIN = 64, 20, 500
+
+
+def _din_batches(world):
+    from recommendsystem_amd.workloads import din_batch
+    out = []
+    for r in range(world):
+        rng = np.random.default_rng(50 + r)
+        out.append([a.cpu() for a in din_batch(rng, B_DIN, T_DIN, V_DIN, "cpu")])
+    return out
+
+
+def _union(batches):
+    q = torch.cat([b[0] for b in batches])
+    h = torch.cat([b[1] for b in batches])
+    offs, base = [torch.zeros(1, dtype=torch.int32)], 0
+    for b in batches:
+        offs.append(b[2][1:] + base)
+        base += int(b[2][-1])
+    return q, h, torch.cat(offs), torch.cat([b[3] for b in batches])
+
+
+def _din_trainer(pg):
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import DINPool
+    d = DINPool(vocab=V_DIN, T=T_DIN, device=torch.device("cuda", 0), seed=2)
+    d.table.optimizer.learning_rate = 1e-2
+    return d, Trainer(d, 1e-2, [d.table], process_group=pg)
+
+
+def _worker_trainer(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d, trn = _din_trainer(dist.group.WORLD)
+    batch = [a.cuda() for a in _din_batches(world)[rank]]
+    for _ in range(STEPS):
+        trn.step(*batch)
+    torch.cuda.synchronize()
+    d.table.check_overflow()
+    params = torch.cat([p.detach().reshape(-1).cpu() for p in d.parameters()]).numpy()
+    out[rank] = (params, d.table.weight.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_generic_trainer_two_ranks():
+    """2-rank DP of the generic Trainer (config-4 DIN harness, small vocab): bitwise-identical
+    replicas, and the single-process Trainer on the union batch within fp32 tolerance (the
+    sparse sums use float atomics, so the two runs differ in the last bits)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_trainer, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    p0, t0 = out[0]
+    p1, t1 = out[1]
+    assert np.array_equal(p0, p1), "dense replicas diverged"
+    assert np.array_equal(t0, t1), "table replicas diverged"
+    d, trn = _din_trainer(None)
+    union = [a.cuda() for a in _union(_din_batches(WORLD))]
+    for _ in range(STEPS):
+        trn.step(*union)
+    torch.cuda.synchronize()
+    want = torch.cat([p.detach().reshape(-1).cpu() for p in d.parameters()]).numpy()
+    assert_close(p0, want, 2e-6, 1e-4, what="dense params (DP vs union batch)")
+    assert_close(t0, d.table.weight.cpu().numpy(), 2e-6, 1e-4, what="table (DP vs union batch)")
+
+
+def test_rccl_flat_all_gather_world1():
+    """RCCL itself ('nccl' on ROCm) on this one-GPU box: a world-1 process group runs the
+    packed exchange through all_gather_into_tensor (the path the 8-GPU node takes)."""
+    from recommendsystem_amd import dist as rdist
+    port = _free_port()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert rdist.uses_flat_all_gather()
+        n_dense, ld, rs, cap = 10, 12, 5, 8
+        send = torch.arange(ld, dtype=torch.float32, device="cuda")
+        send.view(torch.int32)[n_dense] = 3  # record count
+        recv = torch.zeros(ld, device="cuda")
+        recs = torch.arange(cap * rs, dtype=torch.float32, device="cuda")
+        recs_all = torch.zeros(cap * rs, device="cuda")
+        nmax = rdist.exchange_packed(send, recv, n_dense, recs, recs_all, rs)
+        torch.cuda.synchronize()
+        assert nmax == 3
+        assert torch.equal(recv, send)
+        assert torch.equal(recs_all[:3 * rs], recs[:3 * rs])
+    finally:
+        dist.destroy_process_group()

@@ -35,16 +35,19 @@ def _table_grad_expect(rows, offsets, B, F, dx0, combiner="mean"):
 # ------------------------------------------------------------------------------------------
 # H5: rank/multi_head AUTOINT
 # ------------------------------------------------------------------------------------------
-def test_multi_head_ranker_matches_oracle():
+@pytest.mark.parametrize("B,vocab", [(6, 50), (512, None)])
+def test_multi_head_ranker_matches_oracle(B, vocab):
+    """(6, 50): many id collisions; (512, None): config 3's real 200 x 265k table."""
     from recommendsystem_amd.models import MultiHeadConfig, MultiHeadRanker
     from recommendsystem_amd.workloads import multi_head_batch
     rng = np.random.default_rng(31)
-    cfg = MultiHeadConfig(num_fields=200, vocab_per_field=50)
+    cfg = MultiHeadConfig(num_fields=200) if vocab is None else MultiHeadConfig(num_fields=200, vocab_per_field=vocab)
+    if vocab is None:
+        assert cfg.vocab_per_field == 265_000
     m = MultiHeadRanker(cfg, device=DEV, seed=3)
     with torch.no_grad():  # larger expert/gate weights than TruncatedNormal(0.001) to exercise the mixture
         m.mix.kernel.uniform_(-0.05, 0.05)
     _randomise_biases(m, rng)
-    B = 6
     ids, offs, labels = multi_head_batch(rng, B, cfg, DEV)
     il = m.interact
     seed = (il.seed * 1000003 + il._calls) & 0xFFFFFFFFFFFFFFFF
@@ -120,6 +123,23 @@ def test_dssm_matches_oracle():
     loss = m.loss(emb, mask, y)
     loss.backward()
     e64 = c64(emb)
+    o = _dssm_oracle(m, e64, mask, y)
+    assert_close(to_np(out["student_logit"]), to_np(o["s_logit"]), 2e-5, 0, "student logit")
+    assert_close(to_np(out["teacher_logit"]), to_np(o["t_logit"]), 2e-5, 0, "teacher logit")
+    ref_loss = o["loss"]
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    ref_loss.backward()
+    # forward() ran once more than loss() above: only loss()'s backward populated the grads
+    assert_grad_close(to_np(emb.grad), e64.grad.numpy(), "d emb")
+    for p, r in o["params"]:
+        assert_grad_close(to_np(p.grad), r.grad.numpy(), "dssm param")
+
+
+def _dssm_oracle(m, e64, mask, y):
+    """float64 composition of rough_rank DSSM (rough_rank/model.py:118-222) from m's weights on
+    the leaf e64 [B, user+item fields, 16]: loss (student/teacher BCE + KD), logits and the
+    (parameter, fp64 leaf) pairs whose gradients the tests check."""
+    B = e64.shape[0]
     maskc = torch.from_numpy(mask.cpu().numpy()).double()
     ui, ii = m.user_idx.cpu(), m.item_idx.cpu()
     u_emb, pu = _tower_ref(m.user, e64[:, ui].reshape(B, -1), maskc)
@@ -133,43 +153,21 @@ def test_dssm_matches_oracle():
     t_logit = tr.dense(tr.dense(torch.cat([deep, cross], 1), *L["t3"]), *L["t4"])
     s_logit = tr.dense(tr.dense(torch.cat([u_emb, i_emb], 1), *L["s1"], "relu"), *L["s2"])
     yc = torch.from_numpy(y.cpu().numpy()).double()
-    assert_close(to_np(out["student_logit"]), to_np(s_logit), 2e-5, 0, "student logit")
-    assert_close(to_np(out["teacher_logit"]), to_np(t_logit), 2e-5, 0, "teacher logit")
     ref_loss = (tr.keras_bce(yc, torch.sigmoid(s_logit)) + tr.keras_bce(yc, torch.sigmoid(t_logit))
                 + tr.kd_loss(s_logit, t_logit.detach()).mean())
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
-    ref_loss.backward()
-    # forward() ran once more than loss() above: only loss()'s backward populated the grads
-    assert_grad_close(to_np(emb.grad), e64.grad.numpy(), "d emb")
-    for p, r in pu + pi + [(m.cross.W, Wx), (m.cross.b, bx)] + [(getattr(m, n).kernel, L[n][0]) for n in L]:
-        assert_grad_close(to_np(p.grad), r.grad.numpy(), "dssm param")
+    params = pu + pi + [(m.cross.W, Wx), (m.cross.b, bx)] + [(getattr(m, n).kernel, L[n][0]) for n in L]
+    return dict(loss=ref_loss, s_logit=s_logit, t_logit=t_logit, params=params)
 
 
 # ------------------------------------------------------------------------------------------
 # H9: staytime mtl_net
 # ------------------------------------------------------------------------------------------
-def test_staytime_mtl_matches_oracle():
-    from recommendsystem_amd.models import STAYTIME_BINS, StaytimeConfig, StaytimeMTL
-    from recommendsystem_amd.workloads import staytime_labels
-    rng = np.random.default_rng(33)
-    cfg = StaytimeConfig()
-    m = StaytimeMTL(cfg, device=DEV, seed=7)
-    _randomise_biases(m, rng, 0.02)
-    B, F, T = 19, cfg.num_fields, cfg.seq_len
-    emb = torch.from_numpy(rng.uniform(-0.3, 0.3, size=(B, F, 32)).astype(np.float32)).to(DEV).requires_grad_(True)
-    seqs, masks = [], []
-    for s in range(cfg.num_seq):
-        seqs.append(torch.from_numpy(rng.uniform(-0.3, 0.3, size=(B, T, 32)).astype(np.float32)).to(DEV).requires_grad_(True))
-        mk = rng.uniform(size=(B, T)) < 0.6
-        mk[0] = False
-        masks.append(torch.from_numpy(mk).to(DEV))
-    stay, short, long_, sw = (torch.from_numpy(a).to(DEV) for a in staytime_labels(rng, B))
-    loss, outs = m(emb, seqs, masks, True, (stay, short, long_, sw))
-    loss.backward()
-    # ---- oracle ----
-    e64 = c64(emb)
-    s64 = [c64(s) for s in seqs]
-    mk = [torch.from_numpy(x.cpu().numpy()) for x in masks]
+def _staytime_oracle(m, cfg, e64, s64, mk, stay, short, long_, sw):
+    """float64 op-for-op composition of staytime mtl_net (staytime/VideoDnn.py:27-215) from m's
+    weights on leaf inputs e64 [B, F, 32] / s64 [num_seq x [B, T, 32]] (masks mk): the loss of
+    staytime/model.py:20-36, predictions and the weight leaves whose gradients the tests check."""
+    from recommendsystem_amd.models import STAYTIME_BINS
+    B, F = e64.shape[0], cfg.num_fields
     general = [e64[:, f, 0:16] for f in range(F)]
     gate_input = torch.cat([e64[:, f, 16:32] for f in cfg.bias_fields], 1)
     din = []
@@ -222,12 +220,40 @@ def test_staytime_mtl_matches_oracle():
     to = [(c64(l.kernel), c64(l.bias)) for l in m.task_out]
     preds = [torch.sigmoid(torch.cat([fm_logit, torch.relu(mmoe[t + 1] @ dl[t][0] + dl[t][1])], 1) @ to[t][0] + to[t][1])
              for t in range(2)]
-    swc = torch.from_numpy(sw.cpu().numpy()).double()
+    swc = torch.from_numpy(sw.cpu().numpy()).double().reshape(-1)  # [B] (device labels: [B, 1])
     ys = torch.from_numpy(stay.cpu().numpy()).double()
     ce = lambda y, p: -(y * torch.log(p + 1e-6) + (1 - y) * torch.log(1 - p + 1e-6))  # noqa: E731
     ref_loss = (2.0 * torch.mean(tr.custom_kl_loss(ys, P) * swc)
-                + 2.0 * torch.mean(ce(torch.from_numpy(short.cpu().numpy()).double(), preds[0])[:, 0] * swc)
-                + 1.0 * torch.mean(ce(torch.from_numpy(long_.cpu().numpy()).double(), preds[1])[:, 0] * swc))
+                + 2.0 * torch.mean(ce(torch.from_numpy(short.cpu().numpy()).double().reshape(-1, 1), preds[0])[:, 0] * swc)
+                + 1.0 * torch.mean(ce(torch.from_numpy(long_.cpu().numpy()).double().reshape(-1, 1), preds[1])[:, 0] * swc))
+    return dict(loss=ref_loss, preds=preds, P=P, fk=fk, pk=pk, dW=dW, hW=hW)
+
+
+def test_staytime_mtl_matches_oracle():
+    from recommendsystem_amd.models import STAYTIME_BINS, StaytimeConfig, StaytimeMTL
+    from recommendsystem_amd.workloads import staytime_labels
+    rng = np.random.default_rng(33)
+    cfg = StaytimeConfig()
+    m = StaytimeMTL(cfg, device=DEV, seed=7)
+    _randomise_biases(m, rng, 0.02)
+    B, F, T = 19, cfg.num_fields, cfg.seq_len
+    emb = torch.from_numpy(rng.uniform(-0.3, 0.3, size=(B, F, 32)).astype(np.float32)).to(DEV).requires_grad_(True)
+    seqs, masks = [], []
+    for s in range(cfg.num_seq):
+        seqs.append(torch.from_numpy(rng.uniform(-0.3, 0.3, size=(B, T, 32)).astype(np.float32)).to(DEV).requires_grad_(True))
+        mk = rng.uniform(size=(B, T)) < 0.6
+        mk[0] = False
+        masks.append(torch.from_numpy(mk).to(DEV))
+    stay, short, long_, sw = (torch.from_numpy(a).to(DEV) for a in staytime_labels(rng, B))
+    loss, outs = m(emb, seqs, masks, True, (stay, short, long_, sw))
+    loss.backward()
+    # ---- oracle ----
+    e64 = c64(emb)
+    s64 = [c64(s) for s in seqs]
+    mk = [torch.from_numpy(x.cpu().numpy()) for x in masks]
+    o = _staytime_oracle(m, cfg, e64, s64, mk, stay, short, long_, sw)
+    ref_loss, preds, P = o["loss"], o["preds"], o["P"]
+    fk, pk, dW, hW = o["fk"], o["pk"], o["dW"], o["hW"]
     assert_close(to_np(outs["shortplay"]), to_np(preds[0]), 2e-5, 0, "shortplay")
     assert_close(to_np(outs["longplay"]), to_np(preds[1]), 2e-5, 0, "longplay")
     assert_close(to_np(outs["staytime"]), to_np(P), 2e-5, 2e-5, "staytime head")
@@ -277,3 +303,72 @@ def test_workload_trainers_reduce_loss():
     for _ in range(8):
         l1 = float(tr_.step(*batch))
     assert np.isfinite(l1) and l1 < l0
+
+
+# ------------------------------------------------------------------------------------------
+# config 5 at its real size: the 10M x 32 hashed table, staytime_batch, B = 256
+# ------------------------------------------------------------------------------------------
+def test_staytime_rough_rank_10M_table_matches_oracle():
+    """StaytimeRoughRank over the real 10M-row splitmix64-hashed table on
+    a staytime_batch (device-built 400-bin labels): joint loss, the dense gradients of both
+    models, and the sparse push (every touched row's summed gradient) vs the fp64 oracle on
+    lookups it hashes itself."""
+    from recommendsystem_amd.workloads import StaytimeRoughRank, staytime_batch
+    rng = np.random.default_rng(60)
+    j = StaytimeRoughRank(device=DEV, seed=3)
+    R = j.table.rows
+    assert R == 10_000_000
+    _randomise_biases(j, rng, 0.02)
+    B = 256
+    batch = staytime_batch(rng, B, j, DEV)
+    st_ids, seq_ids, seq_offs, rr_ids, stay, short, long_, sw, click, mask = batch
+    loss = j.loss(*batch)
+    loss.backward()
+    torch.cuda.synchronize()
+    cfg, rcfg = j.st_cfg, j.rr_cfg
+    F, nrr = cfg.num_fields, rcfg.user_fields + rcfg.item_fields
+    W = j.table.weight.detach().cpu().numpy()
+    # ---- oracle lookups (hash + gather on the host) ----
+    rows_f = npo.hash_rows(st_ids.cpu().numpy().reshape(-1), np.tile(np.arange(F), B),
+                           np.zeros(F, np.int64), np.full(F, R), "splitmix")
+    e64 = torch.tensor(W[rows_f].astype(np.float64).reshape(B, F, -1), requires_grad=True)
+    s64, mk, srows = [], [], []
+    for s in range(cfg.num_seq):
+        e, m_, r_ = npo.sequence_lookup(seq_ids[s].cpu().numpy(), seq_offs[s].cpu().numpy(), B,
+                                        cfg.seq_len, 0, R, W, "splitmix")
+        s64.append(torch.tensor(e.astype(np.float64), requires_grad=True))
+        mk.append(torch.from_numpy(m_))
+        srows.append(r_.reshape(-1))
+    rows_r = npo.hash_rows(rr_ids.cpu().numpy().reshape(-1), np.tile(np.arange(nrr), B),
+                           np.zeros(nrr, np.int64), np.full(nrr, R), "splitmix")
+    r64 = torch.tensor(W[rows_r][:, 0:16].astype(np.float64).reshape(B, nrr, 16), requires_grad=True)
+    o = _staytime_oracle(j.staytime, cfg, e64, s64, mk, stay, short, long_, sw)
+    d = _dssm_oracle(j.dssm, r64, mask, click)
+    ref_loss = o["loss"] + d["loss"]
+    assert abs(float(loss) - float(ref_loss)) <= 2e-5 * max(1.0, abs(float(ref_loss))), \
+        (float(loss), float(ref_loss))
+    ref_loss.backward()
+    st = j.staytime
+    for p, r in [(st.first.kernel, o["fk"]), (st.pp1.kernel, o["pk"]), (st.dcn.W, o["dW"]),
+                 (st.head.dense.kernel, o["hW"])] + d["params"]:
+        assert_grad_close(to_np(p.grad), r.grad.numpy(), "joint dense param")
+    # ---- the sparse push: row -> sum over all its occurrences (fields, sequences, rr cols 0:16)
+    g: dict[int, np.ndarray] = {}
+
+    def add(rows, grads):
+        for r, gg in zip(rows.tolist(), grads):
+            if r >= 0:
+                g[r] = g[r] + gg if r in g else gg.copy()
+
+    add(rows_f, e64.grad.numpy().reshape(-1, 32))
+    for s in range(cfg.num_seq):
+        add(srows[s], s64[s].grad.numpy().reshape(-1, 32))
+    rg = np.zeros((B * nrr, 32))
+    rg[:, :16] = r64.grad.numpy().reshape(-1, 16)
+    add(rows_r, rg)
+    keys = np.array(sorted(g), dtype=np.int64)
+    assert int(j.table.n_touched[0].item()) == keys.size  # list mode: each row claimed once
+    touched = np.sort(j.table.touched[:keys.size].cpu().numpy().astype(np.int64))
+    assert np.array_equal(touched, keys), "touched-row set differs from the oracle's"
+    got = j.table.grad[torch.from_numpy(keys).to(DEV)].cpu().numpy()
+    assert_grad_close(got, np.stack([g[k] for k in keys]), "10M-table push")

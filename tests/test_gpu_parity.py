@@ -527,10 +527,12 @@ def test_autoint_train_steps_match_oracle(graph, fused):
     idt, lbt = torch.from_numpy(ids).to(DEV), torch.from_numpy(labels).to(DEV)
     if graph:
         trn.load_batch(idt, lbt)
-        # capture() runs 2 eager warm-up steps and records (does not run) one; replay = step 3
+        # capture() runs 2 eager warm-up steps, rolls them back and records (does not run) one
+        # step: every replay is one training step
         trn.capture(warmup=2)
         steps = 3
-        trn.graph.replay()
+        for _ in range(steps):
+            trn.graph.replay()
     else:
         steps = 3
         for _ in range(steps):
