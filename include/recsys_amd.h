@@ -406,6 +406,65 @@ int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float
 /* Grid (= number of per-block partial rows) rs_il_bwd uses for a given batch and workspace. */
 int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats);
 
+
+/* ---------------------------------------------------------------------------------------
+ * H2 / H12 / H13  rank/ctr BaseModel front end and the rank/ctr, rank/finish model pieces
+ * (csrc/front_end.hip).  fp32, row-major, explicit leading dimensions ("_ld").
+ * ------------------------------------------------------------------------------------- */
+/* emb_dict[slot][:, s0:s1] slicing + Concatenate (rank/ctr/base_model.py:134-154): out[b*out_ld
+ * + j] = src[b*src_ld + cols[j]] for a column plan (feature_config.SlotLayout.column_plan). */
+int rs_gather_columns(void* stream, const float* src, int64_t src_ld, int64_t B,
+                      const int32_t* cols, int ncols, float* out, int64_t out_ld);
+/* its backward: dsrc[b*src_ld + cols[j]] += dout[b*out_ld + j] (cols unique within a plan). */
+int rs_scatter_add_columns(void* stream, const float* dout, int64_t out_ld, int64_t B,
+                           const int32_t* cols, int ncols, float* dsrc, int64_t src_ld);
+/* SENet squeeze tf.reduce_mean(emb, axis=1, keepdims=True) per structure field
+ * (rank/ctr/model_init.py:22-24): out[b*out_ld + f] = mean(x[b, seg[f] .. seg[f+1])). */
+int rs_segment_mean(void* stream, const float* x, int64_t x_ld, int64_t B, const int32_t* seg,
+                    int F, float* out, int64_t out_ld);
+/* multiply([emb_input, senet_split_output]) per field with senet_output = alpha * s
+ * (rank/ctr/model_init.py:31-40, alpha = 2): y[b, c] = x[b, c] * (alpha * s[b, colfield[c]]). */
+int rs_field_scale_fwd(void* stream, const float* x, int64_t x_ld, int64_t B,
+                       const int32_t* colfield, int C, const float* s, int64_t s_ld, float alpha,
+                       float* y, int64_t y_ld);
+/* its backward: dx[b, c] (+)= dy[b, c] alpha s[b, f(c)] (dx nullable), ds[b, f] = alpha sum_c dy x
+ * (nullable). */
+int rs_field_scale_bwd(void* stream, const float* dy, int64_t dy_ld, const float* x, int64_t x_ld,
+                       int64_t B, const int32_t* seg, int F, const float* s, int64_t s_ld,
+                       float alpha, float* dx, int64_t dx_ld, int dx_accumulate, float* ds,
+                       int64_t ds_ld);
+/* The per-field Dense(O) maps emb_linear_map_i (rank/ctr/model_init.py:44-46): y[b, f*O + o] =
+ * sum_{c in [seg[f], seg[f+1])} x[b, c] W[c*O + o] + bias[f*O + o]; W packs every field's
+ * [w_f, O] kernel as one [C, O] matrix. */
+int rs_field_linear_fwd(void* stream, const float* x, int64_t x_ld, int64_t B, const int32_t* seg,
+                        int F, int O, const float* W, const float* bias, float* y, int64_t y_ld);
+int64_t rs_field_linear_workspace_floats(int64_t B, int C, int F, int O);
+/* its backward: dx (nullable, += with dx_accumulate), dW [C, O], db [F, O] (fixed-order batch
+ * reduction through the workspace). */
+int rs_field_linear_bwd(void* stream, const float* dy, int64_t dy_ld, const float* x, int64_t x_ld,
+                        int64_t B, const int32_t* seg, const int32_t* colfield, int C, int F, int O,
+                        const float* W, float* dx, int64_t dx_ld, int dx_accumulate, float* dW,
+                        float* db, int dparams_accumulate, float* workspace,
+                        int64_t workspace_floats);
+/* CAN per-sample matmuls (rank/ctr/model_init.py:90-98, 150-154): out = relu(relu(r W1 + b1) W2
+ * + b2), W1 [8,6] | b1 [6] | W2 [6,4] | b2 [4] = the 82 columns of each sample's p row
+ * (tf.split + tf.reshape, row-major).  h_save [B, 6] (nullable) keeps relu(r W1 + b1). */
+int rs_can_fwd(void* stream, const float* r, int64_t r_ld, const float* p, int64_t p_ld, int64_t B,
+               float* out, int64_t out_ld, float* h_save);
+int rs_can_bwd(void* stream, const float* dout, int64_t dout_ld, const float* out, int64_t out_ld,
+               const float* r, int64_t r_ld, const float* p, int64_t p_ld, const float* h,
+               int64_t B, float* dr, int64_t dr_ld, int dr_accumulate, float* dp, int64_t dp_ld);
+/* rank/finish FMLayer (rank/finish/videodnn.py:41-50): y[b] = 0.5 * sum_n ((x V)_n^2 -
+ * (x^2 V^2)_n) + add[b], V = fm_matrix [K, N] (N = 4, 8, 16); add (nullable) = the layer's
+ * Dense(1) linear term (rs_dense_fwd output); xv_save [B, N] nullable (needed by the backward). */
+int rs_fm_proj_fwd(void* stream, const float* x, int64_t x_ld, int64_t B, int K, int N,
+                   const float* V, const float* add, float* y, float* xv_save);
+int64_t rs_fm_proj_workspace_floats(int64_t B, int K, int N);
+int rs_fm_proj_bwd(void* stream, const float* dy, const float* x, int64_t x_ld, int64_t B, int K,
+                   int N, const float* V, const float* xv, float* dx, int64_t dx_ld,
+                   int dx_accumulate, float* dV, int dV_accumulate, float* workspace,
+                   int64_t workspace_floats);
+
 #ifdef __cplusplus
 }
 #endif

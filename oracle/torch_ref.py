@@ -339,3 +339,94 @@ def multi_head_gates(result, We, be, Wg, bg, n_used=7):
         g = torch.softmax(result @ W + b, dim=-1).unsqueeze(-1)                     # :100-107
         outs.append(torch.sum(eo * g, dim=1))                                        # :109-112
     return outs
+
+
+# ==========================================================================================
+# H12 rank/ctr Model.model_layer and H13 rank/finish DeepFM (op for op; weights passed in as
+# {keras layer name: (kernel, bias)}; test infrastructure only).
+# ==========================================================================================
+def rank_ctr_model_layer(structure, gate_inputs, bias, P, il, il_seed, drop_rate=0.2, eps=1e-14,
+                         ppnet_units=(256, 64, 8, 256, 64, 8, 32, 16), num_experts=3,
+                         expert_units=(512, 256), gate_units=(256, 32), tower_units=(64, 8)):
+    """rank/ctr/model_init.py:19-162.  structure = emb_structure_input (list of [B, w_i]),
+    gate_inputs = emb_gate_input, bias = emb_bias_input {type: [tensors]}, il = (W, bias, gamma,
+    beta) of the InteractingLayer.  Returns the two sigmoid outputs BEFORE the clip."""
+    sq = torch.cat([s.mean(dim=1, keepdim=True) for s in structure], dim=1)        # :21-26
+    sq = sq.detach()                                                                 # :28
+    s1 = dense(sq, *P["senet_squeeze_layer"], "relu")                               # :29
+    s2 = 2 * dense(s1, *P["senet_extract_layer"], "sigmoid")                        # :32
+    splits = torch.split(s2, 1, dim=1)                                               # :34
+    rew = [e * sp for e, sp in zip(structure, splits)]                               # :36-40
+    emb3d = [dense(r, *P[f"emb_linear_map_{i}"])[:, None, :] for i, r in enumerate(rew)]  # :43-46
+    auto_in = torch.cat(emb3d, dim=1)                                                # :48
+    B = auto_in.shape[0]
+    auto = interacting_layer(auto_in, *il, layer_num=1, head_num=2, use_res=True, eps=eps,
+                             drop_rate=drop_rate, seed=il_seed).reshape(B, -1)      # :53-59
+    pp = 2 * dense(torch.cat(bias["ppnet"], dim=1), *P["dnn_ppnet_gate"], "sigmoid")  # :64-66
+    gl = torch.split(pp, list(ppnet_units), dim=1)                                   # :68
+    deep = torch.cat(rew, dim=1)                                                     # :72
+    for i in range(2):                                                               # :74-78
+        deep = torch.relu(dense(deep, *P[f"dnn_{i}"]) * gl[i + 6])
+    mult = torch.relu(torch.cat(bias["multiply_user"], 1) * torch.cat(bias["multiply_item"], 1))
+    result = torch.cat([deep, auto, mult], dim=1)                                    # :87
+    can = dense(torch.cat(bias["can"], dim=1), *P["dnn_can"])                         # :90-91
+    c = torch.split(can, [48, 6, 24, 4], dim=1)                                      # :92
+    w1, b1 = c[0].reshape(-1, 8, 6), c[1].reshape(-1, 1, 6)
+    w2, b2 = c[2].reshape(-1, 6, 4), c[3].reshape(-1, 1, 4)
+    gate_in = torch.cat(gate_inputs, dim=1)                                          # :104
+    experts = []
+    for i in range(num_experts):                                                     # :105-114
+        er = result
+        for j, _ in enumerate(expert_units):
+            g = dense(gate_in, *P[f"gate_{i}_{j}_1"], "relu")
+            g = 2 * dense(g, *P[f"gate_{i}_{j}_2"], "sigmoid")
+            er = dense(er, *P[f"expert_output_{i}_{j}"], "relu")
+            er = g * er
+        experts.append(er)
+    ec = torch.stack(experts, dim=1)                                                 # :115
+    outs = []
+    for t in range(2):                                                               # :121-132
+        go = result
+        for j, _ in enumerate(gate_units):
+            go = dense(go, *P[f"gate_{t}_{j}"], "relu")
+        go = torch.softmax(dense(go, *P[f"gate_output_{t}"]), dim=-1)[..., None]
+        r = torch.sum(ec * go, dim=1)
+        for j, _ in enumerate(tower_units):                                          # :139-155
+            if j == 0:
+                r = torch.relu(r * gl[t * 3])
+            r = dense(r, *P[f"task{t}_dnn2_{j}"])
+            r = torch.relu(r * gl[t * 3 + j + 1])
+            if j == len(tower_units) - 1:
+                cr = torch.relu(torch.matmul(r[:, None, :], w1) + b1)
+                cr = torch.relu(torch.matmul(cr, w2) + b2).squeeze(1)
+                r = torch.cat([r, cr], dim=1)
+        outs.append(dense(r, *P[f"output_{t}"], "sigmoid"))                          # :156
+    return outs
+
+
+def fm_layer_finish(x, V, w, b):
+    """rank/finish FMLayer.call (videodnn.py:41-52)."""
+    sum_square = torch.square(x @ V)
+    square_sum = torch.square(x) @ torch.square(V)
+    high = 0.5 * torch.sum(sum_square - square_sum, dim=1, keepdim=True)
+    return high + dense(x, w, b)
+
+
+def deepfm_sub_model(general_list, bias_list, P, hidden=(64, 32)):
+    """rank/finish create_deepFM_sub_model (videodnn.py:69-137) from the per-slot inputs
+    (general_list = gerneral_inputs incl. emb_1568[:, 16:], bias_list = bais_inputs)."""
+    general = torch.cat(general_list, dim=1)
+    fm = fm_layer_finish(general, *P["fm"])
+    bias = torch.cat(bias_list, dim=1)
+    x = general
+    for i, unit in enumerate(hidden):
+        if i == 0:
+            x = dense(x, *P[f"dnn_{i}"], "relu")
+        else:
+            one = dense(bias, *P[f"bais_dnn_one_{i}"], "relu")
+            two = dense(one, *P[f"bais_dnn_two_{i}"], "sigmoid") * 2
+            x = dense(x * two, *P[f"dnn_{i}"], "relu")
+    one = dense(bias, *P["bais_dnn_one_3"], "relu")
+    two = dense(one, *P["bais_dnn_two_3"], "sigmoid") * 2
+    x = x * two
+    return dense(torch.cat([x, fm], dim=1), *P["pred"], "sigmoid")

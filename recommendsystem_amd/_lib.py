@@ -116,6 +116,23 @@ SIGNATURES: dict[str, tuple] = {
     "rs_il_bwd_push": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                               _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64]),
+    "rs_gather_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "rs_scatter_add_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "rs_segment_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "rs_field_scale_fwd": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _f32, _vp, _i64]),
+    "rs_field_scale_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _f32,
+                                  _vp, _i64, _i32, _vp, _i64]),
+    "rs_field_linear_fwd": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _i64]),
+    "rs_field_linear_workspace_floats": (_i64, [_i64, _i32, _i32, _i32]),
+    "rs_field_linear_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i32, _i32, _i32,
+                                   _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _i64]),
+    "rs_can_fwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
+    "rs_can_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                          _i32, _vp, _i64]),
+    "rs_fm_proj_fwd": (_i32, [_vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "rs_fm_proj_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_fm_proj_bwd": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64, _i32,
+                              _vp, _i32, _vp, _i64]),
 }
 
 _LIB = None

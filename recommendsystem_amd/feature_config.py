@@ -10,11 +10,49 @@ base_model.py:82-86, 209-210); feature ids listed in featureid_to_slot share ano
 
 ``SlotLayout`` restates that parse (same iteration orders, same errors) and turns it into the
 device-side plan: one table per slot of width max_embed_size and the column intervals that the
-front end gathers into the concatenated activation (rs_gather_columns, csrc/front_end.hip).
+front end gathers into the concatenated activation (rs_gather_columns, csrc/front_end.hip;
+consumed by rank_models.RankCtrFrontEnd).
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
+
+
+# featureid_to_slot (rank/ctr/base_model.py:89): feature ids whose FeatureSlot -- hence embedding
+# table -- is another slot's (data of the shipped model; sorted by feature id here)
+FEATUREID_TO_SLOT: dict = {
+    "40545": "7777", "40546": "7778", "40547": "7779", "40549": "7781", "40550": "7782", "40551": "7783",
+    "40850": "8082", "40880": "8112", "40882": "8114", "40883": "8115", "40884": "8116", "40885": "8117",
+    "40886": "8118", "40887": "8119", "40888": "8120", "40893": "8125", "40894": "8126", "40904": "8136",
+    "40905": "8137", "40907": "8139", "40908": "8140", "40941": "8173", "40942": "8174", "40943": "8175",
+    "40944": "8176", "40945": "8177", "40946": "8178", "40947": "8179", "40948": "8180", "40949": "8181",
+    "40950": "8182", "40951": "8183", "40952": "8184", "40953": "8185", "40954": "8186", "40955": "8187",
+    "41119": "8351", "41120": "8352", "41121": "8353", "41122": "8354", "41123": "8355", "41129": "8361",
+    "41130": "8362", "41131": "8363", "41132": "8364", "41133": "8365", "41171": "3306", "41187": "2602",
+    "41188": "2602", "41189": "2602", "41196": "3306", "41202": "3306", "41222": "8454", "41223": "8455",
+    "41225": "8457", "41229": "3305", "41230": "3305", "41231": "8463", "41232": "3305", "41233": "8465",
+    "41234": "8466", "41235": "8467", "41236": "8468", "41237": "8469", "41238": "8470", "41239": "8471",
+    "41240": "8472", "41241": "8473", "41242": "8474", "41243": "8475", "41244": "8476", "41245": "8477",
+    "41246": "8478", "41247": "8479", "41248": "8480", "41249": "8481", "41250": "8482", "41251": "8483",
+    "41252": "8484", "41253": "8485", "41262": "8494", "41263": "8495", "41264": "8496", "41265": "8497",
+    "41266": "8498", "41267": "8499", "41268": "8500", "41269": "8501", "41270": "8502", "41271": "8503",
+    "41283": "8515", "41296": "8528", "41300": "8532", "41303": "8535", "41313": "8545", "41331": "8563",
+    "41339": "8571", "41341": "8573", "41674": "3303", "41675": "3303", "41676": "3303", "41831": "9063",
+    "41832": "9064", "41833": "9065", "41834": "9066", "41835": "9067", "41836": "9068", "41837": "9069",
+    "41838": "9070", "41839": "9071", "41840": "9072", "41841": "9073", "41842": "9074", "41854": "9086",
+    "41855": "9087", "41856": "9088", "41857": "9089", "41858": "9090", "41859": "9091", "41860": "9092",
+    "41861": "9093", "42283": "9515", "42284": "9516", "42285": "9517", "42286": "9518", "42287": "9519",
+    "42288": "9520", "42289": "9521", "42290": "9522", "42291": "9523", "42292": "9524", "42293": "9525",
+    "42294": "9526", "42295": "9527", "42296": "9528", "42297": "9529", "42298": "9530", "42299": "9531",
+    "42300": "9532", "42301": "9533", "42302": "9534", "42303": "9535", "42304": "9536", "42305": "9537",
+    "42306": "9538", "42307": "9539", "42308": "9540", "42309": "9541", "42310": "9542", "42311": "9543",
+    "42312": "9544", "42313": "9545", "42314": "9546", "42315": "9547", "42316": "9548", "42317": "9549",
+}
+
+# gate_feature_list (rank/ctr/base_model.py:122): structure fields that also feed the ppnet gate
+# input of the MMoE experts (duplicates kept as the reference lists them; membership is what
+# counts)
+GATE_FEATURE_LIST: tuple = ("1568", "1570", "1578", "1591", "1593", "1614", "1736", "1737", "2039", "2599", "3051", "3303", "3389", "1576", "1577", "1578")
 
 
 @dataclass
