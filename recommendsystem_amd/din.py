@@ -122,6 +122,11 @@ class _DINBase(nn.Module):
                              f"{tuple(keys.shape)}")
         if not self.built:
             self.build(tuple(keys.shape), device=keys.device)
+        from . import ops
+        if ops.custom_ops_enabled():  # torch.ops.ctr.din_pool (traceable, functional grads)
+            v = keys if values is None else values
+            return torch.ops.ctr.din_pool(q, keys, v, lengths, mask, self.W1, self.b1, self.W2,
+                                          self.b2, self.VARIANT)[0]
         return _DINFn.apply(q, keys, values, lengths, mask, self.W1, self.b1, self.W2, self.b2,
                             self.VARIANT)
 

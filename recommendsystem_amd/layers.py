@@ -145,6 +145,11 @@ class InteractingLayer(nn.Module):
         drop = self.dropout_rate if (self.use_dropout and self.training) else 0.0
         seed = (self.seed * 1000003 + self._calls) & 0xFFFFFFFFFFFFFFFF
         self._calls += 1
+        from . import ops
+        if ops.custom_ops_enabled():  # torch.ops.ctr.interacting_fwd (traceable, functional grads)
+            return ops.interacting_layer(inputs.float(), self.kernel, self.bias, self.gamma,
+                                         self.beta, self.layer_num, self.head_num, self.use_res,
+                                         self.epsilon, drop, seed)
         return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
                                     self, seed, drop)
 
@@ -215,6 +220,10 @@ class Dense(nn.Module):
         if not self.built:
             self.build(tuple(x.shape), device=x.device)
         lead = x.shape[:-1]  # Keras Dense = tensordot over the last axis
+        from . import ops
+        if ops.custom_ops_enabled():
+            y = torch.ops.ctr.dense(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act)
+            return y.reshape(*lead, self.units)
         y = _DenseFn.apply(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act)
         return y.reshape(*lead, self.units)
 

@@ -1,0 +1,104 @@
+"""torch.library custom ops (recommendsystem_amd/ops.py, torch.ops.ctr.*): torch.library.opcheck
+(schema, fake/meta kernels, autograd registration, AOTAutograd dispatch) on each op, parity of
+the op path with the layer path, and a torch.compile(backend="aot_eager") trace of a model that
+routes its layers through the ops."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from _tol import assert_close, assert_grad_close, to_np
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _ops():
+    from recommendsystem_amd import ops  # noqa: F401 (registers torch.ops.ctr)
+    yield
+    ops.use_custom_ops(False)
+
+
+def _il_args(B=6, F=26, E=16, U=16, L=3, H=2, drop=0.0, grad=True):
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = (torch.rand(B, F, E, device=DEV, generator=g) - 0.5).requires_grad_(grad)
+    W = ((torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.5).requires_grad_(grad)
+    b = ((torch.rand(4 * U, device=DEV, generator=g) - 0.5) * 0.1).requires_grad_(grad)
+    gm = (1 + (torch.rand(U, device=DEV, generator=g) - 0.5) * 0.1).requires_grad_(grad)
+    bt = ((torch.rand(U, device=DEV, generator=g) - 0.5) * 0.1).requires_grad_(grad)
+    return (x, W, b, gm, bt, L, H, True, 1e-14, drop, 12345)
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.2])
+def test_opcheck_interacting(drop):
+    torch.library.opcheck(torch.ops.ctr.interacting_fwd.default, _il_args(drop=drop))
+
+
+def test_opcheck_dense_and_din_and_lookup():
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.rand(33, 40, device=DEV, generator=g).requires_grad_(True)
+    W = (torch.rand(40, 24, device=DEV, generator=g) - 0.5).requires_grad_(True)
+    b = (torch.rand(24, device=DEV, generator=g) - 0.5).requires_grad_(True)
+    for act in (0, 1, 2):
+        torch.library.opcheck(torch.ops.ctr.dense.default, (x, W, b, act))
+    B, T, H = 5, 12, 16
+    q = torch.rand(B, H, device=DEV, generator=g).requires_grad_(True)
+    k = torch.rand(B, T, H, device=DEV, generator=g).requires_grad_(True)
+    v = torch.rand(B, T, H, device=DEV, generator=g).requires_grad_(True)
+    lens = torch.tensor([12, 3, 7, 12, 1], dtype=torch.int32, device=DEV)
+    W1 = (torch.rand(3 * H, 16, device=DEV, generator=g) - 0.5).requires_grad_(True)
+    b1 = torch.zeros(16, device=DEV).requires_grad_(True)
+    W2 = (torch.rand(16, 1, device=DEV, generator=g) - 0.5).requires_grad_(True)
+    b2 = torch.zeros(1, device=DEV).requires_grad_(True)
+    torch.library.opcheck(torch.ops.ctr.din_pool.default, (q, k, v, lens, None, W1, b1, W2, b2, 0))
+    W1s = (torch.rand(4 * H, 16, device=DEV, generator=g) - 0.5).requires_grad_(True)
+    mask = torch.rand(B, T, device=DEV, generator=g) < 0.7
+    torch.library.opcheck(torch.ops.ctr.din_pool.default, (q, k, k, None, mask, W1s, b1, W2, b2, 1))
+    table = torch.rand(1000, 16, device=DEV)
+    ids = torch.randint(0, 5000, (7, 4), device=DEV)
+    rb = torch.tensor([0, 250, 500, 750], device=DEV)
+    bk = torch.full((4,), 250, device=DEV, dtype=torch.int64)
+    torch.library.opcheck(torch.ops.ctr.embedding_lookup.default, (ids, None, rb, bk, 0, 1, table))
+
+
+def test_op_path_matches_layer_path():
+    from recommendsystem_amd import ops
+    from recommendsystem_amd.layers import InteractingLayer
+    il = InteractingLayer(3, 16, 2, use_res=True, seed=5, device=DEV)
+    x = (torch.rand(9, 26, 16, device=DEV) - 0.5).requires_grad_(True)
+    y0 = il(x)
+    y0.sum().backward()
+    gx0, gW0 = x.grad.clone(), il.kernel.grad.clone()
+    x.grad = None
+    il.kernel.grad.zero_()
+    ops.use_custom_ops(True)
+    y1 = il(x)
+    y1.sum().backward()
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, x.grad)
+    assert torch.equal(gW0, il.kernel.grad)
+
+
+def test_compile_aot_eager_traces_the_ops():
+    from recommendsystem_amd import ops
+    from recommendsystem_amd.layers import Dense, InteractingLayer
+    ops.use_custom_ops(True)
+    il = InteractingLayer(3, 16, 2, use_res=True, seed=7, device=DEV)
+    il.build((1, 26, 16), device=DEV)
+    head = Dense(1, "sigmoid", seed=8, device=DEV)
+    head.build((1, 26 * 16), device=DEV)
+
+    def f(x):
+        return head(il(x).reshape(x.shape[0], -1))
+
+    x = (torch.rand(8, 26, 16, device=DEV) - 0.5)
+    y_eager = f(x)
+    cf = torch.compile(f, backend="aot_eager", fullgraph=True)
+    il._calls = 0
+    y_c = cf(x)
+    assert_close(to_np(y_c), to_np(y_eager), 1e-6, what="compiled vs eager")
+    xr = x.clone().requires_grad_(True)
+    cf(xr).sum().backward()
+    assert xr.grad is not None and torch.isfinite(xr.grad).all()
