@@ -28,7 +28,10 @@ import torch  # noqa: E402
 IL_FWD_FLOPS_PER_SAMPLE = 289_536          # 3 iterations x (proj 53,248 + QK^T 21,632 + PV 21,632)
 TRAIN_FLOPS_PER_SAMPLE = 954_144           # IL 868,608 + MLP 85,536 (train = 3 x fwd)
 FP32_PEAK_TFLOPS = 157.3                   # MI355X dense fp32 (MFMA == vector rate)
+BF16_PEAK_TFLOPS = 2500.0                  # MI355X dense bf16 MFMA (BASELINE.md §3 basis)
 HBM_PEAK_GBS = 8000.0
+STEP_BYTES_PER_SAMPLE = 3_540              # ids + label + gather + row grads
+ADAM_BYTES_PER_ROW = 384                   # + 6 x 16 x 4 B per unique touched row (sparse Adam)
 
 
 def parse():
@@ -77,10 +80,12 @@ def time_kernel(fn, reps):
 
 
 def cpu_baseline(cfg, model, batches_cpu, seconds):
+    """BASELINE.md §2: the fp32 torch-CPU restatement (oracle/torch_ref.py::AutoIntCPU, TF op
+    order) on the host cores, all cores and 1 thread, median of 3 runs each.  Bounded: each run
+    takes whole train steps until seconds / 6 have passed (>= 2 steps)."""
     from oracle import torch_ref as tr
     # the box's CPU share (OMP_NUM_THREADS is set to it; affinity shows the whole machine)
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
     il = {k: v.detach().double().cpu().numpy() for k, v in
           dict(W=model.interact.kernel, bias=model.interact.bias, gamma=model.interact.gamma,
                beta=model.interact.beta).items()}
@@ -91,22 +96,32 @@ def cpu_baseline(cfg, model, batches_cpu, seconds):
     ref = tr.AutoIntCPU(model.table.weight.cpu().numpy(), model.embedding.row_base.cpu().numpy(),
                         model.embedding.bucket.cpu().numpy(), il, deep, logits, ocfg,
                         dtype=torch.float32)
-    ids, labels = batches_cpu[0]
-    ref.step(ids, labels)  # warm-up
-    t0 = time.perf_counter()
-    n = 0
-    while n < 3 or time.perf_counter() - t0 < seconds:
-        ids, labels = batches_cpu[n % len(batches_cpu)]
-        ref.step(ids, labels)
-        n += 1
-    dt = time.perf_counter() - t0
-    steps = n
-    B = ids.shape[0]
-    return {"value": round(B * steps / dt, 1), "unit": "samples/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"{steps} AutoInt train steps at batch {B} (26x16, IL x3, MLP, Adam) of the "
-                      f"TF-semantics fp32 torch-CPU restatement (oracle/torch_ref.py), "
-                      f"{threads} threads, {dt:.1f}s"}
+    B = batches_cpu[0][0].shape[0]
+    per_run = max(seconds / 6.0, 0.5)
+
+    def runs(n_threads):
+        torch.set_num_threads(n_threads)
+        ref.step(*batches_cpu[0])  # warm-up
+        rates, steps_total = [], 0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            n = 0
+            while n < 2 or time.perf_counter() - t0 < per_run:
+                ref.step(*batches_cpu[n % len(batches_cpu)])
+                n += 1
+            rates.append(B * n / (time.perf_counter() - t0))
+            steps_total += n
+        return float(np.median(rates)), steps_total
+
+    multi, n_multi = runs(threads)
+    single, n_single = runs(1)
+    torch.set_num_threads(threads)
+    return {"value": round(multi, 1), "unit": "samples/sec", "cores": threads, "kind": "port",
+            "single_thread": {"value": round(single, 1), "cores": 1},
+            "sample": f"AutoInt train steps at batch {B} (26x16, IL x3, MLP, dense + sparse Adam) of "
+                      f"the TF-semantics fp32 torch-CPU restatement (oracle/torch_ref.py): median of 3 "
+                      f"runs of >= {per_run:.1f} s each, {n_multi} steps on {threads} threads and "
+                      f"{n_single} steps on 1 thread"}
 
 
 WORKLOADS = {
@@ -297,6 +312,16 @@ def main():
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     samples = B * args.steps * world
+    # BASELINE.md §3 step roofline: max(sum bytes / HBM BW, sum flops / peak), per GPU
+    rb = model.embedding.row_base.cpu().numpy()[None, :]
+    uniq = int(np.mean([np.unique(rb + np.remainder(i.numpy(), cfg.vocab_per_field)).size
+                        for i, _ in pool_cpu]))
+    step_bytes = B * STEP_BYTES_PER_SAMPLE + ADAM_BYTES_PER_ROW * uniq
+    step_flops = B * TRAIN_FLOPS_PER_SAMPLE
+    t_bytes = step_bytes / (HBM_PEAK_GBS * 1e9)
+    t_bf16 = step_flops / (BF16_PEAK_TFLOPS * 1e12)
+    t_fp32 = step_flops / (FP32_PEAK_TFLOPS * 1e12)
+    step_s = dt / args.steps
     out = {
         "metric": "samples/sec AutoInt CTR train, 26 fields×16-dim emb, batch 4096, 1/2/4/8 GPU",
         "value": round(samples / dt, 1),
@@ -320,6 +345,14 @@ def main():
                      "launch_us": round(t_bwd * 1e6, 2),
                      "flops_per_launch": bwd_flops},
         "il_fwd_us": round(t_fwd * 1e6, 2),
+        "step_roofline": {
+            "bytes_per_step": step_bytes, "flops_per_step": step_flops, "unique_rows": uniq,
+            "t_bytes_us": round(t_bytes * 1e6, 3), "t_flops_bf16_us": round(t_bf16 * 1e6, 3),
+            "t_flops_fp32_us": round(t_fp32 * 1e6, 3),
+            "frac_bf16_basis": round(max(t_bytes, t_bf16) / step_s, 4),
+            "frac_fp32_basis": round(max(t_bytes, t_fp32) / step_s, 4),
+            "note": "BASELINE.md §3: fraction = roofline time / measured step time; the bf16 "
+                    "basis is the config's stated compute dtype, this step computes in fp32"},
         "step_tflops": round(TRAIN_FLOPS_PER_SAMPLE * samples / dt / 1e12, 3),
         "final_loss": round(loss, 6),
         "cpu_baseline": None,

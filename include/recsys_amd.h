@@ -403,8 +403,9 @@ int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float
                    const int32_t* rows, float* grad_table, int32_t* flag, float* dparams,
                    int dparams_accumulate, float* workspace, int64_t workspace_floats);
 
-/* Grid (= number of per-block partial rows) rs_il_bwd uses for a given batch and workspace. */
-int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats);
+/* Grid (= number of per-block partial rows) rs_il_bwd / rs_il_bwd_push use for this shape and
+ * workspace when dy rows are 16-B aligned (dy_ld % 4 == 0); 0 for an unsupported shape. */
+int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t workspace_floats);
 
 
 /* ---------------------------------------------------------------------------------------

@@ -106,7 +106,7 @@ SIGNATURES: dict[str, tuple] = {
                                  _f32, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
     "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
-    "rs_il_bwd_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i64]),
+    "rs_il_bwd_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i32, _i64]),
     "rs_sparse_adam_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
                                    _f32, _f32]),
     "rs_sparse_adagrad_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),

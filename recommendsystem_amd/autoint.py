@@ -249,7 +249,7 @@ class AutoIntTrainer:
                     blocks=int(lib.rs_mlp_head_partial_blocks(self.B)),
                     il_off=il_off, il_n=il_n,
                     il_blocks=int(lib.rs_il_bwd_partial_blocks(self.B, self.F, self.E, self.U,
-                                                               self.il_ws_n)),
+                                                               self.H, self.il_ws_n)),
                     done=torch.zeros(288, device=dev, dtype=torch.int32))
 
     def _forward_backward_fused(self):

@@ -77,6 +77,9 @@ struct BwdReq {
   const int32_t* push_rows = nullptr;
   float* push_table = nullptr;
   int32_t* push_flag = nullptr;
+  // dry run: write the grid (= number of per-block partial rows) the launch would use and
+  // return without launching (rs_il_bwd_partial_blocks)
+  int* grid_out = nullptr;
 };
 
 constexpr int kMaxFwdWaves = 4;
@@ -533,6 +536,68 @@ __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, cons
       }
     }
   }
+}
+
+// dx of ALL row tiles of the sample at once (one wave owns the sample): the tiles' MFMA chains
+// (and, with RS_IL_DX_KH > 1, k parts of each tile) run as independent accumulators, then each
+// result goes to `emit(rt, et, r, f, e, value)`
+// (rt, et, r compile-time after unrolling: per-lane arrays indexed by them stay in registers).
+// Summation per k part in c order, parts added in order -- fixed, deterministic.
+template <class C, class Emit>
+__device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C>& w, Emit emit) {
+  using M = MfmaW<C>;
+  constexpr int NRT = (C::FMAX + 15) / 16;
+#ifndef RS_IL_DX_KH
+#define RS_IL_DX_KH 1
+#endif
+  constexpr int KH = M::CS % RS_IL_DX_KH == 0 ? RS_IL_DX_KH : 1;  // independent k parts
+  constexpr int CSH = M::CS / KH;
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  f32x4 acc[NRT][KH][M::ET];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+      for (int et = 0; et < M::ET; ++et) acc[rt][kh][et] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cc = 0; cc < CSH; ++cc) {
+    float a4[NRT][KH][4];
+#pragma unroll
+    for (int rt = 0; rt < NRT; ++rt) {
+      const int arow = 16 * rt + j;
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        const int cs = kh * CSH + cc;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (arow < F) v = *reinterpret_cast<const float4*>(G + arow * C::PRS + 16 * cs + 4 * q);
+        a4[rt][kh][0] = v.x; a4[rt][kh][1] = v.y; a4[rt][kh][2] = v.z; a4[rt][kh][3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+          for (int et = 0; et < M::ET; ++et)
+            acc[rt][kh][et] = mfma_16x16x4(a4[rt][kh][t], w.wx[kh * CSH + cc][t][et], acc[rt][kh][et]);
+  }
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et) {
+      const int e = 16 * et + j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * rt + 4 * q + r;
+        float v = acc[rt][0][et][r];
+#pragma unroll
+        for (int kh = 1; kh < KH; ++kh) v += acc[rt][kh][et][r];
+        if (f < F && e < C::E) emit(rt, et, r, f, e, v);
+      }
+    }
 }
 
 // ---- phase: attention forward; optionally keeps P (pre-dropout) for backward ----------------
@@ -1464,6 +1529,399 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
     partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
 }
 
+// ============================== backward kernel, v3 ===========================================
+// One wave = one sample at a time, kWpb3 waves (samples) per block sharing the block-resident W
+// and bias in LDS.  Every phase is wave-local: no workgroup barrier and no partial-row exchange
+// inside the sample loop (v2's 17 barriers and split-j exchanges per sample-iteration were where
+// its waves parked), at the price of 2 waves per SIMD (LDS: ~18 KB per sample).  The next
+// iteration's input rows and the next sample's dy rows are prefetched into registers while the
+// current iteration runs, and written to LDS at the next iteration's start.
+//   P1 projections (MFMA, both row tiles)      P2 attention recompute (lane = (head, row),
+//   P3 LN + ReLU backward (O <- dt, R <- gR)       every key; P stored pre-dropout)
+//   P4 dV (lane = (head, key)) -> DY           P5 dS (in place of P), dQ -> O
+//   P6 dK -> K <- gK; V <- gV, Q <- gQ         P7 dW, db += X^T G; dx = G W^T (-> DY / push)
+constexpr int kWpb3 = 4;
+
+template <class C>
+struct Bwd3Layout {
+  // per-wave region (floats): X | PR (FMAX rows) | O | DY | PM | ST (mean, rstd per row)
+  int x, pr, o, dy, pm, st, per_wave;
+  __host__ __device__ Bwd3Layout(int F) {
+    int off = 0;
+    x = off; off += (F * C::E + 3) & ~3;
+    pr = off; off += (C::FMAX * C::PRS + 3) & ~3;
+    o = off; off += (F * C::OS + 3) & ~3;
+    dy = off; off += (F * C::U + 3) & ~3;
+    pm = off; off += (C::H * F * C::PMS + 3) & ~3;
+    st = off; off += (2 * F + 3) & ~3;
+    per_wave = off;
+  }
+  static constexpr int shared_floats() {  // W [E][WPS] | bias [NC]
+    return ((C::E * C::WPS + 3) & ~3) + ((C::NC + 3) & ~3);
+  }
+};
+
+// n4 float4 of a global row block -> registers (PF float4 per lane) / registers -> LDS
+template <int PF>
+__device__ __forceinline__ void row_prefetch(float4 (&r)[PF], const float* src, int n4) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    const int i = lane + 64 * k;
+    if (i < n4) r[k] = reinterpret_cast<const float4*>(src)[i];
+  }
+}
+
+template <int PF>
+__device__ __forceinline__ void row_commit(float* dst, const float4 (&r)[PF], int n4) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {
+    const int i = lane + 64 * k;
+    if (i < n4) reinterpret_cast<float4*>(dst)[i] = r[k];
+  }
+}
+
+template <class C, bool DROP>
+#ifndef RS_IL_BWD3_OCC
+#define RS_IL_BWD3_OCC 2
+#endif
+__global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
+    const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
+    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
+    int dx_accumulate, float* __restrict__ partials, Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int F = C::EXACT ? C::FMAX : a.F;
+  const Bwd3Layout<C> lay(F);
+  float* const WL = smem;
+  float* const BL = smem + ((C::E * C::WPS + 3) & ~3);
+  float* const base = smem + Bwd3Layout<C>::shared_floats() + wave_id() * lay.per_wave;
+  float* const X = base + lay.x;
+  float* const PR = base + lay.pr;
+  float* const O = base + lay.o;
+  float* const DY = base + lay.dy;
+  float* const PM = base + lay.pm;
+  float* const ST = base + lay.st;
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int HF = C::H * F;
+  const int nrt = (F + 15) / 16;
+
+  for (int k = threadIdx.x; k < C::E * C::NC; k += blockDim.x)
+    WL[(k / C::NC) * C::WPS + k % C::NC] = W[k];
+  for (int k = threadIdx.x; k < C::NC; k += blockDim.x) BL[k] = bias[k];
+  zero_pad_rows<C>(PR, F);
+  __syncthreads();  // the only workgroup barrier before the final reduction
+
+  using M = MfmaW<C>;
+  f32x4 dwacc[M::ET][M::NT];
+  float dbp[M::NT];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
+  float dg[C::CPLN], dbt[C::CPLN], gam[C::CPLN];
+  const int u0 = lane % C::LPR;
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
+
+  constexpr int PFX = (C::FMAX * C::E / 4 + 63) / 64;  // float4 per lane of one sample's rows
+  constexpr int PFY = (C::FMAX * C::U / 4 + 63) / 64;
+  const int nx4 = F * C::E / 4, ny4 = F * C::U / 4;
+  auto x_src = [&](int64_t bb, int itx) -> const float* {
+    return itx == 0 ? x + bb * F * C::E : xsave + ((int64_t)(itx - 1) * a.B + bb) * F * C::U;
+  };
+  const int64_t b_first = (int64_t)blockIdx.x * kWpb3 + w;
+  const int64_t b_step = (int64_t)gridDim.x * kWpb3;
+  float4 px[PFX], py[PFY];
+  if (b_first < a.B) {
+    row_prefetch<PFX>(px, x_src(b_first, a.L - 1), nx4);
+    row_prefetch<PFY>(py, dy + b_first * dy_ld, ny4);  // dy_vec: rows 16-B aligned
+  }
+
+  IL_STAMP_DECL
+  for (int64_t b = b_first; b < a.B; b += b_step) {
+#ifndef RS_BWD3_NOPF
+    row_commit<PFY>(DY, py, ny4);
+#endif
+    for (int it = a.L - 1; it >= 0; --it) {
+      IL_STAMP(0)
+      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+#ifdef RS_BWD3_NOPF
+      row_prefetch<PFX>(px, x_src(b, it), nx4);
+      if (it == a.L - 1) { row_prefetch<PFY>(py, dy + b * dy_ld, ny4); row_commit<PFY>(DY, py, ny4); }
+      row_commit<PFX>(X, px, nx4);
+#else
+      row_commit<PFX>(X, px, nx4);
+      {  // prefetch the next iteration's input (and the next sample's dy) into registers
+        const int64_t bn = it > 0 ? b : b + b_step;
+        if (bn < a.B) {
+          row_prefetch<PFX>(px, x_src(bn, it > 0 ? it - 1 : a.L - 1), nx4);
+          if (it == 0) row_prefetch<PFY>(py, dy + bn * dy_ld, ny4);
+        }
+      }
+#endif
+      wave_lds_sync();
+      IL_STAMP(1)
+      // ---- P1: projections ----
+      {
+        MfmaW<C> mw;
+        mw.load_proj_lds(WL, BL);
+        for (int rt = 0; rt < nrt; ++rt) mfma_project<C>(X, PR, F, rt, mw);
+      }
+      wave_lds_sync();
+      IL_STAMP(2)
+      // ---- P2: attention recompute; P (pre-dropout) -> PM, O ----
+      attention_fwd<C, true, DROP, C::OS>(PR, O, PM, a, b, lseed);
+      wave_lds_sync();
+      IL_STAMP(3)
+      // ---- P3: z = relu(O + R), LN stats, LN + ReLU backward: O <- dt; R <- gR ----
+      for (int f0 = 0; f0 < F; f0 += C::RG) {
+        const int f = f0 + lane / C::LPR;
+        const bool act = f < F;
+        float z[C::CPLN], rr[C::CPLN];
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          float t = act ? O[f * C::OS + u] : 0.f;
+          rr[c] = (a.use_res && act) ? PR[f * C::PRS + 3 * C::U + u] : 0.f;
+          t += rr[c];
+          z[c] = fmaxf(t, 0.f);
+          sum += z[c];
+        }
+        const float mean = group_sum<C::LPR>(sum) * (1.0f / (float)C::U);
+        float sq = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
+        const float var = group_sum<C::LPR>(sq) * (1.0f / (float)C::U);
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        float zh[C::CPLN], g[C::CPLN];
+        float sg = 0.f, sgz = 0.f;
+#pragma unroll
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          zh[c] = (z[c] - mean) * rstd;
+          const float dyv = act ? DY[f * C::U + u] : 0.f;
+          dg[c] = fmaf(dyv, zh[c], dg[c]);
+          dbt[c] += dyv;
+          g[c] = dyv * gam[c];
+          sg += g[c];
+          sgz += g[c] * zh[c];
+        }
+        sg = group_sum<C::LPR>(sg) * (1.0f / (float)C::U);
+        sgz = group_sum<C::LPR>(sgz) * (1.0f / (float)C::U);
+        if (act) {
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
+            const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+            O[f * C::OS + u] = dt;
+            PR[f * C::PRS + 3 * C::U + u] = (a.use_res && rr[c] > 0.f) ? dt : 0.f;
+          }
+        }
+      }
+      wave_lds_sync();
+      IL_STAMP(4)
+      // ---- P4: dV_j = sum_i Pd_ij dO_i (lane = (h, j)) -> DY[j][h dh + d] ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dv[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
+#pragma unroll 4
+        for (int i = 0; i < F; ++i) {
+          float p = PM[(h * F + i) * C::PMS + j];
+          if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+          axpy_row(dv, p, O + i * C::OS + h * C::DH);
+        }
+        if (act) store_row(DY + j * C::U + h * C::DH, dv);
+      }
+      wave_lds_sync();
+      IL_STAMP(5)
+      // ---- P5: dS (in place of P) and dQ (lane = (h, i)) -> O ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, i = act ? r % F : 0;
+        float dO[C::DH];
+        load_row(dO, O + i * C::OS + h * C::DH);
+        const float* vb = PR + 2 * C::U + h * C::DH;
+        const float* kb = PR + C::U + h * C::DH;
+        float* pm_row = PM + (h * F + i) * C::PMS;
+        // two passes over the keys (dP_ij recomputed in the second) instead of a dP row in
+        // registers: one wave holds the whole sample, and 26 live dP values per lane pushed v3
+        // past 256 VGPRs into scratch
+        float D = 0.f;
+#pragma unroll 2
+        for (int j = 0; j < F; ++j) {
+          float dp = dot_row(dO, vb + j * C::PRS);
+          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          D = fmaf(pm_row[j], dp, D);
+        }
+        float dq[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
+#pragma unroll 2
+        for (int j = 0; j < F; ++j) {
+          float dp = dot_row(dO, vb + j * C::PRS);
+          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          const float ds = pm_row[j] * (dp - D) * a.inv_sdh;
+          axpy_row(dq, ds, kb + j * C::PRS);
+          if (act) pm_row[j] = ds;
+        }
+        if (act) store_row(O + i * C::OS + h * C::DH, dq);  // dO_i (read above) dies here
+      }
+      wave_lds_sync();
+      IL_STAMP(6)
+      // ---- P6: dK_j = sum_i dS_ij Q_i (lane = (h, j)); K <- gK ----
+      for (int r0 = 0; r0 < HF; r0 += 64) {
+        const int r = r0 + lane;
+        const bool act = r < HF;
+        const int h = act ? r / F : 0, j = act ? r % F : 0;
+        float dk[C::DH];
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
+#pragma unroll 4
+        for (int i = 0; i < F; ++i) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+        float kr[C::DH];
+        load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] : 0.f;
+        // every lane's K reads (here) precede any K write of the same row: row j is read only
+        // by lane (h, j) in this pass
+        if (act) store_row(PR + j * C::PRS + C::U + h * C::DH, kr);
+      }
+      wave_lds_sync();  // all dK reads of Q done
+      for (int k = lane; k < F * C::U; k += 64) {  // V <- gV (DY), Q <- gQ (O)
+        const int f = k / C::U, c = k % C::U;
+        float* vq = PR + f * C::PRS + 2 * C::U + c;
+        float* qq = PR + f * C::PRS + c;
+        const float gv = DY[k], gq = O[f * C::OS + c];
+        const float v0 = *vq, q0 = *qq;
+        *vq = v0 > 0.f ? gv : 0.f;
+        *qq = q0 > 0.f ? gq : 0.f;
+      }
+      wave_lds_sync();
+      IL_STAMP(7)
+      // ---- P7: dW += X^T G, db += colsum G; dx = G W^T ----
+      for (int rt = 0; rt < nrt; ++rt) mfma_dw<C>(X, PR, F, rt, dwacc, dbp);
+      __builtin_amdgcn_sched_barrier(0);
+      IL_STAMP(8)
+      {
+        MfmaW<C> mw;
+        mw.load_dx_lds(WL);
+        if (it > 0) {  // dL/d(previous output) -> DY
+          mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { DY[f * C::U + e] = v; });
+        } else if (a.push_table) {
+          // fused sparse push: row index and the head's share loaded before the MFMAs; rows
+          // f >= F and rows < 0 (ids outside the table) push nothing
+          constexpr int NRT = (C::FMAX + 15) / 16;
+          const int q = lane >> 4, jx = lane & 15;
+          int32_t rw[NRT][4];
+          float bv[NRT][M::ET][4];
+          const int32_t* rows = a.push_rows + b * F;
+          const float* base_g = dx_accumulate ? dx + b * F * C::E : nullptr;
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int f = 16 * rt + 4 * q + r;
+              rw[rt][r] = f < F ? rows[f] : -1;
+#pragma unroll
+              for (int et = 0; et < M::ET; ++et) {
+                const int e = 16 * et + jx;
+                bv[rt][et][r] = (base_g && f < F && e < C::E) ? base_g[f * C::E + e] : 0.f;
+              }
+            }
+          mfma_dx_all<C>(PR, F, mw, [&](int rt, int et, int r, int, int e, float v) {
+            const int32_t row = rw[rt][r];
+            if (row >= 0) {
+              if (e == 0) scan_mark(a.push_flag, row);
+              atomicAdd(a.push_table + (int64_t)row * C::E + e, v + bv[rt][et][r]);
+            }
+          });
+        } else {
+          float* d = dx + b * F * C::E;
+          if (dx_accumulate)
+            mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { d[f * C::E + e] += v; });
+          else
+            mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { d[f * C::E + e] = v; });
+        }
+      }
+      wave_lds_sync();
+      IL_STAMP(9)
+    }
+  }
+  IL_STAMP_FLUSH(a.stamps)
+
+  // ---- lanes -> wave -> block (wave order 0..kWpb3-1): deterministic ----
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) {
+    dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
+    dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
+  }
+#pragma unroll
+  for (int c = 0; c < C::CPLN; ++c) {
+#pragma unroll
+    for (int o = C::LPR; o < 64; o <<= 1) {
+      dg[c] += __shfl_xor(dg[c], o, 64);
+      dbt[c] += __shfl_xor(dbt[c], o, 64);
+    }
+  }
+  __syncthreads();
+  float* RED = smem;  // W / per-wave regions are dead now
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
+  __syncthreads();
+  {
+    const int q = lane >> 4, jx = lane & 15;
+    for (int ww = 0; ww < kWpb3; ++ww) {
+      if (w == ww) {
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int e = 16 * et + 4 * q + r;
+              if (e < C::E) RED[e * C::NC + 16 * nt + jx] += dwacc[et][nt][r];
+            }
+        if (q == 0) {
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + jx] += dbp[nt];
+        }
+        if (lane < C::LPR) {
+#pragma unroll
+          for (int c = 0; c < C::CPLN; ++c) {
+            const int u = u0 + c * C::LPR;
+            RED[C::E * C::NC + C::NC + u] += dg[c];
+            RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
+    partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
+}
+
+// v3 fits when kWpb3 sample regions + W give 2 blocks per CU; otherwise v2 runs
+template <class C>
+__host__ __forceinline__ size_t bwd3_lds_bytes(int F) {
+  return ((size_t)Bwd3Layout<C>::shared_floats() + (size_t)kWpb3 * Bwd3Layout<C>(F).per_wave) * 4;
+}
+
+// one resident round of v3 blocks on MI355X (2 per CU x 256 CUs); callers size the per-block
+// partial rows with rs_il_bwd_partial_blocks, which applies the same rule
+constexpr int kBwd3Grid = 512;
+
 // grid-level reduction of the per-block partials, fixed order (deterministic); interacting.hip
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
                    int accumulate);
@@ -1501,10 +1959,29 @@ int bwd_launch(const BwdReq& q) {
   a.push_table = q.push_table;
   a.push_flag = q.push_flag;
   a.dy_vec = (q.dy_ld % 4 == 0) && ((uintptr_t)q.dy % 16 == 0);
+  // x / xsave rows are copied 16 B at a time
+  if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
+#ifndef RS_IL_BWD_NO_V3
+  {  // v3 (one wave per sample, no workgroup barriers) when its LDS gives 2 blocks per CU
+    const size_t lds3 = bwd3_lds_bytes<C>(q.F);
+    if (a.dy_vec && lds3 <= kLdsBytes / 2 && (size_t)C::NPARAM * 4 <= lds3) {
+      int64_t grid = (q.B + kWpb3 - 1) / kWpb3;
+      const int64_t max_grid = q.workspace_floats / C::NPARAM;
+      if (grid > kBwd3Grid) grid = kBwd3Grid;
+      if (grid > max_grid) grid = max_grid;
+      if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
+      if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
+      bwd3_kernel<C, DROP><<<(int)grid, 64 * kWpb3, lds3, q.stream>>>(
+          q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
+          q.workspace, a);
+      if (q.dparams)
+        reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+      return rs_status_after_launch();
+    }
+  }
+#endif
   const size_t lds = (size_t)a.per_wave * sizeof(float);
   if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
-  // x / xsave rows are copied to LDS 16 B at a time
-  if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
   // kMaxBwdGrid = one resident round of this kernel on MI355X (6 blocks per CU x 256 CUs at
   // config 2), so no block waits for a second round while others idle.  A fixed rule (not an
   // occupancy query) because callers size the partial-row reduction with
@@ -1513,6 +1990,7 @@ int bwd_launch(const BwdReq& q) {
   const int64_t max_grid = q.workspace_floats / C::NPARAM;
   if (grid > kMaxBwdGrid) grid = kMaxBwdGrid;
   if (grid > max_grid) grid = max_grid;
+  if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
   if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
   bwd2_kernel<C, DROP><<<(int)grid, 128, lds, q.stream>>>(
       q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,

@@ -122,10 +122,22 @@ RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, cons
   return bwd_small(q);
 }
 
-RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int64_t workspace_floats) {
-  (void)F;  // both kernel families use the same grid rule
-  int64_t grid = B < rs_il::kMaxBwdGrid ? B : rs_il::kMaxBwdGrid;
-  const int64_t by_ws = workspace_floats / rs_il_param_count(E, U);
-  if (grid > by_ws) grid = by_ws;
-  return (int)(grid < 0 ? 0 : grid);
+RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
+                                    int64_t workspace_floats) {
+  if (F > 64) {  // il_large.hip's grid rule
+    int64_t grid = B < rs_il::kMaxBwdGrid ? B : rs_il::kMaxBwdGrid;
+    const int64_t by_ws = workspace_floats / rs_il_param_count(E, U);
+    if (grid > by_ws) grid = by_ws;
+    return (int)(grid < 0 ? 0 : grid);
+  }
+  // the F <= 64 kernels pick v3 or v2 per shape: ask the dispatch (dry run, nothing launched).
+  // Pointers only need the alignment the real call has (the fused trainer's dy is 16-B aligned).
+  static const float kDummy[4] __attribute__((aligned(16))) = {0.f, 0.f, 0.f, 0.f};
+  int grid = 0;
+  rs_il::BwdReq q{nullptr, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy,
+                  (int64_t)F * U, B, F, E, U, H, 1, 1, 1e-14f, 0.f, 0, nullptr, 0, nullptr, 0,
+                  nullptr, workspace_floats};
+  q.grid_out = &grid;
+  if (bwd_small(q) != RS_OK) return 0;
+  return grid;
 }

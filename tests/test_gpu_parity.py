@@ -338,7 +338,7 @@ def test_interacting_backward_fused_push(with_base):
             want[r[k]] += dxn[k]
     assert_grad_close(_np(table), want, what="pushed rows")
     assert _scan_marked(flag, 50) == set(r[r >= 0].tolist())
-    nb = int(lib.rs_il_bwd_partial_blocks(B, F, E, U, wsn))
+    nb = int(lib.rs_il_bwd_partial_blocks(B, F, E, U, H, wsn))
     npar = int(lib.rs_il_param_count(E, U))
     assert torch.equal(ws1[:nb * npar], ws2[:nb * npar])
 
