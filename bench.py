@@ -47,7 +47,13 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU sample: run whole train steps until this much time passed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="configs 3-5: run the autograd step eagerly instead of replaying graphs")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
+                    help="config 2 compute mode of the headline line (f32 = the reference's math)")
+    ap.add_argument("--no-bf16", action="store_true",
+                    help="skip the nested bf16-mode result of the f32 run")
     ap.add_argument("--workload", default="autoint",
                     choices=["autoint", "multi_head", "din", "staytime"],
                     help="autoint = the headline (configs[1]); the others are configs 3-5 at their "
@@ -157,15 +163,22 @@ def run_workload(args, world, rank, dev, pg):
         model = W.StaytimeRoughRank(device=dev, seed=0)
         trainer = Trainer(model, 5e-4, [model.table], process_group=pg)
         pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
+    graphed = world == 1 and not args.eager
+    if graphed:  # one HIP graph per pool batch (forward + autograd backward + optimizers)
+        trainer.capture_pool(pool, warmup=1)
+        step = trainer.step_pool
+    else:
+        def step(i):
+            return trainer.step(*pool[i % len(pool)])
     for i in range(args.warmup):
-        trainer.step(*pool[i % len(pool)])
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = trainer.step(*pool[i % len(pool)])
+        loss = step(i)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -181,67 +194,20 @@ def run_workload(args, world, rank, dev, pg):
            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic (SURVEY §8d config generators; random-init weights)",
            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
-                      "parallelism": f"dp{world}", "execution": "eager autograd (not graph-captured)"},
+                      "parallelism": f"dp{world}",
+                      "execution": "one HIP graph per pool batch" if graphed else "eager autograd"},
            "roofline": None, "cpu_baseline": None, "final_loss": round(float(loss), 6)}
     if rank == 0:
         print(json.dumps(out), flush=True)
 
 
-def launch_ranks(args) -> int:
-    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N fresh rank processes through
-    torch.distributed.run and return its exit code.  The parent never touches the GPU (no HIP
-    call before the children exist), so every rank initialises its own device cleanly."""
-    import socket
-    import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
-           str(port), os.path.abspath(__file__), *sys.argv[1:]]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
-
-
-def main():
-    args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per "
-                         "GPU (torch.distributed.run --nproc-per-node N) or let bench.py do it")
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())  # (rehearsal: several ranks per GPU)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.backend)
-        pg = dist.group.WORLD
-        if rank == 0:
-            print(f"[bench] {dist.get_backend(pg)} world size {dist.get_world_size(pg)}",
-                  file=sys.stderr, flush=True)
-        assert dist.get_world_size(pg) == args.gpus
-
+def bench_autoint(args, world, rank, dev, pg, compute_dtype):
+    """Config 2 in one compute mode ("f32": the reference's dtype; "bf16": config 2's stated
+    bf16 mode, rs_set_math_mode).  Returns (result dict, model, cfg, CPU batch pool)."""
     from recommendsystem_amd import _lib
     from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
-    _lib.load()
-    if args.workload != "autoint":
-        run_workload(args, world, rank, dev, pg)
-        if world > 1:
-            torch.distributed.destroy_process_group()
-        return
-
-    cfg = AutoIntConfig()  # config 2: 26 x 16, vocab 100k/field, IL(3, 16, 2), mlp [32,16], [1]
+    # config 2: 26 x 16, vocab 100k/field, IL(3, 16, 2), mlp [32,16], [1]
+    cfg = AutoIntConfig(compute_dtype=compute_dtype)
     B, F = args.batch, cfg.num_fields
     model = AutoInt(cfg, device=dev, seed=0, max_batch=B, world_size=world)
     trainer = AutoIntTrainer(model, B, process_group=pg)
@@ -301,13 +267,15 @@ def main():
              trainer.cat.data_ptr() + 4 * trainer.D, trainer.CW, ptr(trainer.xsave))
 
     trace("kernel timing")
-    t_bwd = time_kernel(il_bwd_once, args.kernel_reps)
-    t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
+    peak = BF16_PEAK_TFLOPS if compute_dtype == "bf16" else FP32_PEAK_TFLOPS
+    with _lib.math_mode(compute_dtype):
+        t_bwd = time_kernel(il_bwd_once, args.kernel_reps)
+        t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
     bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
     achieved = bwd_flops / t_bwd / 1e12
     traffic = None
     tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")  # from tools/profile_round.sh
-    if os.path.exists(tf_path):
+    if compute_dtype == "f32" and os.path.exists(tf_path):
         with open(tf_path) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
@@ -333,15 +301,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": compute_dtype,
         "data": "synthetic (Zipf(1.2) ids over 26x100k vocab, Bernoulli(0.25) labels; random-init weights)",
         "config": {"workload": "configs[1]: AutoInt full train (embedding + 3xInteractingLayer + MLP), "
                                "26 fields x emb 16, per-GPU batch 4096",
                    "global_batch": B * world, "fields": F, "emb_dim": E, "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd2_kernel (InteractingLayer backward + fused sparse push)",
-                     "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd3_kernel (InteractingLayer backward + fused sparse push)",
+                     "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "launch_us": round(t_bwd * 1e6, 2),
                      "flops_per_launch": bwd_flops},
         "il_fwd_us": round(t_fwd * 1e6, 2),
@@ -352,11 +320,75 @@ def main():
             "frac_bf16_basis": round(max(t_bytes, t_bf16) / step_s, 4),
             "frac_fp32_basis": round(max(t_bytes, t_fp32) / step_s, 4),
             "note": "BASELINE.md §3: fraction = roofline time / measured step time; the bf16 "
-                    "basis is the config's stated compute dtype, this step computes in fp32"},
+                    "basis is the config's stated compute dtype"},
         "step_tflops": round(TRAIN_FLOPS_PER_SAMPLE * samples / dt / 1e12, 3),
         "final_loss": round(loss, 6),
         "cpu_baseline": None,
     }
+    return out, model, cfg, pool_cpu
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N fresh rank processes through
+    torch.distributed.run and return its exit code.  The parent never touches the GPU (no HIP
+    call before the children exist), so every rank initialises its own device cleanly."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per "
+                         "GPU (torch.distributed.run --nproc-per-node N) or let bench.py do it")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())  # (rehearsal: several ranks per GPU)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
+        pg = dist.group.WORLD
+        if rank == 0:
+            print(f"[bench] {dist.get_backend(pg)} world size {dist.get_world_size(pg)}",
+                  file=sys.stderr, flush=True)
+        assert dist.get_world_size(pg) == args.gpus
+
+    from recommendsystem_amd import _lib
+    _lib.load()
+    if args.workload != "autoint":
+        run_workload(args, world, rank, dev, pg)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    out, model, cfg, pool_cpu = bench_autoint(args, world, rank, dev, pg, args.dtype)
+    if args.dtype == "f32" and not args.no_bf16:
+        # config 2's bf16 mode beside the fp32 line (same contract, own timed region)
+        o2, *_ = bench_autoint(args, world, rank, dev, pg, "bf16")
+        out["bf16"] = {k: o2[k] for k in ("value", "ms_per_step", "dtype", "roofline",
+                                           "il_fwd_us", "step_roofline", "final_loss")}
+        out["bf16"]["note"] = ("IL projections/dW/dx and head layer-1/2 GEMMs on bf16 MFMA, fp32 "
+                               "accumulation and master weights; accuracy in tests/test_gpu_bf16.py")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(cfg, model, pool_cpu, args.cpu_baseline_seconds)
     if rank == 0:

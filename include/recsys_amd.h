@@ -129,6 +129,28 @@ int rs_sparse_merge_packed(void* stream, const float* records, const int32_t* co
                            int32_t* flag, int64_t table_rows, int32_t cap);
 
 /* ---------------------------------------------------------------------------------------
+ * Math mode (config 2's "bf16" compute mode: BASELINE.json configs[1]).
+ * RS_MATH_F32 (0, default): every kernel computes in fp32, the reference's dtype.
+ * RS_MATH_BF16 (1): the matrix-core GEMMs of the InteractingLayer (projections, dW, dx;
+ * E = U = 16, H = 2, F <= 32) and of the fused MLP head (rs_mlp_head_train: layers 1-2, dW1,
+ * dx0) take bf16-rounded operands with fp32 accumulation; activations, attention, LN, losses,
+ * optimizers, weights and tables stay fp32 (fp32 master weights).  Shapes without bf16 kernels
+ * return -2 in bf16 mode (never a silent fp32 run).  Process-wide, read when a launch is
+ * issued: a captured hipGraph keeps the mode it was captured under.  No reference counterpart
+ * (the reference trains in fp32; cf. tf.keras.mixed_precision's mixed_bfloat16 policy).
+ * ------------------------------------------------------------------------------------- */
+int rs_set_math_mode(int mode);
+int rs_get_math_mode(void);
+
+/* Dropout seed offset (graph-replayed training; cf. PyTorch's CUDA-graph-safe RNG offsets).
+ * dev_offset: a device int64 (or NULL, the default).  While set, every dropout-using launch
+ * (the InteractingLayer entry points) uses seed + *dev_offset * 0x9E3779B97F4A7C15 (mod 2^64),
+ * *dev_offset read by the kernel when it runs: a graph captured once and replayed each step
+ * draws a fresh mask per step when the caller's step counter lives there.  Process-wide, read
+ * at launch (a captured graph keeps the pointer it was captured with). */
+int rs_set_seed_offset(const int64_t* dev_offset);
+
+/* ---------------------------------------------------------------------------------------
  * H3  InteractingLayer (InteractingLayer.py:7-61; rank/multi_head/interacting_layer.py:7-61).
  * x [B, F, E]; W [E, 4U] = [Wq | Wk | Wv | Wr] (Keras Dense kernels), bias [4U],
  * gamma/beta [U] (LayerNormalization), layer_num L with tied weights (L > 1 needs E == U).

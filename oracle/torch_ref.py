@@ -17,8 +17,42 @@ import torch
 from . import ctr_oracle as npo
 
 
-def dense(x, W, b, activation=None):
-    y = torch.tensordot(x, W, dims=([x.dim() - 1], [0])) + b
+def round_bf16(t):
+    """Round to the nearest bf16 (ties to even) and back to t's dtype: the operand rounding of
+    the library's bf16 math mode (v_cvt_pk_bf16_f32).  fp64 inputs are rounded via fp32 first,
+    as the kernels hold fp32 values."""
+    return t.to(torch.float32).to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16MatMul(torch.autograd.Function):
+    """x @ W with both operands rounded to bf16 (exact products, accumulation in x's dtype).
+    bwd_round: the backward GEMMs round theirs too (dx = r(g) r(W)^T, dW = r(x)^T r(g)) -- what
+    the library's MFMA backward does; False: exact backward (the head's VALU layer-2 backward)."""
+
+    @staticmethod
+    def forward(ctx, x, W, bwd_round):
+        ctx.save_for_backward(x, W)
+        ctx.bwd_round = bwd_round
+        return torch.tensordot(round_bf16(x), round_bf16(W), dims=([x.dim() - 1], [0]))
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        r = round_bf16 if ctx.bwd_round else (lambda t: t)
+        gr, xr, Wr = r(g), r(x), r(W)
+        dx = torch.tensordot(gr, Wr, dims=([g.dim() - 1], [1]))
+        dW = torch.tensordot(xr.reshape(-1, x.shape[-1]), gr.reshape(-1, g.shape[-1]),
+                             dims=([0], [0]))
+        return dx, dW, None
+
+
+def dense(x, W, b, activation=None, bf16=None):
+    """Keras Dense.  bf16: None (fp32/fp64 math), "fwd_bwd" or "fwd" (operand rounding of the
+    library's bf16 math mode; see _Bf16MatMul)."""
+    if bf16 is None:
+        y = torch.tensordot(x, W, dims=([x.dim() - 1], [0])) + b
+    else:
+        y = _Bf16MatMul.apply(x, W, bf16 == "fwd_bwd") + b
     if activation == "relu":
         return torch.relu(y)
     if activation == "sigmoid":
@@ -33,8 +67,11 @@ def layer_norm(x, gamma, beta, eps=1e-14):
 
 
 def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=True, eps=1e-14,
-                      drop_rate=0.0, seed=0):
-    """InteractingLayer.py:37-61, op for op (tied weights across layer_num iterations)."""
+                      drop_rate=0.0, seed=0, bf16=False):
+    """InteractingLayer.py:37-61, op for op (tied weights across layer_num iterations).
+    bf16: the projections round their operands as the library's bf16 math mode does (forward and
+    backward GEMMs); attention, LN and everything else unchanged."""
+    mm = "fwd_bwd" if bf16 else None
     U = W.shape[1] // 4
     H = head_num
     Wq, Wk, Wv, Wr = (W[:, j * U:(j + 1) * U] for j in range(4))
@@ -42,10 +79,10 @@ def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=
     B = x.shape[0]
     out = x
     for it in range(layer_num):
-        q = dense(out, Wq, bq, "relu")
-        k = dense(out, Wk, bk, "relu")
-        v = dense(out, Wv, bv, "relu")
-        res = dense(out, Wr, br, "relu") if use_res else None
+        q = dense(out, Wq, bq, "relu", mm)
+        k = dense(out, Wk, bk, "relu", mm)
+        v = dense(out, Wv, bv, "relu", mm)
+        res = dense(out, Wr, br, "relu", mm) if use_res else None
         q = torch.cat(torch.split(q, U // H, dim=2), dim=0)
         k = torch.cat(torch.split(k, U // H, dim=2), dim=0)
         v = torch.cat(torch.split(v, U // H, dim=2), dim=0)
@@ -68,17 +105,23 @@ def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=
     return out
 
 
-def mlp(x, layers, activation):
-    for W, b in layers:
-        x = dense(x, W, b, activation)
+def mlp(x, layers, activation, bf16=None):
+    """bf16: per-layer operand-rounding modes (see dense), or None."""
+    for i, (W, b) in enumerate(layers):
+        x = dense(x, W, b, activation, bf16[i] if bf16 else None)
     return x
 
 
 def autoint_forward(x0, il, deep_layers, logit_layers, cfg):
+    """cfg["bf16"]: the library's bf16 math mode -- IL projections rounded forward and backward;
+    the fused head's deep layer 1 rounded forward and backward (MFMA dx0 / dW1), layer 2 forward
+    only (its backward is fp32 VALU), logits exact (head.hip)."""
     B = x0.shape[0]
+    bf = bool(cfg.get("bf16", False))
     y = interacting_layer(x0, il["W"], il["bias"], il["gamma"], il["beta"], cfg["layer_num"],
-                          cfg["head_num"], cfg["use_res"], cfg.get("ln_eps", 1e-14))
-    deep = mlp(x0.reshape(B, -1), deep_layers, cfg["mlp_activation"])
+                          cfg["head_num"], cfg["use_res"], cfg.get("ln_eps", 1e-14), bf16=bf)
+    deep_modes = (["fwd_bwd"] + ["fwd"] * (len(deep_layers) - 1)) if bf else None
+    deep = mlp(x0.reshape(B, -1), deep_layers, cfg["mlp_activation"], deep_modes)
     result = torch.cat([deep, y.reshape(B, -1)], dim=1)
     s = mlp(result, logit_layers, cfg["logits_activation"])
     return s, torch.clamp(s, 1e-6, 1.0)

@@ -9,6 +9,7 @@ The product path has no fallback: if the library is missing or a call fails, thi
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -36,6 +37,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_adagrad": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32]),
     "rs_sparse_compact": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32]),
     "rs_sparse_merge_rows": (_i32, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32]),
+    "rs_set_math_mode": (_i32, [_i32]),
+    "rs_get_math_mode": (_i32, []),
+    "rs_set_seed_offset": (_i32, [_vp]),
     "rs_il_param_count": (_i32, [_i32, _i32]),
     "rs_il_fwd": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32,
                          _i32, _f32, _u64, _vp, _i64, _vp]),
@@ -231,3 +235,43 @@ def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=Non
     return call("rs_partials_reduce_adam", stream, n, parts, lds, nrows, ncols, outs, scales, offs,
                 ptr(params), ptr(m), ptr(v), ptr(step), ptr(done), lr, beta1, beta2, eps,
                 grad_scale, int(adam))
+
+
+MATH_MODES = {"f32": 0, "bf16": 1}
+
+
+@contextlib.contextmanager
+def math_mode(mode: str):
+    """rs_set_math_mode for the duration of the block ("f32" | "bf16"; include/recsys_amd.h):
+    launches issued -- or captured into a graph -- inside it use that mode."""
+    if mode not in MATH_MODES:
+        raise ValueError(f"math mode must be one of {sorted(MATH_MODES)}, got {mode!r}")
+    prev = load().rs_get_math_mode()
+    call("rs_set_math_mode", MATH_MODES[mode])
+    try:
+        yield
+    finally:
+        call("rs_set_math_mode", prev)
+
+
+_SEED_OFFSET = [None]
+
+
+@contextlib.contextmanager
+def seed_offset(counter):
+    """rs_set_seed_offset(counter) for the duration of the block: dropout launches issued (or
+    captured) inside it add the device int64 `counter`'s value at run time to their seed."""
+    if counter is not None and (counter.dtype != torch.int64 or not counter.is_cuda):
+        raise ValueError("seed offset must be a device int64 tensor")
+    prev = _SEED_OFFSET[0]
+    call("rs_set_seed_offset", ptr(counter))
+    _SEED_OFFSET[0] = counter
+    try:
+        yield
+    finally:
+        call("rs_set_seed_offset", ptr(prev))
+        _SEED_OFFSET[0] = prev
+
+
+def seed_offset_active() -> bool:
+    return _SEED_OFFSET[0] is not None

@@ -49,6 +49,10 @@ class AutoIntConfig:
     lr_sparse: float = 5e-5   # rank/ctr/base_model.py:163
     hash_mode: str = "mod"
     combiner: str = "mean"    # embedding_column(..., combiner='mean') base_model.py:211
+    # "f32" (the reference's dtype) or "bf16": config 2's bf16 compute mode (BASELINE.json
+    # configs[1]) -- the IL and MLP-head GEMMs take bf16 operands with fp32 accumulation, master
+    # weights / tables / optimizer state stay fp32 (rs_set_math_mode, include/recsys_amd.h)
+    compute_dtype: str = "f32"
 
     @staticmethod
     def from_model_config(model_config: dict, **front) -> "AutoIntConfig":
@@ -177,6 +181,13 @@ class AutoIntTrainer:
         self.graph_opt = None
         self.pool_graphs = []
         self.head = self._plan_head()
+        if cfg.compute_dtype not in _lib.MATH_MODES:
+            raise ValueError(f"compute_dtype must be one of {sorted(_lib.MATH_MODES)}")
+        if cfg.compute_dtype == "bf16" and (self.head is None or self.F > 32 or E != 16 or
+                                            U != 16 or self.H != 2 or
+                                            (self.head["N1"], self.head["N2"]) != (32, 16)):
+            raise ValueError("bf16 compute mode has kernels for the config-2 shape only (F <= 32, "
+                             "E = U = 16, H = 2, fused head with mlp [32, 16])")
         # fused path: the IL backward pushes dL/dx0 straight into the table (scan-mode marks)
         self.push = self.head is not None and self.F <= 64
         if self.push:
@@ -319,6 +330,12 @@ class AutoIntTrainer:
                                   1.0 / self.world, adam)
 
     def _forward_backward(self):
+        # math mode of the step; dropout seeds offset by the device step counter (fresh masks on
+        # every graph replay, rs_set_seed_offset)
+        with _lib.math_mode(self.model.cfg.compute_dtype), _lib.seed_offset(self.step_count):
+            self._forward_backward_modal()
+
+    def _forward_backward_modal(self):
         if self.head is not None:
             self._forward_backward_fused()
             if self.world > 1:

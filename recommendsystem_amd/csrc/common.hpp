@@ -23,6 +23,51 @@ static inline int rs_status_after_launch() {
 
 static inline hipStream_t rs_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Math mode (rs_set_math_mode, include/recsys_amd.h): process-wide, read when a launch is issued
+// (so a captured graph keeps the mode it was captured under).  Process-wide rather than per
+// thread because PyTorch's autograd issues the backward launches from its own device thread.
+enum { RS_MATH_F32 = 0, RS_MATH_BF16 = 1 };
+int rs_math_mode_now();
+
+// Dropout seed offset source (rs_set_seed_offset): a device int64 read by the kernel when it
+// runs, so a captured graph replayed step after step draws a new mask each step (the trainers
+// point it at their device step counter).  Read at launch, like the math mode.
+const int64_t* rs_seed_offset_now();
+// off_addr: the device address of the int64 offset, 0 = none (carried as an integer).  The
+// load is one scalar load in inline asm, done once at kernel entry: as a plain C++ load
+// (generic or global pointer) inside the IL kernels' per-iteration loops it tripped a gfx950
+// backend error ("Operand has incorrect register class" on a flat-aperture compare).  Not volatile and no memory clobber: the value is constant for the
+// launch, so the compiler may hoist / merge it.
+__device__ __forceinline__ uint64_t rs_eff_seed(uint64_t seed, uint64_t off_addr) {
+  if (!off_addr) return seed;
+  uint64_t v;
+  asm("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(off_addr));
+  return seed + v * 0x9E3779B97F4A7C15ull;
+}
+
+// bf16 math mode GEMM step.  v_mfma_f32_16x16x16_bf16: lane l = (q, j) supplies A[j][4q + t] and
+// B[4q + t][j] for t = 0..3 as two packed bf16 pairs -- exactly the 4 k-steps the fp32 form
+// takes from that lane (same permuted k), so one instruction replaces a 4-step fp32 chain and
+// every fragment layout of the fp32 kernels is unchanged.  Operands are rounded to nearest-even
+// (v_cvt_pk_bf16_f32); products are exact in fp32 and accumulate in fp32.
+typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> one packed bf16 pair, carried in a float VGPR (lo in bits 0..15)
+__device__ __forceinline__ float pack_bf16(float lo, float hi) {
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(float, v);
+}
+
+__device__ __forceinline__ rs_f32x4 mfma_bf16(float a01, float a23, float b01, float b23,
+                                              rs_f32x4 c) {
+  const s16x4 av = __builtin_bit_cast(s16x4, f32x2{a01, a23});
+  const s16x4 bv = __builtin_bit_cast(s16x4, f32x2{b01, b23});
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, c, 0, 0, 0);
+}
+
 // Wave-local LDS hand-off: make every lane's earlier LDS writes visible to the other lanes of the
 // SAME wave and stop the compiler from moving LDS accesses across this point.  (DS instructions of
 // one wave execute in order; the fences emit the lgkmcnt wait and pin the program order.)

@@ -25,6 +25,7 @@
 // W1 (53 KB at config 2), W2, W3 are staged once per block into LDS (row stride N1 + 4: the
 // dx0 pass reads W1 rows as conflict-free float4s), so no MFMA waits on an L2 round trip.
 // All arithmetic is fp32 (the reference's dtype); only the summation order differs from TF.
+// (bf16 math mode, [N1, N2] = [32, 16] only: the MFMA operands are rounded to bf16.)
 #include "common.hpp"
 
 namespace rs_head {
@@ -119,7 +120,10 @@ __device__ __forceinline__ void stage_rows(float* dst, int lds_stride, const flo
   }
 }
 
-template <int N1, int N2>
+// BF: bf16 math mode (rs_set_math_mode): the layer-1/2 and dx0/dW1 MFMAs take bf16-rounded
+// operands (mfma_bf16, one instruction per 16-deep k chunk, fp32 accumulate); the logits dot,
+// the loss and every stored value stay fp32.
+template <int N1, int N2, bool BF>
 __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   using L = Lay<N1, N2>;
   constexpr int D = L::D;
@@ -175,18 +179,31 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
       const float* wk2 = wcol + (16 * (s + KSPLIT) + 4 * q) * L::W1S;
       const float w0 = wk[0], w1 = wk[L::W1S], w2 = wk[2 * L::W1S], w3 = wk[3 * L::W1S];
       const float v0 = wk2[0], v1 = wk2[L::W1S], v2 = wk2[2 * L::W1S], v3 = wk2[3 * L::W1S];
-      acc0 = mfma(x4.x, w0, acc0); acc1 = mfma(y4.x, v0, acc1);
-      acc0 = mfma(x4.y, w1, acc0); acc1 = mfma(y4.y, v1, acc1);
-      acc0 = mfma(x4.z, w2, acc0); acc1 = mfma(y4.z, v2, acc1);
-      acc0 = mfma(x4.w, w3, acc0); acc1 = mfma(y4.w, v3, acc1);
+      if constexpr (BF) {
+        acc0 = mfma_bf16(pack_bf16(x4.x, x4.y), pack_bf16(x4.z, x4.w), pack_bf16(w0, w1),
+                         pack_bf16(w2, w3), acc0);
+        acc1 = mfma_bf16(pack_bf16(y4.x, y4.y), pack_bf16(y4.z, y4.w), pack_bf16(v0, v1),
+                         pack_bf16(v2, v3), acc1);
+      } else {
+        acc0 = mfma(x4.x, w0, acc0); acc1 = mfma(y4.x, v0, acc1);
+        acc0 = mfma(x4.y, w1, acc0); acc1 = mfma(y4.y, v1, acc1);
+        acc0 = mfma(x4.z, w2, acc0); acc1 = mfma(y4.z, v2, acc1);
+        acc0 = mfma(x4.w, w3, acc0); acc1 = mfma(y4.w, v3, acc1);
+      }
     }
     for (; s < nks; s += KSPLIT) {
       const float4 x4 = *reinterpret_cast<const float4*>(Xs + j * xs + 16 * s + 4 * q);
       const float* wk = wcol + (16 * s + 4 * q) * L::W1S;
-      acc0 = mfma(x4.x, wk[0], acc0);
-      acc0 = mfma(x4.y, wk[L::W1S], acc0);
-      acc0 = mfma(x4.z, wk[2 * L::W1S], acc0);
-      acc0 = mfma(x4.w, wk[3 * L::W1S], acc0);
+      if constexpr (BF) {
+        acc0 = mfma_bf16(pack_bf16(x4.x, x4.y), pack_bf16(x4.z, x4.w),
+                         pack_bf16(wk[0], wk[L::W1S]), pack_bf16(wk[2 * L::W1S], wk[3 * L::W1S]),
+                         acc0);
+      } else {
+        acc0 = mfma(x4.x, wk[0], acc0);
+        acc0 = mfma(x4.y, wk[L::W1S], acc0);
+        acc0 = mfma(x4.z, wk[2 * L::W1S], acc0);
+        acc0 = mfma(x4.w, wk[3 * L::W1S], acc0);
+      }
     }
     // lane holds D[4q + r][j] of tile nt: stash per wave, combine in wave order below
 #pragma unroll
@@ -210,10 +227,15 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
       for (int s = 0; s < N1 / 16; ++s) {
         const float4 x4 = *reinterpret_cast<const float4*>(H1 + j * L::H1S + 16 * s + 4 * q);
         const float* wk = W2s + (16 * s + 4 * q) * N2 + 16 * w + j;
-        acc = mfma(x4.x, wk[0], acc);
-        acc = mfma(x4.y, wk[N2], acc);
-        acc = mfma(x4.z, wk[2 * N2], acc);
-        acc = mfma(x4.w, wk[3 * N2], acc);
+        if constexpr (BF) {
+          acc = mfma_bf16(pack_bf16(x4.x, x4.y), pack_bf16(x4.z, x4.w), pack_bf16(wk[0], wk[N2]),
+                          pack_bf16(wk[2 * N2], wk[3 * N2]), acc);
+        } else {
+          acc = mfma(x4.x, wk[0], acc);
+          acc = mfma(x4.y, wk[N2], acc);
+          acc = mfma(x4.z, wk[2 * N2], acc);
+          acc = mfma(x4.w, wk[3 * N2], acc);
+        }
       }
       const float bb = a.b2[16 * w + j];
 #pragma unroll
@@ -344,10 +366,15 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #pragma unroll
       for (int s = 0; s < N1 / 16; ++s) {
         const float4 w4 = *reinterpret_cast<const float4*>(W1s + e * L::W1S + 16 * s + 4 * q);
-        acc = mfma(dzf[s].x, w4.x, acc);
-        acc = mfma(dzf[s].y, w4.y, acc);
-        acc = mfma(dzf[s].z, w4.z, acc);
-        acc = mfma(dzf[s].w, w4.w, acc);
+        if constexpr (BF) {
+          acc = mfma_bf16(pack_bf16(dzf[s].x, dzf[s].y), pack_bf16(dzf[s].z, dzf[s].w),
+                          pack_bf16(w4.x, w4.y), pack_bf16(w4.z, w4.w), acc);
+        } else {
+          acc = mfma(dzf[s].x, w4.x, acc);
+          acc = mfma(dzf[s].y, w4.y, acc);
+          acc = mfma(dzf[s].z, w4.z, acc);
+          acc = mfma(dzf[s].w, w4.w, acc);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -363,8 +390,13 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #pragma unroll
       for (int nt = 0; nt < NT1; ++nt) {
         f32x4 g = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (BF) {
+          g = mfma_bf16(pack_bf16(xa[0], xa[1]), pack_bf16(xa[2], xa[3]),
+                        pack_bf16(dzb[0][nt], dzb[1][nt]), pack_bf16(dzb[2][nt], dzb[3][nt]), g);
+        } else {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) g = mfma(xa[t], dzb[t][nt], g);
+          for (int t = 0; t < 4; ++t) g = mfma(xa[t], dzb[t][nt], g);
+        }
         // D[4q + r][j] = dW1[16 et + 4q + r][16 nt + j]
 #pragma unroll
         for (int r = 0; r < 4; ++r) part[(16 * et + 4 * q + r) * N1 + 16 * nt + j] = g[r];
@@ -373,12 +405,17 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   }
 }
 
-template <int N1, int N2>
+template <int N1, int N2, bool BF16_OK = false>
 int launch(hipStream_t s, const Args& a, int64_t grid) {
   const Lay<N1, N2> lay(a.K0, a.S, a.T);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (lds > 160 * 1024) return RS_ERR_UNSUPPORTED;
-  head_train_kernel<N1, N2><<<(unsigned)grid, NTH, lds, s>>>(a);
+  if (rs_math_mode_now() == RS_MATH_BF16) {
+    if constexpr (!BF16_OK) return RS_ERR_UNSUPPORTED;  // never a silent fp32 run
+    else head_train_kernel<N1, N2, true><<<(unsigned)grid, NTH, lds, s>>>(a);
+  } else {
+    head_train_kernel<N1, N2, false><<<(unsigned)grid, NTH, lds, s>>>(a);
+  }
   return rs_status_after_launch();
 }
 
@@ -427,7 +464,8 @@ RS_API int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const f
          dx_accumulate, workspace, np};
   hipStream_t s = rs_stream(stream);
 #define RS_HEAD(A, Bn) if (N1 == A && N2 == Bn) return launch<A, Bn>(s, a, grid);
-  RS_HEAD(32, 16) RS_HEAD(64, 32) RS_HEAD(16, 0) RS_HEAD(32, 0) RS_HEAD(64, 0)
+  if (N1 == 32 && N2 == 16) return launch<32, 16, true>(s, a, grid);  // config 2 (bf16 too)
+  RS_HEAD(64, 32) RS_HEAD(16, 0) RS_HEAD(32, 0) RS_HEAD(64, 0)
   RS_HEAD(16, 16) RS_HEAD(32, 32) RS_HEAD(64, 16) RS_HEAD(64, 64)
 #undef RS_HEAD
   return RS_ERR_UNSUPPORTED;

@@ -55,6 +55,7 @@ struct FwdReq {
   int64_t gather_table_rows = 0;
   int32_t* gather_rows = nullptr;
   int gather_hash = 0;
+  int bf16 = 0;  // RS_MATH_BF16 (rs_set_math_mode): bf16 operands on the matrix cores
 };
 
 struct BwdReq {
@@ -80,6 +81,7 @@ struct BwdReq {
   // dry run: write the grid (= number of per-block partial rows) the launch would use and
   // return without launching (rs_il_bwd_partial_blocks)
   int* grid_out = nullptr;
+  int bf16 = 0;  // RS_MATH_BF16 (rs_set_math_mode): bf16 operands on the matrix cores
 };
 
 constexpr int kMaxFwdWaves = 4;
@@ -90,10 +92,13 @@ constexpr int kMaxBwdWaves = 2;
 constexpr int kMaxBwdGrid = RS_IL_BWD_GRID;
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <int E_, int U_, int H_, int FMAX_, bool EXACT_ = false>
+template <int E_, int U_, int H_, int FMAX_, bool EXACT_ = false, bool BF_ = false>
 struct Cfg {
   static constexpr int E = E_, U = U_, H = H_, FMAX = FMAX_;
   static constexpr bool EXACT = EXACT_;                // F == FMAX: no padded keys to mask
+  // bf16 math mode (rs_set_math_mode): projection / dW / dx MFMAs take bf16-rounded operands
+  // (v_mfma_f32_16x16x16_bf16, fp32 accumulate); attention, LN, storage and weights stay fp32
+  static constexpr bool BF = BF_;
   static constexpr int NC = 4 * U;                     // [Q | K | V | R] projection columns
   static constexpr int DH = U / H;
   static constexpr int NCOLW = NC < 64 ? NC : 64;      // lanes per projection row
@@ -144,6 +149,7 @@ struct Args {
   float inv_sdh;    // 1 / sqrt(dh)
   float sc2;        // log2(e) / sqrt(dh): scores go straight to the exp2 domain
   uint64_t seed;
+  uint64_t seed_off;           // rs_set_seed_offset source address (0 = none): seed + *src * K
   int l_x, l_pr, l_o, l_gpr, l_dy, l_pm, l_st, per_wave;  // per-wave LDS carve-up (floats)
   int l_tmp;                   // bwd2 only: partial-row exchange / dV buffer
   int l_x2, l_w, l_b;          // bwd2 only: second X buffer (prefetch), W and bias in LDS
@@ -176,6 +182,7 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.drop_rate = drop_rate;
   a.drop_scale = drop_rate > 0.f ? (float)(1.0 / (1.0 - (double)drop_rate)) : 1.f;
   a.seed = seed;
+  a.seed_off = (uint64_t)(uintptr_t)rs_seed_offset_now();
   int off = 0;
   a.l_x = off; off += r4(F * C::E);
   a.l_pr = off; off += r4(C::FMAX * C::PRS);  // FMAX rows: padded key/value rows stay zero
@@ -300,6 +307,8 @@ __device__ __forceinline__ f32x4 mfma_16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 math mode: pack_bf16 / mfma_bf16 (common.hpp) take the same lane fragments.
+
 template <class C>
 struct MfmaW {
   static constexpr int KS = (C::E + 15) / 16;  // 16-wide k chunks of E
@@ -308,6 +317,8 @@ struct MfmaW {
   static constexpr int CS = C::NC / 16;        // 16-wide c chunks (dx reduction)
   float wp[KS][4][NT];  // projection B: W[16ks + 4q + t][16nt + j]
   float wx[CS][4][ET];  // dx B       : W[16et + j][16cs + 4q + t]
+  // (bf16 mode: [..][0] / [..][1] hold the packed pairs t = 0,1 / 2,3; [2], [3] are never
+  // touched and take no registers)
   float bp[NT];         // bias[16nt + j] (loop-invariant: kept out of the per-row loops)
 
   __device__ __forceinline__ void load(const float* __restrict__ W, const float* __restrict__ bias) {
@@ -329,6 +340,33 @@ struct MfmaW {
           const int k = 16 * ks + 4 * q + t;
           wp[ks][t][nt] = k < C::E ? W[k * C::NC + 16 * nt + j] : 0.f;
         }
+    pack_proj();
+  }
+  __device__ __forceinline__ void pack_proj() {
+    if constexpr (C::BF) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const float p01 = pack_bf16(wp[ks][0][nt], wp[ks][1][nt]);
+          const float p23 = pack_bf16(wp[ks][2][nt], wp[ks][3][nt]);
+          wp[ks][0][nt] = p01;
+          wp[ks][1][nt] = p23;
+        }
+    }
+  }
+  __device__ __forceinline__ void pack_dx() {
+    if constexpr (C::BF) {
+#pragma unroll
+      for (int cs = 0; cs < CS; ++cs)
+#pragma unroll
+        for (int et = 0; et < ET; ++et) {
+          const float p01 = pack_bf16(wx[cs][0][et], wx[cs][1][et]);
+          const float p23 = pack_bf16(wx[cs][2][et], wx[cs][3][et]);
+          wx[cs][0][et] = p01;
+          wx[cs][1][et] = p23;
+        }
+    }
   }
   // the same fragments from a block-resident LDS copy of W ([E][NC], row stride C::WPS) and bias
   __device__ __forceinline__ void load_proj_lds(const float* WL, const float* BL) {
@@ -344,6 +382,7 @@ struct MfmaW {
           const int k = 16 * ks + 4 * q + t;
           wp[ks][t][nt] = k < C::E ? WL[k * C::WPS + 16 * nt + j] : 0.f;
         }
+    pack_proj();
   }
   __device__ __forceinline__ void load_dx_lds(const float* WL) {
     const int q = lane_id() >> 4, j = lane_id() & 15;
@@ -357,6 +396,7 @@ struct MfmaW {
         if (e < C::E) v = *reinterpret_cast<const float4*>(WL + e * C::WPS + 16 * cs + 4 * q);
         wx[cs][0][et] = v.x; wx[cs][1][et] = v.y; wx[cs][2][et] = v.z; wx[cs][3][et] = v.w;
       }
+    pack_dx();
   }
   // dx B operand only
   __device__ __forceinline__ void load_dx(const float* __restrict__ W) {
@@ -370,6 +410,7 @@ struct MfmaW {
           const int e = 16 * et + j;
           wx[cs][t][et] = e < C::E ? W[e * C::NC + 16 * cs + 4 * q + t] : 0.f;
         }
+    pack_dx();
   }
 };
 
@@ -390,10 +431,17 @@ __device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, i
       const float4 v = *reinterpret_cast<const float4*>(X + arow * C::E + 16 * ks + 4 * q);
       a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
     }
+    if constexpr (C::BF) {
+      const float a01 = pack_bf16(a4[0], a4[1]), a23 = pack_bf16(a4[2], a4[3]);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int nt = 0; nt < M::NT; ++nt)
+        acc[nt] = mfma_bf16(a01, a23, w.wp[ks][0][nt], w.wp[ks][1][nt], acc[nt]);
+    } else {
 #pragma unroll
-      for (int nt = 0; nt < M::NT; ++nt) acc[nt] = mfma_16x16x4(a4[t], w.wp[ks][t][nt], acc[nt]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < M::NT; ++nt) acc[nt] = mfma_16x16x4(a4[t], w.wp[ks][t][nt], acc[nt]);
+    }
   }
 #pragma unroll
   for (int nt = 0; nt < M::NT; ++nt) {
@@ -432,13 +480,32 @@ __device__ __forceinline__ void mfma_dw(const float* X, const float* G, int F, i
       dbp[nt] += gb[t][nt];
     }
   }
+  if constexpr (C::BF) {
+    float xp[2][M::ET], gp[2][M::NT];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int et = 0; et < M::ET; ++et) {
+      xp[0][et] = pack_bf16(xa[0][et], xa[1][et]);
+      xp[1][et] = pack_bf16(xa[2][et], xa[3][et]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) {
+      gp[0][nt] = pack_bf16(gb[0][nt], gb[1][nt]);
+      gp[1][nt] = pack_bf16(gb[2][nt], gb[3][nt]);
+    }
 #pragma unroll
     for (int et = 0; et < M::ET; ++et)
 #pragma unroll
       for (int nt = 0; nt < M::NT; ++nt)
-        acc[et][nt] = mfma_16x16x4(xa[t][et], gb[t][nt], acc[et][nt]);
+        acc[et][nt] = mfma_bf16(xp[0][et], xp[1][et], gp[0][nt], gp[1][nt], acc[et][nt]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+        for (int nt = 0; nt < M::NT; ++nt)
+          acc[et][nt] = mfma_16x16x4(xa[t][et], gb[t][nt], acc[et][nt]);
+  }
 }
 
 // dx[f][e] = sum_c G[f][c] W[e][c] for row tile rt; writes rows < F to out[f * ld + e]
@@ -468,10 +535,17 @@ __device__ __forceinline__ void mfma_dx(const float* G, int F, int rt, const Mfm
       const float4 v = *reinterpret_cast<const float4*>(G + arow * C::PRS + 16 * cs + 4 * q);
       a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
     }
+    if constexpr (C::BF) {
+      const float a01 = pack_bf16(a4[0], a4[1]), a23 = pack_bf16(a4[2], a4[3]);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int et = 0; et < M::ET; ++et)
+        acc[et] = mfma_bf16(a01, a23, w.wx[cs][0][et], w.wx[cs][1][et], acc[et]);
+    } else {
 #pragma unroll
-      for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+    }
   }
 #pragma unroll
   for (int et = 0; et < M::ET; ++et) {
@@ -518,10 +592,17 @@ __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, cons
       const float4 v = *reinterpret_cast<const float4*>(G + arow * C::PRS + 16 * cs + 4 * q);
       a4[0] = v.x; a4[1] = v.y; a4[2] = v.z; a4[3] = v.w;
     }
+    if constexpr (C::BF) {
+      const float a01 = pack_bf16(a4[0], a4[1]), a23 = pack_bf16(a4[2], a4[3]);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int et = 0; et < M::ET; ++et)
+        acc[et] = mfma_bf16(a01, a23, w.wx[cs][0][et], w.wx[cs][1][et], acc[et]);
+    } else {
 #pragma unroll
-      for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et) acc[et] = mfma_16x16x4(a4[t], w.wx[cs][t][et], acc[et]);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -574,15 +655,29 @@ __device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C
         a4[rt][kh][0] = v.x; a4[rt][kh][1] = v.y; a4[rt][kh][2] = v.z; a4[rt][kh][3] = v.w;
       }
     }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
+    if constexpr (C::BF) {
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
-        for (int kh = 0; kh < KH; ++kh)
+        for (int kh = 0; kh < KH; ++kh) {
+          const float a01 = pack_bf16(a4[rt][kh][0], a4[rt][kh][1]);
+          const float a23 = pack_bf16(a4[rt][kh][2], a4[rt][kh][3]);
 #pragma unroll
           for (int et = 0; et < M::ET; ++et)
-            acc[rt][kh][et] = mfma_16x16x4(a4[rt][kh][t], w.wx[kh * CSH + cc][t][et], acc[rt][kh][et]);
+            acc[rt][kh][et] = mfma_bf16(a01, a23, w.wx[kh * CSH + cc][0][et],
+                                        w.wx[kh * CSH + cc][1][et], acc[rt][kh][et]);
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+          for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et)
+              acc[rt][kh][et] = mfma_16x16x4(a4[rt][kh][t], w.wx[kh * CSH + cc][t][et], acc[rt][kh][et]);
+    }
   }
 #pragma unroll
   for (int rt = 0; rt < NRT; ++rt)
@@ -695,6 +790,7 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y,
     int64_t y_ld, float* __restrict__ xsave, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);  // dropout seed of this launch
   float* base = smem + wave_id() * a.per_wave;
   float* X = base + a.l_x;
   float* PR = base + a.l_pr;
@@ -733,7 +829,7 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
     }
     wave_lds_sync();
     for (int it = 0; it < a.L; ++it) {
-      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       for (int rt = 0; rt * 16 < F; ++rt) mfma_project<C>(X, PR, F, rt, mw);
       wave_lds_sync();
       // O_i overwrites Q_i in place (only lane (h, i) ever reads Q_i, before writing O_i)
@@ -774,6 +870,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD_OCC) bwd_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);  // dropout seed of this launch
   constexpr int JH = (C::FMAX + 1) / 2;  // keys per wave in the split-j passes
   float* base = smem;
   float* X = base + a.l_x;
@@ -817,7 +914,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD_OCC) bwd_kernel(
     }
     for (int it = a.L - 1; it >= 0; --it) {
       IL_STAMP(0)
-      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       {
         const float* xin = (it == 0) ? (x + b * F * C::E)
                                      : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
@@ -1143,6 +1240,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);  // dropout seed of this launch
   constexpr int JH = (C::FMAX + 1) / 2;  // keys (or queries) per wave in the split passes
   float* const X0 = smem + a.l_x;
   float* const X1 = smem + a.l_x2;
@@ -1201,7 +1299,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     for (int it = a.L - 1; it >= 0; --it) {
       IL_STAMP(0)
-      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       float* const X = par ? X1 : X0;
       vm_wait_all();  // this wave's share of X (and of dy at it == L-1) has landed
       lds_barrier();
@@ -1592,6 +1690,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);  // dropout seed of this launch
   const int F = C::EXACT ? C::FMAX : a.F;
   const Bwd3Layout<C> lay(F);
   float* const WL = smem;
@@ -1649,7 +1748,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
 #endif
     for (int it = a.L - 1; it >= 0; --it) {
       IL_STAMP(0)
-      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
 #ifdef RS_BWD3_NOPF
       row_prefetch<PFX>(px, x_src(b, it), nx4);
       if (it == a.L - 1) { row_prefetch<PFY>(py, dy + b * dy_ld, ny4); row_commit<PFY>(DY, py, ny4); }
@@ -2026,18 +2125,33 @@ int bwd_launch(const BwdReq& q) {
 #endif
 
 // EXACT instantiations (F == FMAX) drop the padded-key mask entirely.
-template <int E, int U, int H, int FMAX, bool EXACT = false>
+// BF16: this shape also has bf16-math-mode instantiations (only the shapes a bf16 benchmark
+// or model runs: each one doubles the unit's compile); without them a bf16 request is
+// RS_ERR_UNSUPPORTED, never a silent fp32 run.
+template <int E, int U, int H, int FMAX, bool EXACT = false, bool BF16 = false>
 int try_fwd(const FwdReq& q) {
   if (q.E != E || q.U != U || q.H != H || q.F > FMAX || (EXACT && q.F != FMAX))
     return RS_ERR_UNSUPPORTED;
+  if (q.bf16) {
+    if constexpr (BF16)
+      return q.drop_rate > 0.f ? fwd_launch<Cfg<E, U, H, FMAX, EXACT, true>, true>(q)
+                               : fwd_launch<Cfg<E, U, H, FMAX, EXACT, true>, false>(q);
+    return RS_ERR_UNSUPPORTED;
+  }
   return q.drop_rate > 0.f ? fwd_launch<Cfg<E, U, H, FMAX, EXACT>, true>(q)
                            : fwd_launch<Cfg<E, U, H, FMAX, EXACT>, false>(q);
 }
 
-template <int E, int U, int H, int FMAX, bool EXACT = false>
+template <int E, int U, int H, int FMAX, bool EXACT = false, bool BF16 = false>
 int try_bwd(const BwdReq& q) {
   if (q.E != E || q.U != U || q.H != H || q.F > FMAX || (EXACT && q.F != FMAX))
     return RS_ERR_UNSUPPORTED;
+  if (q.bf16) {
+    if constexpr (BF16)
+      return q.drop_rate > 0.f ? bwd_launch<Cfg<E, U, H, FMAX, EXACT, true>, true>(q)
+                               : bwd_launch<Cfg<E, U, H, FMAX, EXACT, true>, false>(q);
+    return RS_ERR_UNSUPPORTED;
+  }
   return q.drop_rate > 0.f ? bwd_launch<Cfg<E, U, H, FMAX, EXACT>, true>(q)
                            : bwd_launch<Cfg<E, U, H, FMAX, EXACT>, false>(q);
 }

@@ -42,6 +42,7 @@ struct LFwd {
   int F, L, use_res, drop;
   float eps, drop_rate, inv_keep, sc2, inv_sdh;
   uint64_t seed;
+  uint64_t seed_off;  // rs_set_seed_offset source address (0 = none)
   float *y, *xsave;
   int64_t y_ld;
 };
@@ -52,6 +53,7 @@ struct LBwd {
   int F, L, use_res, drop;
   float eps, drop_rate, inv_keep, sc2, inv_sdh;
   uint64_t seed;
+  uint64_t seed_off;
   float* dx;
   int dx_accumulate;
   float* part;
@@ -121,7 +123,7 @@ __global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
     for (int k = t; k < F * C::E / 4; k += NT) reinterpret_cast<float4*>(xs)[k] = xg[k];
     __syncthreads();
     for (int it = 0; it < a.L; ++it) {
-      const uint32_t kb = a.drop ? dropout_sample_key(splitmix64(a.seed + (uint64_t)it), (uint32_t)b) : 0u;
+      const uint32_t kb = a.drop ? dropout_sample_key(splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it), (uint32_t)b) : 0u;
       project<C>(xs, Qs, F, wcol, bc);
       __syncthreads();
       for (int p = t; p < F * C::H; p += NT) {
@@ -242,7 +244,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
               reinterpret_cast<const float4*>(a.dy + b * a.dy_ld + i * C::U)[q4];
         }
       }
-      const uint64_t lseed = splitmix64(a.seed + (uint64_t)it);
+      const uint64_t lseed = splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it);
       const uint32_t kb = a.drop ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
       __syncthreads();
       project<C>(xs, Qs, F, wcol, bc);
@@ -476,7 +478,7 @@ int run_fwd(const FwdReq& q) {
   using C = LC<E, U, H>;
   LFwd a{q.x, q.W, q.bias, q.gamma, q.beta, q.B, q.F, q.L, q.use_res, q.drop_rate > 0.f,
          q.eps, q.drop_rate, q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
-         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, q.y,
+         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, (uint64_t)(uintptr_t)rs_seed_offset_now(), q.y,
          q.xsave, q.y_ld};
   if (q.B == 0) return RS_OK;
   const size_t lds = fwd_lds(q.F, E, U);
@@ -494,7 +496,7 @@ int run_bwd(const BwdReq& q) {
   LBwd a{q.x, q.xsave, q.dy, q.W, q.bias, q.gamma, q.beta, q.dy_ld, q.B, q.F, q.L, q.use_res,
          q.drop_rate > 0.f, q.eps, q.drop_rate,
          q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
-         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, q.dx,
+         1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, (uint64_t)(uintptr_t)rs_seed_offset_now(), q.dx,
          q.dx_accumulate, q.workspace};
   const size_t lds = bwd_lds(q.F, E, U, H);
   bwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
@@ -509,6 +511,7 @@ int run_bwd(const BwdReq& q) {
 
 // F in (64, 256]: the many-field instantiations (config 3 is E = U = 8, H = 2).
 int il_large_fwd(const FwdReq& q) {
+  if (q.bf16) return RS_ERR_UNSUPPORTED;  // fp32 only (bf16 mode: il_inst_a.hip shapes)
   if (q.F > large::FMAXL || (q.L > 1 && q.E != q.U)) return RS_ERR_UNSUPPORTED;
   if (large::fwd_lds(q.F, q.E, q.U) > 64 * 1024) return RS_ERR_UNSUPPORTED;
   if (q.E == 8 && q.U == 8 && q.H == 2) return large::run_fwd<8, 8, 2>(q);
@@ -518,6 +521,7 @@ int il_large_fwd(const FwdReq& q) {
 }
 
 int il_large_bwd(const BwdReq& q) {
+  if (q.bf16) return RS_ERR_UNSUPPORTED;
   if (q.F > large::FMAXL || (q.L > 1 && q.E != q.U)) return RS_ERR_UNSUPPORTED;
   if (large::bwd_lds(q.F, q.E, q.U, q.H) > 160 * 1024) return RS_ERR_UNSUPPORTED;
   if (q.E == 8 && q.U == 8 && q.H == 2) return large::run_bwd<8, 8, 2>(q);

@@ -22,6 +22,27 @@ namespace rs_il { unsigned long long* g_il_stamps = nullptr; }
 RS_API void rs_il_debug_set_stamps(unsigned long long* p) { rs_il::g_il_stamps = p; }
 #endif
 
+// process-wide math mode (common.hpp); relaxed atomics: a mode change is ordered with the
+// launches of the thread that made it, and other threads see it at their next launch
+static int g_math_mode = RS_MATH_F32;
+int rs_math_mode_now() { return __atomic_load_n(&g_math_mode, __ATOMIC_RELAXED); }
+
+RS_API int rs_set_math_mode(int mode) {
+  if (mode != RS_MATH_F32 && mode != RS_MATH_BF16) return RS_ERR_ARG;
+  __atomic_store_n(&g_math_mode, mode, __ATOMIC_RELAXED);
+  return RS_OK;
+}
+
+RS_API int rs_get_math_mode(void) { return rs_math_mode_now(); }
+
+static const int64_t* g_seed_offset = nullptr;
+const int64_t* rs_seed_offset_now() { return __atomic_load_n(&g_seed_offset, __ATOMIC_RELAXED); }
+
+RS_API int rs_set_seed_offset(const int64_t* dev_offset) {
+  __atomic_store_n(&g_seed_offset, dev_offset, __ATOMIC_RELAXED);
+  return RS_OK;
+}
+
 RS_API int rs_il_param_count(int E, int U) { return E * 4 * U + 4 * U + 2 * U; }
 
 RS_API int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U) {
@@ -40,6 +61,7 @@ RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int 
   if (drop_rate < 0.f || drop_rate >= 1.f || y_ld < (int64_t)F * U) return RS_ERR_ARG;
   rs_il::FwdReq q{rs_stream(stream), x, W, bias, gamma, beta, B, F, E, U, H, L, use_res,
                   eps, drop_rate, seed, y, xsave, y_ld};
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   if (F > 64) return rs_il::il_large_fwd(q);
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
@@ -69,6 +91,7 @@ RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row
   q.gather_table_rows = table_rows;
   q.gather_rows = rows_out;
   q.gather_hash = hash_mode;
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
@@ -96,6 +119,7 @@ RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const flo
   rs_il::BwdReq q{rs_stream(stream), x, xsave, dy, W, bias, gamma, beta, dy_ld, B, F, E, U, H, L,
                   use_res, eps, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
                   workspace, workspace_floats};
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   if (F > 64) return rs_il::il_large_bwd(q);
   return bwd_small(q);
 }
@@ -119,6 +143,7 @@ RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, cons
   q.push_rows = rows;
   q.push_table = grad_table;
   q.push_flag = flag;
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   return bwd_small(q);
 }
 
@@ -138,6 +163,7 @@ RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
                   (int64_t)F * U, B, F, E, U, H, 1, 1, 1e-14f, 0.f, 0, nullptr, 0, nullptr, 0,
                   nullptr, workspace_floats};
   q.grid_out = &grid;
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   if (bwd_small(q) != RS_OK) return 0;
   return grid;
 }

@@ -14,7 +14,9 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
 from ._lib import call, ptr, stream_handle
+from .layers import InteractingLayer
 from .params import ParamArena
 
 
@@ -48,12 +50,23 @@ class Trainer:
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.regs = list(model.regularizers()) if hasattr(model, "regularizers") else []
         self.xbuf = {}
+        self._il_layers = [mod for mod in model.modules() if isinstance(mod, InteractingLayer)] \
+            if hasattr(model, "modules") else []
         if self.world > 1:
             for t in self.tables:
                 self.xbuf[id(t)] = (torch.empty(t.touched_cap, device=dev, dtype=torch.int32),
                                     torch.empty(t.touched_cap, t.dim, device=dev))
 
     def step(self, *batch):
+        # dropout masks: per-step host seeds restart at 0 each step and the device step counter
+        # is added at run time (rs_set_seed_offset), so eager steps and graph replays draw the
+        # same fresh mask per step
+        for mod in self._il_layers:
+            mod._calls = 0
+        with _lib.seed_offset(self.step_count):
+            return self._step(*batch)
+
+    def _step(self, *batch):
         loss = self.model.loss(*batch)
         loss.backward()
         s = stream_handle()
@@ -70,3 +83,44 @@ class Trainer:
         for t in self.tables:
             t.step(grad_scale=scale)
         return loss
+
+    # ---- HIP-graph replay of whole steps (single GPU) --------------------------------------
+    def _state(self):
+        out = [self.arena.data, self.arena.grad, self.m, self.v, self.step_count]
+        for t in self.tables:
+            out += [t.weight, t.grad, t.flag, t.n_touched, t.touched]
+            out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]
+        return out
+
+    def capture_pool(self, batches, warmup: int = 1) -> None:
+        """Record one whole training step per device-resident batch (forward, autograd backward,
+        regularisers, dense Adam, sparse optimizer) into its own HIP graph; step_pool(i) replays
+        batch i with no host work.  All graphs share one memory pool and are replayed in capture
+        order (cyclic), which is what makes sharing it safe.  ``warmup`` eager steps run first
+        (first-call allocations) and are rolled back, so capture changes no training state."""
+        if self.world > 1:
+            raise NotImplementedError("graph capture of the generic trainer is single-GPU (the "
+                                      "data-parallel exchange reads counts on the host)")
+        saved = [t.clone() for t in self._state()]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(warmup):
+                self.step(*batches[i % len(batches)])
+        torch.cuda.current_stream().wait_stream(side)
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        self.graphs, self.graph_loss = [], []
+        for b in batches:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                loss = self.step(*b)
+            self.graphs.append(g)
+            self.graph_loss.append(loss.detach())
+
+    def step_pool(self, i: int):
+        k = i % len(self.graphs)
+        self.graphs[k].replay()
+        return self.graph_loss[k]

@@ -15,7 +15,7 @@ def declared():
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
     for m in re.finditer(r"\b(?:int|int64_t)\s+(rs_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
-        args = [a.strip() for a in m.group(2).split(",") if a.strip()]
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() not in ("", "void")]
         out[m.group(1)] = len(args)
     return out
 
