@@ -118,6 +118,27 @@ __device__ __forceinline__ void glds_copy(float* dst, const float* src, int n4) 
   }
 }
 
+// glds_copy for one wave (lanes 0..63 of the calling wave copy n4 float4; the other waves of the
+// block are not involved).  Complete after vm_wait_all() + wave_lds_sync().
+__device__ __forceinline__ void glds_copy_wave(float* dst, const float* src, int n4) {
+  const int lane = (int)(threadIdx.x & 63);
+  for (int k = lane; k < n4; k += 64) {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(dst + 4 * (k - lane)));  // wave-uniform LDS base of this slot
+    const float* g = src + 4 * k;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds)
+        : "memory");
+  }
+}
+
 // The lane index through an empty volatile asm: every use re-derives it, so the compiler cannot
 // hoist the dozens of lane-dependent LDS addresses of a fused kernel out of its sample loop and
 // keep them live across every phase (measured on the InteractingLayer kernels: backward v2 167 ->

@@ -290,6 +290,38 @@ __device__ __forceinline__ void axpy_row(float (&o)[N], float p, const float* v)
   }
 }
 
+// packed-fp32 forms (v_pk_fma_f32: two fmas per lane per instruction, twice the v_fma_f32 rate;
+// the attention phases of the backward are VALU-issue bound).  Dot products keep two interleaved
+// partial sums (even / odd d), added at the end.  They need even-aligned register pairs: the
+// 128-VGPR forward kernel keeps the scalar forms (the packed ones spill there).
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+template <int N>
+__device__ __forceinline__ float dot_row_pk(const float (&q)[N], const float* p) {
+  const float4* p4 = reinterpret_cast<const float4*>(p);
+  f32x2v acc = {0.f, 0.f};
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) {
+    const float4 k = p4[d4];
+    acc = __builtin_elementwise_fma(f32x2v{q[4 * d4], q[4 * d4 + 1]}, f32x2v{k.x, k.y}, acc);
+    acc = __builtin_elementwise_fma(f32x2v{q[4 * d4 + 2], q[4 * d4 + 3]}, f32x2v{k.z, k.w}, acc);
+  }
+  return acc.x + acc.y;
+}
+
+template <int N>
+__device__ __forceinline__ void axpy_row_pk(float (&o)[N], float p, const float* v) {
+  const float4* v4 = reinterpret_cast<const float4*>(v);
+  const f32x2v pp = {p, p};
+#pragma unroll
+  for (int d4 = 0; d4 < N / 4; ++d4) {
+    const float4 t = v4[d4];
+    const f32x2v lo = __builtin_elementwise_fma(pp, f32x2v{t.x, t.y}, f32x2v{o[4 * d4], o[4 * d4 + 1]});
+    const f32x2v hi = __builtin_elementwise_fma(pp, f32x2v{t.z, t.w}, f32x2v{o[4 * d4 + 2], o[4 * d4 + 3]});
+    o[4 * d4] = lo.x; o[4 * d4 + 1] = lo.y; o[4 * d4 + 2] = hi.x; o[4 * d4 + 3] = hi.y;
+  }
+}
+
 
 // =============================================================================================
 // GEMM-shaped phases on the matrix cores: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate,
@@ -696,7 +728,7 @@ __device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C
 }
 
 // ---- phase: attention forward; optionally keeps P (pre-dropout) for backward ----------------
-template <class C, bool STORE_P, bool DROP, int OSTR = C::OS>
+template <class C, bool STORE_P, bool DROP, int OSTR = C::OS, bool PK = false>
 __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* PM,
                                               const Args& a, int64_t b, uint64_t lseed) {
   const int lane = lane_id();
@@ -714,7 +746,7 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < C::FMAX; ++j) {
-      const float acc = dot_row(q, kb + j * C::PRS);
+      const float acc = PK ? dot_row_pk(q, kb + j * C::PRS) : dot_row(q, kb + j * C::PRS);
       s[j] = (C::EXACT || j < F) ? acc * a.sc2 : -INFINITY;
       mx = fmaxf(mx, s[j]);
     }
@@ -732,7 +764,8 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
       float p = s[j] * inv;
       if (STORE_P && act) pm_row[j] = p;
       if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
-      axpy_row(o, p, vb + j * C::PRS);
+      if constexpr (PK) axpy_row_pk(o, p, vb + j * C::PRS);
+      else axpy_row(o, p, vb + j * C::PRS);
     }
     if (act) {
       float4* orow = reinterpret_cast<float4*>(O + i * OSTR + h * C::DH);
@@ -1640,15 +1673,24 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
 //   P6 dK -> K <- gK; V <- gV, Q <- gQ         P7 dW, db += X^T G; dx = G W^T (-> DY / push)
 constexpr int kWpb3 = 4;
 
+// P3 can form D_i = dO_i . O_i per head when a head's columns sit in whole lane groups of the
+// LN epilogue mapping (DH <= LPR, LPR % DH == 0)
+template <class C>
+constexpr bool kDRowDot = C::DH <= C::LPR && C::LPR % C::DH == 0;
+
 template <class C>
 struct Bwd3Layout {
-  // per-wave region (floats): X | PR (FMAX rows) | O | DY | PM | ST (mean, rstd per row)
-  int x, pr, o, dy, pm, st, per_wave;
+  // per-wave region (floats): XA | XB | PR (FMAX rows) | DY | PM | ST (the fused push's table
+  // rows).  XA / XB alternate as X (this iteration's input rows, stride E) and O (attention
+  // output, stride OS): once O is dead (after P6) the next iteration's input streams into it
+  // (global_load_lds, no registers) while P7 runs, and the two swap.
+  int xa, xb, pr, dy, pm, st, per_wave;
   __host__ __device__ Bwd3Layout(int F) {
+    const int xo = ((F * C::E > F * C::OS ? F * C::E : F * C::OS) + 3) & ~3;
     int off = 0;
-    x = off; off += (F * C::E + 3) & ~3;
+    xa = off; off += xo;
+    xb = off; off += xo;
     pr = off; off += (C::FMAX * C::PRS + 3) & ~3;
-    o = off; off += (F * C::OS + 3) & ~3;
     dy = off; off += (F * C::U + 3) & ~3;
     pm = off; off += (C::H * F * C::PMS + 3) & ~3;
     st = off; off += (2 * F + 3) & ~3;
@@ -1696,9 +1738,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
   float* const WL = smem;
   float* const BL = smem + ((C::E * C::WPS + 3) & ~3);
   float* const base = smem + Bwd3Layout<C>::shared_floats() + wave_id() * lay.per_wave;
-  float* const X = base + lay.x;
+  float* X = base + lay.xa;
   float* const PR = base + lay.pr;
-  float* const O = base + lay.o;
+  float* O = base + lay.xb;
   float* const DY = base + lay.dy;
   float* const PM = base + lay.pm;
   float* const ST = base + lay.st;
@@ -1727,42 +1769,28 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
 #pragma unroll
   for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
 
-  constexpr int PFX = (C::FMAX * C::E / 4 + 63) / 64;  // float4 per lane of one sample's rows
-  constexpr int PFY = (C::FMAX * C::U / 4 + 63) / 64;
   const int nx4 = F * C::E / 4, ny4 = F * C::U / 4;
   auto x_src = [&](int64_t bb, int itx) -> const float* {
     return itx == 0 ? x + bb * F * C::E : xsave + ((int64_t)(itx - 1) * a.B + bb) * F * C::U;
   };
   const int64_t b_first = (int64_t)blockIdx.x * kWpb3 + w;
   const int64_t b_step = (int64_t)gridDim.x * kWpb3;
-  float4 px[PFX], py[PFY];
-  if (b_first < a.B) {
-    row_prefetch<PFX>(px, x_src(b_first, a.L - 1), nx4);
-    row_prefetch<PFY>(py, dy + b_first * dy_ld, ny4);  // dy_vec: rows 16-B aligned
+  if (b_first < a.B) {  // the first sample's input rows and dy (dy_vec: rows 16-B aligned)
+    glds_copy_wave(X, x_src(b_first, a.L - 1), nx4);
+    glds_copy_wave(DY, dy + b_first * dy_ld, ny4);
   }
 
   IL_STAMP_DECL
   for (int64_t b = b_first; b < a.B; b += b_step) {
-#ifndef RS_BWD3_NOPF
-    row_commit<PFY>(DY, py, ny4);
-#endif
     for (int it = a.L - 1; it >= 0; --it) {
       IL_STAMP(0)
       const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
-#ifdef RS_BWD3_NOPF
-      row_prefetch<PFX>(px, x_src(b, it), nx4);
-      if (it == a.L - 1) { row_prefetch<PFY>(py, dy + b * dy_ld, ny4); row_commit<PFY>(DY, py, ny4); }
-      row_commit<PFX>(X, px, nx4);
-#else
-      row_commit<PFX>(X, px, nx4);
-      {  // prefetch the next iteration's input (and the next sample's dy) into registers
-        const int64_t bn = it > 0 ? b : b + b_step;
-        if (bn < a.B) {
-          row_prefetch<PFX>(px, x_src(bn, it > 0 ? it - 1 : a.L - 1), nx4);
-          if (it == 0) row_prefetch<PFY>(py, dy + bn * dy_ld, ny4);
-        }
-      }
-#endif
+      // fused push (it == 0): this sample's table rows, parked in ST (unused by v3) after P1,
+      // so the push at the end of the iteration reads them from LDS
+      vm_wait_all();  // X (and DY at it == L-1) streamed in by the previous iteration
+      int32_t rowv = -1;
+      const bool push_rows_now = it == 0 && a.push_table != nullptr;
+      if (push_rows_now && lane < F) rowv = a.push_rows[b * F + lane];
       wave_lds_sync();
       IL_STAMP(1)
       // ---- P1: projections ----
@@ -1771,22 +1799,24 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         mw.load_proj_lds(WL, BL);
         for (int rt = 0; rt < nrt; ++rt) mfma_project<C>(X, PR, F, rt, mw);
       }
+      if (push_rows_now && lane < F) reinterpret_cast<int32_t*>(ST)[lane] = rowv;
       wave_lds_sync();
       IL_STAMP(2)
       // ---- P2: attention recompute; P (pre-dropout) -> PM, O ----
-      attention_fwd<C, true, DROP, C::OS>(PR, O, PM, a, b, lseed);
+      attention_fwd<C, true, DROP, C::OS, true>(PR, O, PM, a, b, lseed);
       wave_lds_sync();
       IL_STAMP(3)
       // ---- P3: z = relu(O + R), LN stats, LN + ReLU backward: O <- dt; R <- gR ----
       for (int f0 = 0; f0 < F; f0 += C::RG) {
         const int f = f0 + lane / C::LPR;
         const bool act = f < F;
-        float z[C::CPLN], rr[C::CPLN];
+        float z[C::CPLN], rr[C::CPLN], oa[C::CPLN];
         float sum = 0.f;
 #pragma unroll
         for (int c = 0; c < C::CPLN; ++c) {
           const int u = u0 + c * C::LPR;
           float t = act ? O[f * C::OS + u] : 0.f;
+          oa[c] = t;  // the attention output (for D below)
           rr[c] = (a.use_res && act) ? PR[f * C::PRS + 3 * C::U + u] : 0.f;
           t += rr[c];
           z[c] = fmaxf(t, 0.f);
@@ -1813,14 +1843,21 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         }
         sg = group_sum<C::LPR>(sg) * (1.0f / (float)C::U);
         sgz = group_sum<C::LPR>(sgz) * (1.0f / (float)C::U);
-        if (act) {
 #pragma unroll
-          for (int c = 0; c < C::CPLN; ++c) {
-            const int u = u0 + c * C::LPR;
-            const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
-            const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+        for (int c = 0; c < C::CPLN; ++c) {
+          const int u = u0 + c * C::LPR;
+          const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
+          const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
+          if (act) {
             O[f * C::OS + u] = dt;
             PR[f * C::PRS + 3 * C::U + u] = (a.use_res && rr[c] > 0.f) ? dt : 0.f;
+          }
+          if constexpr (kDRowDot<C>) {
+            // D_{h,f} = sum_j P_fj dP_fj = dO_f . O_f over head h's columns (O = sum_j Pd_fj V_j,
+            // dropout included), reduced over the DH lanes of the head: P5 then needs one pass
+            // over the keys instead of two.  Parked in PM's pad column FMAX of row (h, f).
+            const float dd = group_sum<C::DH>(oa[c] * dt);
+            if (act && u % C::DH == 0) PM[((u / C::DH) * F + f) * C::PMS + C::FMAX] = dd;
           }
         }
       }
@@ -1838,7 +1875,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         for (int i = 0; i < F; ++i) {
           float p = PM[(h * F + i) * C::PMS + j];
           if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
-          axpy_row(dv, p, O + i * C::OS + h * C::DH);
+          axpy_row_pk(dv, p, O + i * C::OS + h * C::DH);
         }
         if (act) store_row(DY + j * C::U + h * C::DH, dv);
       }
@@ -1854,25 +1891,29 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         const float* vb = PR + 2 * C::U + h * C::DH;
         const float* kb = PR + C::U + h * C::DH;
         float* pm_row = PM + (h * F + i) * C::PMS;
-        // two passes over the keys (dP_ij recomputed in the second) instead of a dP row in
-        // registers: one wave holds the whole sample, and 26 live dP values per lane pushed v3
-        // past 256 VGPRs into scratch
+        // D_i from P3 (kDRowDot) and one pass over the keys; otherwise two passes (dP_ij
+        // recomputed in the second) rather than a dP row in registers: 26 live dP values per lane
+        // pushed v3 past 256 VGPRs into scratch
         float D = 0.f;
+        if constexpr (kDRowDot<C>) {
+          D = pm_row[C::FMAX];  // from P3
+        } else {
 #pragma unroll 2
-        for (int j = 0; j < F; ++j) {
-          float dp = dot_row(dO, vb + j * C::PRS);
-          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          D = fmaf(pm_row[j], dp, D);
+          for (int j = 0; j < F; ++j) {
+            float dp = dot_row_pk(dO, vb + j * C::PRS);
+            if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+            D = fmaf(pm_row[j], dp, D);
+          }
         }
         float dq[C::DH];
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
 #pragma unroll 2
         for (int j = 0; j < F; ++j) {
-          float dp = dot_row(dO, vb + j * C::PRS);
+          float dp = dot_row_pk(dO, vb + j * C::PRS);
           if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
           const float ds = pm_row[j] * (dp - D) * a.inv_sdh;
-          axpy_row(dq, ds, kb + j * C::PRS);
+          axpy_row_pk(dq, ds, kb + j * C::PRS);
           if (act) pm_row[j] = ds;
         }
         if (act) store_row(O + i * C::OS + h * C::DH, dq);  // dO_i (read above) dies here
@@ -1888,7 +1929,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
 #pragma unroll 4
-        for (int i = 0; i < F; ++i) axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
+        for (int i = 0; i < F; ++i) axpy_row_pk(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
         float kr[C::DH];
         load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
 #pragma unroll
@@ -1908,8 +1949,42 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         *qq = q0 > 0.f ? gq : 0.f;
       }
       wave_lds_sync();
+      {  // O is dead: stream the next iteration's input rows into it (and at it == 0, when DY is
+         // dead too, the next sample's dy) while P7 runs
+        const int64_t bn = it > 0 ? b : b + b_step;
+        if (bn < a.B) {
+          glds_copy_wave(O, x_src(bn, it > 0 ? it - 1 : a.L - 1), nx4);
+          if (it == 0) glds_copy_wave(DY, dy + bn * dy_ld, ny4);
+        }
+      }
       IL_STAMP(7)
       // ---- P7: dW += X^T G, db += colsum G; dx = G W^T ----
+      // fused push with the head's share (dx_base): its values for this lane's (row, col)
+      // slots, loaded before the dW MFMAs so dW + dx cover the round trip
+      constexpr int NRT7 = (C::FMAX + 15) / 16;
+      float bv[NRT7][M::ET][4];
+      if (it == 0 && a.push_table && dx_accumulate) {
+        const float* base_g = dx + b * F * C::E;
+        // lane re-derived (laundered): keeps LLVM from turning the 8 slot addresses into
+        // loop-carried pointers over b (they were spilled to scratch)
+        const int ln = lane_id(), q = ln >> 4, jx = ln & 15;
+#pragma unroll
+        for (int rt = 0; rt < NRT7; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et) {
+              const int f = 16 * rt + 4 * q + r, e = 16 * et + jx;
+              bv[rt][et][r] = (f < F && e < C::E) ? base_g[f * C::E + e] : 0.f;
+            }
+      } else {
+#pragma unroll
+        for (int rt = 0; rt < NRT7; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et) bv[rt][et][r] = 0.f;
+      }
       for (int rt = 0; rt < nrt; ++rt) mfma_dw<C>(X, PR, F, rt, dwacc, dbp);
       __builtin_amdgcn_sched_barrier(0);
       IL_STAMP(8)
@@ -1924,21 +1999,15 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
           constexpr int NRT = (C::FMAX + 15) / 16;
           const int q = lane >> 4, jx = lane & 15;
           int32_t rw[NRT][4];
-          float bv[NRT][M::ET][4];
-          const int32_t* rows = a.push_rows + b * F;
-          const float* base_g = dx_accumulate ? dx + b * F * C::E : nullptr;
+          const int32_t* rows = reinterpret_cast<const int32_t*>(ST);  // parked after P1
 #pragma unroll
           for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int f = 16 * rt + 4 * q + r;
               rw[rt][r] = f < F ? rows[f] : -1;
-#pragma unroll
-              for (int et = 0; et < M::ET; ++et) {
-                const int e = 16 * et + jx;
-                bv[rt][et][r] = (base_g && f < F && e < C::E) ? base_g[f * C::E + e] : 0.f;
-              }
             }
+          (void)jx;
           mfma_dx_all<C>(PR, F, mw, [&](int rt, int et, int r, int, int e, float v) {
             const int32_t row = rw[rt][r];
             if (row >= 0) {
@@ -1955,7 +2024,10 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
         }
       }
       wave_lds_sync();
-      IL_STAMP(9)
+      if (it > 0) { IL_STAMP(9) } else { IL_STAMP(10) }  // dx -> DY / dx -> push (it == 0)
+      float* const t = X;  // the next iteration's input is in O's buffer
+      X = O;
+      O = t;
     }
   }
   IL_STAMP_FLUSH(a.stamps)

@@ -8,6 +8,6 @@ mkdir -p gpurun_out/$R
 for w in multi_head din staytime; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 5 > gpurun_out/$R/bench_$w.log 2>&1 || { echo "bench $w failed rc=$?"; tail -20 gpurun_out/$R/bench_$w.log; exit 1; }
   grep '^{' gpurun_out/$R/bench_$w.log
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/prof_$w -o prof -- python3 bench.py --workload $w --steps 10 --warmup 3 > gpurun_out/$R/prof_$w.log 2>&1 || { echo "prof $w failed rc=$?"; tail -20 gpurun_out/$R/prof_$w.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$R/prof_$w -o prof -- python3 bench.py --workload $w --steps 10 --warmup 3 > gpurun_out/$R/prof_$w.log 2>&1 || { echo "prof $w failed rc=$?"; tail -20 gpurun_out/$R/prof_$w.log; exit 1; }
 done
 echo done

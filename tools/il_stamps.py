@@ -21,8 +21,8 @@ call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be
 for _ in range(3):
     call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
 torch.cuda.synchronize()
-v = st.cpu().tolist()[:9]
-names = ["x load/prefetch", "projection(MFMA)", "attn recompute", "LN bwd", "dV", "dS/dQ", "dK + G", "dW (MFMA)", "dx (MFMA)"]
+v = st.cpu().tolist()[:10]
+names = ["x load/prefetch", "projection(MFMA)", "attn recompute", "LN bwd", "dV", "dS/dQ", "dK + G", "dW (MFMA)", "dx (MFMA) it>0", "dx+push it=0"]
 tot = sum(v)
 for n, c in zip(names, v):
     print(f"{n:18s} {100.0 * c / tot:6.1f}%")
