@@ -1678,6 +1678,12 @@ constexpr int kWpb3 = 4;
 template <class C>
 constexpr bool kDRowDot = C::DH <= C::LPR && C::LPR % C::DH == 0;
 
+// P3 with lane = (row, head) when H == 2 and the rows fit one pass: each lane owns one head's DH
+// columns of one row, so the LN sums need one DPP step (the row's other head) instead of
+// log2(LPR) per sum, D_i is lane-local, and the row's loads/stores are float4s
+template <class C>
+constexpr bool kLnPair = C::H == 2 && C::DH % 4 == 0 && C::DH <= 16 && C::FMAX <= 32;
+
 template <class C>
 struct Bwd3Layout {
   // per-wave region (floats): XA | XB | PR (FMAX rows) | DY | PM | ST (the fused push's table
@@ -1696,8 +1702,8 @@ struct Bwd3Layout {
     st = off; off += (2 * F + 3) & ~3;
     per_wave = off;
   }
-  static constexpr int shared_floats() {  // W [E][WPS] | bias [NC]
-    return ((C::E * C::WPS + 3) & ~3) + ((C::NC + 3) & ~3);
+  static constexpr int shared_floats() {  // W [E][WPS] | bias [NC] | gamma [U]
+    return ((C::E * C::WPS + 3) & ~3) + ((C::NC + 3) & ~3) + ((C::U + 3) & ~3);
   }
 };
 
@@ -1752,6 +1758,8 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
   for (int k = threadIdx.x; k < C::E * C::NC; k += blockDim.x)
     WL[(k / C::NC) * C::WPS + k % C::NC] = W[k];
   for (int k = threadIdx.x; k < C::NC; k += blockDim.x) BL[k] = bias[k];
+  float* const GL = BL + ((C::NC + 3) & ~3);
+  for (int k = threadIdx.x; k < C::U; k += blockDim.x) GL[k] = gamma[k];
   zero_pad_rows<C>(PR, F);
   __syncthreads();  // the only workgroup barrier before the final reduction
 
@@ -1768,6 +1776,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
   const int u0 = lane % C::LPR;
 #pragma unroll
   for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
+  float dg2[C::DH], dbt2[C::DH];  // kLnPair: this lane's head columns (lane & 1), all its rows
+#pragma unroll
+  for (int d = 0; d < C::DH; ++d) { dg2[d] = 0.f; dbt2[d] = 0.f; }
 
   const int nx4 = F * C::E / 4, ny4 = F * C::U / 4;
   auto x_src = [&](int64_t bb, int itx) -> const float* {
@@ -1807,6 +1818,64 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
       wave_lds_sync();
       IL_STAMP(3)
       // ---- P3: z = relu(O + R), LN stats, LN + ReLU backward: O <- dt; R <- gR ----
+      if constexpr (kLnPair<C>) {
+        const int ln = lane_id(), f = ln >> 1, h = ln & 1;
+        const bool act = f < F;
+        const int fr = act ? f : 0;
+        float oa[C::DH], rr[C::DH], dyv[C::DH], gm[C::DH], z[C::DH];
+        load_row(oa, O + fr * C::OS + h * C::DH);
+        load_row(rr, PR + fr * C::PRS + 3 * C::U + h * C::DH);
+        load_row(dyv, DY + fr * C::U + h * C::DH);
+        load_row(gm, GL + h * C::DH);
+        float sum = 0.f;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) {
+          if (!a.use_res) rr[d] = 0.f;
+          if (!act) dyv[d] = 0.f;
+          z[d] = fmaxf(oa[d] + rr[d], 0.f);
+          sum += z[d];
+        }
+        const float mean = group_sum<2>(sum) * (1.0f / (float)C::U);
+        float sq = 0.f;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) { const float t = z[d] - mean; sq += t * t; }
+        const float var = group_sum<2>(sq) * (1.0f / (float)C::U);
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        float sg = 0.f, sgz = 0.f;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) {
+          const float zh = (z[d] - mean) * rstd;
+          dg2[d] = fmaf(dyv[d], zh, dg2[d]);
+          dbt2[d] += dyv[d];
+          const float g = dyv[d] * gm[d];
+          sg += g;
+          sgz += g * zh;
+          rr[d] = z[d] > 0.f ? 1.f : 0.f;  // ReLU mask of z (TF ReluGrad: x > 0)
+          z[d] = zh;
+          gm[d] = g;
+        }
+        sg = group_sum<2>(sg) * (1.0f / (float)C::U);
+        sgz = group_sum<2>(sgz) * (1.0f / (float)C::U);
+        float dt[C::DH];
+        float dd = 0.f;
+#pragma unroll
+        for (int d = 0; d < C::DH; ++d) {
+          const float dz = (gm[d] - sg - z[d] * sgz) * rstd;
+          dt[d] = rr[d] != 0.f ? dz : 0.f;
+          dd = fmaf(oa[d], dt[d], dd);
+        }
+        if (act) {
+          // gR = dt where the residual projection R > 0 (its own ReLU)
+          float rv[C::DH], gr[C::DH];
+          load_row(rv, PR + f * C::PRS + 3 * C::U + h * C::DH);
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) gr[d] = (a.use_res && rv[d] > 0.f) ? dt[d] : 0.f;
+          store_row(O + f * C::OS + h * C::DH, dt);
+          store_row(PR + f * C::PRS + 3 * C::U + h * C::DH, gr);
+          // D_{h,f} = dO_f . O_f over head h (see kDRowDot), lane-local here
+          PM[(h * F + f) * C::PMS + C::FMAX] = dd;
+        }
+      } else
       for (int f0 = 0; f0 < F; f0 += C::RG) {
         const int f = f0 + lane / C::LPR;
         const bool act = f < F;
@@ -2038,12 +2107,22 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
     dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
     dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
   }
+  if constexpr (kLnPair<C>) {  // lanes of one head parity hold the same columns
 #pragma unroll
-  for (int c = 0; c < C::CPLN; ++c) {
+    for (int d = 0; d < C::DH; ++d)
 #pragma unroll
-    for (int o = C::LPR; o < 64; o <<= 1) {
-      dg[c] += __shfl_xor(dg[c], o, 64);
-      dbt[c] += __shfl_xor(dbt[c], o, 64);
+      for (int o = 2; o < 64; o <<= 1) {
+        dg2[d] += __shfl_xor(dg2[d], o, 64);
+        dbt2[d] += __shfl_xor(dbt2[d], o, 64);
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < C::CPLN; ++c) {
+#pragma unroll
+      for (int o = C::LPR; o < 64; o <<= 1) {
+        dg[c] += __shfl_xor(dg[c], o, 64);
+        dbt[c] += __shfl_xor(dbt[c], o, 64);
+      }
     }
   }
   __syncthreads();
@@ -2067,7 +2146,16 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
 #pragma unroll
           for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + jx] += dbp[nt];
         }
-        if (lane < C::LPR) {
+        if constexpr (kLnPair<C>) {
+          if (lane < 2) {
+#pragma unroll
+            for (int d = 0; d < C::DH; ++d) {
+              const int u = lane * C::DH + d;
+              RED[C::E * C::NC + C::NC + u] += dg2[d];
+              RED[C::E * C::NC + C::NC + C::U + u] += dbt2[d];
+            }
+          }
+        } else if (lane < C::LPR) {
 #pragma unroll
           for (int c = 0; c < C::CPLN; ++c) {
             const int u = u0 + c * C::LPR;
