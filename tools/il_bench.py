@@ -20,8 +20,19 @@ def main(B=4096, F=26, E=16, U=16, H=2, L=3, reps=50):
     fwd = lambda: call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs))
     bwd = lambda: call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
     red = lambda: call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(dx), 0, ptr(dp), 0, ptr(ws), wsn)
+    # fused push variants (the trainer's launch): uniform rows (no hot rows) and Zipf-like rows
+    # (1/3 of the ids on one row per field), with and without the head's dx share to add
+    T = 26 * 100_000
+    rows_u = (torch.arange(B * F, device=dev, dtype=torch.int32) * 7919) % T
+    hot = torch.rand(B * F, device=dev, generator=g) < 0.33
+    rows_z = torch.where(hot, (torch.arange(B * F, device=dev) % F).to(torch.int32) * 100_000, rows_u)
+    table = torch.zeros(T, E, device=dev); flag = torch.full((T,), -1, dtype=torch.int32, device=dev)
+    base = torch.randn(B, F * E, device=dev, generator=g)
+    def push(rows, bp):
+        return lambda: call("rs_il_bwd_push", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(bp), ptr(rows), ptr(table), ptr(flag), None, 0, ptr(ws), wsn)
     out = {}
-    for name, fn in (("fwd", fwd), ("bwd", bwd), ("bwd+reduce", red)):
+    for name, fn in (("fwd", fwd), ("bwd", bwd), ("bwd+reduce", red), ("push_uniform", push(rows_u, None)),
+                     ("push_uniform_base", push(rows_u, base)), ("push_hot_base", push(rows_z, base))):
         fn(); torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
