@@ -31,8 +31,11 @@ def main(B=4096, F=26, E=16, U=16, H=2, L=3, reps=50):
     def push(rows, bp):
         return lambda: call("rs_il_bwd_push", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(bp), ptr(rows), ptr(table), ptr(flag), None, 0, ptr(ws), wsn)
     out = {}
+    only = os.environ.get("IL_BENCH_ONLY")  # one variant (PMC passes: one kernel per dispatch kind)
     for name, fn in (("fwd", fwd), ("bwd", bwd), ("bwd+reduce", red), ("push_uniform", push(rows_u, None)),
                      ("push_uniform_base", push(rows_u, base)), ("push_hot_base", push(rows_z, base))):
+        if only and name != only:
+            continue
         fn(); torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -40,8 +43,10 @@ def main(B=4096, F=26, E=16, U=16, H=2, L=3, reps=50):
         e1.record(); torch.cuda.synchronize()
         out[name + "_us"] = round(e0.elapsed_time(e1) / reps * 1e3, 2)
     fl = 289_536 * B
-    out["fwd_tflops"] = round(fl / out["fwd_us"] / 1e6, 2)
-    out["bwd_tflops"] = round(2 * fl / out["bwd_us"] / 1e6, 2)
+    if "fwd_us" in out:
+        out["fwd_tflops"] = round(fl / out["fwd_us"] / 1e6, 2)
+    if "bwd_us" in out:
+        out["bwd_tflops"] = round(2 * fl / out["bwd_us"] / 1e6, 2)
     print(json.dumps(out))
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
-"""HBM traffic of the InteractingLayer backward from the rocprofv3 PMC passes of
-tools/profile_round.sh (FETCH_SIZE and WRITE_SIZE in separate passes over tools/il_bench.py).
+"""HBM traffic of the InteractingLayer backward + fused push (the launch bench.py times) from the
+rocprofv3 PMC passes of tools/profile_round.sh (FETCH_SIZE and WRITE_SIZE in separate passes over
+IL_BENCH_ONLY=push_hot_base tools/il_bench.py: one bwd3 launch kind per pass).
 MI355X_MICROARCH.md (HBM): FETCH_SIZE reports half the bytes of wide coalesced reads on gfx950
 (x2 correction); WRITE_SIZE is exact for 16-B streaming stores.  Both are in KB per dispatch.
     python tools/traffic_json.py gpurun_out/r01 profiles/il_bwd_traffic.json"""
@@ -9,9 +10,12 @@ import json
 import sys
 
 B, F, E, U, L = 4096, 26, 16, 16, 3
-# algorithmic bytes of one rs_il_bwd launch (dparams NULL): read x (B F E), xsave ((L-1) B F U),
-# dy (B F U), write dx (B F E), write the per-block parameter partials (grid x 1120)
-ALG = 4 * (B * F * E + (L - 1) * B * F * U + B * F * U + B * F * E)
+GRID, NPARAM = 512, 1120  # kBwd3Grid blocks, per-block parameter partial row
+# algorithmic bytes of one rs_il_bwd_push launch (dparams NULL): read x (B F E), xsave
+# ((L-1) B F U), dy (B F U), the head's share dx_base (B F E), the rows (B F int32); add dL/dx0
+# into the table (B F E floats) and mark the flags (B F int32); write the per-block partials
+ALG = 4 * (B * F * E + (L - 1) * B * F * U + B * F * U + B * F * E + B * F + B * F * E + B * F) \
+    + 4 * GRID * NPARAM
 
 
 def mean_counter(root, name, kernel_sub):
@@ -24,19 +28,19 @@ def mean_counter(root, name, kernel_sub):
 
 
 def main(root, out):
-    k = "bwd2_kernel"
+    k = "bwd3_kernel"
     fetch, n1 = mean_counter(root, "FETCH_SIZE", k)
     write, n2 = mean_counter(root, "WRITE_SIZE", k)
-    partial_bytes = 1536 * 1120 * 4
     res = {
-        "kernel": "rs_il::bwd2_kernel<Cfg<16,16,2,26,true>,false> (B=4096, F=26, E=U=16, H=2, L=3)",
+        "kernel": "rs_il::bwd3_kernel<Cfg<16,16,2,26,true,false>,false> via rs_il_bwd_push "
+                  "(B=4096, F=26, E=U=16, H=2, L=3; hot rows, head share added)",
         "hbm_bytes_per_launch": round((2 * fetch + write) * 1024) if fetch and write else None,
         "fetch_size_kb": fetch, "write_size_kb": write, "dispatches": [n1, n2],
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads; "
                       "MI355X_MICROARCH.md HBM), WRITE_SIZE as is; both KB per dispatch",
-        "algorithmic_bytes_per_launch": ALG + partial_bytes,
+        "algorithmic_bytes_per_launch": ALG,
         "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) "
-                  "over tools/il_bench.py",
+                  "over IL_BENCH_ONLY=push_hot_base tools/il_bench.py",
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
