@@ -141,6 +141,119 @@ WORKLOADS = {
 }
 
 
+# algorithmic work of the configs-3-5 dominant kernels
+IL200_FWD_FLOPS_PER_SAMPLE = 1_382_400   # F=200, E=U=8, H=2: proj 102 400 + QK^T 640 000 + PV 640 000
+PUSH_BYTES_PER_ID = 4 + 64 + 128 + 4     # row index, dout row, grad row read + write, flag
+PUSH_BYTES_PER_SLOT = 4                  # every (sample, position) slot's row index is read
+
+
+def workload_roofline(args, model, pool, B, dev):
+    """Dominant kernel of configs 3-5 (rocprof, profiles/r02/prof_*), timed live with HIP events on
+    torch's current stream (the stream it is launched on) with the workload's own shapes:
+      multi_head  rs_il::large::bwd_kernel  -- InteractingLayer backward, F = 200 (48 % of the step)
+      din         sparse_grad_accum_kernel  -- the history push, B x 100 slots (28 %)
+      staytime    gemm_kernel (rs_dense_*)  -- the GEMM engine, on the widest expert layer
+                  [B, 1712] x [1712, 256] (the GEMMs are ~40 % of the step, spread over shapes)"""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    lib = _lib.load()
+    s = stream_handle()
+    g = torch.Generator(device=dev).manual_seed(7)
+    if args.workload == "multi_head":
+        F, E, U, H = model.cfg.num_fields, model.cfg.embed_dim, model.cfg.embed_dim, 2
+        il = model.interact
+        x = torch.rand(B, F, E, device=dev, generator=g) - 0.5
+        dy = torch.randn(B, F * U, device=dev, generator=g)
+        dx = torch.empty_like(x)
+        wsn = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+        ws = torch.empty(wsn, device=dev)
+        t = time_kernel(lambda: call(
+            "rs_il_bwd", s, ptr(x), None, ptr(dy), F * U, B, F, E, U, H, 1, ptr(il.kernel),
+            ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, il.dropout_rate, 11, ptr(dx),
+            0, None, 0, ptr(ws), wsn), args.kernel_reps)
+        fl = 2 * IL200_FWD_FLOPS_PER_SAMPLE * B
+        return {"bound": "mfma", "kernel": "rs_il::large::bwd_kernel<LC<8,8,2>> (IL backward, F=200, "
+                "dropout .2)", "achieved": round(fl / t / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(fl / t / 1e12 / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "launch_us": round(t * 1e6, 2), "flops_per_launch": fl}
+    if args.workload == "din":
+        qids, hids, hoffs, _ = pool[0]
+        T, vocab = model.T, model.table.rows
+        o = hoffs.long()
+        lens = torch.clamp(o[1:] - o[:-1], max=T)
+        pos = torch.arange(T, device=dev)[None, :]
+        idx = torch.clamp(o[:-1, None] + pos, max=hids.numel() - 1)
+        rows = torch.where(pos < lens[:, None], hids[idx] % vocab,
+                           torch.full_like(idx, -1)).to(torch.int32).reshape(-1).contiguous()
+        dout = torch.randn(B, T, model.table.dim, device=dev, generator=g)
+        tab = model.table
+        t = time_kernel(lambda: tab.accumulate(rows, None, B, T, dout, T * tab.dim, tab.dim, 0),
+                        args.kernel_reps)
+        nvalid = int(lens.sum())
+        by = PUSH_BYTES_PER_SLOT * B * T + PUSH_BYTES_PER_ID * nvalid
+        return {"bound": "hbm", "kernel": "sparse_grad_accum_kernel (history push, B x 100 slots, "
+                f"{nvalid} ids)", "achieved": round(by / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(by / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                "launch_us": round(t * 1e6, 2), "bytes_per_launch": by}
+    K, N = 1712, 256
+    X = torch.randn(B, K, device=dev, generator=g)
+    Wt = torch.randn(K, N, device=dev, generator=g) * 0.02
+    bt = torch.zeros(N, device=dev)
+    Y = torch.empty(B, N, device=dev)
+    t = time_kernel(lambda: call("rs_dense_fwd", s, ptr(X), B, K, K, ptr(Wt), ptr(bt), N, 1, ptr(Y), N),
+                    args.kernel_reps)
+    fl = 2 * B * K * N
+    return {"bound": "mfma", "kernel": f"gemm_kernel via rs_dense_fwd [{B}x{K}]x[{K}x{N}] relu (staytime "
+            "expert layer 1)", "achieved": round(fl / t / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(fl / t / 1e12 / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "launch_us": round(t * 1e6, 2), "flops_per_launch": fl}
+
+
+def workload_cpu_baseline(args, model, rng, B):
+    """configs 3-4: the fp32 torch-CPU TF-semantics train step (oracle/torch_ref.py
+    MultiHeadCPU / DINPoolCPU, kind "port") on a bounded sample of the workload (smaller batch
+    for config 3: its IL materialises [2B, 200, 200] scores), median of 3 runs, all threads and
+    1 thread.  Config 5 has no CPU port yet (None)."""
+    from oracle import torch_ref as tr
+    from recommendsystem_amd import workloads as W
+    if args.workload == "staytime":
+        return None
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    if args.workload == "multi_head":
+        Bc = 256
+        ref = tr.MultiHeadCPU(model)
+        batches = [ref.prepare(*(t.cpu() for t in W.multi_head_batch(rng, Bc, model.cfg, "cpu")))
+                   for _ in range(2)]
+    else:
+        Bc = B
+        ref = tr.DINPoolCPU(model)
+        batches = [ref.prepare(*(t.cpu() for t in W.din_batch(rng, Bc, model.T, model.table.rows, "cpu")))
+                   for _ in range(2)]
+    per_run = max(args.cpu_baseline_seconds / 6.0, 0.5)
+
+    def runs(n):
+        torch.set_num_threads(n)
+        ref.step(*batches[0])
+        rates, tot = [], 0
+        for _ in range(3):
+            t0, k = time.perf_counter(), 0
+            while k < 2 or time.perf_counter() - t0 < per_run:
+                ref.step(*batches[k % len(batches)])
+                k += 1
+            rates.append(Bc * k / (time.perf_counter() - t0))
+            tot += k
+        return float(np.median(rates)), tot
+
+    multi, nm = runs(threads)
+    single, ns = runs(1)
+    torch.set_num_threads(threads)
+    return {"value": round(multi, 1), "unit": "samples/sec", "cores": threads, "kind": "port",
+            "single_thread": {"value": round(single, 1), "cores": 1},
+            "sample": f"{args.workload} train steps at batch {Bc} of the TF-semantics fp32 torch-CPU "
+                      f"restatement (oracle/torch_ref.py {type(ref).__name__}): median of 3 runs of "
+                      f">= {per_run:.1f} s, {nm} steps on {threads} threads, {ns} on 1 thread"}
+
+
 def run_workload(args, world, rank, dev, pg):
     """Configs 3-5 through the generic Trainer (eager autograd composition of the kernels)."""
     from recommendsystem_amd.models import MultiHeadConfig, MultiHeadRanker
@@ -188,6 +301,10 @@ def run_workload(args, world, rank, dev, pg):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     samples = B * args.steps * world
+    roofline = workload_roofline(args, model, pool, B, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
+        cpu = workload_cpu_baseline(args, model, rng, B)
     out = {"metric": f"samples/sec {args.workload} train ({desc})", "value": round(samples / dt, 1),
            "unit": "samples/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
@@ -196,7 +313,7 @@ def run_workload(args, world, rank, dev, pg):
            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                       "parallelism": f"dp{world}",
                       "execution": "one HIP graph per pool batch" if graphed else "eager autograd"},
-           "roofline": None, "cpu_baseline": None, "final_loss": round(float(loss), 6)}
+           "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(float(loss), 6)}
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -67,7 +67,7 @@ def layer_norm(x, gamma, beta, eps=1e-14):
 
 
 def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=True, eps=1e-14,
-                      drop_rate=0.0, seed=0, bf16=False):
+                      drop_rate=0.0, seed=0, bf16=False, torch_mask=False):
     """InteractingLayer.py:37-61, op for op (tied weights across layer_num iterations).
     bf16: the projections round their operands as the library's bf16 math mode does (forward and
     backward GEMMs); attention, LN and everything else unchanged."""
@@ -89,7 +89,10 @@ def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=
         w = torch.matmul(q, k.transpose(1, 2))
         w = w / float((U // H) ** 0.5)
         w = torch.softmax(w, dim=-1)
-        if drop_rate > 0.0:
+        if drop_rate > 0.0 and torch_mask:  # CPU baseline: TF-style RNG mask (throughput only)
+            w = torch.where(torch.rand_like(w) >= drop_rate, w * (1.0 / (1.0 - drop_rate)),
+                            torch.zeros_like(w))
+        elif drop_rate > 0.0:
             HB, Fq, Fk = w.shape
             hh, bb = divmod(torch.arange(HB).numpy(), B)
             keep = npo.dropout_keep(npo.layer_seed(seed, it), bb[:, None, None], hh[:, None, None],
@@ -473,3 +476,132 @@ def deepfm_sub_model(general_list, bias_list, P, hidden=(64, 32)):
     two = dense(one, *P["bais_dnn_two_3"], "sigmoid") * 2
     x = x * two
     return dense(torch.cat([x, fm], dim=1), *P["pred"], "sigmoid")
+
+
+# ==========================================================================================
+# CPU train steps of configs 3 and 4 (the bench's cpu_baseline legs; kind "port"): the same
+# unfused TF-semantics op sequences as above in fp32 on the host, dense Adam (tf.keras form) and
+# sparse Adam on the touched rows (tensornet form), from copies of a device model's weights.
+# ==========================================================================================
+class _CPUTrainBase:
+    def _init_opt(self, lr_dense, lr_sparse):
+        self.m = [torch.zeros_like(p) for p in self.dense_list]
+        self.v = [torch.zeros_like(p) for p in self.dense_list]
+        self.m_tab = torch.zeros_like(self.table)
+        self.v_tab = torch.zeros_like(self.table)
+        self.t = 0
+        self.lr_dense, self.lr_sparse = lr_dense, lr_sparse
+
+    def _update(self, loss, leaves, rows):
+        grads = torch.autograd.grad(loss, leaves + self.dense_list)
+        gl, gd = grads[:len(leaves)], grads[len(leaves):]
+        with torch.no_grad():
+            self.t += 1
+            b1, b2, eps = 0.9, 0.999, 1e-8
+            lr_t = self.lr_dense * (1 - b2 ** self.t) ** 0.5 / (1 - b1 ** self.t)
+            for p_, g, m, v in zip(self.dense_list, gd, self.m, self.v):
+                m.mul_(b1).add_(g, alpha=1 - b1)
+                v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                p_.sub_(lr_t * m / (v.sqrt() + eps))
+            r = torch.cat([x.reshape(-1) for x in rows])
+            g = torch.cat([x.reshape(rr.numel(), -1) for x, rr in zip(gl, rows)])
+            keep = r >= 0
+            r, g = r[keep], g[keep]
+            uniq, inv = torch.unique(r, return_inverse=True)
+            gsum = torch.zeros(uniq.numel(), self.table.shape[1]).index_add_(0, inv, g)
+            m = self.m_tab[uniq].mul_(b1).add_(gsum, alpha=1 - b1)
+            v = self.v_tab[uniq].mul_(b2).addcmul_(gsum, gsum, value=1 - b2)
+            self.m_tab[uniq] = m
+            self.v_tab[uniq] = v
+            self.table[uniq] -= self.lr_sparse * m / (eps + v.sqrt())
+        return float(loss.detach())
+
+
+def _cpu(t):
+    return t.detach().float().cpu().clone().requires_grad_(True)
+
+
+class DINPoolCPU(_CPUTrainBase):
+    """Config 4 (workloads.DINPool): query lookup, history lookup, din.py DIN pool, Dense(1,
+    sigmoid) on [pooled, q], cross_entropy (rank/multi_head/model.py:18-22), backward, Adam."""
+
+    def __init__(self, model, lr_dense=5e-5, lr_sparse=5e-5):
+        self.table = model.table.weight.detach().float().cpu().clone()
+        self.vocab, self.T = model.table.rows, model.T
+        d = model.din
+        self.W1, self.b1, self.W2, self.b2 = (_cpu(p) for p in (d.W1, d.b1, d.W2, d.b2))
+        self.Wo, self.bo = _cpu(model.out.kernel), _cpu(model.out.bias)
+        self.dense_list = [self.W1, self.b1, self.W2, self.b2, self.Wo, self.bo]
+        self._init_opt(lr_dense, lr_sparse)
+
+    def prepare(self, qids, hids, hoffs, labels):
+        """Host-side batch (the pre-generated input): query rows [B], padded history rows [B, T]
+        (-1 past the length), lengths [B], labels."""
+        q = torch.as_tensor(qids).long() % self.vocab
+        h, o = torch.as_tensor(hids).long() % self.vocab, torch.as_tensor(hoffs).long()
+        B = q.numel()
+        lens = torch.clamp(o[1:] - o[:-1], max=self.T)
+        pos = torch.arange(self.T)[None, :]
+        idx = torch.clamp(o[:-1, None] + pos, max=max(h.numel() - 1, 0))
+        rows = torch.where(pos < lens[:, None], h[idx], torch.full_like(idx, -1))
+        return q, rows, lens, torch.as_tensor(labels).float().reshape(B, -1)
+
+    def step(self, q, rows, lens, y):
+        qe = self.table.index_select(0, q).requires_grad_(True)
+        he = self.table.index_select(0, rows.clamp(min=0).reshape(-1)).reshape(*rows.shape, -1)
+        he = torch.where((rows >= 0)[..., None], he, torch.zeros_like(he)).requires_grad_(True)
+        pooled = din_pool(qe, he, he, lens, self.W1, self.b1, self.W2, self.b2)
+        p = dense(torch.cat([pooled, qe], 1), self.Wo, self.bo, "sigmoid")
+        loss = torch.mean(torch.sum(-y * torch.log(p + 1e-6) - (1 - y) * torch.log(1 - p + 1e-6), 1))
+        return self._update(loss, [qe, he], [q, rows])
+
+
+class MultiHeadCPU(_CPUTrainBase):
+    """Config 3 (models.MultiHeadRanker, rank/multi_head/multidnn.py:14-259): multi-hot mean
+    lookup, IL(1, 8, 2, dropout .2, res), deep Dense(32, 16), 7 experts / 7 softmax gates, 7
+    sigmoid towers, cross_entropy, backward, Adam (L1L2 / L2 regularisers omitted: <1 % of the
+    work)."""
+
+    def __init__(self, model, lr_dense=1e-5, lr_sparse=5e-5):
+        self.table = model.table.weight.detach().float().cpu().clone()
+        self.cfg = cfg = model.cfg
+        il = model.interact
+        self.il = [_cpu(p) for p in (il.kernel, il.bias, il.gamma, il.beta)]
+        self.eps = il.epsilon
+        self.deep = [(_cpu(l.kernel), _cpu(l.bias)) for l in model.deep]
+        self.Wc, self.bc = _cpu(model.mix.kernel), _cpu(model.mix.bias)
+        self.TW, self.Tb = _cpu(model.towers.W), _cpu(model.towers.b)
+        self.row_base = model.embedding.row_base.cpu().long()
+        self.bucket = model.embedding.bucket.cpu().long()
+        self.dense_list = self.il + [t for l in self.deep for t in l] + [self.Wc, self.bc, self.TW, self.Tb]
+        self._init_opt(lr_dense, lr_sparse)
+
+    def prepare(self, ids, offsets, labels):
+        ids, offs = torch.as_tensor(ids).long(), torch.as_tensor(offsets).long()
+        F = self.cfg.num_fields
+        nseg = offs.numel() - 1
+        cnt = offs[1:] - offs[:-1]
+        seg = torch.repeat_interleave(torch.arange(nseg), cnt)
+        f = seg % F
+        rows = self.row_base[f] + torch.remainder(ids, self.bucket[f])
+        return rows, seg, cnt.clamp(min=1).float(), torch.as_tensor(labels).float()
+
+    def step(self, rows, seg, cnt, y):
+        cfg = self.cfg
+        B, F, E = y.shape[0], cfg.num_fields, cfg.embed_dim
+        e = self.table.index_select(0, rows).requires_grad_(True)
+        x0 = (torch.zeros(B * F, E).index_add(0, seg, e) / cnt[:, None]).reshape(B, F, E)
+        auto = interacting_layer(x0, *self.il, 1, 2, True, self.eps, drop_rate=cfg.dropout_rate,
+                                 torch_mask=True).reshape(B, -1)
+        deep = mlp(x0.reshape(B, -1), self.deep, "relu")
+        result = torch.cat([deep, auto], 1)
+        D, NE, ns = 32, 7, 7
+        We = [self.Wc[:, k * D:(k + 1) * D] for k in range(NE)]
+        be = [self.bc[k * D:(k + 1) * D] for k in range(NE)]
+        Wg = [self.Wc[:, NE * D + t * ns:NE * D + (t + 1) * ns] for t in range(7)]
+        bg = [self.bc[NE * D + t * ns:NE * D + (t + 1) * ns] for t in range(7)]
+        outs = multi_head_gates(result, We, be, Wg, bg, 7)
+        preds = torch.cat([torch.sigmoid(o @ self.TW[t] + self.Tb[t]).reshape(B, 1)
+                           for t, o in enumerate(outs)], 1)
+        loss = cross_entropy(y, preds)
+        return self._update(loss, [e], [rows])
