@@ -68,6 +68,21 @@ int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* 
                               int32_t* flag, int32_t* touched, int32_t* n_touched,
                               int32_t touched_cap);
 
+/* Deterministic variant of rs_sparse_grad_accumulate: sort by row + segmented sum,
+ * so each touched row receives the sum of its occurrences in ascending id order with one plain
+ * read-modify-write -- bitwise reproducible run to run (the atomic push reproduces only the row
+ * set).  Same arguments and marking/claiming semantics, plus table_rows (ids outside the table
+ * push nothing), n_ids (ids in the batch: offsets[B*F], or B*F single-hot -- no host read back)
+ * and a workspace of >= rs_sparse_sorted_workspace_bytes(n_ids) bytes.  dim <= 128.  Async on
+ * the stream (hipcub radix sort / run-length encode / scan + two kernels): graph-capturable. */
+int64_t rs_sparse_sorted_workspace_bytes(int64_t n_ids);
+int rs_sparse_grad_accumulate_sorted(void* stream, const int32_t* rows, const int32_t* offsets,
+                                     int64_t B, int F, const float* dout, int64_t dout_ld,
+                                     int64_t dout_fstride, int dim, int combiner,
+                                     int64_t table_rows, float* grad_table, int32_t* flag,
+                                     int32_t* touched, int32_t* n_touched, int32_t touched_cap,
+                                     void* workspace, int64_t workspace_bytes, int64_t n_ids);
+
 /* H11 sparse optimizers on the touched rows (tensornet tn.core.Adam / tn.core.AdaGrad handed to
  * EmbeddingFeatures: rank/ctr/base_model.py:163, rank/multi_head/multidnn.py:235,
  * staytime/VideoDnn.py:233).  Zero the gradient rows, release the flags, reset the count.

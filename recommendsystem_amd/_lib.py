@@ -37,6 +37,10 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_adagrad": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32]),
     "rs_sparse_compact": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32]),
     "rs_sparse_merge_rows": (_i32, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32]),
+    "rs_sparse_sorted_workspace_bytes": (_i64, [_i64]),
+    "rs_sparse_grad_accumulate_sorted": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32,
+                                                _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _i64,
+                                                _i64]),
     "rs_set_math_mode": (_i32, [_i32]),
     "rs_get_math_mode": (_i32, []),
     "rs_set_seed_offset": (_i32, [_vp]),

@@ -127,7 +127,8 @@ class AutoIntTrainer:
     ``capture()`` records the step into a torch.cuda.CUDAGraph (hipGraph); ``step()`` replays it.
     """
 
-    def __init__(self, model: AutoInt, batch_size: int, process_group=None):
+    def __init__(self, model: AutoInt, batch_size: int, process_group=None,
+                 deterministic: bool = False):
         self.model = m = model
         cfg = m.cfg
         self.B = B = int(batch_size)
@@ -188,8 +189,14 @@ class AutoIntTrainer:
                                             (self.head["N1"], self.head["N2"]) != (32, 16)):
             raise ValueError("bf16 compute mode has kernels for the config-2 shape only (F <= 32, "
                              "E = U = 16, H = 2, fused head with mlp [32, 16])")
-        # fused path: the IL backward pushes dL/dx0 straight into the table (scan-mode marks)
-        self.push = self.head is not None and self.F <= 64
+        # fused path: the IL backward pushes dL/dx0 straight into the table (scan-mode marks);
+        # deterministic: dL/dx0 is stored and pushed by the sorted segmented sum instead (bitwise
+        # reproducible embedding gradients; one more launch and a dx0 round trip)
+        self.deterministic = bool(deterministic)
+        self.push = self.head is not None and self.F <= 64 and not self.deterministic
+        if self.deterministic:
+            m.table.deterministic = True
+            m.table.sorted_workspace(B * F)
         if self.push:
             m.table.mode = "scan"
         # data parallel, fused path: packed exchange (dist.exchange_packed) -- the dense partials

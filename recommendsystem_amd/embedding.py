@@ -85,6 +85,10 @@ class SparseTable:
         # mark flag[] and the optimizer sweeps it (no returning atomics in the push; best when
         # the table is not much larger than ~100x the rows a step touches)
         self.mode = "list"
+        # deterministic pushes (rs_sparse_grad_accumulate_sorted: sort + segmented sum, bitwise
+        # reproducible) instead of the LDS-hash + float-atomic push; workspace grown on demand
+        self.deterministic = False
+        self._sorted_ws = None
         # autograd anchor: lets the lookup's backward run (it returns no dense gradient)
         self.anchor = torch.zeros((), device=device, dtype=torch.float32, requires_grad=True)
 
@@ -92,10 +96,28 @@ class SparseTable:
     def accumulate(self, rows: torch.Tensor, offsets: torch.Tensor | None, B: int, F: int,
                    dout: torch.Tensor, dout_ld: int, dout_fstride: int, combiner: int) -> None:
         scan = self.mode == "scan"
+        if self.deterministic:
+            n = rows.numel()
+            ws = self.sorted_workspace(n)
+            call("rs_sparse_grad_accumulate_sorted", stream_handle(), ptr(rows), ptr(offsets), B, F,
+                 ptr(dout), dout_ld, dout_fstride, self.dim, combiner, self.rows, ptr(self.grad),
+                 ptr(self.flag), None if scan else ptr(self.touched),
+                 None if scan else ptr(self.n_touched), self.touched_cap, ptr(ws), ws.numel(), n)
+            return
         call("rs_sparse_grad_accumulate", stream_handle(), ptr(rows), ptr(offsets), B, F, ptr(dout),
              dout_ld, dout_fstride, self.dim, combiner, ptr(self.grad), ptr(self.flag),
              None if scan else ptr(self.touched), None if scan else ptr(self.n_touched),
              self.touched_cap)
+
+    def sorted_workspace(self, n_ids: int) -> torch.Tensor:
+        """Workspace of the deterministic push for n_ids ids (kept and reused; reserve the
+        largest batch before capturing a graph)."""
+        need = int(_lib.load().rs_sparse_sorted_workspace_bytes(n_ids))
+        if need < 0:
+            raise ValueError(f"{n_ids} ids: too many for the deterministic push")
+        if self._sorted_ws is None or self._sorted_ws.numel() < need:
+            self._sorted_ws = torch.empty(need, device=self.weight.device, dtype=torch.uint8)
+        return self._sorted_ws
 
     def check_overflow(self) -> None:
         """Raise if any step since the last check claimed more rows than the touched list holds
