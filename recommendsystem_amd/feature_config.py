@@ -149,3 +149,18 @@ class SlotLayout:
             base = pos[slot] * self.max_embed_size
             cols.extend(range(base + a, base + b))
         return cols
+
+# staytime Config.SLOTS / SEQ_SLOTS (staytime/config.py:4-16): the VarLen int64 slots of
+# parse_input_func (parse.py:22-23) and the behaviour sequences (data.dataset_reader's default)
+STAYTIME_SLOTS = (
+    '1568', '1570', '1571', '1574', '1575', '1576', '1577', '1578', '1579', '1581', '1582',
+    '1583', '1585', '1587', '1589', '1591', '1592', '1593', '1594', '1595', '1599', '1601',
+    '1611', '1612', '1614', '1616', '1623', '1636', '1736', '1737', '1738', '1739', '1740',
+    '1741', '1743', '1744', '1749', '2039', '2040', '2041', '2042', '2043', '2044', '2050',
+    '2051', '2052', '2123', '2125', '2127', '2128', '2130', '2131', '2135', '2139', '2142',
+    '2144', '2147', '2149', '2151', '2152', '2154', '2156', '2544', '2597', '3051', '3365',
+    '3369', '3376', '3370', '1745', '2045', '1632', '1735', '2153', '2047', '2244', '2046',
+    '2150', '2247', '1625', '1624', '2148', '2159', '2146', '2242', '2260', '2155', '2259',
+    '2615', '4500', '4386',
+)
+STAYTIME_SEQ_SLOTS = ('2125', '2128', '2130')

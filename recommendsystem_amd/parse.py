@@ -75,8 +75,11 @@ def landing_flags(extra_info: Sequence[str | bytes]) -> np.ndarray:
 
 
 def _to_device(v, device):
+    """host column -> device int64 (pinned host tensors copy asynchronously)."""
     if isinstance(v, tuple):          # ragged (values, row_splits)
-        return tuple(torch.as_tensor(np.asarray(a), dtype=torch.int64).to(device) for a in v)
+        return tuple(_to_device(a, device) for a in v)
+    if isinstance(v, torch.Tensor):
+        return v.to(device=device, dtype=torch.int64, non_blocking=v.is_pinned())
     return torch.as_tensor(np.asarray(v), dtype=torch.int64).to(device)
 
 
@@ -87,7 +90,8 @@ def parse_input_func(example: dict, device: str | torch.device = "cuda",
     if "watch_duration" not in ex or "video_duration" not in ex:
         raise KeyError("parse_input_func: watch_duration and video_duration are required "
                        "(FixedLenFeature without default, parse.py:19-20)")
-    wt = torch.as_tensor(np.asarray(ex.pop("watch_duration")), dtype=torch.int64)
+    wt = ex.pop("watch_duration")
+    wt = wt.to(torch.int64) if isinstance(wt, torch.Tensor) else torch.as_tensor(np.asarray(wt), dtype=torch.int64)
     B = wt.numel()
     extra_info = list(ex.pop("extra_info", ["label"] * B))              # parse.py:18 default
     if len(extra_info) != B:
@@ -95,7 +99,7 @@ def parse_input_func(example: dict, device: str | torch.device = "cuda",
     landing = torch.from_numpy(landing_flags(extra_info))
     features = {k: _to_device(v, device) for k, v in ex.items()}
     features["example_id"] = extra_info                                 # parse.py:27
-    stay, short, long_, sw = staytime_labels(wt.to(device), landing)
+    stay, short, long_, sw = staytime_labels(wt.to(device, non_blocking=wt.is_pinned()), landing)
     y = {f"{prefix}_staytime": stay, f"{prefix}_shortplay": short,
          f"{prefix}_longplay": long_}
     return features, y, sw
