@@ -268,6 +268,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         float q[C::DH];
         ld<C::DH>(q, Qs + i * C::U + h * C::DH);
         float mx = -INFINITY;
+#pragma unroll 4
         for (int j = 0; j < F; ++j) {
           float k[C::DH];
           ld<C::DH>(k, Ks + j * C::U + h * C::DH);
@@ -278,6 +279,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
 #pragma unroll
         for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
         const uint32_t* mrow = mask + (h * F + i) * W32;
+#pragma unroll 4
         for (int j = 0; j < F; ++j) {
           float k[C::DH], v[C::DH];
           ld<C::DH>(k, Ks + j * C::U + h * C::DH);
@@ -355,6 +357,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
         const float msc = stm[h * F + i], il = sti[h * F + i], D = std_[h * F + i];
         const uint32_t* mrow = mask + (h * F + i) * W32;
+#pragma unroll 4
         for (int j = 0; j < F; ++j) {
           float k[C::DH], v[C::DH];
           ld<C::DH>(k, Ks + j * C::U + h * C::DH);
@@ -379,6 +382,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         for (int d = 0; d < C::DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
         const int jw = j >> 5;
         const uint32_t jb = 1u << (j & 31);
+#pragma unroll 4
         for (int i = 0; i < F; ++i) {
           float q[C::DH], g[C::DH];
           ld<C::DH>(q, Qs + i * C::U + h * C::DH);
