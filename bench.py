@@ -213,16 +213,21 @@ def workload_cpu_baseline(args, model, rng, B):
     """configs 3-4: the fp32 torch-CPU TF-semantics train step (oracle/torch_ref.py
     MultiHeadCPU / DINPoolCPU, kind "port") on a bounded sample of the workload (smaller batch
     for config 3: its IL materialises [2B, 200, 200] scores), median of 3 runs, all threads and
-    1 thread.  Config 5 has no CPU port yet (None)."""
+    1 thread.  Config 5: oracle/model_oracles.py StaytimeRoughRankCPU (host copy of the 10M x 32
+    table, sparse AdaGrad) on device-generated staytime batches copied to the host."""
     from oracle import torch_ref as tr
     from recommendsystem_amd import workloads as W
-    if args.workload == "staytime":
-        return None
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     if args.workload == "multi_head":
         Bc = 256
         ref = tr.MultiHeadCPU(model)
         batches = [ref.prepare(*(t.cpu() for t in W.multi_head_batch(rng, Bc, model.cfg, "cpu")))
+                   for _ in range(2)]
+    elif args.workload == "staytime":
+        from oracle.model_oracles import StaytimeRoughRankCPU
+        Bc = 256
+        ref = StaytimeRoughRankCPU(model)
+        batches = [ref.prepare(W.staytime_batch(rng, Bc, model, model.table.weight.device))
                    for _ in range(2)]
     else:
         Bc = B
@@ -250,7 +255,7 @@ def workload_cpu_baseline(args, model, rng, B):
     return {"value": round(multi, 1), "unit": "samples/sec", "cores": threads, "kind": "port",
             "single_thread": {"value": round(single, 1), "cores": 1},
             "sample": f"{args.workload} train steps at batch {Bc} of the TF-semantics fp32 torch-CPU "
-                      f"restatement (oracle/torch_ref.py {type(ref).__name__}): median of 3 runs of "
+                      f"restatement ({type(ref).__module__}.{type(ref).__name__}): median of 3 runs of "
                       f">= {per_run:.1f} s, {nm} steps on {threads} threads, {ns} on 1 thread"}
 
 

@@ -11,6 +11,8 @@ import torch
 
 from oracle import ctr_oracle as npo
 from oracle import torch_ref as tr
+from oracle.model_oracles import dssm_oracle as _dssm_oracle
+from oracle.model_oracles import staytime_oracle as _staytime_oracle
 from _tol import assert_close, assert_grad_close, to_np
 
 pytestmark = pytest.mark.gpu
@@ -92,23 +94,6 @@ def test_multi_head_ranker_matches_oracle(B, vocab):
 # ------------------------------------------------------------------------------------------
 # H8: rough_rank DSSM
 # ------------------------------------------------------------------------------------------
-def _tower_ref(tower, x, mask=None):
-    mix = tower.ple.mix
-    Wc, bc = c64(mix.kernel), c64(mix.bias)
-    D, S, P, T = mix.D, 4, 4, mix.n_task
-    ek = lambda e: ([Wc[:, e * D:(e + 1) * D]], [bc[e * D:(e + 1) * D]])  # noqa: E731
-    ns, NE = mix.n_sel, mix.n_exp
-    gk = lambda t: ([Wc[:, NE * D + t * ns:NE * D + (t + 1) * ns]], [bc[NE * D + t * ns:NE * D + (t + 1) * ns]])  # noqa: E731
-    outs = tr.ple(x, [ek(e) for e in range(S)], [[ek(S + t * P + j) for j in range(P)] for t in range(T)],
-                  [gk(t) for t in range(T)])
-    heads = [(c64(h.layers[0].kernel), c64(h.layers[0].bias)) for h in tower.heads]
-    embs = [tr.dnn(o, [k], [b], "relu", "linear") for o, (k, b) in zip(outs, heads)]
-    params = [(mix.kernel, Wc), (mix.bias, bc)] + [(h.layers[0].kernel, k) for h, (k, _) in zip(tower.heads, heads)]
-    if mask is not None:
-        return torch.where(mask.reshape(-1, 1) == 1, embs[1], embs[0]), params
-    return embs[0], params
-
-
 def test_dssm_matches_oracle():
     from recommendsystem_amd.models import DSSM, DSSMConfig
     rng = np.random.default_rng(32)
@@ -135,100 +120,9 @@ def test_dssm_matches_oracle():
         assert_grad_close(to_np(p.grad), r.grad.numpy(), "dssm param")
 
 
-def _dssm_oracle(m, e64, mask, y):
-    """float64 composition of rough_rank DSSM (rough_rank/model.py:118-222) from m's weights on
-    the leaf e64 [B, user+item fields, 16]: loss (student/teacher BCE + KD), logits and the
-    (parameter, fp64 leaf) pairs whose gradients the tests check."""
-    B = e64.shape[0]
-    maskc = torch.from_numpy(mask.cpu().numpy()).double()
-    ui, ii = m.user_idx.cpu(), m.item_idx.cpu()
-    u_emb, pu = _tower_ref(m.user, e64[:, ui].reshape(B, -1), maskc)
-    i_emb, pi = _tower_ref(m.item, e64[:, ii].reshape(B, -1))
-    wc = e64.reshape(B, -1)
-    Wx, bx = c64(m.cross.W), c64(m.cross.b)
-    D = wc.shape[1]
-    cross = tr.crossnet(wc, [Wx[l].reshape(D, 1) for l in range(2)], [bx[l].reshape(D, 1) for l in range(2)])
-    L = {n: (c64(getattr(m, n).kernel), c64(getattr(m, n).bias)) for n in ("t1", "t2", "t3", "t4", "s1", "s2")}
-    deep = tr.dense(tr.dense(wc, *L["t1"], "relu"), *L["t2"], "relu")
-    t_logit = tr.dense(tr.dense(torch.cat([deep, cross], 1), *L["t3"]), *L["t4"])
-    s_logit = tr.dense(tr.dense(torch.cat([u_emb, i_emb], 1), *L["s1"], "relu"), *L["s2"])
-    yc = torch.from_numpy(y.cpu().numpy()).double()
-    ref_loss = (tr.keras_bce(yc, torch.sigmoid(s_logit)) + tr.keras_bce(yc, torch.sigmoid(t_logit))
-                + tr.kd_loss(s_logit, t_logit.detach()).mean())
-    params = pu + pi + [(m.cross.W, Wx), (m.cross.b, bx)] + [(getattr(m, n).kernel, L[n][0]) for n in L]
-    return dict(loss=ref_loss, s_logit=s_logit, t_logit=t_logit, params=params)
-
-
 # ------------------------------------------------------------------------------------------
 # H9: staytime mtl_net
 # ------------------------------------------------------------------------------------------
-def _staytime_oracle(m, cfg, e64, s64, mk, stay, short, long_, sw):
-    """float64 op-for-op composition of staytime mtl_net (staytime/VideoDnn.py:27-215) from m's
-    weights on leaf inputs e64 [B, F, 32] / s64 [num_seq x [B, T, 32]] (masks mk): the loss of
-    staytime/model.py:20-36, predictions and the weight leaves whose gradients the tests check."""
-    from recommendsystem_amd.models import STAYTIME_BINS
-    B, F = e64.shape[0], cfg.num_fields
-    general = [e64[:, f, 0:16] for f in range(F)]
-    gate_input = torch.cat([e64[:, f, 16:32] for f in cfg.bias_fields], 1)
-    din = []
-    for s, q in enumerate(cfg.query_fields):
-        d = m.dins[s]
-        din.append(tr.din_softmax_pool(general[q], s64[s][:, :, 0:16], mk[s], *[c64(p) for p in (d.W1, d.b1, d.W2, d.b2)]))
-    sq, ex = m.senet.squeeze, m.senet.excite
-    rew, cross_term, fm_logit = tr.senet_fm(general, c64(sq.kernel), c64(sq.bias), c64(ex.kernel), c64(ex.bias))
-    mult = tr.multiply_relu([general[i] for i in cfg.user_fields], [general[j] for j in cfg.item_fields])
-    ff = m.ffm
-    ffm = tr.ffm_block([general[i] for i in cfg.user_fields], [general[j] for j in cfg.item_fields],
-                       *[c64(p) for p in (ff.Wx, ff.bx, ff.Wy, ff.by)])
-    concated = torch.cat(rew + [cross_term, mult, ffm] + din, 1)
-    Hs, NE = list(cfg.hidden_units), cfg.num_experts
-    fk, fb = c64(m.first.kernel), c64(m.first.bias)
-    pk, pb = c64(m.pp1.kernel), c64(m.pp1.bias)
-    offs_f = np.cumsum([0] + m.first.units)
-    offs_p = np.cumsum([0] + m.pp1.units)
-    pp2 = [(c64(l.kernel), c64(l.bias)) for l in m.pp2]
-    rest = [(c64(l.kernel), c64(l.bias)) for l in m.exp_rest]
-    experts, k = [], 0
-    for i in range(NE):
-        deep = concated
-        for j in range(len(Hs)):
-            q = i * len(Hs) + j
-            g1 = torch.relu(gate_input @ pk[:, offs_p[q]:offs_p[q + 1]] + pb[offs_p[q]:offs_p[q + 1]])
-            g2 = 2 * torch.sigmoid(g1 @ pp2[q][0] + pp2[q][1])
-            if j == 0:
-                deep = torch.relu(deep @ fk[:, offs_f[i]:offs_f[i + 1]] + fb[offs_f[i]:offs_f[i + 1]])
-            else:
-                deep = torch.relu(deep @ rest[k][0] + rest[k][1])
-                k += 1
-            deep = g2 * deep
-        experts.append(deep)
-    ec = torch.stack(experts, 1)
-    gl2 = [(c64(l.kernel), c64(l.bias)) for l in m.gate_l2]
-    go = [(c64(l.kernel), c64(l.bias)) for l in m.gate_out]
-    mmoe = []
-    for t in range(cfg.num_tasks):
-        a = torch.relu(concated @ fk[:, offs_f[NE + t]:offs_f[NE + t + 1]] + fb[offs_f[NE + t]:offs_f[NE + t + 1]])
-        a = torch.relu(a @ gl2[t][0] + gl2[t][1])
-        gsm = torch.softmax(a @ go[t][0] + go[t][1], -1).unsqueeze(-1)
-        mmoe.append(torch.sum(ec * gsm, 1))
-    dW, db = c64(m.dcn.W), c64(m.dcn.b)
-    D = concated.shape[1]
-    cross = tr.deep_cross_layer(concated, [dW[l].reshape(D, 1) for l in range(3)], [db[l] for l in range(3)])
-    hW, hb = c64(m.head.dense.kernel), c64(m.head.dense.bias)
-    P = tr.staytime_head(torch.cat([mmoe[0], cross], 1), hW, hb, STAYTIME_BINS)
-    dl = [(c64(l.kernel), c64(l.bias)) for l in m.deep_logit]
-    to = [(c64(l.kernel), c64(l.bias)) for l in m.task_out]
-    preds = [torch.sigmoid(torch.cat([fm_logit, torch.relu(mmoe[t + 1] @ dl[t][0] + dl[t][1])], 1) @ to[t][0] + to[t][1])
-             for t in range(2)]
-    swc = torch.from_numpy(sw.cpu().numpy()).double().reshape(-1)  # [B] (device labels: [B, 1])
-    ys = torch.from_numpy(stay.cpu().numpy()).double()
-    ce = lambda y, p: -(y * torch.log(p + 1e-6) + (1 - y) * torch.log(1 - p + 1e-6))  # noqa: E731
-    ref_loss = (2.0 * torch.mean(tr.custom_kl_loss(ys, P) * swc)
-                + 2.0 * torch.mean(ce(torch.from_numpy(short.cpu().numpy()).double().reshape(-1, 1), preds[0])[:, 0] * swc)
-                + 1.0 * torch.mean(ce(torch.from_numpy(long_.cpu().numpy()).double().reshape(-1, 1), preds[1])[:, 0] * swc))
-    return dict(loss=ref_loss, preds=preds, P=P, fk=fk, pk=pk, dW=dW, hW=hW)
-
-
 def test_staytime_mtl_matches_oracle():
     from recommendsystem_amd.models import STAYTIME_BINS, StaytimeConfig, StaytimeMTL
     from recommendsystem_amd.workloads import staytime_labels
