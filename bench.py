@@ -54,6 +54,9 @@ def parse():
                     help="config 2 compute mode of the headline line (f32 = the reference's math)")
     ap.add_argument("--no-bf16", action="store_true",
                     help="skip the nested bf16-mode result of the f32 run")
+    ap.add_argument("--shard-table", action="store_true",
+                    help="staytime at N > 1: owner-shard the 10M x 32 table over the ranks (N2, "
+                         "all-to-all lookups and pushes) instead of replicating it")
     ap.add_argument("--workload", default="autoint",
                     choices=["autoint", "multi_head", "din", "staytime"],
                     help="autoint = the headline (configs[1]); the others are configs 3-5 at their "
@@ -278,7 +281,8 @@ def run_workload(args, world, rank, dev, pg):
         trainer = Trainer(model, 5e-5, [model.table], process_group=pg)
         pool = [W.din_batch(rng, B, 100, 1_000_000, dev) for _ in range(args.pool)]
     else:
-        model = W.StaytimeRoughRank(device=dev, seed=0)
+        shard = pg if (world > 1 and args.shard_table) else None  # N2 owner-sharded 10M table
+        model = W.StaytimeRoughRank(device=dev, seed=0, shard_group=shard)
         trainer = Trainer(model, 5e-4, [model.table], process_group=pg)
         pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
     graphed = world == 1 and not args.eager
@@ -317,8 +321,9 @@ def run_workload(args, world, rank, dev, pg):
            "data": "synthetic (SURVEY §8d config generators; random-init weights)",
            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                       "parallelism": f"dp{world}",
+                      "table": "owner-sharded" if getattr(model.table, "sharded", False) else "replicated",
                       "execution": "one HIP graph per pool batch" if graphed else "eager autograd"},
-           "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(float(loss), 6)}
+           "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(float(loss.detach()), 6)}
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -37,6 +37,7 @@ extern "C" {
  * segment).  row = row_base[f] + H(id) % bucket[f] with H = identity (hash_mode 0) or
  * splitmix64 (1).  out[b*out_ld + f*out_fstride + e] = combiner(rows)[e], combiner 0 = sum,
  * 1 = mean, 2 = sqrtn; empty segment -> 0.  rows_out[k] (nullable) receives the row of ids[k].
+ * table == out == NULL (rows_out required): rows only (owner-sharded tables, below).
  * ------------------------------------------------------------------------------------- */
 int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32_t* offsets, int64_t B,
                             int F, const int64_t* row_base, const int64_t* bucket, int hash_mode,
@@ -82,6 +83,28 @@ int rs_sparse_grad_accumulate_sorted(void* stream, const int32_t* rows, const in
                                      int64_t table_rows, float* grad_table, int32_t* flag,
                                      int32_t* touched, int32_t* n_touched, int32_t touched_cap,
                                      void* workspace, int64_t workspace_bytes, int64_t n_ids);
+
+/* N2 owner-sharded tables (SURVEY §8(e) owner = row % N; tensornet's PS split,
+ * rank/ctr/base_model.py:89-102 / staytime/VideoDnn.py:233).  rs_embedding_lookup_fwd and
+ * rs_sequence_lookup_fwd with table == out == NULL write only rows_out (and mask / lengths): the
+ * id -> row half.  rs_owner_route orders the n rows by owner (stable: ascending position within an
+ * owner; rows < 0 or >= table_rows dropped), writing send_local[i] = row / world, send_pos[i] =
+ * the row's position and counts[w] = rows owned by w (device int32 [world]); workspace >=
+ * rs_owner_route_workspace_bytes(n, world) (-1: n or world out of range; world <= 1024).
+ * rs_gather_rows: dst[i] = src[idx[i]] (idx < 0: zero row); rs_scatter_rows: dst[idx[i]] =
+ * src[i] (idx < 0 skipped); rows of dim floats (dim % 4 == 0), leading dimensions in floats.
+ * rs_segment_expand: dE[k] = scale(s) * dout[b*dout_ld + f*dout_fstride] for every id k of
+ * segment s = b*F + f (offsets [B*F+1]; the combiner's per-id gradient of a VarLen lookup). */
+int64_t rs_owner_route_workspace_bytes(int64_t n, int world);
+int rs_owner_route(void* stream, const int32_t* rows, int64_t n, int world, int64_t table_rows,
+                   int32_t* send_local, int32_t* send_pos, int32_t* counts, void* workspace,
+                   int64_t workspace_bytes);
+int rs_gather_rows(void* stream, const float* src, int64_t src_ld, const int32_t* idx, int64_t n,
+                   int dim, float* dst, int64_t dst_ld);
+int rs_scatter_rows(void* stream, const float* src, int64_t src_ld, const int32_t* idx, int64_t n,
+                    int dim, float* dst, int64_t dst_ld);
+int rs_segment_expand(void* stream, const float* dout, int64_t dout_ld, int64_t dout_fstride,
+                      const int32_t* offsets, int64_t B, int F, int combiner, int dim, float* dE);
 
 /* H11 sparse optimizers on the touched rows (tensornet tn.core.Adam / tn.core.AdaGrad handed to
  * EmbeddingFeatures: rank/ctr/base_model.py:163, rank/multi_head/multidnn.py:235,

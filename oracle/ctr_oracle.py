@@ -271,6 +271,37 @@ def adagrad_sparse(w, g, g2, lr):
 
 
 # ------------------------------------------------------------------------------------------
+# N2 owner-sharded tables (owner = row % N; tensornet's PS split its tables by
+# key on the host, rank/ctr/base_model.py:89-102).  Pinned routing of csrc/sharded.hip.
+# ------------------------------------------------------------------------------------------
+def owner_route(rows, world: int, table_rows: int):
+    """rows int [n] (-1 or >= table_rows: no row) -> (send_local, send_pos, counts): the valid
+    rows stably ordered by owner (row % world), local index row // world, original position, and
+    the per-owner counts."""
+    rows = np.asarray(rows, dtype=np.int64)
+    pos = np.arange(rows.size)
+    ok = (rows >= 0) & (rows < table_rows)
+    key = np.where(ok, rows % world, world)
+    order = np.argsort(key, kind="stable")
+    order = order[ok[order]]
+    counts = np.bincount(key[ok], minlength=world)[:world]
+    return (rows[order] // world).astype(np.int32), pos[order].astype(np.int32), counts.astype(np.int32)
+
+
+def sharded_lookup_reference(rows_per_rank, world: int, table_rows: int, table):
+    """Every rank's per-id rows gathered through the owners (what the route + all-to-all + gather
+    + scatter sequence computes): table[rows] with zero rows where rows < 0."""
+    out = []
+    for rows in rows_per_rank:
+        rows = np.asarray(rows, dtype=np.int64)
+        e = np.zeros((rows.size, table.shape[1]), dtype=table.dtype)
+        ok = (rows >= 0) & (rows < table_rows)
+        e[ok] = table[rows[ok]]
+        out.append(e)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 # H1 sequence lookup (tn embedding_column(combiner=None, seq_max_len) -> (emb3d, mask);
 # staytime/VideoDnn.py:217-244, consumed at :58-68).  Pinned: the first seq_max_len ids of a
 # sample are kept, positions past the sample's length are zero rows with mask False.

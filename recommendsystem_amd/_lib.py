@@ -41,6 +41,11 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_grad_accumulate_sorted": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32,
                                                 _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _i64,
                                                 _i64]),
+    "rs_owner_route_workspace_bytes": (_i64, [_i64, _i32]),
+    "rs_owner_route": (_i32, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _i64]),
+    "rs_gather_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
+    "rs_scatter_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
+    "rs_segment_expand": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i32, _vp]),
     "rs_set_math_mode": (_i32, [_i32]),
     "rs_get_math_mode": (_i32, []),
     "rs_set_seed_offset": (_i32, [_vp]),

@@ -59,6 +59,14 @@ __global__ void __launch_bounds__(256) embed_lookup_fwd_kernel(
     const int64_t beg = offsets ? offsets[s] : s;
     const int64_t end = offsets ? offsets[s + 1] : s + 1;
     const int64_t base = row_base[f], bk = bucket[f];
+    if (!table) {  // rows only (owner-sharded tables gather remotely): no table read, no store
+      if (l == 0)
+        for (int64_t k = beg; k < end; ++k) {
+          const int64_t row = hash_row(ids[k], base, bk, hash_mode);
+          rows_out[k] = (row >= 0 && row < table_rows) ? (int32_t)row : -1;
+        }
+      continue;
+    }
     float* dst = out + b * out_ld + (int64_t)f * out_fstride;
     for (int v0 = 0; v0 < nvec; v0 += G) {
       const int v = v0 + l;
@@ -88,7 +96,10 @@ RS_API int rs_embedding_lookup_fwd(void* stream, const int64_t* ids, const int32
                                    const int64_t* bucket, int hash_mode, int combiner,
                                    const float* table, int64_t table_rows, int dim, float* out,
                                    int64_t out_ld, int64_t out_fstride, int32_t* rows_out) {
-  if (!ids || !row_base || !bucket || !table || !out || B < 0 || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  // table == out == NULL: rows-only mode (rows_out required), the id -> row half of the lookup
+  const bool rows_only = !table && !out;
+  if (!ids || !row_base || !bucket || B < 0 || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  if (rows_only ? !rows_out : (!table || !out)) return RS_ERR_ARG;
   if (table_rows <= 0 || table_rows > INT32_MAX) return RS_ERR_ARG;  // rows_out is int32
   if (dim % 4 != 0 || out_ld % 4 != 0 || out_fstride % 4 != 0) return RS_ERR_ARG;
   const int64_t nseg = B * (int64_t)F;
@@ -145,11 +156,13 @@ __global__ void __launch_bounds__(256) seq_lookup_fwd_kernel(
     const bool on = t < n;
     int64_t row = -1;
     if (on) row = hash_row(ids[beg + t], row_base, bucket, hash_mode);
-    float* dst = out + b * out_ss + (int64_t)t * out_rs;
-    for (int v = l; v < nvec; v += G) {
-      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (on) val = reinterpret_cast<const float4*>(table + row * dim)[v];
-      reinterpret_cast<float4*>(dst)[v] = val;
+    if (table) {  // NULL table and out: rows / mask / lengths only
+      float* dst = out + b * out_ss + (int64_t)t * out_rs;
+      for (int v = l; v < nvec; v += G) {
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (on) val = reinterpret_cast<const float4*>(table + row * dim)[v];
+        reinterpret_cast<float4*>(dst)[v] = val;
+      }
     }
     if (l == 0) {
       if (rows_out) rows_out[p] = (int32_t)row;
@@ -164,7 +177,8 @@ RS_API int rs_sequence_lookup_fwd(void* stream, const int64_t* ids, const int32_
                                   int hash_mode, const float* table, int dim, float* out,
                                   int64_t out_ss, int64_t out_rs, uint8_t* mask, int64_t mask_ld,
                                   int32_t* lengths, int32_t* rows_out) {
-  if (!offsets || !table || !out || B < 0 || T <= 0 || dim <= 0 || bucket <= 0) return RS_ERR_ARG;
+  if (!offsets || B < 0 || T <= 0 || dim <= 0 || bucket <= 0) return RS_ERR_ARG;
+  if ((!table) != (!out) || (!table && !rows_out)) return RS_ERR_ARG;  // rows-only: both NULL
   if (dim % 4 != 0 || out_ss % 4 != 0 || out_rs % 4 != 0) return RS_ERR_ARG;
   const int64_t npos = B * (int64_t)T;
   if (npos == 0) return RS_OK;

@@ -4,6 +4,9 @@
 
   dense  : the model's flat gradient arena is ONE all-reduce bucket (AutoInt: 15.4 K floats,
            latency-bound; staytime+rough_rank: ~3.5 M floats = 14 MB, still one bucket).
+  sharded: owner-sharded tables (embedding.ShardedSparseTable, row owner = row % world) move
+           lookups and gradients with two variable-split all-to-alls each way instead
+           (all_to_all_v; counts first).
   sparse : each rank pre-reduces its touched rows locally (rs_sparse_grad_accumulate), compacts
            them into (rows, grads) lists, the lists are all-gathered (counts first, then lists
            padded to the max count with row -1), and every rank merges the lists IN RANK ORDER
@@ -115,3 +118,24 @@ def merge_reference(rows_all, grads_all, table_grad):
                 touched.append(row)
             table_grad[row] += grads_all[r, u]
     return touched
+
+
+def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None) -> None:
+    """Variable-split all-to-all along dim 0 (rank r's slice of inp goes to rank r; out holds the
+    slices from ranks 0..world-1 in rank order).  RCCL moves device tensors directly; gloo stages
+    device tensors through host memory (backend chosen by name, as in _all_gather_flat)."""
+    if inp.is_cuda and dist.get_backend(group) != "nccl":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), list(out_splits), list(in_splits), group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=group)
+
+
+def exchange_counts(counts: torch.Tensor, group=None):
+    """counts [world] int32 (ids this rank sends to each owner) -> (send_splits, recv_splits) as
+    host lists: one 1-element-per-rank all-to-all and the step's host synchronisation."""
+    world = counts.numel()
+    recv = torch.empty_like(counts)
+    all_to_all_v(recv, counts, [1] * world, [1] * world, group)
+    return counts.tolist(), recv.tolist()

@@ -58,16 +58,18 @@ class SparseTable:
     """One HBM-resident embedding table with its optimizer slots and step bookkeeping."""
 
     def __init__(self, rows: int, dim: int, optimizer=None, device=None, init_scale: float = 0.05,
-                 seed: int = 0, max_touched: int | None = None):
+                 seed: int = 0, max_touched: int | None = None, initial: torch.Tensor | None = None):
         if dim % 4 != 0:
             raise ValueError("embedding dim must be a multiple of 4 (16-byte rows)")
         device = torch.device(device or "cuda")
         self.rows, self.dim = int(rows), int(dim)
         self.optimizer = optimizer or SparseAdam()
-        gen = torch.Generator().manual_seed(seed)
-        w = (torch.rand(self.rows, self.dim, generator=gen) * 2.0 - 1.0) * init_scale
-        if isinstance(self.optimizer, SparseAdaGrad):
-            w = w * (self.optimizer.initial_scale / max(init_scale, 1e-30))
+        if initial is not None:  # explicit initial rows (a ShardedSparseTable shard)
+            if tuple(initial.shape) != (self.rows, self.dim):
+                raise ValueError("initial must be [rows, dim]")
+            w = initial
+        else:
+            w = self.initial_weight(self.rows, self.dim, self.optimizer, init_scale, seed)
         self.weight = w.to(device=device, dtype=torch.float32)
         self.grad = torch.zeros(self.rows, self.dim, device=device, dtype=torch.float32)
         self.flag = torch.full((self.rows,), -1, device=device, dtype=torch.int32)
@@ -91,6 +93,16 @@ class SparseTable:
         self._sorted_ws = None
         # autograd anchor: lets the lookup's backward run (it returns no dense gradient)
         self.anchor = torch.zeros((), device=device, dtype=torch.float32, requires_grad=True)
+
+    @staticmethod
+    def initial_weight(rows, dim, optimizer, init_scale=0.05, seed=0) -> torch.Tensor:
+        """The table's initial values on the host: U(-s, s) from a seeded generator (AdaGrad:
+        tn.core.AdaGrad's initial_scale)."""
+        gen = torch.Generator().manual_seed(seed)
+        w = (torch.rand(rows, dim, generator=gen) * 2.0 - 1.0) * init_scale
+        if isinstance(optimizer, SparseAdaGrad):
+            w = w * (optimizer.initial_scale / max(init_scale, 1e-30))
+        return w
 
     # ---- push / update -----------------------------------------------------------------
     def accumulate(self, rows: torch.Tensor, offsets: torch.Tensor | None, B: int, F: int,
@@ -151,6 +163,192 @@ class SparseTable:
             call("rs_sparse_adagrad", s, ptr(self.weight), ptr(self.g2sum), ptr(self.grad),
                  ptr(self.flag), ptr(self.touched), ptr(self.n_touched), self.dim,
                  self.touched_cap, o.learning_rate, grad_scale)
+
+
+class ShardedSparseTable:
+    """N2 owner-sharded table: the rows of a SparseTable of ``rows`` rows split over
+    the ``world`` ranks of a process group by owner = row % world; this rank keeps rows rank,
+    rank + world, ... (local index row // world) with their optimizer slots, as ``local``, a
+    SparseTable of ceil((rows - rank) / world) rows.  Initial values equal the replicated
+    SparseTable(rows, seed=seed)'s rows.  Lookups hash ids to global rows on the requesting rank,
+    route them to their owners (rs_owner_route + all_to_all_v), the owners gather
+    (rs_gather_rows) and send the rows back (rs_scatter_rows into id order); backward sends the
+    per-id gradients the same way and the owner pushes them into its shard, so the sparse
+    optimizer step (``step``) is local and no table-sized exchange runs.  The routing needs the
+    per-owner counts on the host (one small all-to-all per lookup and per backward), so a step
+    over a sharded table runs eagerly (no graph capture).  Everything else (``weight``, ``grad``,
+    ``optimizer``, ``step``, ``check_overflow``, ...) is the local shard's."""
+
+    sharded = True
+
+    def __init__(self, rows: int, dim: int, optimizer=None, device=None, init_scale: float = 0.05,
+                 seed: int = 0, max_touched: int | None = None, process_group=None):
+        import torch.distributed as dist
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group)
+        self.rank = dist.get_rank(process_group)
+        self.rows, self.dim = int(rows), int(dim)
+        if self.rows > 2**31 - 1:
+            raise ValueError("row indices are int32")
+        optimizer = optimizer or SparseAdam()
+        full = SparseTable.initial_weight(self.rows, self.dim, optimizer, init_scale, seed)
+        shard = full[self.rank::self.world].clone()
+        del full
+        self.local = SparseTable(shard.shape[0], dim, optimizer, device=device, initial=shard,
+                                 max_touched=max_touched)
+        self._route_ws = None
+
+    def __getattr__(self, name):  # the shard's state and methods
+        if name == "local":
+            raise AttributeError(name)
+        return getattr(self.local, name)
+
+    @property
+    def deterministic(self):
+        return self.local.deterministic
+
+    @deterministic.setter
+    def deterministic(self, v):
+        self.local.deterministic = bool(v)
+
+    @property
+    def mode(self):
+        return self.local.mode
+
+    @mode.setter
+    def mode(self, v):
+        self.local.mode = v
+
+    def _workspace(self, n):
+        need = int(_lib.load().rs_owner_route_workspace_bytes(n, self.world))
+        if need < 0:
+            raise ValueError(f"{n} ids / world {self.world}: out of range for the owner route")
+        if self._route_ws is None or self._route_ws.numel() < need:
+            self._route_ws = torch.empty(need, device=self.local.weight.device, dtype=torch.uint8)
+        return self._route_ws
+
+    def route(self, rows: torch.Tensor):
+        """Global rows int32 [n] (-1 = no row) -> the routing plan shared by gather and push:
+        (send_pos [nv], send_splits, recv_splits, recv_local [nr])."""
+        from .dist import all_to_all_v, exchange_counts
+        n, dev = rows.numel(), rows.device
+        send_local = torch.empty(n, device=dev, dtype=torch.int32)
+        send_pos = torch.empty(n, device=dev, dtype=torch.int32)
+        counts = torch.empty(self.world, device=dev, dtype=torch.int32)
+        ws = self._workspace(n)
+        call("rs_owner_route", stream_handle(), ptr(rows), n, self.world, self.rows, ptr(send_local),
+             ptr(send_pos), ptr(counts), ptr(ws), ws.numel())
+        sc, rc = exchange_counts(counts, self.pg)
+        nv, nr = sum(sc), sum(rc)
+        recv_local = torch.empty(nr, device=dev, dtype=torch.int32)
+        all_to_all_v(recv_local, send_local[:nv], rc, sc, self.pg)
+        return send_pos[:nv], sc, rc, recv_local
+
+    def gather(self, rows: torch.Tensor):
+        """-> (E [n, dim] with E[k] = table[rows[k]] (zero where rows[k] < 0), plan)."""
+        from .dist import all_to_all_v
+        plan = self.route(rows)
+        send_pos, sc, rc, recv_local = plan
+        dev, d = rows.device, self.dim
+        served = torch.empty(recv_local.numel(), d, device=dev)
+        if served.numel():
+            call("rs_gather_rows", stream_handle(), ptr(self.local.weight), d, ptr(recv_local),
+                 recv_local.numel(), d, ptr(served), d)
+        back = torch.empty(send_pos.numel(), d, device=dev)
+        all_to_all_v(back, served, sc, rc, self.pg)
+        E = torch.zeros(rows.numel(), d, device=dev)
+        if back.numel():
+            call("rs_scatter_rows", stream_handle(), ptr(back), d, ptr(send_pos), send_pos.numel(),
+                 d, ptr(E), d)
+        return E, plan
+
+    def push(self, dE: torch.Tensor, plan) -> None:
+        """Per-id gradients dE [n, dim] (the rows of gather's E) -> the owners' gradient rows."""
+        from .dist import all_to_all_v
+        send_pos, sc, rc, recv_local = plan
+        d = self.dim
+        g = torch.empty(send_pos.numel(), d, device=dE.device)
+        if g.numel():
+            call("rs_gather_rows", stream_handle(), ptr(dE), d, ptr(send_pos), send_pos.numel(), d,
+                 ptr(g), d)
+        recv = torch.empty(recv_local.numel(), d, device=dE.device)
+        all_to_all_v(recv, g, rc, sc, self.pg)
+        if recv.numel():
+            self.local.accumulate(recv_local, None, recv_local.numel(), 1, recv, d, d,
+                                  COMBINERS["sum"])
+
+
+def is_sharded(table) -> bool:
+    return getattr(type(table), "sharded", False)
+
+
+class _ShardedLookupFn(torch.autograd.Function):
+    """EmbeddingFeatures over a ShardedSparseTable: rows-only hash, remote gather, local pooling
+    (VarLen: rs_embedding_lookup_fwd over the gathered per-id rows as a table indexed by id
+    position); backward expands the combiner (rs_segment_expand) and pushes to the owners."""
+
+    @staticmethod
+    def forward(ctx, anchor, ids, offsets, layer, out_buf):
+        B, F = layer._batch_fields(ids, offsets)
+        t = layer.table
+        n, d, dev, s = ids.numel(), t.dim, ids.device, stream_handle()
+        rows = torch.empty(n, device=dev, dtype=torch.int32)
+        call("rs_embedding_lookup_fwd", s, ptr(ids), ptr(offsets), B, F, ptr(layer.row_base),
+             ptr(layer.bucket), layer.hash_mode, layer.combiner, None, t.rows, d, None, F * d, d,
+             ptr(rows))
+        E, plan = t.gather(rows)
+        out = out_buf if out_buf is not None else torch.empty(B, F, d, device=dev)
+        if offsets is None:
+            out.view(B * F, d).copy_(E)
+        elif n == 0:
+            out.zero_()
+        else:
+            pos = torch.arange(n, device=dev, dtype=torch.int64)
+            base = torch.zeros(F, device=dev, dtype=torch.int64)
+            bucket = torch.full((F,), n, device=dev, dtype=torch.int64)
+            call("rs_embedding_lookup_fwd", s, ptr(pos), ptr(offsets), B, F, ptr(base), ptr(bucket),
+                 HASH_MODES["mod"], layer.combiner, ptr(E), n, d, ptr(out), F * d, d, None)
+        ctx.layer, ctx.B, ctx.F, ctx.n, ctx.plan = layer, B, F, n, plan
+        ctx.save_for_backward(offsets if offsets is not None else torch.empty(0))
+        ctx.has_offsets = offsets is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (offsets,) = ctx.saved_tensors
+        layer, d = ctx.layer, ctx.layer.table.dim
+        dout = dout.contiguous()
+        if not ctx.has_offsets:
+            dE = dout.view(ctx.B * ctx.F, d)  # one id per segment: every combiner scales by 1
+        else:
+            dE = torch.empty(ctx.n, d, device=dout.device)
+            call("rs_segment_expand", stream_handle(), ptr(dout), ctx.F * d, d, ptr(offsets), ctx.B,
+                 ctx.F, layer.combiner, d, ptr(dE))
+        layer.table.push(dE, ctx.plan)
+        return None, None, None, None, None
+
+
+class _ShardedSeqLookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, ids, offsets, layer):
+        t = layer.table
+        B, T, d, dev = offsets.numel() - 1, layer.seq_max_len, t.dim, ids.device
+        mask = torch.empty(B, T, device=dev, dtype=torch.uint8)
+        lengths = torch.empty(B, device=dev, dtype=torch.int32)
+        rows = torch.empty(B * T, device=dev, dtype=torch.int32)
+        call("rs_sequence_lookup_fwd", stream_handle(), ptr(ids), ptr(offsets), B, T,
+             layer.row_base, layer.bucket, layer.hash_mode, None, d, None, T * d, d, ptr(mask), T,
+             ptr(lengths), ptr(rows))
+        E, plan = t.gather(rows)
+        ctx.layer, ctx.B, ctx.plan = layer, B, plan
+        ctx.mark_non_differentiable(mask, lengths)
+        return E.view(B, T, d), mask.view(torch.bool), lengths
+
+    @staticmethod
+    def backward(ctx, dout, _dmask, _dlen):
+        d = ctx.layer.table.dim
+        ctx.layer.table.push(dout.contiguous().view(-1, d), ctx.plan)
+        return None, None, None, None
 
 
 class _LookupFn(torch.autograd.Function):
@@ -228,7 +426,8 @@ class EmbeddingFeatures(nn.Module):
         ids = ids.contiguous()
         if offsets is not None:
             offsets = offsets.to(torch.int32).contiguous()
-        return _LookupFn.apply(self.table.anchor, ids, offsets, self, out)
+        fn = _ShardedLookupFn if is_sharded(self.table) else _LookupFn
+        return fn.apply(self.table.anchor, ids, offsets, self, out)
 
 
 class _SeqLookupFn(torch.autograd.Function):
@@ -287,5 +486,6 @@ class SequenceEmbedding(nn.Module):
             B, n = ids.shape
             offsets = torch.arange(0, B * n + 1, n, device=ids.device, dtype=torch.int32)
         offsets = offsets.to(device=ids.device, dtype=torch.int32).contiguous()
-        emb, mask, lengths = _SeqLookupFn.apply(self.table.anchor, ids.reshape(-1).contiguous(), offsets, self)
+        fn = _ShardedSeqLookupFn if is_sharded(self.table) else _SeqLookupFn
+        emb, mask, lengths = fn.apply(self.table.anchor, ids.reshape(-1).contiguous(), offsets, self)
         return (emb, mask, lengths) if return_lengths else (emb, mask)

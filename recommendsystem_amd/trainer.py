@@ -5,6 +5,7 @@ harness): what tensornet's ``model.fit`` runs per batch (SURVEY §3 call stacks)
     loss.backward()                     (kernels write weight grads in place into the arena)
     grads += l1 sign(w) + 2 l2 w        (Keras kernel regularisers, rs_l1l2_grad)
     [DP] all-reduce the flat dense gradient (one RCCL bucket), rank-ordered sparse exchange
+         (owner-sharded tables: none -- their backward already pushed to the owners)
     dense Adam over the arena (one launch, zero_grad fused), sparse optimizer per table
 
 Dense Adam follows tn.optimizer.Optimizer(tn.core.Adam(lr, .9, .999, 1e-8)) with tf.keras bias
@@ -16,6 +17,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr, stream_handle
+from .embedding import is_sharded
 from .layers import InteractingLayer
 from .params import ParamArena
 
@@ -54,6 +56,8 @@ class Trainer:
             if hasattr(model, "modules") else []
         if self.world > 1:
             for t in self.tables:
+                if is_sharded(t):
+                    continue
                 self.xbuf[id(t)] = (torch.empty(t.touched_cap, device=dev, dtype=torch.int32),
                                     torch.empty(t.touched_cap, t.dim, device=dev))
 
@@ -76,7 +80,8 @@ class Trainer:
             from .dist import allreduce_flat
             allreduce_flat(self.arena.grad, self.pg)
             for t in self.tables:
-                exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])
+                if not is_sharded(t):
+                    exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])
         scale = 1.0 / self.world
         call("rs_dense_adam", s, ptr(self.arena.data), ptr(self.arena.grad), ptr(self.m), ptr(self.v),
              self.arena.n, ptr(self.step_count), self.lr, self.b1, self.b2, self.eps, scale, 1)

@@ -21,8 +21,8 @@ import torch
 from torch import nn
 
 from .din import DIN
-from .embedding import (EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam,
-                        SparseTable)
+from .embedding import (EmbeddingFeatures, SequenceEmbedding, ShardedSparseTable, SparseAdaGrad,
+                        SparseAdam, SparseTable)
 from .layers import Dense
 from .models import (DSSM, STAYTIME_BINS, DSSMConfig, MultiHeadConfig, MultiHeadRanker,
                      StaytimeConfig, StaytimeMTL)
@@ -101,13 +101,20 @@ class StaytimeRoughRank(nn.Module):
     reads columns 0:16)."""
 
     def __init__(self, rows=10_000_000, device=None, seed=0, st_cfg=None, rr_cfg=None,
-                 max_touched=None):
+                 max_touched=None, shard_group=None):
+        """shard_group: a process group -> the table is owner-sharded over its ranks
+        (ShardedSparseTable, N2); None -> one replicated table."""
         super().__init__()
         dev = torch.device(device or "cuda")
         self.st_cfg = st_cfg or StaytimeConfig()
         self.rr_cfg = rr_cfg or DSSMConfig()
-        self.table = SparseTable(rows, self.st_cfg.emb_dim, SparseAdaGrad(), device=dev, seed=seed,
-                                 max_touched=max_touched)
+        if shard_group is not None:
+            self.table = ShardedSparseTable(rows, self.st_cfg.emb_dim, SparseAdaGrad(), device=dev,
+                                            seed=seed, max_touched=max_touched,
+                                            process_group=shard_group)
+        else:
+            self.table = SparseTable(rows, self.st_cfg.emb_dim, SparseAdaGrad(), device=dev,
+                                     seed=seed, max_touched=max_touched)
         F = self.st_cfg.num_fields
         self.fields = EmbeddingFeatures(self.table, [rows] * F, row_base=[0] * F, combiner="mean",
                                         hash_mode="splitmix")

@@ -1,0 +1,264 @@
+"""GPU: N2 owner-sharded tables (csrc/sharded.hip + embedding.ShardedSparseTable).
+
+  * rs_owner_route bit-exact vs oracle/ctr_oracle.py::owner_route (worlds 1-8, invalid rows,
+    empty input), rs_gather_rows / rs_scatter_rows / rs_segment_expand vs torch indexing, the
+    rows-only lookup modes vs the full lookups' rows;
+  * world size 2 on one device (gloo transport; RCCL on a node runs the same code): lookups over a
+    sharded table equal the oracle's lookups of the whole table, and the owners' gradient rows
+    equal every rank's per-id gradients summed at their rows;
+  * config 5 (StaytimeRoughRank, sparse AdaGrad) trained 3 DP steps with the table owner-sharded
+    matches the same DP run over the replicated table (all-gather exchange): losses, dense
+    parameters and the whole table reassembled from the shards.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ctr_oracle as npo
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _call(name, *a):
+    from recommendsystem_amd._lib import call
+    return call(name, *a)
+
+
+def _route(rows, world, table_rows):
+    from recommendsystem_amd._lib import load, ptr, stream_handle
+    n = rows.numel()
+    ws = torch.empty(int(load().rs_owner_route_workspace_bytes(n, world)), device=DEV, dtype=torch.uint8)
+    sl = torch.full((n,), -7, device=DEV, dtype=torch.int32)
+    sp = torch.full((n,), -7, device=DEV, dtype=torch.int32)
+    c = torch.full((world,), -7, device=DEV, dtype=torch.int32)
+    _call("rs_owner_route", stream_handle(), ptr(rows), n, world, table_rows, ptr(sl), ptr(sp), ptr(c),
+          ptr(ws), ws.numel())
+    torch.cuda.synchronize()
+    return sl.cpu().numpy(), sp.cpu().numpy(), c.cpu().numpy()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("n", [0, 1, 1000, 300_000])
+def test_owner_route_matches_oracle(world, n):
+    rng = np.random.default_rng(world * 7 + n)
+    R = 1_000_003
+    rows = rng.integers(-1, R + 50, size=n).astype(np.int32)  # some -1 and some >= R
+    sl, sp, c = _route(torch.from_numpy(rows).to(DEV), world, R)
+    esl, esp, ec = npo.owner_route(rows, world, R)
+    assert np.array_equal(c, ec)
+    nv = int(ec.sum())
+    assert np.array_equal(sl[:nv], esl) and np.array_equal(sp[:nv], esp)
+
+
+def test_gather_scatter_expand_rows():
+    from recommendsystem_amd._lib import ptr, stream_handle
+    g = torch.Generator().manual_seed(3)
+    for dim in (4, 16, 32, 128, 260):
+        src = torch.randn(500, dim + 4, generator=g).to(DEV)
+        idx = torch.randint(-1, 500, (777,), generator=g, dtype=torch.int32).to(DEV)
+        dst = torch.full((777, dim), 9.0, device=DEV)
+        _call("rs_gather_rows", stream_handle(), ptr(src), dim + 4, ptr(idx), 777, dim, ptr(dst), dim)
+        i = idx.long()
+        want = torch.where((i >= 0)[:, None], src[i.clamp(min=0), :dim], torch.zeros((), device=DEV))
+        assert torch.equal(dst, want)
+        perm = torch.randperm(600, generator=g)[:400].to(torch.int32).to(DEV)
+        perm[::7] = -1
+        back = torch.full((600, dim), 5.0, device=DEV)
+        _call("rs_scatter_rows", stream_handle(), ptr(dst), dim, ptr(perm), 400, dim, ptr(back), dim)
+        p = perm.long()
+        want = torch.full((600, dim), 5.0, device=DEV)
+        want[p[p >= 0]] = dst[:400][p >= 0]
+        assert torch.equal(back, want)
+    B, F, dim = 37, 3, 16
+    lens = torch.randint(0, 4, (B * F,), generator=g)
+    offs = torch.cat([torch.zeros(1, dtype=torch.int64), lens.cumsum(0)]).to(torch.int32)
+    dout = torch.randn(B, F, dim, generator=g)
+    dout_d, offs_d = dout.to(DEV), offs.to(DEV)  # held: a temporary's block is reused at once
+    for comb in range(3):
+        dE = torch.zeros(int(offs[-1]), dim, device=DEV)
+        _call("rs_segment_expand", stream_handle(), ptr(dout_d), F * dim, dim, ptr(offs_d), B, F, comb,
+              dim, ptr(dE))
+        want = torch.zeros_like(dE.cpu())
+        for s in range(B * F):
+            k0, k1 = int(offs[s]), int(offs[s + 1])
+            sc = float(npo.combiner_scale(k1 - k0, ["sum", "mean", "sqrtn"][comb], np.float32))
+            want[k0:k1] = dout.reshape(-1, dim)[s] * sc
+        torch.testing.assert_close(dE.cpu(), want, rtol=1e-6, atol=0)
+
+
+def test_rows_only_lookup_modes():
+    """table == out == NULL: the lookups write the same rows (and mask / lengths) as the full
+    lookups and touch nothing else."""
+    from recommendsystem_amd._lib import ptr, stream_handle
+    rng = np.random.default_rng(5)
+    B, F, dim, R = 64, 4, 16, 5000
+    table = torch.randn(R, dim, device=DEV)
+    lens = rng.integers(0, 4, size=B * F)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)).to(DEV)
+    ids = torch.from_numpy(rng.integers(0, 1 << 40, size=int(lens.sum())).astype(np.int64)).to(DEV)
+    base = torch.tensor([0, 1000, 2000, 4000], device=DEV)
+    bk = torch.tensor([1000, 1000, 2000, 1000], device=DEV)
+    r_full = torch.empty(ids.numel(), device=DEV, dtype=torch.int32)
+    r_only = torch.full_like(r_full, -9)
+    out = torch.empty(B, F, dim, device=DEV)
+    _call("rs_embedding_lookup_fwd", stream_handle(), ptr(ids), ptr(offs), B, F, ptr(base), ptr(bk), 1, 1,
+          ptr(table), R, dim, ptr(out), F * dim, dim, ptr(r_full))
+    _call("rs_embedding_lookup_fwd", stream_handle(), ptr(ids), ptr(offs), B, F, ptr(base), ptr(bk), 1, 1,
+          None, R, dim, None, F * dim, dim, ptr(r_only))
+    assert torch.equal(r_full, r_only)
+    T = 7
+    so = torch.from_numpy(np.concatenate([[0], np.cumsum(rng.integers(0, 10, size=B))]).astype(np.int32)).to(DEV)
+    sids = torch.from_numpy(rng.integers(0, 1 << 40, size=int(so[-1])).astype(np.int64)).to(DEV)
+    res = []
+    for tbl in (table, None):
+        m = torch.full((B, T), 3, device=DEV, dtype=torch.uint8)
+        ln = torch.full((B,), -5, device=DEV, dtype=torch.int32)
+        rr = torch.full((B * T,), -9, device=DEV, dtype=torch.int32)
+        o = torch.empty(B, T, dim, device=DEV) if tbl is not None else None
+        _call("rs_sequence_lookup_fwd", stream_handle(), ptr(sids), ptr(so), B, T, 0, R, 1, ptr(tbl), dim,
+              ptr(o), T * dim, dim, ptr(m), T, ptr(ln), ptr(rr))
+        res.append((m, ln, rr))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------
+# world size 2 on one GPU
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+ROWS, DIM, WORLD = 20_011, 16, 2
+
+
+def _lookup_batch(rank):
+    rng = np.random.default_rng(80 + rank)
+    B, F = 96, 3
+    offs = np.concatenate([[0], np.cumsum(rng.integers(0, 5, size=B * F))]).astype(np.int32)
+    ids = rng.integers(0, 1 << 40, size=int(offs[-1])).astype(np.int64)
+    single = rng.integers(0, 1 << 40, size=(B, F)).astype(np.int64)
+    soffs = np.concatenate([[0], np.cumsum(rng.integers(0, 12, size=B))]).astype(np.int32)
+    sids = rng.integers(0, 1 << 40, size=int(soffs[-1])).astype(np.int64)
+    return ids, offs, single, sids, soffs
+
+
+def _lookup_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from recommendsystem_amd.embedding import (EmbeddingFeatures, SequenceEmbedding,
+                                               ShardedSparseTable, SparseAdaGrad)
+    t = ShardedSparseTable(ROWS, DIM, SparseAdaGrad(), device=DEV, seed=4, process_group=dist.group.WORLD)
+    ids, offs, single, sids, soffs = (torch.from_numpy(x).to(DEV) for x in _lookup_batch(rank))
+    var = EmbeddingFeatures(t, [9000, 9000, 2011], combiner="mean", hash_mode="splitmix")
+    one = EmbeddingFeatures(t, [ROWS] * 3, row_base=[0] * 3, combiner="sqrtn", hash_mode="splitmix")
+    seq = SequenceEmbedding(t, ROWS, 8, hash_mode="splitmix")
+    ev, eo = var(ids, offs), one(single)
+    es, mask = seq(sids, soffs)
+    gen = torch.Generator().manual_seed(rank)
+    dv, do, ds = (torch.randn(x.shape, generator=gen).to(DEV) for x in (ev, eo, es))
+    torch.autograd.backward([ev, eo, es], [dv, do, ds])
+    torch.cuda.synchronize()
+    out[rank] = dict(ev=ev.detach().cpu().numpy(), eo=eo.detach().cpu().numpy(),
+                     es=es.detach().cpu().numpy(), mask=mask.cpu().numpy(), dv=dv.cpu().numpy(),
+                     do=do.cpu().numpy(), ds=ds.cpu().numpy(), grad=t.grad.cpu().numpy(),
+                     n_touched=int(t.n_touched[0]), touched=t.touched.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_lookups_world2_match_oracle():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_lookup_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    from recommendsystem_amd.embedding import SparseAdaGrad, SparseTable
+    W = SparseTable.initial_weight(ROWS, DIM, SparseAdaGrad(), 0.05, 4).numpy().astype(np.float64)
+    gsum = np.zeros((ROWS, DIM))
+    hit = np.zeros(ROWS, bool)
+    rb = np.array([0, 9000, 18000])
+    for r in range(WORLD):
+        ids, offs, single, sids, soffs = _lookup_batch(r)
+        o = out[r]
+        B = single.shape[0]
+        ev, rv = npo.embedding_lookup(ids, offs, B, 3, rb, [9000, 9000, 2011], W, "splitmix", "mean")
+        np.testing.assert_allclose(o["ev"], ev, rtol=1e-6, atol=1e-6)
+        eo, ro = npo.embedding_lookup(single, None, B, 3, np.zeros(3, np.int64), [ROWS] * 3, W,
+                                      "splitmix", "sqrtn")
+        np.testing.assert_allclose(o["eo"], eo, rtol=1e-6, atol=1e-6)
+        es, m, sr = npo.sequence_lookup(sids, soffs, B, 8, 0, ROWS, W, "splitmix")
+        assert np.array_equal(o["es"], es.astype(np.float32))
+        assert np.array_equal(o["mask"], m)
+        seg = np.repeat(np.arange(B * 3), np.diff(offs))
+        cnt = np.diff(offs)[seg]
+        np.add.at(gsum, rv, o["dv"].reshape(-1, DIM)[seg] / cnt[:, None])
+        np.add.at(gsum, ro, o["do"].reshape(-1, DIM))
+        ok = sr.reshape(-1) >= 0
+        np.add.at(gsum, sr.reshape(-1)[ok], o["ds"].reshape(-1, DIM)[ok])
+        hit[rv] = hit[ro] = True
+        hit[sr.reshape(-1)[ok]] = True
+    for r in range(WORLD):
+        np.testing.assert_allclose(out[r]["grad"], gsum[r::WORLD], rtol=1e-5, atol=1e-5)
+        mine = np.flatnonzero(hit[r::WORLD])  # local rows claimed exactly once each
+        assert out[r]["n_touched"] == mine.size
+        assert np.array_equal(np.sort(out[r]["touched"][:mine.size]), mine)
+
+
+STEPS, B5 = 3, 64
+
+
+def _train_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import StaytimeRoughRank, staytime_batch
+    pg = dist.group.WORLD
+    res = {}
+    for kind in ("replicated", "sharded"):
+        j = StaytimeRoughRank(rows=ROWS, device=DEV, seed=3, shard_group=pg if kind == "sharded" else None)
+        trn = Trainer(j, 5e-4, [j.table], process_group=pg)
+        rng = np.random.default_rng(90 + rank)
+        batches = [staytime_batch(rng, B5, j, DEV) for _ in range(2)]
+        losses = [float(trn.step(*batches[s % 2])) for s in range(STEPS)]
+        torch.cuda.synchronize()
+        j.table.check_overflow()
+        params = torch.cat([p.detach().reshape(-1).cpu() for p in j.parameters()]).numpy()
+        res[kind] = (losses, params, j.table.weight.cpu().numpy(), j.table.g2sum.cpu().numpy())
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config5_sharded_dp_matches_replicated_dp():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_train_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    rep0, rep1 = out[0]["replicated"], out[1]["replicated"]
+    assert np.array_equal(rep0[2], rep1[2])  # replicated tables stay bitwise identical
+    table = np.empty_like(rep0[2])
+    g2 = np.empty_like(rep0[3])
+    for r in range(WORLD):
+        losses, params, w, g = out[r]["sharded"]
+        rl, rp = out[r]["replicated"][:2]
+        np.testing.assert_allclose(losses, rl, rtol=2e-5)
+        np.testing.assert_allclose(params, rp, rtol=1e-4, atol=2e-6)
+        table[r::WORLD], g2[r::WORLD] = w, g
+    np.testing.assert_allclose(table, rep0[2], rtol=1e-4, atol=2e-6)
+    np.testing.assert_allclose(g2, rep0[3], rtol=1e-4, atol=1e-7)
+    from recommendsystem_amd.embedding import SparseAdaGrad, SparseTable
+    init = SparseTable.initial_weight(ROWS, 32, SparseAdaGrad(), 0.05, 3).numpy()
+    assert (np.abs(table - init).max(1) > 0).sum() > 1000  # the shards really trained
