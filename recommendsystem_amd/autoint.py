@@ -98,7 +98,10 @@ class AutoInt(nn.Module):
 
     # autograd-composable forward (autoint:18-56); returns the clipped prediction p
     def forward(self, ids: torch.Tensor, offsets: torch.Tensor | None = None) -> torch.Tensor:
-        x0 = self.embedding(ids, offsets)                       # [B, F, E]  (autoint:22-26)
+        return self.dense_forward(self.embedding(ids, offsets))  # [B, F, E]  (autoint:22-26)
+
+    def dense_forward(self, x0: torch.Tensor) -> torch.Tensor:
+        """The dense sub_model over the field embeddings x0 [B, F, E] (export.autoint_sub_model)."""
         B = x0.shape[0]
         il = self.interact(x0).reshape(B, -1)                   # :30-36
         deep = self.deep(x0.reshape(B, -1))                     # :39-41

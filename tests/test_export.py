@@ -1,0 +1,120 @@
+"""N4 export contract on CPU: checkpoints (safetensors) round-trip the dense parameters, the dense
+Adam state and the sparse tables with their optimizer slots; owner-sharded checkpoints written
+by a gloo world-2 run load into a replicated table and into a world-3 sharded one; mismatched
+models are refused.  The named outputs / sub_models run kernels: tests/test_gpu_export.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from recommendsystem_amd import export
+
+ROWS = 3001
+
+
+def _model(seed, shard_group=None):
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import StaytimeRoughRank
+    j = StaytimeRoughRank(rows=ROWS, device="cpu", seed=seed, shard_group=shard_group)
+    return j, Trainer(j, 5e-4, [j.table], process_group=shard_group)
+
+
+def _perturb(j, trn, seed):
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        trn.m.copy_(torch.randn(trn.m.shape, generator=g))
+        trn.v.copy_(torch.rand(trn.v.shape, generator=g))
+        trn.step_count.fill_(7)
+        j.table.g2sum.add_(torch.rand(j.table.g2sum.shape, generator=g))
+
+
+def _state(j, trn):
+    return ([p.detach().clone() for p in j.parameters()], trn.m.clone(), trn.v.clone(),
+            trn.step_count.clone(), j.table.weight.clone(), j.table.g2sum.clone())
+
+
+def test_checkpoint_round_trip(tmp_path):
+    a, ta = _model(1)
+    _perturb(a, ta, 0)
+    f = export.save_checkpoint(str(tmp_path), a, ta)
+    assert os.path.basename(f) == "ckpt.safetensors"
+    b, tb = _model(2)
+    assert not torch.equal(a.table.weight, b.table.weight)
+    export.load_checkpoint(str(tmp_path), b, tb)
+    for x, y in zip(_state(a, ta), _state(b, tb)):
+        if isinstance(x, list):
+            assert all(torch.equal(p, q) for p, q in zip(x, y))
+        else:
+            assert torch.equal(x, y)
+
+
+def test_checkpoint_refuses_mismatch(tmp_path):
+    a, ta = _model(1)
+    export.save_checkpoint(str(tmp_path), a, ta)
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import StaytimeRoughRank
+    c = StaytimeRoughRank(rows=ROWS + 1, device="cpu", seed=1)
+    with pytest.raises(ValueError):
+        export.load_checkpoint(str(tmp_path), c, Trainer(c, 5e-4, [c.table]))
+    os.makedirs(tmp_path / "empty")
+    with pytest.raises(FileNotFoundError):
+        export.load_checkpoint(str(tmp_path / "empty"), a, ta)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _save_worker(rank, world, port, path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    j, trn = _model(5, dist.group.WORLD)
+    _perturb(j, trn, 10 + rank)  # each owner's slots differ
+    export.save_checkpoint(path, j, trn)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _load_worker(rank, world, port, path, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    j, trn = _model(9, dist.group.WORLD)
+    export.load_checkpoint(path, j, trn)
+    out[rank] = (j.table.weight.numpy().copy(), j.table.g2sum.numpy().copy(),
+                 torch.cat([p.detach().reshape(-1) for p in j.parameters()]).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_checkpoint_reshards(tmp_path):
+    path = str(tmp_path)
+    mp.spawn(_save_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+    assert sorted(os.listdir(path)) == ["ckpt.rank0-of-2.safetensors", "ckpt.rank1-of-2.safetensors"]
+    # into one replicated table: row g comes from owner g % 2 at local index g // 2
+    rep, trep = _model(3)
+    export.load_checkpoint(path, rep, trep)
+    from safetensors.torch import load_file
+    parts = [load_file(os.path.join(path, f"ckpt.rank{r}-of-2.safetensors")) for r in range(2)]
+    for r in range(2):
+        assert torch.equal(rep.table.weight[r::2], parts[r]["table0/weight"])
+        assert torch.equal(rep.table.g2sum[r::2], parts[r]["table0/g2sum"])
+    assert torch.equal(trep.m, parts[0]["adam/m"]) and int(trep.step_count) == 7
+    # into a world-3 sharded table
+    out = mp.Manager().dict()
+    mp.spawn(_load_worker, args=(3, _free_port(), path, out), nprocs=3, join=True)
+    W, G = rep.table.weight.numpy(), rep.table.g2sum.numpy()
+    dense = torch.cat([p.detach().reshape(-1) for p in rep.parameters()]).numpy()
+    for r in range(3):
+        w, g, d = out[r]
+        assert np.array_equal(w, W[r::3]) and np.array_equal(g, G[r::3])
+        assert np.array_equal(d, dense)
