@@ -371,10 +371,18 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
   if (B * (int64_t)F == 0) return RS_OK;
   int G = 1;
   while (G < dim && G < 64) G <<= 1;
-  // LDS table: cap slots of dim floats (<= 64 KB), tile = cap/2 samples (load factor <= 1/2
-  // for single-hot fields)
+  // LDS table: cap slots of dim floats, tile = cap/2 samples (load factor <= 1/2 for single-hot
+  // fields)
+  // Many single-hot "fields" over one shared row space (a sequence's T positions, config 5's 91
+  // fields hashed into one table) repeat the same hot rows in every field's blocks, and the
+  // flush's same-row global atomics serialise: there a block takes a 4x larger tile (up to
+  // 2048 slots, ~147 KB of the CU's 160 KB LDS at dim 16) so each hot row is flushed 4x less
+  // often (config-4 history push 55 -> 36 us).  Few fields (config 2's 26 disjoint ranges) keep
+  // the 64 KB table: more blocks in flight beat fewer flushes there.
   int cap = 1024;
-  while (cap > 32 && (size_t)cap * (dim + 2) * 4 > 64 * 1024) cap >>= 1;
+  const size_t lds_budget = (!offsets && F >= 32) ? 150 * 1024 : 64 * 1024;
+  if (lds_budget > 64 * 1024) cap = 4096;
+  while (cap > 32 && (size_t)cap * (dim + 2) * 4 > lds_budget) cap >>= 1;
   const int tile = cap / 2;
   dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
   const size_t lds = ((size_t)cap * (dim + 2) + 4) * 4;

@@ -1,16 +1,17 @@
 // Deterministic sparse push: the backward half of EmbeddingFeatures
 // (tensornet's PS push; rank/ctr/base_model.py:203-217, staytime/VideoDnn.py:217-244) as
 // sort + segmented sum instead of float atomics, so every touched row's gradient is the sum of
-// its occurrences in ascending id order -- bitwise reproducible run to run and independent of
+// its occurrences in a fixed order (the sorted run layout) -- bitwise reproducible run to run and independent of
 // scheduling (rs_sparse_grad_accumulate's LDS hash + atomics reproduce the row SET exactly but not
 // the last bits of each sum).
 //
 //   1. keys = rows (uint32; -1 -> 0xFFFFFFFF sorts last), values = id index k
 //   2. hipcub radix sort by key (stable: equal rows keep ascending k)
 //   3. run-length encode the sorted keys -> unique rows, counts; exclusive scan -> run starts
-//   4. one lane group per run: sum scale(segment) * dout[segment] over the run in order, add it to
-//      grad_table[row] with a plain read-modify-write (the run owns its row: no atomics), mark /
-//      claim the row exactly like the atomic push.
+//   4. one wave per run: the lanes sum strided slices of the run's occurrences
+//      (scale(segment) * dout[segment]) in order and combine them with a fixed butterfly, then add
+//      the total to grad_table[row] with a plain read-modify-write (the run owns its row: no
+//      atomics), and mark / claim the row exactly like the atomic push.
 // Every step is an async launch on the caller's stream (run count stays on the device), so the
 // sequence is graph-capturable; the caller provides the workspace
 // (rs_sparse_sorted_workspace_bytes).
@@ -46,49 +47,94 @@ __global__ void seg_of_kernel(const int32_t* __restrict__ offsets, int64_t nseg,
     for (int32_t k = offsets[s]; k < offsets[s + 1]; ++k) seg[k] = (int32_t)s;
 }
 
-__global__ void __launch_bounds__(256) sorted_reduce_kernel(
+// One wave per run (grid-stride over the device run count): lane l sums the run's occurrences
+// l, l + 64, l + 128, ... in order, 16 dims per pass (4 float4 loads per occurrence), then the 64
+// lane sums are combined by a fixed xor butterfly and lane e writes dim e.  Every association is
+// fixed by the run's layout, never by scheduling: bitwise reproducible, and a Zipf-hot row with
+// thousands of occurrences costs ~count/512 load round trips instead of count.
+constexpr int kRedWaves = 4;
+
+__global__ void __launch_bounds__(64 * kRedWaves) sorted_reduce_kernel(
     const uint32_t* __restrict__ ukeys, const int32_t* __restrict__ idx,
     const int32_t* __restrict__ run_start, const int32_t* __restrict__ run_len,
     const int32_t* __restrict__ num_runs, const int32_t* __restrict__ seg,
     const int32_t* __restrict__ offsets, int F, const float* __restrict__ dout, int64_t dout_ld,
-    int64_t dout_fstride, int dim, int combiner, int G, int64_t table_rows,
+    int64_t dout_fstride, int dim, int combiner, int64_t table_rows,
     float* __restrict__ grad_table, int32_t* __restrict__ flag, int32_t* __restrict__ touched,
     int32_t* __restrict__ n_touched, int32_t touched_cap) {
-  const int per_block = blockDim.x / G;
-  const int64_t r = (int64_t)blockIdx.x * per_block + threadIdx.x / G;
-  const int l = threadIdx.x % G;
-  if (r >= *num_runs) return;
-  const uint32_t key = ukeys[r];
-  if (key == 0xFFFFFFFFu || (int64_t)key >= table_rows) return;  // invalid ids push nothing
-  const int32_t row = (int32_t)key;
-  const int32_t beg = run_start[r], end = beg + run_len[r];
-  float acc[2] = {0.f, 0.f};  // dim <= 2 * G (G = 64 at most: dim <= 128)
-  for (int32_t i = beg; i < end; ++i) {
-    const int32_t k = idx[i];
-    const int32_t s = seg ? seg[k] : k;
-    const int64_t b = s / F, f = s - b * F;
-    const float sc = comb_scale(offsets ? offsets[s + 1] - offsets[s] : 1, combiner);
-    const float* src = dout + b * dout_ld + f * dout_fstride;
+  const int lane = threadIdx.x & 63;
+  const int64_t nruns = *num_runs;
+  const int64_t wstride = (int64_t)gridDim.x * kRedWaves;
+  for (int64_t r = (int64_t)blockIdx.x * kRedWaves + (threadIdx.x >> 6); r < nruns; r += wstride) {
+    const uint32_t key = ukeys[r];
+    if (key == 0xFFFFFFFFu || (int64_t)key >= table_rows) continue;  // invalid ids push nothing
+    const int32_t row = (int32_t)key;
+    const int32_t beg = run_start[r], end = beg + run_len[r];
+    float* dst = grad_table + (int64_t)row * dim;
+    for (int e0 = 0; e0 < dim; e0 += 16) {
+      const int ne = dim - e0 < 16 ? dim - e0 : 16;  // dim % 4 == 0: whole float4s
+      float acc[16];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = l + u * G;
-      if (e < dim) acc[u] = fmaf(src[e], sc, acc[u]);
-    }
-  }
-  float* dst = grad_table + (int64_t)row * dim;
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      // UN occurrences per lane in flight: their ids, then their rows, are loaded before any is
+      // accumulated (a hot run is ~count/64 dependent idx -> dout round trips otherwise); the
+      // accumulation order per lane stays ascending
+      constexpr int UN = 8;
+      for (int32_t i0 = beg + lane; i0 < end; i0 += 64 * UN) {
+        int32_t kk[UN];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int e = l + u * G;
-    if (e < dim) dst[e] += acc[u];
-  }
-  if (l == 0) {
-    if (touched) {
-      if (atomicCAS(&flag[row], -1, -2) == -1) {
-        const int32_t t = atomicAdd(n_touched, 1);
-        if (t < touched_cap) touched[t] = row;
+        for (int u = 0; u < UN; ++u) kk[u] = i0 + 64 * u < end ? idx[i0 + 64 * u] : -1;
+        float4 t[UN][4];
+        float sc[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+          sc[u] = 0.f;
+          if (kk[u] >= 0) {
+            const int32_t s = seg ? seg[kk[u]] : kk[u];
+            const int64_t b = s / F, f = s - b * F;
+            sc[u] = comb_scale(offsets ? offsets[s + 1] - offsets[s] : 1, combiner);
+            const float4* src = reinterpret_cast<const float4*>(dout + b * dout_ld + f * dout_fstride + e0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) t[u][v] = 4 * v < ne ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+          if (kk[u] < 0) continue;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            acc[4 * v + 0] = fmaf(t[u][v].x, sc[u], acc[4 * v + 0]);
+            acc[4 * v + 1] = fmaf(t[u][v].y, sc[u], acc[4 * v + 1]);
+            acc[4 * v + 2] = fmaf(t[u][v].z, sc[u], acc[4 * v + 2]);
+            acc[4 * v + 3] = fmaf(t[u][v].w, sc[u], acc[4 * v + 3]);
+          }
+        }
       }
-    } else {
-      flag[row] = -2;  // scan mark
+      if (end - beg > 1) {  // a single occurrence needs no combine (lane 0 holds it)
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[e] += __shfl_xor(acc[e], m, 64);
+      }
+      // lane e (e < ne) writes dim e0 + e; after the butterfly every lane holds the totals, and
+      // with one occurrence lane 0 holds them: broadcast lane 0's values in that case
+      float mine = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float v = end - beg > 1 ? acc[e] : __shfl(acc[e], 0, 64);
+        if (lane == e) mine = v;
+      }
+      if (lane < ne) dst[e0 + lane] += mine;
+    }
+    if (lane == 0) {
+      if (touched) {
+        if (atomicCAS(&flag[row], -1, -2) == -1) {
+          const int32_t t = atomicAdd(n_touched, 1);
+          if (t < touched_cap) touched[t] = row;
+        }
+      } else {
+        flag[row] = -2;  // scan mark
+      }
     }
   }
 }
@@ -147,6 +193,7 @@ RS_API int rs_sparse_grad_accumulate_sorted(void* stream, const int32_t* rows,
                                             int64_t workspace_bytes, int64_t n_ids) {
   if (!rows || !dout || !grad_table || !flag || !workspace || F <= 0 || B < 0) return RS_ERR_ARG;
   if (dim <= 0 || dim > 128 || table_rows <= 0 || (touched && !n_touched)) return RS_ERR_ARG;
+  if (dim % 4 || dout_ld % 4 || dout_fstride % 4) return RS_ERR_ARG;  // float4 rows
   if (combiner < RS_COMB_SUM || combiner > RS_COMB_SQRTN) return RS_ERR_ARG;
   // n_ids: ids in the batch (offsets[B*F] with offsets; B*F without -- passed by the caller so
   // that nothing is read back to the host)
@@ -175,13 +222,12 @@ RS_API int rs_sparse_grad_accumulate_sorted(void* stream, const int32_t* rows,
   tb = w.temp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.counts, w.starts, ni, s) != hipSuccess)
     return RS_ERR_LAUNCH;
-  int G = 1;
-  while (G < dim && G < 64) G <<= 1;
-  const int per_block = 256 / G;
-  const int64_t grid = (n_ids + per_block - 1) / per_block;  // runs <= ids; extra groups exit
-  sorted_reduce_kernel<<<(unsigned)grid, 256, 0, s>>>(
+  // one wave per run, grid-stride (the run count stays on the device)
+  int64_t grid = (n_ids + kRedWaves - 1) / kRedWaves;
+  if (grid > 4096) grid = 4096;
+  sorted_reduce_kernel<<<(unsigned)grid, 64 * kRedWaves, 0, s>>>(
       w.ukeys, w.idx_out, w.starts, w.counts, w.num_runs, offsets ? w.seg : nullptr, offsets, F,
-      dout, dout_ld, dout_fstride, dim, combiner, G, table_rows, grad_table, flag, touched,
+      dout, dout_ld, dout_fstride, dim, combiner, table_rows, grad_table, flag, touched,
       n_touched, touched_cap);
   return rs_status_after_launch();
 }
