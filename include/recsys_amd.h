@@ -224,6 +224,23 @@ int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
               const float* gamma, const float* beta, float eps, int use_res, float drop_rate,
               uint64_t seed, float* dx, int dx_accumulate, float* dparams,
               int dparams_accumulate, float* workspace, int64_t workspace_floats);
+/* Saved-attention pair for the many-field kernels (F > 64, rank/multi_head config 3): the
+ * forward also writes, per (iteration, sample), the attention output before the epilogue, the
+ * softmax row statistics and the dropout keep bits into asave, and the backward reads them instead
+ * of recomputing the attention forward and re-hashing the mask (same results as the plain pair).
+ * asave >= rs_il_attn_save_floats(B, F, U, H, L) floats (0 when F <= 64: there asave may be NULL
+ * and the calls are exactly rs_il_fwd / rs_il_bwd). */
+int64_t rs_il_attn_save_floats(int64_t B, int F, int U, int H, int L);
+int rs_il_fwd_saved(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
+                    const float* W, const float* bias, const float* gamma, const float* beta,
+                    float eps, int use_res, float drop_rate, uint64_t seed, float* y,
+                    int64_t y_ld, float* xsave, float* asave, int64_t asave_floats);
+int rs_il_bwd_saved(void* stream, const float* x, const float* xsave, const float* dy,
+                    int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L, const float* W,
+                    const float* bias, const float* gamma, const float* beta, float eps,
+                    int use_res, float drop_rate, uint64_t seed, float* dx, int dx_accumulate,
+                    float* dparams, int dparams_accumulate, float* workspace,
+                    int64_t workspace_floats, const float* asave, int64_t asave_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H6/H7  DIN behaviour-sequence attention pooling.

@@ -56,6 +56,12 @@ SIGNATURES: dict[str, tuple] = {
                                 _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp,
                                 _i64, _vp]),
     "rs_il_bwd_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_il_attn_save_floats": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "rs_il_fwd_saved": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                               _f32, _i32, _f32, _u64, _vp, _i64, _vp, _vp, _i64]),
+    "rs_il_bwd_saved": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
+                               _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _i32, _vp, _i32, _vp,
+                               _i64, _vp, _i64]),
     "rs_il_bwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp,
                          _vp, _vp, _f32, _i32, _f32, _u64, _vp, _i32, _vp, _i32, _vp, _i64]),
     "rs_dense_fwd": (_i32, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _i32, _i32, _vp, _i64]),

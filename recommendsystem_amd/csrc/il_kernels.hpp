@@ -45,6 +45,9 @@ struct FwdReq {
   uint64_t seed;
   float *y, *xsave;
   int64_t y_ld;  // row stride of y (>= F*U): lets the layer write into a concat buffer
+  // many-field path (F > 64): the attention save the backward reads instead of recomputing
+  // (rs_il_fwd_saved; layout il_large.hip::save_stride), or null
+  float* asave = nullptr;
   // fused single-hot gather (rs_il_fwd_gather): x[b, f, :] = table[hash(ids[b, f])] is read
   // straight into LDS, stored to x (the head's and the backward's input) and the hashed rows to
   // gather_rows -- replaces the rs_embedding_lookup_fwd launch and the re-read of x
@@ -72,6 +75,7 @@ struct BwdReq {
   int dparams_accumulate;
   float* workspace;
   int64_t workspace_floats;
+  const float* asave = nullptr;  // rs_il_bwd_saved: the forward's attention save (F > 64)
   // fused sparse push (rs_il_bwd_push): dL/dx of the first iteration is added (with dx's
   // current contents when dx_accumulate) straight into push_table rows push_rows[b * F + f],
   // marking push_flag[row] = -2 (scan mode) instead of being stored to dx

@@ -8,13 +8,14 @@
 //     and attention output are 38 KB of LDS (4 blocks / CU in forward);
 //   * projections: thread = (column of [Wq|Wk|Wv|Wr], row group), the column's E weights in
 //     VGPRs, x rows as broadcast float4 LDS reads;
-//   * attention: thread = (head, query row); the F x F scores are never stored: a max pass and
-//     an exp pass (one v_exp_f32 per score, base-2 domain) over K/V rows read as broadcast float4
-//     (all lanes of a wave share the head, so every K/V read is one address per wave);
-//   * backward recomputes the iteration, then two passes over the score matrix: pass A with
-//     thread = query row (dQ), pass B with thread = key row (dK, dV), each row's gradient in
-//     VGPRs -- no F x F buffer, no atomics.  The dropout mask is hashed once per iteration into an
-//     LDS bitmask (F x F x H bits = 10 KB at F = 200) read by both passes;
+//   * attention: thread = query row covering every head (a K/V row is read once per key for all
+//     heads, as broadcast float4 LDS reads); the F x F scores are never stored: a max pass and an
+//     exp pass (one v_exp_f32 per score, base-2 domain);
+//   * the forward can save O, the softmax row stats and the dropout keep bits per sample
+//     (rs_il_fwd_saved, 21 KB at F = 200); the backward then skips the attention recompute and
+//     the mask hashing (without a save it recomputes them into LDS), and makes two passes over
+//     the score matrix: pass A with thread = query row (dQ), pass B with thread = key row (dK,
+//     dV), each row's gradient in VGPRs -- no F x F buffer, no atomics;
 //   * weight gradients in registers across the block's samples, one partial row per block,
 //     column_reduce over blocks (deterministic).
 #include "il_kernels.hpp"
@@ -45,6 +46,7 @@ struct LFwd {
   uint64_t seed_off;  // rs_set_seed_offset source address (0 = none)
   float *y, *xsave;
   int64_t y_ld;
+  float* asave;  // attention save (rs_il_fwd_saved) or null
 };
 
 struct LBwd {
@@ -57,7 +59,16 @@ struct LBwd {
   float* dx;
   int dx_accumulate;
   float* part;
+  const float* asave;  // forward's attention save (rs_il_bwd_saved) or null: no recompute
 };
+
+// Attention save of one (iteration, sample): O [F][U] (attention output before the epilogue) |
+// row stats [F][H] x {scaled max, 1 / sum} | dropout keep bits [H][F][ceil(F/32)] (uint32).
+// Written by the forward, it lets the backward skip the max pass, the O pass and the per-pair
+// mask hashing.
+__host__ __device__ inline int64_t save_stride(int F, int U, int H) {
+  return (int64_t)F * U + 2 * (int64_t)H * F + (int64_t)H * F * ((F + 31) / 32);
+}
 
 template <int N>
 __device__ __forceinline__ void ld(float (&v)[N], const float* p) {
@@ -73,11 +84,12 @@ __device__ __forceinline__ void st(float* p, const float (&v)[N]) {
   for (int k = 0; k < N / 4; ++k)
     reinterpret_cast<float4*>(p)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
 }
-template <int N>
-__device__ __forceinline__ float dot(const float (&a)[N], const float (&b)[N]) {
+// dot product of head h's DH-slice of two U-rows
+template <class C>
+__device__ __forceinline__ float hdot(const float (&a)[C::U], const float (&b)[C::U], int h) {
   float s = 0.f;
 #pragma unroll
-  for (int d = 0; d < N; ++d) s = fmaf(a[d], b[d], s);
+  for (int d = 0; d < C::DH; ++d) s = fmaf(a[h * C::DH + d], b[h * C::DH + d], s);
   return s;
 }
 
@@ -94,6 +106,81 @@ __device__ __forceinline__ void project(const float* xs, float* Qs, int F, const
 #pragma unroll
     for (int e = 0; e < C::E; ++e) acc = fmaf(xr[e], wcol[e], acc);
     dst[f * C::U] = fmaxf(acc, 0.f);
+  }
+}
+
+// Attention forward, one thread per query row i covering every head (K/V rows are read once per
+// key for all heads, as broadcast float4 LDS reads): a max pass, then an exp pass accumulating O
+// and the keep bits word by word.  O -> Os (LDS); optionally stats -> st4[i*H+h].xy (LDS),
+// keep bits -> mask (LDS), and O / stats / bits -> sv (the global attention save).
+template <class C>
+__device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, const float* Vs,
+                                          float* Os, int F, float sc2, bool drop, uint32_t kb,
+                                          float drop_rate, float inv_keep, float4* st4,
+                                          uint32_t* mask, float* sv) {
+  const int W32 = (F + 31) / 32;
+  for (int i = threadIdx.x; i < F; i += NT) {
+    float q[C::U];
+    ld<C::U>(q, Qs + i * C::U);
+    float mx[C::H];
+#pragma unroll
+    for (int h = 0; h < C::H; ++h) mx[h] = -INFINITY;
+#pragma unroll 4
+    for (int j = 0; j < F; ++j) {
+      float k[C::U];
+      ld<C::U>(k, Ks + j * C::U);
+#pragma unroll
+      for (int h = 0; h < C::H; ++h) mx[h] = fmaxf(mx[h], hdot<C>(q, k, h));
+    }
+    float msc[C::H], l[C::H], o[C::U];
+#pragma unroll
+    for (int h = 0; h < C::H; ++h) { msc[h] = mx[h] * sc2; l[h] = 0.f; }
+#pragma unroll
+    for (int u = 0; u < C::U; ++u) o[u] = 0.f;
+    for (int w = 0; w < W32; ++w) {
+      const int jn = F - 32 * w < 32 ? F - 32 * w : 32;
+      uint32_t bits[C::H];
+#pragma unroll
+      for (int h = 0; h < C::H; ++h) bits[h] = 0u;
+#pragma unroll 2
+      for (int jj = 0; jj < jn; ++jj) {
+        const int j = 32 * w + jj;
+        float k[C::U], v[C::U];
+        ld<C::U>(k, Ks + j * C::U);
+        ld<C::U>(v, Vs + j * C::U);
+#pragma unroll
+        for (int h = 0; h < C::H; ++h) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), sc2, -msc[h]));
+          l[h] += e;
+          const bool keep = !drop || dropout_keep_k(kb, h, i, j, drop_rate);
+          bits[h] |= (uint32_t)keep << jj;
+          const float ek = keep ? e : 0.f;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) o[h * C::DH + d] = fmaf(ek, v[h * C::DH + d], o[h * C::DH + d]);
+        }
+      }
+      if (drop) {
+#pragma unroll
+        for (int h = 0; h < C::H; ++h) {
+          if (mask) mask[(h * F + i) * W32 + w] = bits[h];
+          if (sv) reinterpret_cast<uint32_t*>(sv + F * C::U + 2 * C::H * F)[(h * F + i) * W32 + w] = bits[h];
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < C::H; ++h) {
+      const float il = 1.0f / l[h];
+      const float inv = (drop ? inv_keep : 1.f) * il;
+#pragma unroll
+      for (int d = 0; d < C::DH; ++d) o[h * C::DH + d] *= inv;
+      if (st4) { st4[i * C::H + h].x = msc[h]; st4[i * C::H + h].y = il; }
+      if (sv) {
+        sv[F * C::U + 2 * (i * C::H + h)] = msc[h];
+        sv[F * C::U + 2 * (i * C::H + h) + 1] = il;
+      }
+    }
+    st<C::U>(Os + i * C::U, o);
+    if (sv) st<C::U>(sv + i * C::U, o);
   }
 }
 
@@ -126,35 +213,8 @@ __global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
       const uint32_t kb = a.drop ? dropout_sample_key(splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it), (uint32_t)b) : 0u;
       project<C>(xs, Qs, F, wcol, bc);
       __syncthreads();
-      for (int p = t; p < F * C::H; p += NT) {
-        const int h = p / F, i = p % F;
-        float q[C::DH];
-        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
-        float mx = -INFINITY;
-        for (int j = 0; j < F; ++j) {
-          float k[C::DH];
-          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-          mx = fmaxf(mx, dot<C::DH>(q, k));
-        }
-        const float msc = mx * a.sc2;
-        float l = 0.f, o[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
-        for (int j = 0; j < F; ++j) {
-          float k[C::DH], v[C::DH];
-          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
-          const float e = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc));
-          l += e;
-          const float ek = (!a.drop || dropout_keep_k(kb, h, i, j, a.drop_rate)) ? e : 0.f;
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) o[d] = fmaf(ek, v[d], o[d]);
-        }
-        const float inv = (a.drop ? a.inv_keep : 1.f) / l;
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) o[d] *= inv;
-        st<C::DH>(Os + i * C::U + h * C::DH, o);
-      }
+      float* sv = a.asave ? a.asave + ((int64_t)it * a.B + b) * save_stride(F, C::U, C::H) : nullptr;
+      attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, nullptr, nullptr, sv);
       __syncthreads();
       const bool last = it == a.L - 1;
       for (int i = t; i < F; i += NT) {
@@ -201,10 +261,8 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
   float* Gs = Os + F * C::U;               // dY -> dA (= dO) -> dx of this iteration
   float* DKs = Gs + F * C::U;
   float* DVs = DKs + F * C::U;
-  float* stm = DVs + F * C::U;             // [H][F] scaled max
-  float* sti = stm + C::H * F;             // [H][F] 1 / sum
-  float* std_ = sti + C::H * F;            // [H][F] D = dO . O
-  uint32_t* mask = reinterpret_cast<uint32_t*>(std_ + C::H * F);  // [H][F][W32]
+  float4* st4 = reinterpret_cast<float4*>(DVs + F * C::U);   // [F][H] {scaled max, 1/sum, D, -}
+  uint32_t* mask = reinterpret_cast<uint32_t*>(st4 + F * C::H);  // [H][F][W32]
   const int t = threadIdx.x;
   float wcol[C::E];
   {
@@ -216,9 +274,6 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
   float gam[C::U];
 #pragma unroll
   for (int u = 0; u < C::U; ++u) gam[u] = a.gamma[u];
-  float bet[C::U];
-#pragma unroll
-  for (int u = 0; u < C::U; ++u) bet[u] = a.beta[u];
   // dx mapping: thread -> (row group, e); the row of W for e in registers
   const int xe = t % C::E, xrg = t / C::E;
   constexpr int XRG = NT / C::E;
@@ -244,62 +299,33 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
               reinterpret_cast<const float4*>(a.dy + b * a.dy_ld + i * C::U)[q4];
         }
       }
-      const uint64_t lseed = splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it);
-      const uint32_t kb = a.drop ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
-      __syncthreads();
-      project<C>(xs, Qs, F, wcol, bc);
-      if (a.drop) {
-        for (int p = t; p < F * C::H; p += NT) {
-          const int h = p / F, i = p % F;
-          for (int w = 0; w < W32; ++w) {
-            uint32_t bits = 0;
-            for (int jj = 0; jj < 32; ++jj) {
-              const int j = 32 * w + jj;
-              if (j < F && dropout_keep_k(kb, h, i, j, a.drop_rate)) bits |= 1u << jj;
-            }
-            mask[(h * F + i) * W32 + w] = bits;
-          }
+      if (a.asave) {
+        // the forward's O, row stats and keep bits into their LDS regions
+        const float* sv = a.asave + ((int64_t)it * a.B + b) * save_stride(F, C::U, C::H);
+        for (int k = t; k < F * C::U / 4; k += NT)
+          reinterpret_cast<float4*>(Os)[k] = reinterpret_cast<const float4*>(sv)[k];
+        for (int k = t; k < C::H * F; k += NT) {
+          const float2 mi = reinterpret_cast<const float2*>(sv + F * C::U)[k];
+          st4[k].x = mi.x;
+          st4[k].y = mi.y;
         }
+        if (a.drop) {
+          const uint32_t* mg = reinterpret_cast<const uint32_t*>(sv + F * C::U + 2 * C::H * F);
+          for (int k = t; k < C::H * F * W32; k += NT) mask[k] = mg[k];
+        }
+        __syncthreads();
+        project<C>(xs, Qs, F, wcol, bc);
+        __syncthreads();
+      } else {
+        const uint64_t lseed = splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it);
+        const uint32_t kb = a.drop ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
+        __syncthreads();
+        project<C>(xs, Qs, F, wcol, bc);
+        __syncthreads();
+        attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, st4, mask, nullptr);
+        __syncthreads();
       }
-      __syncthreads();
-      // ---- recompute the attention forward: stats and O ----
-      for (int p = t; p < F * C::H; p += NT) {
-        const int h = p / F, i = p % F;
-        float q[C::DH];
-        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
-        float mx = -INFINITY;
-#pragma unroll 4
-        for (int j = 0; j < F; ++j) {
-          float k[C::DH];
-          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-          mx = fmaxf(mx, dot<C::DH>(q, k));
-        }
-        const float msc = mx * a.sc2;
-        float l = 0.f, o[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
-        const uint32_t* mrow = mask + (h * F + i) * W32;
-#pragma unroll 4
-        for (int j = 0; j < F; ++j) {
-          float k[C::DH], v[C::DH];
-          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
-          const float e = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc));
-          l += e;
-          const float ek = (!a.drop || ((mrow[j >> 5] >> (j & 31)) & 1u)) ? e : 0.f;
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) o[d] = fmaf(ek, v[d], o[d]);
-        }
-        const float il = 1.0f / l;
-        const float inv = (a.drop ? a.inv_keep : 1.f) * il;
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) o[d] *= inv;
-        st<C::DH>(Os + i * C::U + h * C::DH, o);
-        stm[h * F + i] = msc;
-        sti[h * F + i] = il;
-      }
-      __syncthreads();
-      // ---- epilogue backward: LN, ReLU, residual; D = dO . O per (head, row) ----
+      // ---- epilogue backward: LN, ReLU, residual; D = dO . O per (row, head) ----
       for (int i = t; i < F; i += NT) {
         float o[C::U], r[C::U], z[C::U], g[C::U];
         ld<C::U>(o, Os + i * C::U);
@@ -339,76 +365,86 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         st<C::U>(Gs + i * C::U, da);
         st<C::U>(Rs + i * C::U, dr);
 #pragma unroll
-        for (int h = 0; h < C::H; ++h) {
-          float dsum = 0.f;
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) dsum = fmaf(da[h * C::DH + d], o[h * C::DH + d], dsum);
-          std_[h * F + i] = dsum;
-        }
+        for (int h = 0; h < C::H; ++h) st4[i * C::H + h].z = hdot<C>(da, o, h);
       }
       __syncthreads();
-      // ---- pass A (thread = query row): dQ; pass B (thread = key row): dK, dV ----
-      for (int p = t; p < F * C::H; p += NT) {
-        const int h = p / F, i = p % F;
-        float q[C::DH], g[C::DH], dq[C::DH];
-        ld<C::DH>(q, Qs + i * C::U + h * C::DH);
-        ld<C::DH>(g, Gs + i * C::U + h * C::DH);
+      // ---- pass A (thread = query row, all heads): dQ -> Os ----
+      for (int i = t; i < F; i += NT) {
+        float q[C::U], g[C::U], dq[C::U];
+        ld<C::U>(q, Qs + i * C::U);
+        ld<C::U>(g, Gs + i * C::U);
 #pragma unroll
-        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
-        const float msc = stm[h * F + i], il = sti[h * F + i], D = std_[h * F + i];
-        const uint32_t* mrow = mask + (h * F + i) * W32;
-#pragma unroll 4
-        for (int j = 0; j < F; ++j) {
-          float k[C::DH], v[C::DH];
-          ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-          ld<C::DH>(v, Vs + j * C::U + h * C::DH);
-          const float pe = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -msc)) * il;
-          float dP = dot<C::DH>(g, v);
-          if (a.drop) dP = ((mrow[j >> 5] >> (j & 31)) & 1u) ? dP * a.inv_keep : 0.f;
-          const float dS = pe * (dP - D);
+        for (int u = 0; u < C::U; ++u) dq[u] = 0.f;
+        float msc[C::H], il[C::H], D[C::H];
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) dq[d] = fmaf(dS, k[d], dq[d]);
+        for (int h = 0; h < C::H; ++h) {
+          const float4 sh = st4[i * C::H + h];
+          msc[h] = sh.x; il[h] = sh.y; D[h] = sh.z;
+        }
+        for (int w = 0; w < W32; ++w) {
+          const int jn = F - 32 * w < 32 ? F - 32 * w : 32;
+          uint32_t mw[C::H];
+#pragma unroll
+          for (int h = 0; h < C::H; ++h) mw[h] = a.drop ? mask[(h * F + i) * W32 + w] : ~0u;
+#pragma unroll 2
+          for (int jj = 0; jj < jn; ++jj) {
+            const int j = 32 * w + jj;
+            float k[C::U], v[C::U];
+            ld<C::U>(k, Ks + j * C::U);
+            ld<C::U>(v, Vs + j * C::U);
+#pragma unroll
+            for (int h = 0; h < C::H; ++h) {
+              const float pe = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), a.sc2, -msc[h])) * il[h];
+              float dP = hdot<C>(g, v, h);
+              if (a.drop) dP = ((mw[h] >> jj) & 1u) ? dP * a.inv_keep : 0.f;
+              const float dS = pe * (dP - D[h]);
+#pragma unroll
+              for (int d = 0; d < C::DH; ++d) dq[h * C::DH + d] = fmaf(dS, k[h * C::DH + d], dq[h * C::DH + d]);
+            }
+          }
         }
 #pragma unroll
-        for (int d = 0; d < C::DH; ++d) dq[d] = q[d] > 0.f ? dq[d] * a.inv_sdh : 0.f;
-        st<C::DH>(Os + i * C::U + h * C::DH, dq);
+        for (int u = 0; u < C::U; ++u) dq[u] = q[u] > 0.f ? dq[u] * a.inv_sdh : 0.f;
+        st<C::U>(Os + i * C::U, dq);
       }
-      for (int p = t; p < F * C::H; p += NT) {
-        const int h = p / F, j = p % F;
-        float k[C::DH], v[C::DH], dk[C::DH], dv[C::DH];
-        ld<C::DH>(k, Ks + j * C::U + h * C::DH);
-        ld<C::DH>(v, Vs + j * C::U + h * C::DH);
+      // ---- pass B (thread = key row, all heads): dK, dV ----
+      for (int j = t; j < F; j += NT) {
+        float k[C::U], v[C::U], dk[C::U], dv[C::U];
+        ld<C::U>(k, Ks + j * C::U);
+        ld<C::U>(v, Vs + j * C::U);
 #pragma unroll
-        for (int d = 0; d < C::DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
-        const int jw = j >> 5;
-        const uint32_t jb = 1u << (j & 31);
-#pragma unroll 4
+        for (int u = 0; u < C::U; ++u) { dk[u] = 0.f; dv[u] = 0.f; }
+        const int jw = j >> 5, jbit = j & 31;
+#pragma unroll 2
         for (int i = 0; i < F; ++i) {
-          float q[C::DH], g[C::DH];
-          ld<C::DH>(q, Qs + i * C::U + h * C::DH);
-          ld<C::DH>(g, Gs + i * C::U + h * C::DH);
-          const float pe = __builtin_amdgcn_exp2f(fmaf(dot<C::DH>(q, k), a.sc2, -stm[h * F + i])) *
-                           sti[h * F + i];
-          float dP = dot<C::DH>(g, v), pd = pe;
-          if (a.drop) {
-            const bool keep = (mask[(h * F + i) * W32 + jw] & jb) != 0u;
-            dP = keep ? dP * a.inv_keep : 0.f;
-            pd = keep ? pe * a.inv_keep : 0.f;
-          }
-          const float dS = pe * (dP - std_[h * F + i]);
+          float q[C::U], g[C::U];
+          ld<C::U>(q, Qs + i * C::U);
+          ld<C::U>(g, Gs + i * C::U);
 #pragma unroll
-          for (int d = 0; d < C::DH; ++d) {
-            dk[d] = fmaf(dS, q[d], dk[d]);
-            dv[d] = fmaf(pd, g[d], dv[d]);
+          for (int h = 0; h < C::H; ++h) {
+            const float4 sh = st4[i * C::H + h];
+            const float pe = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), a.sc2, -sh.x)) * sh.y;
+            float dP = hdot<C>(g, v, h), pd = pe;
+            if (a.drop) {
+              const bool keep = ((mask[(h * F + i) * W32 + jw] >> jbit) & 1u) != 0u;
+              dP = keep ? dP * a.inv_keep : 0.f;
+              pd = keep ? pe * a.inv_keep : 0.f;
+            }
+            const float dS = pe * (dP - sh.z);
+#pragma unroll
+            for (int d = 0; d < C::DH; ++d) {
+              dk[h * C::DH + d] = fmaf(dS, q[h * C::DH + d], dk[h * C::DH + d]);
+              dv[h * C::DH + d] = fmaf(pd, g[h * C::DH + d], dv[h * C::DH + d]);
+            }
           }
         }
 #pragma unroll
-        for (int d = 0; d < C::DH; ++d) {
-          dk[d] = k[d] > 0.f ? dk[d] * a.inv_sdh : 0.f;
-          dv[d] = v[d] > 0.f ? dv[d] : 0.f;
+        for (int u = 0; u < C::U; ++u) {
+          dk[u] = k[u] > 0.f ? dk[u] * a.inv_sdh : 0.f;
+          dv[u] = v[u] > 0.f ? dv[u] : 0.f;
         }
-        st<C::DH>(DKs + j * C::U + h * C::DH, dk);
-        st<C::DH>(DVs + j * C::U + h * C::DH, dv);
+        st<C::U>(DKs + j * C::U, dk);
+        st<C::U>(DVs + j * C::U, dv);
       }
       __syncthreads();
       // ---- projection backward: dZ = [dQ (Os) | dK | dV | dR (Rs)] ----
@@ -471,7 +507,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
 
 inline size_t fwd_lds(int F, int E, int U) { return (size_t)F * (E + 5 * U) * 4; }
 inline size_t bwd_lds(int F, int E, int U, int H) {
-  const size_t main = (size_t)F * (E + 8 * U) * 4 + (size_t)3 * H * F * 4 +
+  const size_t main = (size_t)F * (E + 8 * U) * 4 + (size_t)4 * H * F * 4 +
                       (size_t)H * F * ((F + 31) / 32) * 4;
   const size_t red = (size_t)NT * 2 * U * 4;
   return main > red ? main : red;
@@ -483,7 +519,7 @@ int run_fwd(const FwdReq& q) {
   LFwd a{q.x, q.W, q.bias, q.gamma, q.beta, q.B, q.F, q.L, q.use_res, q.drop_rate > 0.f,
          q.eps, q.drop_rate, q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
          1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, (uint64_t)(uintptr_t)rs_seed_offset_now(), q.y,
-         q.xsave, q.y_ld};
+         q.xsave, q.y_ld, q.asave};
   if (q.B == 0) return RS_OK;
   const size_t lds = fwd_lds(q.F, E, U);
   int64_t grid = q.B < 4096 ? q.B : 4096;
@@ -501,7 +537,7 @@ int run_bwd(const BwdReq& q) {
          q.drop_rate > 0.f, q.eps, q.drop_rate,
          q.drop_rate > 0.f ? 1.0f / (1.0f - q.drop_rate) : 1.0f,
          1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, (uint64_t)(uintptr_t)rs_seed_offset_now(), q.dx,
-         q.dx_accumulate, q.workspace};
+         q.dx_accumulate, q.workspace, q.asave};
   const size_t lds = bwd_lds(q.F, E, U, H);
   bwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
   int st = rs_status_after_launch();
@@ -512,6 +548,10 @@ int run_bwd(const BwdReq& q) {
 }
 
 }  // namespace large
+
+int64_t il_attn_save_floats(int64_t B, int F, int U, int H, int L) {
+  return F > 64 ? (int64_t)L * B * large::save_stride(F, U, H) : 0;
+}
 
 // F in (64, 256]: the many-field instantiations (config 3 is E = U = 8, H = 2).
 int il_large_fwd(const FwdReq& q) {

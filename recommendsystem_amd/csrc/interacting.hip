@@ -9,6 +9,7 @@ RS_IL_DECLARE_UNIT(il_unit_b)
 RS_IL_DECLARE_UNIT(il_unit_c)
 int il_large_fwd(const FwdReq& q);  // il_large.hip: F in (64, 256]
 int il_large_bwd(const BwdReq& q);
+int64_t il_attn_save_floats(int64_t B, int F, int U, int H, int L);
 
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
                    int accumulate) {
@@ -51,10 +52,10 @@ RS_API int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U) {
   return grid * (int64_t)rs_il_param_count(E, U);
 }
 
-RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
-                     const float* W, const float* bias, const float* gamma, const float* beta,
-                     float eps, int use_res, float drop_rate, uint64_t seed, float* y,
-                     int64_t y_ld, float* xsave) {
+static int il_fwd_impl(void* stream, const float* x, int64_t B, int F, int E, int U, int H,
+                       int L, const float* W, const float* bias, const float* gamma,
+                       const float* beta, float eps, int use_res, float drop_rate, uint64_t seed,
+                       float* y, int64_t y_ld, float* xsave, float* asave) {
   if (!x || !W || !bias || !gamma || !beta || !y || B < 0 || F <= 0 || L <= 0 || H <= 0)
     return RS_ERR_ARG;
   if (U % H != 0 || (L > 1 && (E != U || !xsave))) return RS_ERR_ARG;
@@ -62,11 +63,36 @@ RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int 
   rs_il::FwdReq q{rs_stream(stream), x, W, bias, gamma, beta, B, F, E, U, H, L, use_res,
                   eps, drop_rate, seed, y, xsave, y_ld};
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  q.asave = asave;
   if (F > 64) return rs_il::il_large_fwd(q);
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
   return r;
+}
+
+RS_API int rs_il_fwd(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
+                     const float* W, const float* bias, const float* gamma, const float* beta,
+                     float eps, int use_res, float drop_rate, uint64_t seed, float* y,
+                     int64_t y_ld, float* xsave) {
+  return il_fwd_impl(stream, x, B, F, E, U, H, L, W, bias, gamma, beta, eps, use_res, drop_rate,
+                     seed, y, y_ld, xsave, nullptr);
+}
+
+RS_API int64_t rs_il_attn_save_floats(int64_t B, int F, int U, int H, int L) {
+  if (B < 0 || F <= 0 || U <= 0 || H <= 0 || L <= 0) return 0;
+  return rs_il::il_attn_save_floats(B, F, U, H, L);
+}
+
+RS_API int rs_il_fwd_saved(void* stream, const float* x, int64_t B, int F, int E, int U, int H,
+                           int L, const float* W, const float* bias, const float* gamma,
+                           const float* beta, float eps, int use_res, float drop_rate,
+                           uint64_t seed, float* y, int64_t y_ld, float* xsave, float* asave,
+                           int64_t asave_floats) {
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need > 0 && (!asave || asave_floats < need)) return RS_ERR_ARG;
+  return il_fwd_impl(stream, x, B, F, E, U, H, L, W, bias, gamma, beta, eps, use_res, drop_rate,
+                     seed, y, y_ld, xsave, need > 0 ? asave : nullptr);
 }
 
 RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row_base,
@@ -105,13 +131,12 @@ static int bwd_small(const rs_il::BwdReq& q) {
   return r;
 }
 
-RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
-                     int64_t dy_ld, int64_t B,
-                     int F, int E, int U, int H, int L, const float* W, const float* bias,
-                     const float* gamma, const float* beta, float eps, int use_res,
-                     float drop_rate, uint64_t seed, float* dx, int dx_accumulate,
-                     float* dparams, int dparams_accumulate, float* workspace,
-                     int64_t workspace_floats) {
+static int il_bwd_impl(void* stream, const float* x, const float* xsave, const float* dy,
+                       int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                       const float* W, const float* bias, const float* gamma, const float* beta,
+                       float eps, int use_res, float drop_rate, uint64_t seed, float* dx,
+                       int dx_accumulate, float* dparams, int dparams_accumulate,
+                       float* workspace, int64_t workspace_floats, const float* asave) {
   if (!x || !dy || !W || !bias || !gamma || !beta || !dx || !workspace) return RS_ERR_ARG;
   if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
     return RS_ERR_ARG;
@@ -120,8 +145,35 @@ RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const flo
                   use_res, eps, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
                   workspace, workspace_floats};
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  q.asave = asave;
   if (F > 64) return rs_il::il_large_bwd(q);
   return bwd_small(q);
+}
+
+RS_API int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
+                     int64_t dy_ld, int64_t B,
+                     int F, int E, int U, int H, int L, const float* W, const float* bias,
+                     const float* gamma, const float* beta, float eps, int use_res,
+                     float drop_rate, uint64_t seed, float* dx, int dx_accumulate,
+                     float* dparams, int dparams_accumulate, float* workspace,
+                     int64_t workspace_floats) {
+  return il_bwd_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta, eps,
+                     use_res, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
+                     workspace, workspace_floats, nullptr);
+}
+
+RS_API int rs_il_bwd_saved(void* stream, const float* x, const float* xsave, const float* dy,
+                           int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                           const float* W, const float* bias, const float* gamma,
+                           const float* beta, float eps, int use_res, float drop_rate,
+                           uint64_t seed, float* dx, int dx_accumulate, float* dparams,
+                           int dparams_accumulate, float* workspace, int64_t workspace_floats,
+                           const float* asave, int64_t asave_floats) {
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need > 0 && (!asave || asave_floats < need)) return RS_ERR_ARG;
+  return il_bwd_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta, eps,
+                     use_res, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
+                     workspace, workspace_floats, need > 0 ? asave : nullptr);
 }
 
 RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,

@@ -43,16 +43,20 @@ class _InteractingFn(torch.autograd.Function):
         U, H, L = layer.unit_num, layer.head_num, layer.layer_num
         y = torch.empty(B, F, U, device=x.device, dtype=torch.float32)
         xsave = torch.empty(max(L - 1, 0), B, F, U, device=x.device, dtype=torch.float32)
-        call("rs_il_fwd", stream_handle(), ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma),
-             ptr(beta), layer.epsilon, int(layer.use_res), drop_rate, seed, ptr(y), F * U,
-             ptr(xsave) if L > 1 else None)
-        ctx.save_for_backward(x, xsave, W, bias, gamma, beta)
+        # many-field shapes (F > 64): the forward also saves the attention output, softmax stats
+        # and dropout bits so the backward does not recompute them (rs_il_fwd_saved)
+        n_save = int(_lib.load().rs_il_attn_save_floats(B, F, U, H, L))
+        asave = torch.empty(n_save, device=x.device, dtype=torch.float32)
+        call("rs_il_fwd_saved", stream_handle(), ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias),
+             ptr(gamma), ptr(beta), layer.epsilon, int(layer.use_res), drop_rate, seed, ptr(y),
+             F * U, ptr(xsave) if L > 1 else None, ptr(asave) if n_save else None, n_save)
+        ctx.save_for_backward(x, xsave, W, bias, gamma, beta, asave)
         ctx.layer, ctx.seed, ctx.drop_rate = layer, seed, drop_rate
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, xsave, W, bias, gamma, beta = ctx.saved_tensors
+        x, xsave, W, bias, gamma, beta, asave = ctx.saved_tensors
         layer = ctx.layer
         dy = dy.contiguous()
         B, F, E = x.shape
@@ -65,10 +69,11 @@ class _InteractingFn(torch.autograd.Function):
         in_place = block is not None
         dparams = block if in_place else torch.empty(
             sum(p.numel() for p in params), device=x.device, dtype=torch.float32)
-        call("rs_il_bwd", stream_handle(), ptr(x), ptr(xsave) if L > 1 else None, ptr(dy), F * U,
-             B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), layer.epsilon,
+        call("rs_il_bwd_saved", stream_handle(), ptr(x), ptr(xsave) if L > 1 else None, ptr(dy),
+             F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), layer.epsilon,
              int(layer.use_res), ctx.drop_rate, ctx.seed, ptr(dx), 0, ptr(dparams),
-             1 if in_place else 0, ptr(ws), ws_n)
+             1 if in_place else 0, ptr(ws), ws_n, ptr(asave) if asave.numel() else None,
+             asave.numel())
         if in_place:
             return dx, None, None, None, None, None, None, None
         outs, off = [], 0

@@ -400,6 +400,58 @@ def test_interacting_many_fields_dropout(F, L):
     assert_grad_close(_np(il.beta.grad), bet.grad.numpy(), what="dbeta")
 
 
+@pytest.mark.parametrize("F,E,U,H,L,drop", [(200, 8, 8, 2, 1, 0.2), (200, 8, 8, 2, 1, 0.0),
+                                             (97, 8, 8, 1, 1, 0.2), (80, 16, 16, 2, 2, 0.1)])
+def test_interacting_saved_pair_equals_recompute(F, E, U, H, L, drop):
+    """rs_il_fwd_saved / rs_il_bwd_saved (F > 64: the backward reads the forward's attention
+    output, softmax stats and keep bits) give bit-identical y, dx and parameter gradients to the
+    recomputing pair rs_il_fwd / rs_il_bwd; a short save buffer is refused."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    lib = _lib.load()
+    B = 37
+    g = torch.Generator(device=DEV).manual_seed(F + L)
+    x = torch.rand(B, F, E, device=DEV, generator=g) - 0.5
+    W = (torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.6
+    b = (torch.rand(4 * U, device=DEV, generator=g) - 0.5) * 0.2
+    gm = torch.rand(U, device=DEV, generator=g) + 0.5
+    bt = (torch.rand(U, device=DEV, generator=g) - 0.5) * 0.2
+    dy = torch.randn(B, F * U, device=DEV, generator=g)
+    s = stream_handle()
+    n_save = int(lib.rs_il_attn_save_floats(B, F, U, H, L))
+    assert n_save == L * B * (F * U + 2 * H * F + H * F * ((F + 31) // 32))
+    asave = torch.empty(n_save, device=DEV)
+    ws_n = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+    npar = E * 4 * U + 4 * U + 2 * U
+    outs = []
+    for saved in (False, True):
+        y = torch.empty(B, F * U, device=DEV)
+        xs = torch.empty(max(L - 1, 1), B, F, U, device=DEV)
+        dx = torch.empty_like(x)
+        dp = torch.empty(npar, device=DEV)
+        ws = torch.empty(ws_n, device=DEV)
+        common = (ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77, ptr(y), F * U,
+                  ptr(xs) if L > 1 else None)
+        if saved:
+            call("rs_il_fwd_saved", s, ptr(x), B, F, E, U, H, L, *common, ptr(asave), n_save)
+            call("rs_il_bwd_saved", s, ptr(x), ptr(xs) if L > 1 else None, ptr(dy), F * U, B, F,
+                 E, U, H, L, ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77, ptr(dx), 0,
+                 ptr(dp), 0, ptr(ws), ws_n, ptr(asave), n_save)
+        else:
+            call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, *common)
+            call("rs_il_bwd", s, ptr(x), ptr(xs) if L > 1 else None, ptr(dy), F * U, B, F, E, U,
+                 H, L, ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77, ptr(dx), 0, ptr(dp),
+                 0, ptr(ws), ws_n)
+        torch.cuda.synchronize()
+        outs.append((y, dx, dp))
+    for a, c, name in zip(outs[0], outs[1], ("y", "dx", "dparams")):
+        assert torch.equal(a, c), f"{name}: saved pair differs from recompute"
+    rc = lib.rs_il_fwd_saved(s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(b), ptr(gm), ptr(bt),
+                             1e-14, 1, drop, 77, ptr(outs[0][0]), F * U,
+                             ptr(xs) if L > 1 else None, ptr(asave), n_save - 1)
+    assert rc == -1
+
+
 def test_interacting_rank_error():
     from recommendsystem_amd.layers import InteractingLayer
     il = InteractingLayer(1, 16, 2, device=DEV)

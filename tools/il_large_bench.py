@@ -28,8 +28,15 @@ def main(B=4096, F=200, E=8, U=8, H=2, reps=10, drop=0.2):
                        drop, 3, ptr(y), F * U, None)
     bwd = lambda: call("rs_il_bwd", s, ptr(x), None, ptr(dy), F * U, B, F, E, U, H, 1, ptr(W), ptr(b),  # noqa: E731
                        ptr(gm), ptr(bt), 1e-14, 1, drop, 3, ptr(dx), 0, None, 0, ptr(ws), wsn)
+    ns = int(lib.rs_il_attn_save_floats(B, F, U, H, 1))
+    asave = torch.empty(ns, device=dev)
+    fwds = lambda: call("rs_il_fwd_saved", s, ptr(x), B, F, E, U, H, 1, ptr(W), ptr(b), ptr(gm),  # noqa: E731
+                        ptr(bt), 1e-14, 1, drop, 3, ptr(y), F * U, None, ptr(asave), ns)
+    bwds = lambda: call("rs_il_bwd_saved", s, ptr(x), None, ptr(dy), F * U, B, F, E, U, H, 1,  # noqa: E731
+                        ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 3, ptr(dx), 0, None, 0,
+                        ptr(ws), wsn, ptr(asave), ns)
     out = {}
-    for name, fn in (("fwd", fwd), ("bwd", bwd)):
+    for name, fn in (("fwd", fwd), ("bwd", bwd), ("fwd_saved", fwds), ("bwd_saved", bwds)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,6 +49,7 @@ def main(B=4096, F=200, E=8, U=8, H=2, reps=10, drop=0.2):
     fl = 1_382_400 * B
     out["fwd_tflops"] = round(fl / out["fwd_us"] / 1e6, 2)
     out["bwd_tflops"] = round(2 * fl / out["bwd_us"] / 1e6, 2)
+    out["bwd_saved_tflops"] = round(2 * fl / out["bwd_saved_us"] / 1e6, 2)
     print(json.dumps(out))
 
 
