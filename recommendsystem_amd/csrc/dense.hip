@@ -17,6 +17,9 @@
 //                fixed-order reduce (deterministic, no float atomics)
 #include "common.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 enum { RS_ACT_NONE = 0, RS_ACT_RELU = 1, RS_ACT_SIGMOID = 2 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -235,16 +238,37 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
 
 struct GemmPlan { int bm, bn, splits; int64_t rchunk; };
 
+// Tile / split-K policy.  256 CUs take ~4 resident 256-thread GEMM blocks each, so a launch wants
+// ~1k blocks: 64-row tiles only when that still gives >= big_min tiles, and reductions split
+// (deterministic partials + column_reduce) while the tile count is below split_below, towards
+// split_target blocks with >= min_rows reduction rows per split.  RS_GEMM_TUNE="a,b,c,d"
+// overrides (host-side, read once; tools/gemm_tune.sh).
+struct GemmTune { int big_min, split_below, split_target, min_rows; };
+static const GemmTune& gemm_tune() {
+  static const GemmTune t = [] {
+    GemmTune v{512, 512, 1024, 128};
+    if (const char* e = getenv("RS_GEMM_TUNE")) {
+      GemmTune o = v;
+      if (sscanf(e, "%d,%d,%d,%d", &o.big_min, &o.split_below, &o.split_target, &o.min_rows) == 4 &&
+          o.split_target > 0 && o.min_rows >= GBK)
+        v = o;
+    }
+    return v;
+  }();
+  return t;
+}
+
 static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
+  const GemmTune& tu = gemm_tune();
   GemmPlan p;
   p.bn = N <= 32 ? 32 : 64;
   const int64_t tn = (N + p.bn - 1) / p.bn;
-  p.bm = ((M + 63) / 64) * tn >= 240 ? 64 : 32;
+  p.bm = ((M + 63) / 64) * tn >= tu.big_min ? 64 : 32;
   const int64_t tiles = ((M + p.bm - 1) / p.bm) * tn;
   p.splits = 1;
-  if (allow_split && tiles < 128) {
-    int64_t s = (256 + tiles - 1) / tiles;
-    const int64_t max_s = (R + 255) / 256;  // keep >= 256 reduction rows per split
+  if (allow_split && tiles < tu.split_below) {
+    int64_t s = (tu.split_target + tiles - 1) / tiles;
+    const int64_t max_s = (R + tu.min_rows - 1) / tu.min_rows;  // >= min_rows rows per split
     if (s > max_s) s = max_s;
     p.splits = (int)(s < 1 ? 1 : s);
   }
