@@ -24,6 +24,9 @@ namespace rs_il {
 namespace large {
 
 constexpr int NT = 256;
+#ifndef RS_ILL_SKIP
+#define RS_ILL_SKIP 0  // profiling variants only: bit 1 passes A/B, 2 projection bwd, 4 epilogue
+#endif
 constexpr int FMAXL = 256;
 
 template <int E_, int U_, int H_>
@@ -84,13 +87,28 @@ __device__ __forceinline__ void st(float* p, const float (&v)[N]) {
   for (int k = 0; k < N / 4; ++k)
     reinterpret_cast<float4*>(p)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
 }
-// dot product of head h's DH-slice of two U-rows
+// dot product of head h's DH-slice of two U-rows, packed (v_pk_fma_f32: even / odd partial
+// sums, added at the end)
 template <class C>
 __device__ __forceinline__ float hdot(const float (&a)[C::U], const float (&b)[C::U], int h) {
-  float s = 0.f;
+  f32x2v acc = {0.f, 0.f};
 #pragma unroll
-  for (int d = 0; d < C::DH; ++d) s = fmaf(a[h * C::DH + d], b[h * C::DH + d], s);
-  return s;
+  for (int d = 0; d < C::DH; d += 2)
+    acc = __builtin_elementwise_fma(f32x2v{a[h * C::DH + d], a[h * C::DH + d + 1]},
+                                    f32x2v{b[h * C::DH + d], b[h * C::DH + d + 1]}, acc);
+  return acc.x + acc.y;
+}
+// o[h-slice] += p * x[h-slice], packed
+template <class C>
+__device__ __forceinline__ void haxpy(float (&o)[C::U], float p, const float (&x)[C::U], int h) {
+  const f32x2v pp = {p, p};
+#pragma unroll
+  for (int d = 0; d < C::DH; d += 2) {
+    const f32x2v r = __builtin_elementwise_fma(pp, f32x2v{x[h * C::DH + d], x[h * C::DH + d + 1]},
+                                               f32x2v{o[h * C::DH + d], o[h * C::DH + d + 1]});
+    o[h * C::DH + d] = r.x;
+    o[h * C::DH + d + 1] = r.y;
+  }
 }
 
 // projection: P_c[f] = relu(x_f . W[:, c] + b_c) into the Q|K|V|R region of column c
@@ -155,8 +173,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
           const bool keep = !drop || dropout_keep_k(kb, h, i, j, drop_rate);
           bits[h] |= (uint32_t)keep << jj;
           const float ek = keep ? e : 0.f;
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) o[h * C::DH + d] = fmaf(ek, v[h * C::DH + d], o[h * C::DH + d]);
+          haxpy<C>(o, ek, v, h);
         }
       }
       if (drop) {
@@ -326,7 +343,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         __syncthreads();
       }
       // ---- epilogue backward: LN, ReLU, residual; D = dO . O per (row, head) ----
-      for (int i = t; i < F; i += NT) {
+      for (int i = t; i < F && (RS_ILL_SKIP & 4) == 0; i += NT) {
         float o[C::U], r[C::U], z[C::U], g[C::U];
         ld<C::U>(o, Os + i * C::U);
         ld<C::U>(r, Rs + i * C::U);
@@ -368,83 +385,113 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         for (int h = 0; h < C::H; ++h) st4[i * C::H + h].z = hdot<C>(da, o, h);
       }
       __syncthreads();
-      // ---- pass A (thread = query row, all heads): dQ -> Os ----
-      for (int i = t; i < F; i += NT) {
-        float q[C::U], g[C::U], dq[C::U];
-        ld<C::U>(q, Qs + i * C::U);
-        ld<C::U>(g, Gs + i * C::U);
+      // ---- passes A and B side by side: threads [0, NT/2) run pass A (dQ -> Os) over query
+      // rows {r, r + NH}, threads [NT/2, NT) pass B (dK, dV) over key rows {r, r + NH}, NH =
+      // ceil(F/2).  Two rows per thread halve the broadcast K/V (pass A) and Q/dO/stats (pass B)
+      // LDS reads per score -- the passes are LDS-read bound -- and the two halves overlap.
+      {
+        const int NH = (F + 1) / 2;
+        const int half = t / (NT / 2), r = t % (NT / 2);
+        const int r1 = r + NH;
+        const bool has1 = r1 < F;
+        const int rr1 = has1 ? r1 : r;  // duplicate row 0's work when F is odd (not stored)
+        if ((RS_ILL_SKIP & 1) == 0 && half == 0 && r < NH) {
+          float q0[C::U], g0[C::U], q1[C::U], g1[C::U], dq0[C::U], dq1[C::U];
+          ld<C::U>(q0, Qs + r * C::U);
+          ld<C::U>(g0, Gs + r * C::U);
+          ld<C::U>(q1, Qs + rr1 * C::U);
+          ld<C::U>(g1, Gs + rr1 * C::U);
 #pragma unroll
-        for (int u = 0; u < C::U; ++u) dq[u] = 0.f;
-        float msc[C::H], il[C::H], D[C::H];
+          for (int u = 0; u < C::U; ++u) { dq0[u] = 0.f; dq1[u] = 0.f; }
+          float4 s0[C::H], s1[C::H];
 #pragma unroll
-        for (int h = 0; h < C::H; ++h) {
-          const float4 sh = st4[i * C::H + h];
-          msc[h] = sh.x; il[h] = sh.y; D[h] = sh.z;
-        }
-        for (int w = 0; w < W32; ++w) {
-          const int jn = F - 32 * w < 32 ? F - 32 * w : 32;
-          uint32_t mw[C::H];
-#pragma unroll
-          for (int h = 0; h < C::H; ++h) mw[h] = a.drop ? mask[(h * F + i) * W32 + w] : ~0u;
-#pragma unroll 2
-          for (int jj = 0; jj < jn; ++jj) {
-            const int j = 32 * w + jj;
-            float k[C::U], v[C::U];
-            ld<C::U>(k, Ks + j * C::U);
-            ld<C::U>(v, Vs + j * C::U);
+          for (int h = 0; h < C::H; ++h) { s0[h] = st4[r * C::H + h]; s1[h] = st4[rr1 * C::H + h]; }
+          for (int w = 0; w < W32; ++w) {
+            const int jn = F - 32 * w < 32 ? F - 32 * w : 32;
+            uint32_t m0[C::H], m1[C::H];
 #pragma unroll
             for (int h = 0; h < C::H; ++h) {
-              const float pe = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), a.sc2, -msc[h])) * il[h];
-              float dP = hdot<C>(g, v, h);
-              if (a.drop) dP = ((mw[h] >> jj) & 1u) ? dP * a.inv_keep : 0.f;
-              const float dS = pe * (dP - D[h]);
+              m0[h] = a.drop ? mask[(h * F + r) * W32 + w] : ~0u;
+              m1[h] = a.drop ? mask[(h * F + rr1) * W32 + w] : ~0u;
+            }
+#pragma unroll 1
+            for (int jj = 0; jj < jn; ++jj) {
+              const int j = 32 * w + jj;
+              float k[C::U], v[C::U];
+              ld<C::U>(k, Ks + j * C::U);
+              ld<C::U>(v, Vs + j * C::U);
 #pragma unroll
-              for (int d = 0; d < C::DH; ++d) dq[h * C::DH + d] = fmaf(dS, k[h * C::DH + d], dq[h * C::DH + d]);
+              for (int h = 0; h < C::H; ++h) {
+                const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q0, k, h), a.sc2, -s0[h].x)) * s0[h].y;
+                const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q1, k, h), a.sc2, -s1[h].x)) * s1[h].y;
+                float dP0 = hdot<C>(g0, v, h), dP1 = hdot<C>(g1, v, h);
+                if (a.drop) {
+                  dP0 = ((m0[h] >> jj) & 1u) ? dP0 * a.inv_keep : 0.f;
+                  dP1 = ((m1[h] >> jj) & 1u) ? dP1 * a.inv_keep : 0.f;
+                }
+                haxpy<C>(dq0, pe0 * (dP0 - s0[h].z), k, h);
+                haxpy<C>(dq1, pe1 * (dP1 - s1[h].z), k, h);
+              }
             }
           }
-        }
 #pragma unroll
-        for (int u = 0; u < C::U; ++u) dq[u] = q[u] > 0.f ? dq[u] * a.inv_sdh : 0.f;
-        st<C::U>(Os + i * C::U, dq);
-      }
-      // ---- pass B (thread = key row, all heads): dK, dV ----
-      for (int j = t; j < F; j += NT) {
-        float k[C::U], v[C::U], dk[C::U], dv[C::U];
-        ld<C::U>(k, Ks + j * C::U);
-        ld<C::U>(v, Vs + j * C::U);
+          for (int u = 0; u < C::U; ++u) {
+            dq0[u] = q0[u] > 0.f ? dq0[u] * a.inv_sdh : 0.f;
+            dq1[u] = q1[u] > 0.f ? dq1[u] * a.inv_sdh : 0.f;
+          }
+          st<C::U>(Os + r * C::U, dq0);
+          if (has1) st<C::U>(Os + r1 * C::U, dq1);
+        } else if ((RS_ILL_SKIP & 1) == 0 && half == 1 && r < NH) {
+          float k0[C::U], v0[C::U], k1[C::U], v1[C::U];
+          float dk0[C::U], dv0[C::U], dk1[C::U], dv1[C::U];
+          ld<C::U>(k0, Ks + r * C::U);
+          ld<C::U>(v0, Vs + r * C::U);
+          ld<C::U>(k1, Ks + rr1 * C::U);
+          ld<C::U>(v1, Vs + rr1 * C::U);
 #pragma unroll
-        for (int u = 0; u < C::U; ++u) { dk[u] = 0.f; dv[u] = 0.f; }
-        const int jw = j >> 5, jbit = j & 31;
-#pragma unroll 2
-        for (int i = 0; i < F; ++i) {
-          float q[C::U], g[C::U];
-          ld<C::U>(q, Qs + i * C::U);
-          ld<C::U>(g, Gs + i * C::U);
+          for (int u = 0; u < C::U; ++u) { dk0[u] = 0.f; dv0[u] = 0.f; dk1[u] = 0.f; dv1[u] = 0.f; }
+          const int jw0 = r >> 5, jb0 = r & 31, jw1 = rr1 >> 5, jb1 = rr1 & 31;
+#pragma unroll 1
+          for (int i = 0; i < F; ++i) {
+            float q[C::U], g[C::U];
+            ld<C::U>(q, Qs + i * C::U);
+            ld<C::U>(g, Gs + i * C::U);
 #pragma unroll
-          for (int h = 0; h < C::H; ++h) {
-            const float4 sh = st4[i * C::H + h];
-            const float pe = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), a.sc2, -sh.x)) * sh.y;
-            float dP = hdot<C>(g, v, h), pd = pe;
-            if (a.drop) {
-              const bool keep = ((mask[(h * F + i) * W32 + jw] >> jbit) & 1u) != 0u;
-              dP = keep ? dP * a.inv_keep : 0.f;
-              pd = keep ? pe * a.inv_keep : 0.f;
-            }
-            const float dS = pe * (dP - sh.z);
-#pragma unroll
-            for (int d = 0; d < C::DH; ++d) {
-              dk[h * C::DH + d] = fmaf(dS, q[h * C::DH + d], dk[h * C::DH + d]);
-              dv[h * C::DH + d] = fmaf(pd, g[h * C::DH + d], dv[h * C::DH + d]);
+            for (int h = 0; h < C::H; ++h) {
+              const float4 sh = st4[i * C::H + h];
+              const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k0, h), a.sc2, -sh.x)) * sh.y;
+              const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k1, h), a.sc2, -sh.x)) * sh.y;
+              float dP0 = hdot<C>(g, v0, h), pd0 = pe0;
+              float dP1 = hdot<C>(g, v1, h), pd1 = pe1;
+              if (a.drop) {
+                const uint32_t* mr = mask + (h * F + i) * W32;
+                const bool keep0 = ((mr[jw0] >> jb0) & 1u) != 0u;
+                const bool keep1 = ((mr[jw1] >> jb1) & 1u) != 0u;
+                dP0 = keep0 ? dP0 * a.inv_keep : 0.f;
+                pd0 = keep0 ? pe0 * a.inv_keep : 0.f;
+                dP1 = keep1 ? dP1 * a.inv_keep : 0.f;
+                pd1 = keep1 ? pe1 * a.inv_keep : 0.f;
+              }
+              haxpy<C>(dk0, pe0 * (dP0 - sh.z), q, h);
+              haxpy<C>(dv0, pd0, g, h);
+              haxpy<C>(dk1, pe1 * (dP1 - sh.z), q, h);
+              haxpy<C>(dv1, pd1, g, h);
             }
           }
-        }
 #pragma unroll
-        for (int u = 0; u < C::U; ++u) {
-          dk[u] = k[u] > 0.f ? dk[u] * a.inv_sdh : 0.f;
-          dv[u] = v[u] > 0.f ? dv[u] : 0.f;
+          for (int u = 0; u < C::U; ++u) {
+            dk0[u] = k0[u] > 0.f ? dk0[u] * a.inv_sdh : 0.f;
+            dv0[u] = v0[u] > 0.f ? dv0[u] : 0.f;
+            dk1[u] = k1[u] > 0.f ? dk1[u] * a.inv_sdh : 0.f;
+            dv1[u] = v1[u] > 0.f ? dv1[u] : 0.f;
+          }
+          st<C::U>(DKs + r * C::U, dk0);
+          st<C::U>(DVs + r * C::U, dv0);
+          if (has1) {
+            st<C::U>(DKs + r1 * C::U, dk1);
+            st<C::U>(DVs + r1 * C::U, dv1);
+          }
         }
-        st<C::U>(DKs + j * C::U, dk);
-        st<C::U>(DVs + j * C::U, dv);
       }
       __syncthreads();
       // ---- projection backward: dZ = [dQ (Os) | dK | dV | dR (Rs)] ----
@@ -455,7 +502,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
 #pragma unroll
       for (int k = 0; k < C::WK; ++k) {
         const int idx = t + NT * k;
-        if (idx < C::E * C::NC) {
+        if ((RS_ILL_SKIP & 2) == 0 && idx < C::E * C::NC) {
           const int e = idx / C::NC, c = idx % C::NC;
           const float* dz = dzb(c);
           float s = 0.f;
@@ -469,7 +516,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         for (int f = 0; f < F; ++f) s += dz[f * C::U];
         dbc += s;
       }
-      for (int f = xrg; f < F; f += XRG) {
+      for (int f = xrg; f < F && (RS_ILL_SKIP & 2) == 0; f += XRG) {
         float s = 0.f;
 #pragma unroll
         for (int c = 0; c < C::NC; ++c) s = fmaf(dzb(c)[f * C::U], wrow[c], s);
