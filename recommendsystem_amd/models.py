@@ -256,8 +256,8 @@ class MultiHeadRanker(nn.Module):
         for layer in self.deep:
             deep = layer(deep)                                  # :61-63
         result = torch.cat([deep, auto], dim=1)                 # :71
-        gated_out = self.mix(result)                            # :77-120
-        return self.towers(torch.cat(gated_out, dim=1))         # :122-204 -> [B, 7]
+        gated_out = self.mix.forward_flat(result)               # :77-120, the 7 outputs side by side
+        return self.towers(gated_out)                           # :122-204 -> [B, 7]
 
     def loss(self, ids, offsets, labels):
         """rank/multi_head/model.py:18-22 per output, summed by Keras over the 7 outputs."""

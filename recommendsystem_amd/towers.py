@@ -204,12 +204,18 @@ class ExpertGateLayer(nn.Module):
         o = self.n_exp * self.D + t * self.n_sel
         return self.bias[o:o + self.n_sel]
 
-    def forward(self, x):
+    def forward_flat(self, x):
+        """All task outputs side by side, [B, n_task * D] (= torch.cat(forward(x), 1)): consumers
+        that concatenate the task outputs anyway take this and skip the per-slice backward
+        (7 zero-fills + copies + adds per step at config 3)."""
         if not self.built:
             self.build(tuple(x.shape), device=x.device)
         x = _rows(x)
         Z = _DenseFn.apply(x, self.kernel, self.bias, 0)
-        Y = _MixFn.apply(Z, self.sel, self.n_exp, self.D, self.n_task, self.n_sel, self.e_act)
+        return _MixFn.apply(Z, self.sel, self.n_exp, self.D, self.n_task, self.n_sel, self.e_act)
+
+    def forward(self, x):
+        Y = self.forward_flat(x)
         return [Y[:, t * self.D:(t + 1) * self.D] for t in range(self.n_task)]
 
 
