@@ -36,6 +36,59 @@ from .towers import (DNN, PLE, CrossNet, DeepCrossLayer, ExpertGateLayer, FFMBlo
 # ============================================================================================
 # small fused pieces
 # ============================================================================================
+class _SplitColsFn(torch.autograd.Function):
+    """Column blocks of y [B, sum sizes] (views); the backward is ONE concat of the
+    blocks' gradients (autograd's per-view backward would zero-fill a full-width gradient per block
+    and add them up: 2N elementwise launches per step instead of one)."""
+
+    @staticmethod
+    def forward(ctx, y, sizes):
+        ctx.sizes = sizes
+        return tuple(torch.split(y, sizes, dim=1))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        B = next(g.shape[0] for g in grads if g is not None)
+        ref = next(g for g in grads if g is not None)
+        parts = [g if g is not None else ref.new_zeros(B, n) for g, n in zip(grads, ctx.sizes)]
+        return torch.cat(parts, dim=1), None
+
+
+class _EmbFanoutFn(torch.autograd.Function):
+    """staytime trunk inputs read from the field embeddings emb [B, F, 32] (VideoDnn.py:45-47,
+    57-77): general = emb[:, :, 0:16], the bias-field gate input emb[:, bias, 16:32] flattened,
+    and the DIN queries general[:, q, :].  One backward builds d_emb once (autograd's per-view
+    backward zero-fills an emb-sized gradient per view and adds them)."""
+
+    @staticmethod
+    def forward(ctx, emb, bias_idx, qidx):
+        B, F, W = emb.shape
+        ctx.shape, ctx.qidx = (B, F, W), qidx
+        ctx.save_for_backward(bias_idx)
+        general = emb[:, :, 0:16]
+        gate = emb.index_select(1, bias_idx)[:, :, 16:32].reshape(B, -1)
+        return (general, gate, *[emb[:, q, 0:16] for q in qidx])
+
+    @staticmethod
+    def backward(ctx, dgen, dgate, *dqs):
+        (bias_idx,) = ctx.saved_tensors
+        B, F, W = ctx.shape
+        ref = next(g for g in (dgen, dgate, *dqs) if g is not None)
+        d = ref.new_zeros(B, F, W)
+        if dgen is not None:
+            d[:, :, 0:16] = dgen
+        for q, dq in zip(ctx.qidx, dqs):
+            if dq is not None:
+                d[:, q, 0:16] += dq
+        if dgate is not None:
+            d[:, :, 16:32].index_add_(1, bias_idx, dgate.reshape(B, -1, 16))
+        return d, None, None
+
+
+def split_cols(y, sizes):
+    return list(_SplitColsFn.apply(y, list(sizes)))
+
+
 class SharedInputDense(nn.Module):
     """Several Keras Dense(u_i, act) layers applied to the SAME input: one [K, sum u] kernel,
     one GEMM; ``forward`` returns the per-layer column views."""
@@ -76,11 +129,7 @@ class SharedInputDense(nn.Module):
         if not self.built:
             self.build(tuple(x.shape), device=x.device)
         y = _DenseFn.apply(_rows(x), self.kernel, self.bias, self.act)
-        out, o = [], 0
-        for u in self.units:
-            out.append(y[:, o:o + u])
-            o += u
-        return out
+        return split_cols(y, self.units)
 
 
 class _GroupedHeadFn(torch.autograd.Function):
@@ -461,10 +510,11 @@ class StaytimeMTL(nn.Module):
     def _trunk(self, emb, seqs, masks):
         cfg = self.cfg
         B, F, _ = emb.shape
-        general = emb[:, :, 0:16]                                                  # :47
-        gate_input = emb.index_select(1, self.bias_idx)[:, :, 16:32].reshape(B, -1)  # :45-46,127
-        din = [self.dins[s](general[:, q, :], seqs[s][:, :, 0:16], masks[s])       # :57-77
-               for s, q in enumerate(self.query_idx)]
+        # general = emb[:, :, 0:16] (:47); gate input = bias fields' [16:32] (:45-46,127); DIN
+        # queries = general of the query fields (:57-77)
+        general, gate_input, *queries = _EmbFanoutFn.apply(emb, self.bias_idx, list(self.query_idx))
+        din = [self.dins[s](queries[s], seqs[s][:, :, 0:16], masks[s])
+               for s in range(len(self.query_idx))]
         rew, cross_term, fm_logit = self.senet(general)                            # :81-115
         ffm, mult = self.ffm(emb.reshape(B, -1))       # fields read in place (field stride 32)
         concated = torch.cat([rew, cross_term, mult, ffm] + din, dim=1)            # :122-123
@@ -494,7 +544,7 @@ class StaytimeMTL(nn.Module):
         mm = _MixFn.apply(Z, self.sel, cfg.num_experts, cfg.hidden_units[-1], cfg.num_tasks,
                           cfg.num_experts, 0)                                       # :153-164
         Hh = cfg.hidden_units[-1]
-        mmoe = [mm[:, t * Hh:(t + 1) * Hh] for t in range(cfg.num_tasks)]
+        mmoe = split_cols(mm, [Hh] * cfg.num_tasks)
         cross = self.dcn(concated)                                                  # :167
         ext = torch.cat([mmoe[0], cross], dim=1)                                    # :168
         short = self.task_out[0](torch.cat([fm_logit, self.deep_logit[0](mmoe[1])], dim=1))  # :182-185
