@@ -241,16 +241,18 @@ struct GemmPlan { int bm, bn, splits; int64_t rchunk; };
 // Tile / split-K policy.  256 CUs take ~4 resident 256-thread GEMM blocks each, so a launch wants
 // ~1k blocks: 64-row tiles only when that still gives >= big_min tiles, and reductions split
 // (deterministic partials + column_reduce) while the tile count is below split_below, towards
-// split_target blocks with >= min_rows reduction rows per split.  RS_GEMM_TUNE="a,b,c,d"
+// split_target blocks with >= min_rows reduction rows per split; launches that cannot split
+// (forward, data gradient) take 32-column tiles below narrow_below tiles.  RS_GEMM_TUNE="a,b,c,d[,e]"
 // overrides (host-side, read once; tools/gemm_tune.sh).
-struct GemmTune { int big_min, split_below, split_target, min_rows; };
+struct GemmTune { int big_min, split_below, split_target, min_rows, narrow_below; };
 static const GemmTune& gemm_tune() {
   static const GemmTune t = [] {
-    GemmTune v{512, 512, 1024, 128};
+    GemmTune v{512, 512, 1024, 128, 512};
     if (const char* e = getenv("RS_GEMM_TUNE")) {
       GemmTune o = v;
-      if (sscanf(e, "%d,%d,%d,%d", &o.big_min, &o.split_below, &o.split_target, &o.min_rows) == 4 &&
-          o.split_target > 0 && o.min_rows >= GBK)
+      const int n = sscanf(e, "%d,%d,%d,%d,%d", &o.big_min, &o.split_below, &o.split_target,
+                           &o.min_rows, &o.narrow_below);
+      if (n >= 4 && o.split_target > 0 && o.min_rows >= GBK)
         v = o;
     }
     return v;
@@ -264,7 +266,11 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
   p.bn = N <= 32 ? 32 : 64;
   const int64_t tn = (N + p.bn - 1) / p.bn;
   p.bm = ((M + 63) / 64) * tn >= tu.big_min ? 64 : 32;
-  const int64_t tiles = ((M + p.bm - 1) / p.bm) * tn;
+  int64_t tiles = ((M + p.bm - 1) / p.bm) * tn;
+  if (!allow_split && p.bn == 64 && tiles < tu.narrow_below) {  // no split-K: narrower tiles
+    p.bn = 32;
+    tiles = ((M + p.bm - 1) / p.bm) * ((N + 31) / 32);
+  }
   p.splits = 1;
   if (allow_split && tiles < tu.split_below) {
     int64_t s = (tu.split_target + tiles - 1) / tiles;
