@@ -186,40 +186,53 @@ RS_API int rs_sparse_adagrad(void* stream, float* table, float* g2sum, float* gr
 constexpr int kScanBlock = 256;
 
 template <bool ADAM>
-__device__ __forceinline__ void scan_update4(float* __restrict__ table, float* __restrict__ m,
-                                             float* __restrict__ v,
-                                             float* __restrict__ grad_table, int64_t o, float lr,
-                                             float b1, float b2, float eps, float grad_scale) {
-  float4 g = *reinterpret_cast<const float4*>(grad_table + o);
-  float4 w = *reinterpret_cast<const float4*>(table + o);
-  float4 mm = *reinterpret_cast<const float4*>(m + o);
-  float4 vv = ADAM ? *reinterpret_cast<const float4*>(v + o) : mm;
-  float* gp = &g.x; float* wp = &w.x; float* mp = &mm.x; float* vp = &vv.x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float gk = gp[k] * grad_scale;
-    if (ADAM) {
-      mp[k] = b1 * mp[k] + (1.0f - b1) * gk;
-      vp[k] = b2 * vp[k] + (1.0f - b2) * gk * gk;
-      wp[k] -= lr * mp[k] / (eps + sqrtf(vp[k]));
-    } else {  // AdaGrad: m holds g2sum
-      mp[k] += gk * gk;
-      wp[k] -= lr * gk / sqrtf(mp[k]);
-    }
+struct ScanRow {
+  float4 g, w, mm, vv;
+  __device__ __forceinline__ void load(const float* __restrict__ table, const float* __restrict__ m,
+                                       const float* __restrict__ v,
+                                       const float* __restrict__ grad_table, int64_t o) {
+    g = *reinterpret_cast<const float4*>(grad_table + o);
+    w = *reinterpret_cast<const float4*>(table + o);
+    mm = *reinterpret_cast<const float4*>(m + o);
+    vv = ADAM ? *reinterpret_cast<const float4*>(v + o) : mm;
   }
-  *reinterpret_cast<float4*>(table + o) = w;
-  *reinterpret_cast<float4*>(m + o) = mm;
-  if (ADAM) *reinterpret_cast<float4*>(v + o) = vv;
-  *reinterpret_cast<float4*>(grad_table + o) = make_float4(0.f, 0.f, 0.f, 0.f);
-}
+  __device__ __forceinline__ void update_store(float* __restrict__ table, float* __restrict__ m,
+                                               float* __restrict__ v, float* __restrict__ grad_table,
+                                               int64_t o, float lr, float b1, float b2, float eps,
+                                               float grad_scale) {
+    float* gp = &g.x; float* wp = &w.x; float* mp = &mm.x; float* vp = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = gp[k] * grad_scale;
+      if (ADAM) {
+        mp[k] = b1 * mp[k] + (1.0f - b1) * gk;
+        vp[k] = b2 * vp[k] + (1.0f - b2) * gk * gk;
+        wp[k] -= lr * mp[k] / (eps + sqrtf(vp[k]));
+      } else {  // AdaGrad: m holds g2sum
+        mp[k] += gk * gk;
+        wp[k] -= lr * gk / sqrtf(mp[k]);
+      }
+    }
+    *reinterpret_cast<float4*>(table + o) = w;
+    *reinterpret_cast<float4*>(m + o) = mm;
+    if (ADAM) *reinterpret_cast<float4*>(v + o) = vv;
+    *reinterpret_cast<float4*>(grad_table + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+};
 
+// Flag sweep: every wave walks its 64-row chunks (flags prefetched one chunk ahead), appends the
+// marked rows to a per-wave LDS list (clearing their flags) and updates the collected rows only
+// when the list is full or its chunks are done -- at ~1 % touched rows a chunk holds about one
+// marked row, so batching turns one dependent HBM round trip per chunk into one per list.  The
+// list is processed two passes at a time (both passes' loads issued before either's stores).
 template <bool ADAM>
 __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
     float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
     float lr, float b1, float b2, float eps, float grad_scale) {
-  __shared__ int32_t lists[kScanBlock];  // 64 row slots per wave
-  int32_t* list = lists + (threadIdx.x & ~63);
+  constexpr int LCAP = 256;  // rows per wave list
+  __shared__ uint32_t lists[(kScanBlock / 64) * LCAP];
+  uint32_t* list = lists + (threadIdx.x >> 6) * LCAP;
   const int lane = threadIdx.x & 63;
   const int64_t nchunks = (nrows + 63) / 64;
   const int64_t nwaves = (int64_t)gridDim.x * (kScanBlock / 64);
@@ -228,6 +241,27 @@ __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
   const int lpr = nv < 64 ? nv : 64;   // lanes per row
   const int rpp = 64 / lpr;            // rows per pass
   const int sub = lane % lpr, slot = lane / lpr;
+  int n = 0;                           // wave-uniform list length
+  auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int p0 = 0; p0 < n; p0 += 2 * rpp) {
+      const int k0 = p0 + slot, k1 = p0 + rpp + slot;
+      const bool on0 = slot < rpp && k0 < n, on1 = slot < rpp && k1 < n;
+      const int64_t r0 = on0 ? (int64_t)list[k0] : 0, r1 = on1 ? (int64_t)list[k1] : 0;
+      for (int e4 = sub; e4 < nv; e4 += lpr) {
+        ScanRow<ADAM> x0, x1;
+        const int64_t o0 = r0 * dim + 4 * e4, o1 = r1 * dim + 4 * e4;
+        if (on0) x0.load(table, m, v, grad_table, o0);
+        if (on1) x1.load(table, m, v, grad_table, o1);
+        if (on0) x0.update_store(table, m, v, grad_table, o0, lr, b1, b2, eps, grad_scale);
+        if (on1) x1.update_store(table, m, v, grad_table, o1, lr, b1, b2, eps, grad_scale);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // list reuse
+    n = 0;
+  };
   int64_t c = gw;
   int32_t fl = -1;
   if (c < nchunks && c * 64 + lane < nrows) fl = flag[c * 64 + lane];
@@ -240,30 +274,20 @@ __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
     const bool hit = fl != -1;
     const uint64_t mask = __ballot(hit);
     if (mask) {
+      const int cnt = __popcll(mask);
+      if (n + cnt > LCAP) flush();
       const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
       if (hit) {
-        list[rank] = lane;
+        list[n + rank] = (uint32_t)(row0 + lane);
         flag[row0 + lane] = -1;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int n = __popcll(mask);
-      for (int p0 = 0; p0 < n; p0 += rpp) {
-        const int k = p0 + slot;
-        if (slot < rpp && k < n) {
-          const int64_t row = row0 + list[k];
-          for (int e4 = sub; e4 < nv; e4 += lpr)
-            scan_update4<ADAM>(table, m, v, grad_table, row * dim + 4 * e4, lr, b1, b2, eps,
-                               grad_scale);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // list reuse by the next chunk
+      n += cnt;
     }
     fl = fn;
     c = cn;
   }
+  if (n) flush();
 }
 
 static int64_t scan_grid(int64_t nrows) {
@@ -284,7 +308,8 @@ static void launch_scan_opt(hipStream_t s, unsigned grid, float* table, float* m
 RS_API int rs_sparse_adam_scan(void* stream, float* table, float* m, float* v, float* grad_table,
                                int32_t* flag, int64_t table_rows, int dim, float lr, float beta1,
                                float beta2, float eps, float grad_scale) {
-  if (!table || !m || !v || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0)
+  if (!table || !m || !v || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0 ||
+      table_rows > (int64_t)UINT32_MAX)
     return RS_ERR_ARG;
   if (table_rows == 0) return RS_OK;
   launch_scan_opt<true>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, m, v,
@@ -295,7 +320,8 @@ RS_API int rs_sparse_adam_scan(void* stream, float* table, float* m, float* v, f
 RS_API int rs_sparse_adagrad_scan(void* stream, float* table, float* g2sum, float* grad_table,
                                   int32_t* flag, int64_t table_rows, int dim, float lr,
                                   float grad_scale) {
-  if (!table || !g2sum || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0)
+  if (!table || !g2sum || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0 ||
+      table_rows > (int64_t)UINT32_MAX)
     return RS_ERR_ARG;
   if (table_rows == 0) return RS_OK;
   launch_scan_opt<false>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, g2sum,
