@@ -66,7 +66,8 @@ struct LBwd {
 };
 
 // Attention save of one (iteration, sample): O [F][U] (attention output before the epilogue) |
-// row stats [F][H] x {scaled max, 1 / sum} | dropout keep bits [H][F][ceil(F/32)] (uint32).
+// row stats [F][H] x {scaled max, 1 / sum} | dropout keep bits [F][ceil(F/32)][H] (uint32: query
+// row, key word, head -- both heads' words adjacent for one 8-byte LDS read).
 // Written by the forward, it lets the backward skip the max pass, the O pass and the per-pair
 // mask hashing.
 __host__ __device__ inline int64_t save_stride(int F, int U, int H) {
@@ -179,8 +180,8 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
       if (drop) {
 #pragma unroll
         for (int h = 0; h < C::H; ++h) {
-          if (mask) mask[(h * F + i) * W32 + w] = bits[h];
-          if (sv) reinterpret_cast<uint32_t*>(sv + F * C::U + 2 * C::H * F)[(h * F + i) * W32 + w] = bits[h];
+          if (mask) mask[(i * W32 + w) * C::H + h] = bits[h];
+          if (sv) reinterpret_cast<uint32_t*>(sv + F * C::U + 2 * C::H * F)[(i * W32 + w) * C::H + h] = bits[h];
         }
       }
     }
@@ -279,7 +280,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
   float* DKs = Gs + F * C::U;
   float* DVs = DKs + F * C::U;
   float4* st4 = reinterpret_cast<float4*>(DVs + F * C::U);   // [F][H] {scaled max, 1/sum, D, -}
-  uint32_t* mask = reinterpret_cast<uint32_t*>(st4 + F * C::H);  // [H][F][W32]
+  uint32_t* mask = reinterpret_cast<uint32_t*>(st4 + F * C::H);  // [F][W32][H]
   const int t = threadIdx.x;
   float wcol[C::E];
   {
@@ -411,8 +412,8 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
             uint32_t m0[C::H], m1[C::H];
 #pragma unroll
             for (int h = 0; h < C::H; ++h) {
-              m0[h] = a.drop ? mask[(h * F + r) * W32 + w] : ~0u;
-              m1[h] = a.drop ? mask[(h * F + rr1) * W32 + w] : ~0u;
+              m0[h] = a.drop ? mask[(r * W32 + w) * C::H + h] : ~0u;
+              m1[h] = a.drop ? mask[(rr1 * W32 + w) * C::H + h] : ~0u;
             }
 #pragma unroll 1
             for (int jj = 0; jj < jn; ++jj) {
@@ -464,9 +465,9 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
               float dP0 = hdot<C>(g, v0, h), pd0 = pe0;
               float dP1 = hdot<C>(g, v1, h), pd1 = pe1;
               if (a.drop) {
-                const uint32_t* mr = mask + (h * F + i) * W32;
-                const bool keep0 = ((mr[jw0] >> jb0) & 1u) != 0u;
-                const bool keep1 = ((mr[jw1] >> jb1) & 1u) != 0u;
+                const uint32_t* mr = mask + i * W32 * C::H + h;  // [i][w][h]: both heads' words adjacent
+                const bool keep0 = ((mr[jw0 * C::H] >> jb0) & 1u) != 0u;
+                const bool keep1 = ((mr[jw1 * C::H] >> jb1) & 1u) != 0u;
                 dP0 = keep0 ? dP0 * a.inv_keep : 0.f;
                 pd0 = keep0 ? pe0 * a.inv_keep : 0.f;
                 dP1 = keep1 ? dP1 * a.inv_keep : 0.f;
