@@ -131,6 +131,17 @@ int rs_sparse_adagrad_scan(void* stream, float* table, float* g2sum, float* grad
                            int32_t* flag, int64_t table_rows, int dim, float lr,
                            float grad_scale);
 
+/* Overflow recovery for the list-mode optimizers: launch right after rs_sparse_adam /
+ * rs_sparse_adagrad on the same stream (same n_touched).  Exits at once unless a push claimed more
+ * rows than the touched list holds (the sticky overflow word n_touched[288] is set); then sweeps
+ * the table like the scan-mode optimizer and updates the claimed rows the list could not hold. */
+int rs_sparse_adam_recover(void* stream, float* table, float* m, float* v, float* grad_table,
+                           int32_t* flag, const int32_t* n_touched, int64_t table_rows, int dim,
+                           float lr, float beta1, float beta2, float eps, float grad_scale);
+int rs_sparse_adagrad_recover(void* stream, float* table, float* g2sum, float* grad_table,
+                              int32_t* flag, const int32_t* n_touched, int64_t table_rows, int dim,
+                              float lr, float grad_scale);
+
 /* Scan-mode compaction for the DP exchange: move every marked row into (rows_out, grads_out)
  * (gradient row zeroed, flag cleared), *n_out = count (slots past cap are dropped),
  * rows_out[count .. cap) = -1. */
@@ -493,7 +504,8 @@ int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t work
  * + j] = src[b*src_ld + cols[j]] for a column plan (feature_config.SlotLayout.column_plan). */
 int rs_gather_columns(void* stream, const float* src, int64_t src_ld, int64_t B,
                       const int32_t* cols, int ncols, float* out, int64_t out_ld);
-/* its backward: dsrc[b*src_ld + cols[j]] += dout[b*out_ld + j] (cols unique within a plan). */
+/* its backward: dsrc[b*src_ld + cols[j]] += dout[b*out_ld + j] (atomic adds: a column named
+ * twice in a plan receives both gradients). */
 int rs_scatter_add_columns(void* stream, const float* dout, int64_t out_ld, int64_t B,
                            const int32_t* cols, int ncols, float* dsrc, int64_t src_ld);
 /* SENet squeeze tf.reduce_mean(emb, axis=1, keepdims=True) per structure field

@@ -129,6 +129,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_adam_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
                                    _f32, _f32]),
     "rs_sparse_adagrad_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),
+    "rs_sparse_adam_recover": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32,
+                                      _f32, _f32, _f32]),
+    "rs_sparse_adagrad_recover": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),
     "rs_sparse_compact_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i32]),
     "rs_sparse_pack_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32]),
     "rs_sparse_merge_packed": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i64, _i32]),

@@ -58,8 +58,9 @@ __global__ void __launch_bounds__(kBlk) scatter_add_cols_kernel(const float* __r
   for (int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlk) {
     const int64_t b = i / ncols;
     const int j = (int)(i - b * ncols);
-    float* d = dsrc + b * src_ld + cols[j];
-    *d += dout[b * out_ld + j];  // columns are unique within one plan: no two threads collide
+    // a plan may name a column twice (the same interval sliced twice): the gradients add up, so
+    // the update is an atomic (no-return global f32 add; as cheap as a plain RMW when unique)
+    atomicAdd(dsrc + b * src_ld + cols[j], dout[b * out_ld + j]);
   }
 }
 

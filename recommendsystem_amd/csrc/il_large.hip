@@ -69,9 +69,11 @@ struct LBwd {
 // row stats [F][H] x {scaled max, 1 / sum} | dropout keep bits [F][ceil(F/32)][H] (uint32: query
 // row, key word, head -- both heads' words adjacent for one 8-byte LDS read).
 // Written by the forward, it lets the backward skip the max pass, the O pass and the per-pair
-// mask hashing.
+// mask hashing.  The stride is padded to 4 floats so every sample's save starts 16-B aligned
+// (float4 accesses of O).
 __host__ __device__ inline int64_t save_stride(int F, int U, int H) {
-  return (int64_t)F * U + 2 * (int64_t)H * F + (int64_t)H * F * ((F + 31) / 32);
+  const int64_t n = (int64_t)F * U + 2 * (int64_t)H * F + (int64_t)H * F * ((F + 31) / 32);
+  return (n + 3) & ~(int64_t)3;
 }
 
 template <int N>

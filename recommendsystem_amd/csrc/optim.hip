@@ -229,7 +229,8 @@ template <bool ADAM>
 __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
     float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
-    float lr, float b1, float b2, float eps, float grad_scale) {
+    float lr, float b1, float b2, float eps, float grad_scale, const int32_t* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // overflow-recovery sweep with nothing to recover
   constexpr int LCAP = 256;  // rows per wave list
   __shared__ uint32_t lists[(kScanBlock / 64) * LCAP];
   uint32_t* list = lists + (threadIdx.x >> 6) * LCAP;
@@ -300,9 +301,9 @@ static int64_t scan_grid(int64_t nrows) {
 template <bool ADAM>
 static void launch_scan_opt(hipStream_t s, unsigned grid, float* table, float* m, float* v,
                             float* grad, int32_t* flag, int64_t nrows, int dim, float lr, float b1,
-                            float b2, float eps, float gs) {
+                            float b2, float eps, float gs, const int32_t* gate = nullptr) {
   sparse_scan_opt_kernel<ADAM><<<grid, kScanBlock, 0, s>>>(table, m, v, grad, flag, nrows, dim, lr,
-                                                           b1, b2, eps, gs);
+                                                           b1, b2, eps, gs, gate);
 }
 
 RS_API int rs_sparse_adam_scan(void* stream, float* table, float* m, float* v, float* grad_table,
@@ -327,6 +328,41 @@ RS_API int rs_sparse_adagrad_scan(void* stream, float* table, float* g2sum, floa
   launch_scan_opt<false>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, g2sum,
                          nullptr, grad_table, flag, table_rows, dim, lr, 0.f, 0.f, 0.f,
                          grad_scale);
+  return rs_status_after_launch();
+}
+
+// Overflow recovery of the list-mode optimizers (rs_sparse_adam / rs_sparse_adagrad).  A push that
+// claimed more rows than the touched list holds leaves the unlisted rows claimed (flag -2) with
+// their gradient in grad_table; the list-mode launch then records the overflow in the sticky word
+// n_touched[RS_TOUCHED_OVERFLOW].  Launched right after the list-mode optimizer on the same
+// stream, this sweep reads that word and exits at once when it is zero; otherwise it is the scan
+// optimizer over the whole table, which updates exactly the rows still marked (listed rows were
+// released to -1 by the list launch).  The word stays set until SparseTable.check_overflow
+// clears it, so every later step is swept too: overflow costs speed, never updates.
+RS_API int rs_sparse_adam_recover(void* stream, float* table, float* m, float* v, float* grad_table,
+                                  int32_t* flag, const int32_t* n_touched, int64_t table_rows,
+                                  int dim, float lr, float beta1, float beta2, float eps,
+                                  float grad_scale) {
+  if (!table || !m || !v || !grad_table || !flag || !n_touched || dim <= 0 || dim % 4 ||
+      table_rows < 0 || table_rows > (int64_t)UINT32_MAX)
+    return RS_ERR_ARG;
+  if (table_rows == 0) return RS_OK;
+  launch_scan_opt<true>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, m, v,
+                        grad_table, flag, table_rows, dim, lr, beta1, beta2, eps, grad_scale,
+                        n_touched + RS_TOUCHED_OVERFLOW);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_adagrad_recover(void* stream, float* table, float* g2sum, float* grad_table,
+                                     int32_t* flag, const int32_t* n_touched, int64_t table_rows,
+                                     int dim, float lr, float grad_scale) {
+  if (!table || !g2sum || !grad_table || !flag || !n_touched || dim <= 0 || dim % 4 ||
+      table_rows < 0 || table_rows > (int64_t)UINT32_MAX)
+    return RS_ERR_ARG;
+  if (table_rows == 0) return RS_OK;
+  launch_scan_opt<false>(rs_stream(stream), (unsigned)scan_grid(table_rows), table, g2sum,
+                         nullptr, grad_table, flag, table_rows, dim, lr, 0.f, 0.f, 0.f,
+                         grad_scale, n_touched + RS_TOUCHED_OVERFLOW);
   return rs_status_after_launch();
 }
 

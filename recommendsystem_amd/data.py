@@ -206,30 +206,38 @@ def shard_files(files: Sequence[str], shard_num: int, shard_id: int) -> list[str
 
 def interleave(files: Sequence[str], cycle_length: int = 4, block_length: int = 8,
                verify_crc: bool = True) -> Iterator[bytes]:
+    """``Dataset.from_tensor_slices(files).interleave(TFRecordDataset, cycle_length,
+    block_length)`` in its deterministic order (staytime/parse.py:80-84; the parallel form with
+    ``deterministic`` order yields the sequential order).  tf.data's interleave keeps
+    ``cycle_length`` slots and a cursor: an open slot yields up to ``block_length`` records and
+    the cursor moves on; a slot whose file runs out is emptied and the cursor moves on at once; an
+    empty slot the cursor reaches takes the next pending file (while any remain) and reads from
+    it, otherwise it is skipped."""
+    if cycle_length < 1 or block_length < 1:
+        raise ValueError("cycle_length and block_length must be >= 1")
     pending = list(files)
-    slots: list = []
-    while pending and len(slots) < cycle_length:
-        slots.append(tfrecord_iter(pending.pop(0), verify_crc))
-    k = 0
-    while slots:
+    slots: list = [None] * cycle_length
+    n_open, k, blk = 0, 0, 0
+    while pending or n_open:
         it = slots[k]
-        exhausted = False
-        for _ in range(block_length):
-            try:
-                yield next(it)
-            except StopIteration:
-                exhausted = True
-                break
-        if exhausted:
+        if it is None:
             if pending:
                 slots[k] = tfrecord_iter(pending.pop(0), verify_crc)
-                continue  # the replacement file is read from this slot at once (tf.data order)
-            slots.pop(k)
-            if not slots:
-                return
-            k %= len(slots)
+                n_open += 1
+            else:
+                k, blk = (k + 1) % cycle_length, 0
             continue
-        k = (k + 1) % len(slots)
+        try:
+            rec = next(it)
+        except StopIteration:
+            slots[k] = None
+            n_open -= 1
+            k, blk = (k + 1) % cycle_length, 0
+            continue
+        yield rec
+        blk += 1
+        if blk == block_length:
+            k, blk = (k + 1) % cycle_length, 0
 
 
 def batch(records: Iterator[bytes], batch_size: int) -> Iterator[list[bytes]]:

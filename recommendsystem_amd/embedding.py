@@ -98,11 +98,26 @@ class SparseTable:
     def initial_weight(rows, dim, optimizer, init_scale=0.05, seed=0) -> torch.Tensor:
         """The table's initial values on the host: U(-s, s) from a seeded generator (AdaGrad:
         tn.core.AdaGrad's initial_scale)."""
+        return SparseTable.initial_shard(rows, dim, optimizer, init_scale, seed, 0, 1)
+
+    @staticmethod
+    def initial_shard(rows, dim, optimizer, init_scale=0.05, seed=0, rank=0, world=1,
+                      chunk_rows=1 << 16) -> torch.Tensor:
+        """Rows rank, rank + world, ... of ``initial_weight(rows, ...)``, drawn in row chunks from
+        the same seeded stream (a chunked draw continues the generator exactly where one draw of
+        the whole table would be), so a rank holds only its shard plus one chunk on the host."""
         gen = torch.Generator().manual_seed(seed)
-        w = (torch.rand(rows, dim, generator=gen) * 2.0 - 1.0) * init_scale
+        scale = init_scale
         if isinstance(optimizer, SparseAdaGrad):
-            w = w * (optimizer.initial_scale / max(init_scale, 1e-30))
-        return w
+            scale = optimizer.initial_scale / max(init_scale, 1e-30)
+        parts = []
+        for r0 in range(0, rows, chunk_rows):
+            n = min(chunk_rows, rows - r0)
+            w = (torch.rand(n, dim, generator=gen) * 2.0 - 1.0) * init_scale
+            if isinstance(optimizer, SparseAdaGrad):
+                w = w * scale
+            parts.append(w[(rank - r0) % world::world].clone() if world > 1 else w)
+        return torch.cat(parts) if parts else torch.empty(0, dim)
 
     # ---- push / update -----------------------------------------------------------------
     def accumulate(self, rows: torch.Tensor, offsets: torch.Tensor | None, B: int, F: int,
@@ -134,8 +149,9 @@ class SparseTable:
     def check_overflow(self) -> None:
         """Raise if any step since the last check claimed more rows than the touched list holds
         (list mode; csrc/optim.hip records the largest such count in the sticky word
-        n_touched[288] and updates only the first touched_cap rows).  Reads the device: call it
-        outside the timed / captured region."""
+        n_touched[288]; the rows past touched_cap are still updated, by the recovery sweep of
+        ``step``, which runs every step until this check clears the word).  Reads the device:
+        call it outside the timed / captured region."""
         n = int(self.n_touched[288].item())
         if n:
             self.n_touched[288].zero_()
@@ -155,14 +171,25 @@ class SparseTable:
                 call("rs_sparse_adagrad_scan", s, ptr(self.weight), ptr(self.g2sum), ptr(self.grad),
                      ptr(self.flag), self.rows, self.dim, o.learning_rate, grad_scale)
             return
+        # a touched list smaller than the table can overflow: the gated sweep after the list
+        # launch updates the claimed rows it could not hold (exits at once otherwise)
+        recover = self.touched_cap < self.rows
         if isinstance(o, SparseAdam):
             call("rs_sparse_adam", s, ptr(self.weight), ptr(self.m), ptr(self.v), ptr(self.grad),
                  ptr(self.flag), ptr(self.touched), ptr(self.n_touched), self.dim,
                  self.touched_cap, o.learning_rate, o.beta1, o.beta2, o.epsilon, grad_scale)
+            if recover:
+                call("rs_sparse_adam_recover", s, ptr(self.weight), ptr(self.m), ptr(self.v),
+                     ptr(self.grad), ptr(self.flag), ptr(self.n_touched), self.rows, self.dim,
+                     o.learning_rate, o.beta1, o.beta2, o.epsilon, grad_scale)
         else:
             call("rs_sparse_adagrad", s, ptr(self.weight), ptr(self.g2sum), ptr(self.grad),
                  ptr(self.flag), ptr(self.touched), ptr(self.n_touched), self.dim,
                  self.touched_cap, o.learning_rate, grad_scale)
+            if recover:
+                call("rs_sparse_adagrad_recover", s, ptr(self.weight), ptr(self.g2sum),
+                     ptr(self.grad), ptr(self.flag), ptr(self.n_touched), self.rows, self.dim,
+                     o.learning_rate, grad_scale)
 
 
 class ShardedSparseTable:
@@ -191,9 +218,8 @@ class ShardedSparseTable:
         if self.rows > 2**31 - 1:
             raise ValueError("row indices are int32")
         optimizer = optimizer or SparseAdam()
-        full = SparseTable.initial_weight(self.rows, self.dim, optimizer, init_scale, seed)
-        shard = full[self.rank::self.world].clone()
-        del full
+        shard = SparseTable.initial_shard(self.rows, self.dim, optimizer, init_scale, seed,
+                                          self.rank, self.world)
         self.local = SparseTable(shard.shape[0], dim, optimizer, device=device, initial=shard,
                                  max_touched=max_touched)
         self._route_ws = None

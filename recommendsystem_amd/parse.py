@@ -1,8 +1,9 @@
 """staytime input parsing: ``parse_input_func`` of ``staytime/parse.py:16-71`` on an
 already-decoded batch, with the label construction on the GPU (``rs_staytime_labels``).
 
-The reference parses serialized ``tf.Example`` protos; TFRecord decoding is outside this path
-(DESIGN.md §9), so a batch arrives as a dict of decoded columns:
+The reference parses serialized ``tf.Example`` protos; here the TFRecord framing and the
+``tf.train.Example`` decode happen in ``data.py`` (``dataset_reader`` / ``decode_batch``), so a batch
+arrives at this function as a dict of decoded columns:
 
     {"extra_info": [str] * B (default "label", parse.py:18),
      "video_duration": int64 [B], "watch_duration": int64 [B],

@@ -46,7 +46,8 @@ def relu(x):
 # autograd wrappers of the front-end kernels
 # ============================================================================================
 class _GatherColsFn(torch.autograd.Function):
-    """out[b, j] = src[b, cols[j]] (rs_gather_columns); backward scatter-adds (cols unique)."""
+    """out[b, j] = src[b, cols[j]] (rs_gather_columns); backward scatter-adds (atomic: a column
+    named twice in a plan receives both gradients, as TF's slice + concat gradient does)."""
 
     @staticmethod
     def forward(ctx, src, cols):

@@ -52,6 +52,7 @@ class Trainer:
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.regs = list(model.regularizers()) if hasattr(model, "regularizers") else []
         self.xbuf = {}
+        self.on_dense_grad = None  # test hook: called with the exchanged flat dense gradient
         self._il_layers = [mod for mod in model.modules() if isinstance(mod, InteractingLayer)] \
             if hasattr(model, "modules") else []
         if self.world > 1:
@@ -83,6 +84,8 @@ class Trainer:
                 if not is_sharded(t):
                     exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])
         scale = 1.0 / self.world
+        if self.on_dense_grad is not None:
+            self.on_dense_grad(self.arena.grad, scale)
         call("rs_dense_adam", s, ptr(self.arena.data), ptr(self.arena.grad), ptr(self.m), ptr(self.v),
              self.arena.n, ptr(self.step_count), self.lr, self.b1, self.b2, self.eps, scale, 1)
         for t in self.tables:

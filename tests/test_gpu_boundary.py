@@ -67,7 +67,11 @@ def test_il_fwd_gather_rows_outside_table():
     assert torch.isfinite(y).all()
 
 
-def test_touched_list_overflow_is_reported():
+def test_touched_list_overflow_is_reported_and_recovered():
+    """A push claiming more rows than the touched list holds: every claimed row is still updated
+    (exactly once per step: the list launch takes the first cap rows, the gated recovery sweep
+    the rest), flags and gradient rows are released, the overflow is reported, and a later
+    step without overflow updates its rows normally."""
     from recommendsystem_amd.embedding import SparseAdam, SparseTable
     t = SparseTable(1000, 8, SparseAdam(1e-2), device=DEV, seed=1, max_touched=4)
     B, F = 10, 1
@@ -78,7 +82,20 @@ def test_touched_list_overflow_is_reported():
     t.step()
     torch.cuda.synchronize()
     changed = (t.weight != w0).any(dim=1).nonzero().reshape(-1).cpu().tolist()
-    assert len(changed) == 4 and set(changed) <= set(rows.cpu().tolist())
+    assert sorted(changed) == rows.cpu().tolist()
+    # first sparse Adam step without bias correction: w -= lr * m / (eps + sqrt(v)), m = .1 g,
+    # v = .001 g^2 -> lr * .1 / sqrt(.001) for g = 1
+    step = float((w0 - t.weight)[rows.long()].mean())
+    assert abs(step - 1e-2 * 0.1 / (1e-8 + 0.001 ** 0.5)) < 1e-6
+    assert bool((t.flag == -1).all()) and bool((t.grad == 0).all())
+    assert int(t.n_touched[0]) == 0
     with pytest.raises(RuntimeError, match="overflow"):
         t.check_overflow()
     t.check_overflow()  # the sticky word was cleared by the report
+    w1 = t.weight.clone()
+    t.accumulate(rows[:3], None, 3, F, dout[:3], 8, 8, 0)
+    t.step()
+    torch.cuda.synchronize()
+    changed = (t.weight != w1).any(dim=1).nonzero().reshape(-1).cpu().tolist()
+    assert sorted(changed) == rows[:3].cpu().tolist()
+    t.check_overflow()

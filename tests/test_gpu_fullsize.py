@@ -23,7 +23,7 @@ import torch
 
 from oracle import ctr_oracle as npo
 from oracle import torch_ref as tr
-from _tol import assert_close, assert_grad_close, to_np
+from _tol import adam_close as _adam_close, assert_close, assert_grad_close, to_np
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -31,28 +31,6 @@ DEV = "cuda"
 
 def _zipf(rng, shape, vocab, a=1.2):
     return np.minimum(rng.zipf(a, size=shape) - 1, vocab - 1).astype(np.int64)
-
-
-def _adam_close(got, want, grad, what, atol=2e-6, rtol=1e-4, tiny=1e-6, max_frac=1e-3,
-                grad_abs=None, cancel=1e-2, prev_ill=None):
-    """Adam-updated parameters.  An entry is ill-conditioned when its gradient is ~0
-    (|g| <= tiny * max|g|) or, given grad_abs = the sum of the |contributions| that make up g,
-    when those contributions cancel to less than `cancel` of their magnitude (the fp32 sum then
-    carries a relative error far above fp32 epsilon, and Adam's update m/(sqrt(v)+eps) passes
-    it on at full scale).  Ill-conditioned entries may differ, but must be rare; all others
-    must match.  prev_ill: entries ill-conditioned at an earlier step (their Adam moments carry
-    the difference forward).  Returns this step's ill-conditioned mask (including prev_ill)."""
-    got, want, grad = (np.asarray(a, dtype=np.float64).reshape(-1) for a in (got, want, grad))
-    ill = np.abs(grad) <= tiny * max(float(np.abs(grad).max(initial=0.0)), 1e-30)
-    if grad_abs is not None:
-        ill |= np.abs(grad) < cancel * np.asarray(grad_abs, dtype=np.float64).reshape(-1)
-    if prev_ill is not None:
-        ill |= prev_ill
-    bad = np.abs(got - want) > atol + rtol * np.abs(want)
-    assert not np.any(bad & ~ill), (f"{what}: {int(np.sum(bad & ~ill))} mismatches, max|err| "
-                                    f"{np.abs(got - want)[~ill].max():.3e}")
-    assert np.sum(bad) <= max(2, max_frac * got.size), f"{what}: {int(np.sum(bad))} ill-conditioned"
-    return ill
 
 
 def test_bench_step_matches_oracle_full_size():

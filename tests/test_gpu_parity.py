@@ -401,7 +401,8 @@ def test_interacting_many_fields_dropout(F, L):
 
 
 @pytest.mark.parametrize("F,E,U,H,L,drop", [(200, 8, 8, 2, 1, 0.2), (200, 8, 8, 2, 1, 0.0),
-                                             (97, 8, 8, 1, 1, 0.2), (80, 16, 16, 2, 2, 0.1)])
+                                             (97, 8, 8, 1, 1, 0.2), (65, 8, 8, 2, 2, 0.2),
+                                             (80, 16, 16, 2, 2, 0.1)])
 def test_interacting_saved_pair_equals_recompute(F, E, U, H, L, drop):
     """rs_il_fwd_saved / rs_il_bwd_saved (F > 64: the backward reads the forward's attention
     output, softmax stats and keep bits) give bit-identical y, dx and parameter gradients to the
@@ -419,7 +420,8 @@ def test_interacting_saved_pair_equals_recompute(F, E, U, H, L, drop):
     dy = torch.randn(B, F * U, device=DEV, generator=g)
     s = stream_handle()
     n_save = int(lib.rs_il_attn_save_floats(B, F, U, H, L))
-    assert n_save == L * B * (F * U + 2 * H * F + H * F * ((F + 31) // 32))
+    stride = F * U + 2 * H * F + H * F * ((F + 31) // 32)
+    assert n_save == L * B * (stride + (-stride) % 4)  # 16-B aligned per-sample saves
     asave = torch.empty(n_save, device=DEV)
     ws_n = int(lib.rs_il_bwd_workspace_floats(B, E, U))
     npar = E * 4 * U + 4 * U + 2 * U

@@ -52,6 +52,15 @@ def test_front_end_kernels():
     want = torch.ones(B, S, device=DEV)
     want[:, cols.long()] += src[:, cols.long()]
     assert torch.equal(dsrc, want)
+    # a plan naming columns twice: both gradients arrive
+    dup = torch.tensor([3, 3, 11, 3, 11], dtype=torch.int32, device=DEV)
+    g = torch.from_numpy(rng.normal(size=(B, 5)).astype(np.float32)).to(DEV)
+    dsrc = torch.zeros(B, S, device=DEV)
+    call("rs_scatter_add_columns", stream_handle(), ptr(g), 5, B, ptr(dup), 5, ptr(dsrc), S)
+    g64 = g.double()
+    torch.testing.assert_close(dsrc[:, 3].double(), g64[:, 0] + g64[:, 1] + g64[:, 3], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(dsrc[:, 11].double(), g64[:, 2] + g64[:, 4], rtol=1e-6, atol=1e-6)
+    assert int((dsrc != 0).sum()) == 2 * B
     # segments incl. an empty one
     seg = torch.tensor([0, 3, 3, 10, 50], dtype=torch.int32, device=DEV)
     m = torch.empty(B, 4, device=DEV)

@@ -181,3 +181,15 @@ def test_sharded_table_protocol_world2():
         np.add.at(gsum, srows.reshape(-1)[ok], o["ds"].reshape(-1, DIM)[ok])
     for r in range(WORLD):  # owner r holds rows r, r + 2, ...
         np.testing.assert_allclose(out[r]["grad"], gsum[r::WORLD], rtol=1e-5, atol=1e-6)
+
+
+def test_initial_shard_equals_slice_of_full_table():
+    """ShardedSparseTable draws only its own rows (row chunks of the same seeded stream): every
+    rank's shard equals rows rank::world of the replicated table's initial values."""
+    from recommendsystem_amd.embedding import SparseAdaGrad, SparseAdam, SparseTable
+    for opt in (SparseAdam(), SparseAdaGrad()):
+        full = SparseTable.initial_weight(10_007, 8, opt, 0.05, 9)
+        for world in (1, 2, 3, 8):
+            for rank in range(world):
+                got = SparseTable.initial_shard(10_007, 8, opt, 0.05, 9, rank, world, chunk_rows=999)
+                assert torch.equal(got, full[rank::world])
