@@ -8,7 +8,12 @@ A step = one full training step on one synthetic batch: embedding lookup, IL x3,
 MLP, clip + cross_entropy, backward, (N > 1: dense all-reduce + sparse row exchange), dense Adam
 and sparse Adam on the touched rows.  Batches (Zipf(1.2) ids over 26 x 100k vocab, Bernoulli(0.25)
 labels) are pre-generated in HBM; each has its own captured HIP graph that reads it in place.
-Prints ONE JSON line on rank 0 (value = samples/s over all ranks, weak scaling).
+Prints ONE JSON line on rank 0 (value = samples/s over all ranks).
+
+Batch semantics (SURVEY §8(c) decision 6): the primary series is STRONG scaling -- the global
+batch (--global-batch, default 4096 = configs[1]) is split over the N ranks, per-GPU 4096 / N --
+and the same run also times the WEAK series (per-GPU --batch, default 4096) as a nested "weak"
+object.  At N = 1 the two are the same workload and only one is timed.
 """
 from __future__ import annotations
 
@@ -42,7 +47,15 @@ def parse():
                          "to rehearse the DP path with several ranks on one GPU)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (config 2: 4096)")
+    ap.add_argument("--batch", type=int, default=4096,
+                    help="per-GPU batch of the weak-scaling series (config 2: 4096)")
+    ap.add_argument("--global-batch", type=int, default=4096,
+                    help="global batch of the strong-scaling series (the primary line): per-GPU "
+                         "batch = global / N")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="which series is the line's value (the other is nested unless --no-other)")
+    ap.add_argument("--no-other", action="store_true",
+                    help="N > 1: skip the nested other-scaling series")
     ap.add_argument("--pool", type=int, default=8, help="distinct pre-generated batches")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="bounded CPU sample: run whole train steps until this much time passed")
@@ -335,14 +348,23 @@ def run_workload(args, world, rank, dev, pg):
         print(json.dumps(out), flush=True)
 
 
-def bench_autoint(args, world, rank, dev, pg, compute_dtype):
+def per_gpu_batch(args, world, scaling):
+    if scaling == "weak":
+        return args.batch
+    if args.global_batch % world:
+        raise SystemExit(f"--global-batch {args.global_batch} does not split over {world} ranks")
+    return args.global_batch // world
+
+
+def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     """Config 2 in one compute mode ("f32": the reference's dtype; "bf16": config 2's stated
-    bf16 mode, rs_set_math_mode).  Returns (result dict, model, cfg, CPU batch pool)."""
+    bf16 mode, rs_set_math_mode) and one batch series (strong: global batch split over the
+    ranks; weak: per-GPU batch fixed).  Returns (result dict, model, cfg, CPU batch pool)."""
     from recommendsystem_amd import _lib
     from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
     # config 2: 26 x 16, vocab 100k/field, IL(3, 16, 2), mlp [32,16], [1]
     cfg = AutoIntConfig(compute_dtype=compute_dtype)
-    B, F = args.batch, cfg.num_fields
+    B, F = per_gpu_batch(args, world, scaling), cfg.num_fields
     model = AutoInt(cfg, device=dev, seed=0, max_batch=B, world_size=world)
     trainer = AutoIntTrainer(model, B, process_group=pg)
 
@@ -388,17 +410,19 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype):
     def il_bwd_once():
         # the exact launch the step makes: backward + fused sparse push into the gradient table
         # (scan-mode marks); it adds into table.grad, which only matters after the timed region
+        # (the saved pair: it reads the forward's attention save left by the last step)
         t = model.table
-        call("rs_il_bwd_push", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
+        call("rs_il_bwd_push_saved", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
              trainer.dcat.data_ptr() + 4 * trainer.D, trainer.CW, B, F, E, U, H, L,
              ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
              ptr(trainer.dx0), ptr(trainer.rows), ptr(t.grad), ptr(t.flag), None, 0,
-             ptr(trainer.il_ws), trainer.il_ws_n)
+             ptr(trainer.il_ws), trainer.il_ws_n, ptr(trainer.asave), trainer.asave_n)
 
     def il_fwd_once():
-        call("rs_il_fwd", stream_handle(), ptr(trainer.x0), B, F, E, U, H, L, ptr(il.kernel),
-             ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
-             trainer.cat.data_ptr() + 4 * trainer.D, trainer.CW, ptr(trainer.xsave))
+        call("rs_il_fwd_saved", stream_handle(), ptr(trainer.x0), B, F, E, U, H, L,
+             ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
+             trainer.cat.data_ptr() + 4 * trainer.D, trainer.CW, ptr(trainer.xsave),
+             ptr(trainer.asave), trainer.asave_n)
 
     trace("kernel timing")
     peak = BF16_PEAK_TFLOPS if compute_dtype == "bf16" else FP32_PEAK_TFLOPS
@@ -433,15 +457,17 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype):
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": compute_dtype,
         "data": "synthetic (Zipf(1.2) ids over 26x100k vocab, Bernoulli(0.25) labels; random-init weights)",
         "config": {"workload": "configs[1]: AutoInt full train (embedding + 3xInteractingLayer + MLP), "
-                               "26 fields x emb 16, per-GPU batch 4096",
-                   "global_batch": B * world, "fields": F, "emb_dim": E, "layer_num": L,
+                               f"26 fields x emb 16, global batch {B * world} ({scaling} scaling)",
+                   "global_batch": B * world, "per_gpu_batch": B, "fields": F, "emb_dim": E,
+                   "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd3_kernel (InteractingLayer backward + fused sparse push)",
+        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd4_kernel (InteractingLayer backward over the "
+                               "forward's attention save + fused sparse push)",
                      "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "launch_us": round(t_bwd * 1e6, 2),
@@ -515,10 +541,18 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    out, model, cfg, pool_cpu = bench_autoint(args, world, rank, dev, pg, args.dtype)
+    out, model, cfg, pool_cpu = bench_autoint(args, world, rank, dev, pg, args.dtype, args.scaling)
+    other = "weak" if args.scaling == "strong" else "strong"
+    if world > 1 and not args.no_other and per_gpu_batch(args, world, other) != out["config"]["per_gpu_batch"]:
+        # the other batch series in the same run (own timed region, same contract)
+        o3, *_ = bench_autoint(args, world, rank, dev, pg, args.dtype, other)
+        out[other] = {k: o3[k] for k in ("value", "ms_per_step", "scaling", "roofline", "il_fwd_us",
+                                         "final_loss")}
+        out[other]["global_batch"] = o3["config"]["global_batch"]
+        out[other]["per_gpu_batch"] = o3["config"]["per_gpu_batch"]
     if args.dtype == "f32" and not args.no_bf16:
         # config 2's bf16 mode beside the fp32 line (same contract, own timed region)
-        o2, *_ = bench_autoint(args, world, rank, dev, pg, "bf16")
+        o2, *_ = bench_autoint(args, world, rank, dev, pg, "bf16", args.scaling)
         out["bf16"] = {k: o2[k] for k in ("value", "ms_per_step", "dtype", "roofline",
                                            "il_fwd_us", "step_roofline", "final_loss")}
         out["bf16"]["note"] = ("IL projections/dW/dx and head layer-1/2 GEMMs on bf16 MFMA, fp32 "

@@ -235,12 +235,17 @@ int rs_il_bwd(void* stream, const float* x, const float* xsave, const float* dy,
               const float* gamma, const float* beta, float eps, int use_res, float drop_rate,
               uint64_t seed, float* dx, int dx_accumulate, float* dparams,
               int dparams_accumulate, float* workspace, int64_t workspace_floats);
-/* Saved-attention pair for the many-field kernels (F > 64, rank/multi_head config 3): the
- * forward also writes, per (iteration, sample), the attention output before the epilogue, the
- * softmax row statistics and the dropout keep bits into asave, and the backward reads them instead
- * of recomputing the attention forward and re-hashing the mask (same results as the plain pair).
- * asave >= rs_il_attn_save_floats(B, F, U, H, L) floats (0 when F <= 64: there asave may be NULL
- * and the calls are exactly rs_il_fwd / rs_il_bwd). */
+/* Saved-attention pairs: the forward also writes, per (iteration, sample), the attention output
+ * before the epilogue and the softmax row statistics into asave, and the backward reads them
+ * instead of recomputing the attention forward.
+ *   F > 64 (many-field kernels, rank/multi_head config 3): + the dropout keep bits; same results
+ *     as the plain pair.
+ *   F <= 32, U == 16, H == 2 (config 2): O [F][U] | (scaled max, 1/sum) [H*F][2] per (iteration,
+ *     sample); the backward runs the LN backward first and the attention backward in two key
+ *     sweeps (bwd4_kernel).  Within the gradient tolerance of the plain pair (the softmax weights
+ *     come from the saved stats instead of a re-run of the max / sum).
+ * asave >= rs_il_attn_save_floats(B, F, U, H, L) floats (0 for other shapes: there asave may be
+ * NULL and the calls are exactly rs_il_fwd / rs_il_bwd). */
 int64_t rs_il_attn_save_floats(int64_t B, int F, int U, int H, int L);
 int rs_il_fwd_saved(void* stream, const float* x, int64_t B, int F, int E, int U, int H, int L,
                     const float* W, const float* bias, const float* gamma, const float* beta,
@@ -490,6 +495,23 @@ int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float
                    int use_res, float drop_rate, uint64_t seed, const float* dx_base,
                    const int32_t* rows, float* grad_table, int32_t* flag, float* dparams,
                    int dparams_accumulate, float* workspace, int64_t workspace_floats);
+
+/* The saved pair's fused-front-end forward and fused-push backward (asave as rs_il_fwd_saved /
+ * rs_il_bwd_saved; the AutoInt trainer's launches). */
+int rs_il_fwd_gather_saved(void* stream, const int64_t* ids, const int64_t* row_base,
+                           const int64_t* bucket, int hash_mode, const float* table,
+                           int64_t table_rows, float* x, int32_t* rows_out, int64_t B, int F,
+                           int E, int U, int H, int L, const float* W, const float* bias,
+                           const float* gamma, const float* beta, float eps, int use_res,
+                           float drop_rate, uint64_t seed, float* y, int64_t y_ld, float* xsave,
+                           float* asave, int64_t asave_floats);
+int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave, const float* dy,
+                         int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                         const float* W, const float* bias, const float* gamma, const float* beta,
+                         float eps, int use_res, float drop_rate, uint64_t seed,
+                         const float* dx_base, const int32_t* rows, float* grad_table,
+                         int32_t* flag, float* dparams, int dparams_accumulate, float* workspace,
+                         int64_t workspace_floats, const float* asave, int64_t asave_floats);
 
 /* Grid (= number of per-block partial rows) rs_il_bwd / rs_il_bwd_push use for this shape and
  * workspace when dy rows are 16-B aligned (dy_ld % 4 == 0); 0 for an unsupported shape. */

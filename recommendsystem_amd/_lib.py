@@ -138,6 +138,12 @@ SIGNATURES: dict[str, tuple] = {
     "rs_il_bwd_push": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                               _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64]),
+    "rs_il_bwd_push_saved": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
+                                    _vp, _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp,
+                                    _vp, _i32, _vp, _i64, _vp, _i64]),
+    "rs_il_fwd_gather_saved": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _i32,
+                                      _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32,
+                                      _u64, _vp, _i64, _vp, _vp, _i64]),
     "rs_gather_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
     "rs_scatter_add_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
     "rs_segment_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),

@@ -168,6 +168,11 @@ class AutoIntTrainer:
         self.dx0 = torch.empty(B, F * E, **f32)
         lib = _lib.load()
         self.il_ws_n = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+        # the saved-attention pair (rs_il_fwd_gather_saved / rs_il_bwd_push_saved; 0 floats for
+        # shapes without one): the forward's attention output + softmax stats per (iteration,
+        # sample), so the backward skips the softmax re-run (config 2: 25 MB at B = 4096)
+        self.asave_n = int(lib.rs_il_attn_save_floats(B, F, U, self.H, self.L))
+        self.asave = torch.empty(max(self.asave_n, 1), **f32)
         ws_dense = max(int(lib.rs_dense_bwd_weight_workspace_floats(B, l.input_dim, l.units))
                        for l in self.deep_layers + self.logit_layers)
         self.dense_ws_n = ws_dense
@@ -291,11 +296,11 @@ class AutoIntTrainer:
                  self.cat.data_ptr() + 4 * D, CW, ptr(self.xsave) if L > 1 else None)
         else:  # single-hot lookup + concat + IL forward in one launch (x0 and the hashed rows
             # are by-products for the head and the push)
-            call("rs_il_fwd_gather", s, ptr(self.ids), ptr(emb.row_base), ptr(emb.bucket),
+            call("rs_il_fwd_gather_saved", s, ptr(self.ids), ptr(emb.row_base), ptr(emb.bucket),
                  emb.hash_mode, ptr(t.weight), t.rows, ptr(self.x0), ptr(self.rows), B, F, E, U,
                  H, L, ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon,
                  int(il.use_res), drop, il.seed, self.cat.data_ptr() + 4 * D, CW,
-                 ptr(self.xsave) if L > 1 else None)
+                 ptr(self.xsave) if L > 1 else None, ptr(self.asave), self.asave_n)
         d = self.deep_layers
         lg = self.logit_layers[0]
         d2 = d[1] if hd["N2"] else None
@@ -308,16 +313,19 @@ class AutoIntTrainer:
              hd["ws"].numel())
         if self.push:
             # dL/dx0 = head share (dx0) + IL share, added straight into the table rows
-            call("rs_il_bwd_push", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+            call("rs_il_bwd_push_saved", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
                  self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
                  ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
                  ptr(self.dx0), ptr(self.rows), ptr(t.grad), ptr(t.flag), None, 0,
-                 ptr(self.il_ws), self.il_ws_n)
+                 ptr(self.il_ws), self.il_ws_n, ptr(self.asave), self.asave_n)
             return
-        call("rs_il_bwd", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+        # (F > 64: the forward above is the plain one, no save to read)
+        saved = F <= 64 and self.asave_n > 0
+        name, tail = ("rs_il_bwd_saved", (ptr(self.asave), self.asave_n)) if saved else ("rs_il_bwd", ())
+        call(name, s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
              self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
              ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed, ptr(self.dx0),
-             1, None, 0, ptr(self.il_ws), self.il_ws_n)
+             1, None, 0, ptr(self.il_ws), self.il_ws_n, *tail)
         t.accumulate(self.rows, None, B, F, self.dx0, F * E, E, emb.combiner)
 
     def _reduce_dense(self, adam: bool):

@@ -139,6 +139,35 @@ __device__ __forceinline__ void glds_copy_wave(float* dst, const float* src, int
   }
 }
 
+// glds_copy_wave for n 4-byte words (global_load_lds_dword: 64 words per wave instruction, any
+// 4-B alignment).  Complete after vm_wait_all() + wave_lds_sync().
+__device__ __forceinline__ void glds_copy_wave_u32(void* dst, const void* src, int n) {
+  const int lane = (int)(threadIdx.x & 63);
+  for (int k = lane; k < n; k += 64) {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(static_cast<uint32_t*>(dst) + (k - lane)));
+    const uint32_t* g = static_cast<const uint32_t*>(src) + k;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds)
+        : "memory");
+  }
+}
+
+// Global dword load the compiler does not track (no vmcnt wait of its own): the caller waits with
+// an explicit s_waitcnt naming the value (vm_wait_regs) before any use.
+__device__ __forceinline__ float gload_untracked(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
 // The lane index through an empty volatile asm: every use re-derives it, so the compiler cannot
 // hoist the dozens of lane-dependent LDS addresses of a fused kernel out of its sample loop and
 // keep them live across every phase (measured on the InteractingLayer kernels: backward v2 167 ->

@@ -169,9 +169,20 @@ struct Args {
   int32_t* g_rows;
   int64_t g_table_rows;
   int g_hash;
+  // F <= 32 saved path (rs_il_fwd_saved / rs_il_bwd_saved, small_save_stride): per (iteration,
+  // sample) the forward writes the attention output O [F][U] and the softmax row stats
+  // [H*F] x {scaled max, 1 / sum}; the backward reads them instead of re-running the softmax
+  float* osave;
+  const float* osave_in;
 };
 
 static inline int r4(int v) { return (v + 3) & ~3; }
+
+// floats per (iteration, sample) of the small-F attention save: O [F][U] | stats [H*F][2],
+// padded to 16 B
+__host__ __device__ inline int64_t small_save_stride(int F, int U, int H) {
+  return ((int64_t)F * U + 2 * (int64_t)H * F + 3) & ~(int64_t)3;
+}
 
 template <class C>
 Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate, uint64_t seed,
@@ -217,6 +228,8 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
   a.g_rows = nullptr;
   a.g_table_rows = 0;
   a.g_hash = 0;
+  a.osave = nullptr;
+  a.osave_in = nullptr;
   return a;
 }
 
@@ -734,7 +747,8 @@ __device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C
 // ---- phase: attention forward; optionally keeps P (pre-dropout) for backward ----------------
 template <class C, bool STORE_P, bool DROP, int OSTR = C::OS, bool PK = false>
 __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* PM,
-                                              const Args& a, int64_t b, uint64_t lseed) {
+                                              const Args& a, int64_t b, uint64_t lseed,
+                                              float* gsave = nullptr) {
   const int lane = lane_id();
   const int F = a.F;
   for (int r0 = 0; r0 < C::H * F; r0 += 64) {
@@ -776,6 +790,13 @@ __device__ __forceinline__ void attention_fwd(const float* PR, float* O, float* 
 #pragma unroll
       for (int d4 = 0; d4 < C::DH / 4; ++d4)
         orow[d4] = make_float4(o[4 * d4], o[4 * d4 + 1], o[4 * d4 + 2], o[4 * d4 + 3]);
+      if (gsave) {  // the saved path: O row and (max, 1/sum) for the backward (bwd4_kernel)
+        float4* g = reinterpret_cast<float4*>(gsave + i * C::U + h * C::DH);
+#pragma unroll
+        for (int d4 = 0; d4 < C::DH / 4; ++d4)
+          g[d4] = make_float4(o[4 * d4], o[4 * d4 + 1], o[4 * d4 + 2], o[4 * d4 + 3]);
+        *reinterpret_cast<float2*>(gsave + F * C::U + 2 * (h * F + i)) = make_float2(mx, inv);
+      }
     }
   }
 }
@@ -870,7 +891,9 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
       for (int rt = 0; rt * 16 < F; ++rt) mfma_project<C>(X, PR, F, rt, mw);
       wave_lds_sync();
       // O_i overwrites Q_i in place (only lane (h, i) ever reads Q_i, before writing O_i)
-      attention_fwd<C, false, DROP, C::PRS>(PR, PR, nullptr, a, b, lseed);
+      float* gsave = a.osave ? a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, C::U, C::H)
+                             : nullptr;
+      attention_fwd<C, false, DROP, C::PRS>(PR, PR, nullptr, a, b, lseed, gsave);
       wave_lds_sync();
       if (it == a.L - 1) {
         epilogue<C, 0, C::PRS>(PR, PR, nullptr, y + b * y_ld, C::U, a, gam, bet);
@@ -2181,6 +2204,502 @@ __host__ __forceinline__ size_t bwd3_lds_bytes(int F) {
   return ((size_t)Bwd3Layout<C>::shared_floats() + (size_t)kWpb3 * Bwd3Layout<C>(F).per_wave) * 4;
 }
 
+// ============================== backward kernel, v4 (saved path) ===============================
+// rs_il_bwd_saved / rs_il_bwd_push_saved for F <= 32 with two heads: the forward wrote, per
+// (iteration, sample), the attention output O and the softmax row stats (scaled max, 1 / sum)
+// (small_save_stride).  With O known, the LN + ReLU backward runs right after the projections,
+// so dO and D_i = dO_i . O_i are known before the attention backward, and the attention backward
+// needs two passes over the keys instead of v3's four (recompute, dV, dS/dQ, dK):
+//   Q-pass, lane = (head, query i), one sweep over the keys j:
+//     P_ij = exp2(q_i . k_j * log2e / sqrt(dh) - max_i) / sum_i   (saved stats: no max/sum pass)
+//     dP_ij = dO_i . v_j ;  dS_ij = P_ij (dP_ij - D_i) / sqrt(dh) ;  dq_i += dS_ij k_j
+//     (P_ij parked in PM for the K-pass; dq_i to DY)
+//   K-pass, lane = (head, key j), one sweep over the queries i:
+//     dv_j += Pd_ij dO_i ;  dS_ij recomputed from P_ij and dP_ij = dO_i . v_j (v_j in registers,
+//     the same fma order as the Q-pass, so the same value) ;  dk_j += dS_ij q_i
+// Per sample-iteration that is 4 LDS row reads per key instead of v3's 12, and no PV product.
+// Buffers per wave: BA / BB alternate as X (the iteration's input) and S (the saved O | stats;
+// after the LN backward it holds dO).  The X operand of dW is taken into registers right after
+// the projections, so BA takes the next iteration's save straight away (global_load_lds) and BB
+// the next iteration's input once dO is dead (after the K-pass).  The fused push's row indices
+// and the head's dx share are fetched at the start of iteration 0 by loads the compiler does not
+// track, and waited for with an explicit vmcnt that leaves the younger prefetches in flight.
+template <class C>
+constexpr bool kSaved4 = kLnPair<C> && C::H * C::FMAX <= 64;
+// unroll of the two key sweeps (a full unroll of 26 keys lets the scheduler hoist every LDS row
+// read and spills)
+#ifndef RS_IL4_UNROLL_Q
+#define RS_IL4_UNROLL_Q 2
+#endif
+#ifndef RS_IL4_UNROLL_K
+#define RS_IL4_UNROLL_K 2
+#endif
+#define RS_PRAGMA_(x) _Pragma(#x)
+#define RS_UNROLL(n) RS_PRAGMA_(unroll n)
+
+template <class C>
+struct Bwd4Layout {
+  int ba, bb, pr, dy, pm, st, rows, sv, per_wave;
+  __host__ __device__ Bwd4Layout(int F) {
+    sv = (int)small_save_stride(F, C::U, C::H);
+    const int xe = F * C::E;
+    const int xo = ((xe > sv ? xe : sv) + 3) & ~3;
+    int off = 0;
+    ba = off; off += xo;
+    bb = off; off += xo;
+    pr = off; off += (C::FMAX * C::PRS + 3) & ~3;
+    dy = off; off += (F * C::U + 3) & ~3;
+    pm = off; off += (C::H * F * C::PMS + 3) & ~3;
+    st = off; off += (C::H * F + 3) & ~3;     // D_i per (head, row)
+    rows = off; off += (F + 3) & ~3;          // the fused push's table rows (int32)
+    per_wave = off;
+  }
+};
+
+template <class C>
+__host__ __forceinline__ size_t bwd4_lds_bytes(int F) {
+  return ((size_t)Bwd3Layout<C>::shared_floats() + (size_t)kWpb3 * Bwd4Layout<C>(F).per_wave) * 4;
+}
+
+template <int N>
+__device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b)[N]) {
+  f32x2v acc = {0.f, 0.f};
+#pragma unroll
+  for (int d = 0; d < N; d += 2)
+    acc = __builtin_elementwise_fma(f32x2v{a[d], a[d + 1]}, f32x2v{b[d], b[d + 1]}, acc);
+  return acc.x + acc.y;
+}
+
+template <int N>
+__device__ __forceinline__ void axpy_reg_pk(float (&o)[N], float p, const float (&v)[N]) {
+  const f32x2v pp = {p, p};
+#pragma unroll
+  for (int d = 0; d < N; d += 2) {
+    const f32x2v r = __builtin_elementwise_fma(pp, f32x2v{v[d], v[d + 1]}, f32x2v{o[d], o[d + 1]});
+    o[d] = r.x; o[d + 1] = r.y;
+  }
+}
+
+// dW += X^T G over row tile rt with the X operand already in registers (xa[t][et] = X[16rt+4q+t]
+// [16et+j], as mfma_dw loads it)
+template <class C>
+__device__ __forceinline__ void mfma_dw_xreg(const float (&xa)[4][MfmaW<C>::ET], const float* G,
+                                             int F, int rt,
+                                             f32x4 (&acc)[MfmaW<C>::ET][MfmaW<C>::NT],
+                                             float (&dbp)[MfmaW<C>::NT]) {
+  using M = MfmaW<C>;
+  const int q = lane_id() >> 4, j = lane_id() & 15;
+  float gb[4][M::NT];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int f = 16 * rt + 4 * q + t;
+    const bool ok = f < F;
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) {
+      gb[t][nt] = ok ? G[f * C::PRS + 16 * nt + j] : 0.f;
+      dbp[nt] += gb[t][nt];
+    }
+  }
+  if constexpr (C::BF) {
+    float xp[2][M::ET], gp[2][M::NT];
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et) {
+      xp[0][et] = pack_bf16(xa[0][et], xa[1][et]);
+      xp[1][et] = pack_bf16(xa[2][et], xa[3][et]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) {
+      gp[0][nt] = pack_bf16(gb[0][nt], gb[1][nt]);
+      gp[1][nt] = pack_bf16(gb[2][nt], gb[3][nt]);
+    }
+#pragma unroll
+    for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+      for (int nt = 0; nt < M::NT; ++nt)
+        acc[et][nt] = mfma_bf16(xp[0][et], xp[1][et], gp[0][nt], gp[1][nt], acc[et][nt]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+        for (int nt = 0; nt < M::NT; ++nt)
+          acc[et][nt] = mfma_16x16x4(xa[t][et], gb[t][nt], acc[et][nt]);
+  }
+}
+
+// glds wave instructions a copy of n4 float4 (n words) issues
+__host__ __device__ constexpr int glds_instrs4(int n4) { return (n4 + 63) / 64; }
+
+template <class C, bool DROP>
+#ifndef RS_IL_BWD4_OCC
+#define RS_IL_BWD4_OCC 2
+#endif
+__global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
+    const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
+    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
+    int dx_accumulate, float* __restrict__ partials, Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  static_assert(kSaved4<C>, "bwd4 needs H == 2, F <= 32 (one lane per (head, row))");
+  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);
+  const int F = C::EXACT ? C::FMAX : a.F;
+  const Bwd4Layout<C> lay(F);
+  float* const WL = smem;
+  float* const BL = smem + ((C::E * C::WPS + 3) & ~3);
+  float* const GL = BL + ((C::NC + 3) & ~3);
+  float* const base = smem + Bwd3Layout<C>::shared_floats() + wave_id() * lay.per_wave;
+  float* XB = base + lay.ba;  // this iteration's input X
+  float* SB = base + lay.bb;  // this iteration's save: O | stats, then dO
+  float* const PR = base + lay.pr;
+  float* const DY = base + lay.dy;
+  float* const PM = base + lay.pm;
+  float* const DL = base + lay.st;
+  int32_t* const RW = reinterpret_cast<int32_t*>(base + lay.rows);
+  const int lane = lane_id();
+  const int w = wave_id();
+  constexpr int H = C::H, DH = C::DH, U = C::U;
+  const int HF = H * F;
+  const int nrt = (F + 15) / 16;
+  const int sv = lay.sv;
+
+  for (int k = threadIdx.x; k < C::E * C::NC; k += blockDim.x)
+    WL[(k / C::NC) * C::WPS + k % C::NC] = W[k];
+  for (int k = threadIdx.x; k < C::NC; k += blockDim.x) BL[k] = bias[k];
+  for (int k = threadIdx.x; k < C::U; k += blockDim.x) GL[k] = gamma[k];
+  zero_pad_rows<C>(PR, F);
+  __syncthreads();
+
+  using M = MfmaW<C>;
+  constexpr int NRT = (C::FMAX + 15) / 16;
+  f32x4 dwacc[M::ET][M::NT];
+  float dbp[M::NT];
+#pragma unroll
+  for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+    for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
+  float dg2[DH], dbt2[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) { dg2[d] = 0.f; dbt2[d] = 0.f; }
+
+  const int nx4 = F * C::E / 4, ny4 = F * U / 4, ns4 = sv / 4;
+  auto x_src = [&](int64_t bb, int itx) -> const float* {
+    return itx == 0 ? x + bb * F * C::E : xsave + ((int64_t)(itx - 1) * a.B + bb) * F * U;
+  };
+  auto s_src = [&](int64_t bb, int itx) -> const float* {
+    return a.osave_in + ((int64_t)itx * a.B + bb) * sv;
+  };
+  const int64_t b_first = (int64_t)blockIdx.x * kWpb3 + w;
+  const int64_t b_step = (int64_t)gridDim.x * kWpb3;
+  if (b_first < a.B) {
+    glds_copy_wave(XB, x_src(b_first, a.L - 1), nx4);
+    glds_copy_wave(SB, s_src(b_first, a.L - 1), ns4);
+    glds_copy_wave(DY, dy + b_first * dy_ld, ny4);
+  }
+  // the fused push's share of the head (dx_accumulate): 4 rows x ET columns per row tile
+  const bool push = a.push_table != nullptr;
+  const bool with_base = push && dx_accumulate;
+
+  for (int64_t b = b_first; b < a.B; b += b_step) {
+    for (int it = a.L - 1; it >= 0; --it) {
+      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
+      const int64_t bn = it > 0 ? b : b + b_step;  // the next iteration's sample
+      const int itn = it > 0 ? it - 1 : a.L - 1;
+      const bool has_next = bn < a.B;
+      vm_wait_all();  // X, the save (and dy) of this iteration, and the previous push's atomics
+      wave_lds_sync();
+      const bool push_now = it == 0 && push;
+      float bv[NRT][M::ET][4];
+      if (push_now) {
+        glds_copy_wave_u32(RW, a.push_rows + b * F, F);
+        if (with_base) {
+          const float* base_g = dx + b * F * C::E;
+          const int q = lane >> 4, jx = lane & 15;
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int f = 16 * rt + 4 * q + r, e = 16 * et + jx;
+                const int fc = f < F ? f : F - 1;
+                bv[rt][et][r] = gload_untracked(base_g + fc * C::E + (e < C::E ? e : 0));
+              }
+        }
+      }
+      // ---- P1: projections (MFMA); dW's X operand into registers ----
+      {
+        MfmaW<C> mw;
+        mw.load_proj_lds(WL, BL);
+        for (int rt = 0; rt < nrt; ++rt) mfma_project<C>(XB, PR, F, rt, mw);
+      }
+      float xa[NRT][4][M::ET];
+      {
+        const int q = lane >> 4, jx = lane & 15;
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et) {
+              const int f = 16 * rt + 4 * q + t, e = 16 * et + jx;
+              xa[rt][t][et] = (f < F && e < C::E) ? XB[f * C::E + e] : 0.f;
+            }
+      }
+      wave_lds_sync();  // X dead: the next iteration's save streams into its buffer
+      if (has_next) glds_copy_wave(XB, s_src(bn, itn), ns4);
+      // ---- P3: z = relu(O + R), LN + ReLU backward (lane = (row, head)): SB <- dO, R <- gR,
+      //      D_{h,f} = dO_f . O_f over head h ----
+      {
+        const int f = lane >> 1, h = lane & 1;
+        const bool act = f < F;
+        const int fr = act ? f : 0;
+        float oa[DH], rr[DH], dyv[DH], gm[DH], z[DH];
+        load_row(oa, SB + fr * U + h * DH);
+        load_row(rr, PR + fr * C::PRS + 3 * U + h * DH);
+        load_row(dyv, DY + fr * U + h * DH);
+        load_row(gm, GL + h * DH);
+        float sum = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          if (!a.use_res) rr[d] = 0.f;
+          if (!act) dyv[d] = 0.f;
+          z[d] = fmaxf(oa[d] + rr[d], 0.f);
+          sum += z[d];
+        }
+        const float mean = group_sum<2>(sum) * (1.0f / (float)U);
+        float sq = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) { const float t = z[d] - mean; sq += t * t; }
+        const float var = group_sum<2>(sq) * (1.0f / (float)U);
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        float sg = 0.f, sgz = 0.f;
+        float gr[DH];
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          const float zh = (z[d] - mean) * rstd;
+          dg2[d] = fmaf(dyv[d], zh, dg2[d]);
+          dbt2[d] += dyv[d];
+          const float g = dyv[d] * gm[d];
+          sg += g;
+          sgz += g * zh;
+          gr[d] = rr[d];         // R (for its ReLU mask below)
+          rr[d] = z[d] > 0.f ? 1.f : 0.f;
+          z[d] = zh;
+          gm[d] = g;
+        }
+        sg = group_sum<2>(sg) * (1.0f / (float)U);
+        sgz = group_sum<2>(sgz) * (1.0f / (float)U);
+        float dt[DH];
+        float dd = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          const float dz = (gm[d] - sg - z[d] * sgz) * rstd;
+          dt[d] = rr[d] != 0.f ? dz : 0.f;
+          dd = fmaf(oa[d], dt[d], dd);
+          gr[d] = (a.use_res && gr[d] > 0.f) ? dt[d] : 0.f;
+        }
+        if (act) {
+          store_row(SB + f * U + h * DH, dt);
+          store_row(PR + f * C::PRS + 3 * U + h * DH, gr);
+          DL[h * F + f] = dd;
+        }
+      }
+      wave_lds_sync();
+      // ---- Q-pass (lane = (h, i)): P -> PM, dq -> DY ----
+      {
+        const bool act = lane < HF;
+        const int h = act ? lane / F : 0, i = act ? lane - h * F : 0;
+        float qv[DH], dO[DH], dq[DH];
+        load_row(qv, PR + i * C::PRS + h * DH);
+        load_row(dO, SB + i * U + h * DH);
+        const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (h * F + i));
+        const float D = DL[h * F + i];
+        const float* kb = PR + U + h * DH;
+        const float* vb = PR + 2 * U + h * DH;
+        float* pm_row = PM + (h * F + i) * C::PMS;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) dq[d] = 0.f;
+        const int nj = C::EXACT ? C::FMAX : F;
+RS_UNROLL(RS_IL4_UNROLL_Q)
+        for (int j = 0; j < nj; ++j) {
+          const float s = dot_row_pk(qv, kb + j * C::PRS) * a.sc2;
+          const float p = __builtin_amdgcn_exp2f(s - stt.x) * stt.y;
+          if (act) pm_row[j] = p;
+          float dp = dot_row_pk(dO, vb + j * C::PRS);
+          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+          const float ds = p * (dp - D) * a.inv_sdh;
+          axpy_row_pk(dq, ds, kb + j * C::PRS);
+        }
+        if (act) store_row(DY + i * U + h * DH, dq);
+      }
+      wave_lds_sync();
+      // ---- K-pass (lane = (h, j)): dV, dK -> V, K slots as gV, gK ----
+      {
+        const bool act = lane < HF;
+        const int h = act ? lane / F : 0, j = act ? lane - h * F : 0;
+        float vj[DH], dv[DH], dk[DH];
+        load_row(vj, PR + j * C::PRS + 2 * U + h * DH);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) { dv[d] = 0.f; dk[d] = 0.f; }
+        const float* pcol = PM + h * F * C::PMS + j;
+        const float* dl = DL + h * F;
+        const int ni = C::EXACT ? C::FMAX : F;
+RS_UNROLL(RS_IL4_UNROLL_K)
+        for (int i = 0; i < ni; ++i) {
+          const float P = pcol[i * C::PMS];
+          const float D = dl[i];
+          float dOi[DH];
+          load_row(dOi, SB + i * U + h * DH);
+          float pd = P;
+          float dp = dot_reg_pk(dOi, vj);
+          if (DROP) {
+            const bool keep = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate);
+            pd = keep ? P * a.drop_scale : 0.f;
+            dp = keep ? dp * a.drop_scale : 0.f;
+          }
+          axpy_reg_pk(dv, pd, dOi);
+          const float ds = P * (dp - D) * a.inv_sdh;
+          axpy_row_pk(dk, ds, PR + i * C::PRS + h * DH);
+        }
+        float kj[DH];
+        load_row(kj, PR + j * C::PRS + U + h * DH);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          dv[d] = vj[d] > 0.f ? dv[d] : 0.f;
+          dk[d] = kj[d] > 0.f ? dk[d] : 0.f;
+        }
+        // row j's K / V are read only by this lane in this pass
+        if (act) {
+          store_row(PR + j * C::PRS + 2 * U + h * DH, dv);
+          store_row(PR + j * C::PRS + U + h * DH, dk);
+        }
+      }
+      wave_lds_sync();  // every lane's Q-row reads are done
+      for (int k = lane; k < F * U; k += 64) {  // Q <- gQ (dq in DY)
+        const int f = k / U, c = k - f * U;
+        float* qq = PR + f * C::PRS + c;
+        *qq = *qq > 0.f ? DY[k] : 0.f;
+      }
+      wave_lds_sync();
+      // dO (SB) and dq (DY) are dead: the next iteration's input (and the next sample's dy)
+      if (has_next) {
+        glds_copy_wave(SB, x_src(bn, itn), nx4);
+        if (it == 0) glds_copy_wave(DY, dy + bn * dy_ld, ny4);
+      }
+      // ---- P7: dW += X^T G, db += colsum G; dx = G W^T ----
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt)
+        if (rt < nrt) mfma_dw_xreg<C>(xa[rt], PR, F, rt, dwacc, dbp);
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        MfmaW<C> mw;
+        mw.load_dx_lds(WL);
+        if (it > 0) {
+          mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { DY[f * U + e] = v; });
+        } else if (push) {
+          // the rows (and the head's share) were fetched at the start of this iteration; the
+          // prefetches issued since (the next save, input and dy) stay in flight
+          if (has_next) {
+            constexpr int kYoung = C::EXACT
+                ? glds_instrs4((int)(((C::FMAX * C::U + 2 * C::H * C::FMAX + 3) & ~3) / 4)) +
+                      glds_instrs4(C::FMAX * C::E / 4) + glds_instrs4(C::FMAX * C::U / 4)
+                : 3;
+            asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kYoung) : "memory");
+          } else {
+            vm_wait_all();
+          }
+          // the asm loads' registers: tie them to the wait (no use may move above it)
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(bv[rt][et][r]));
+          wave_lds_sync();  // RW landed in LDS
+          const int q = lane >> 4;
+          int32_t rw[NRT][4];
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int f = 16 * rt + 4 * q + r;
+              rw[rt][r] = f < F ? RW[f] : -1;
+            }
+          mfma_dx_all<C>(PR, F, mw, [&](int rt, int et, int r, int, int e, float v) {
+            const int32_t row = rw[rt][r];
+            if (row >= 0) {
+              if (e == 0) scan_mark(a.push_flag, row);
+              atomicAdd(a.push_table + (int64_t)row * C::E + e, with_base ? v + bv[rt][et][r] : v);
+            }
+          });
+        } else {
+          float* d = dx + b * F * C::E;
+          if (dx_accumulate)
+            mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { d[f * C::E + e] += v; });
+          else
+            mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { d[f * C::E + e] = v; });
+        }
+      }
+      wave_lds_sync();
+      float* const t = XB;  // XB holds the next save, SB the next input
+      XB = SB;
+      SB = t;
+    }
+  }
+
+  // ---- lanes -> wave -> block (wave order 0..kWpb3-1): deterministic ----
+#pragma unroll
+  for (int nt = 0; nt < M::NT; ++nt) {
+    dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
+    dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
+  }
+#pragma unroll
+  for (int d = 0; d < DH; ++d)
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) {
+      dg2[d] += __shfl_xor(dg2[d], o, 64);
+      dbt2[d] += __shfl_xor(dbt2[d], o, 64);
+    }
+  __syncthreads();
+  float* RED = smem;
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
+  __syncthreads();
+  {
+    const int q = lane >> 4, jx = lane & 15;
+    for (int ww = 0; ww < kWpb3; ++ww) {
+      if (w == ww) {
+#pragma unroll
+        for (int et = 0; et < M::ET; ++et)
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int e = 16 * et + 4 * q + r;
+              if (e < C::E) RED[e * C::NC + 16 * nt + jx] += dwacc[et][nt][r];
+            }
+        if (q == 0) {
+#pragma unroll
+          for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + jx] += dbp[nt];
+        }
+        if (lane < 2) {
+#pragma unroll
+          for (int d = 0; d < DH; ++d) {
+            const int u = lane * DH + d;
+            RED[C::E * C::NC + C::NC + u] += dg2[d];
+            RED[C::E * C::NC + C::NC + C::U + u] += dbt2[d];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
+    partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
+}
+
 // one resident round of v3 blocks on MI355X (2 per CU x 256 CUs); callers size the per-block
 // partial rows with rs_il_bwd_partial_blocks, which applies the same rule
 constexpr int kBwd3Grid = 512;
@@ -2201,6 +2720,7 @@ int fwd_launch(const FwdReq& q) {
   a.g_table_rows = q.gather_table_rows;
   a.g_rows = q.gather_rows;
   a.g_hash = q.gather_hash;
+  if constexpr (kSaved4<C>) a.osave = q.asave;  // the saved path's O + softmax stats
   const size_t per_wave = (size_t)a.per_wave * sizeof(float);
   int wpb = (int)(kLdsBytes / per_wave);
   if (wpb > kMaxFwdWaves) wpb = kMaxFwdWaves;
@@ -2225,6 +2745,26 @@ int bwd_launch(const BwdReq& q) {
   // x / xsave rows are copied 16 B at a time
   if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
 #ifndef RS_IL_BWD_NO_V3
+  if constexpr (kSaved4<C>) {  // v4: the forward's O + softmax stats (rs_il_bwd_saved)
+    const size_t lds3 = bwd3_lds_bytes<C>(q.F), lds4 = bwd4_lds_bytes<C>(q.F);
+    if (q.asave && a.dy_vec && lds3 <= kLdsBytes / 2 && lds4 <= kLdsBytes / 2 &&
+        (size_t)C::NPARAM * 4 <= lds4 && q.F <= C::FMAX && q.F >= 1) {
+      // same grid rule as v3 (rs_il_bwd_partial_blocks answers for both)
+      int64_t grid = (q.B + kWpb3 - 1) / kWpb3;
+      const int64_t max_grid = q.workspace_floats / C::NPARAM;
+      if (grid > kBwd3Grid) grid = kBwd3Grid;
+      if (grid > max_grid) grid = max_grid;
+      if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
+      if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
+      a.osave_in = q.asave;
+      bwd4_kernel<C, DROP><<<(int)grid, 64 * kWpb3, lds4, q.stream>>>(
+          q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
+          q.workspace, a);
+      if (q.dparams)
+        reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+      return rs_status_after_launch();
+    }
+  }
   {  // v3 (one wave per sample, no workgroup barriers) when its LDS gives 2 blocks per CU
     const size_t lds3 = bwd3_lds_bytes<C>(q.F);
     if (a.dy_vec && lds3 <= kLdsBytes / 2 && (size_t)C::NPARAM * 4 <= lds3) {

@@ -600,7 +600,10 @@ int run_bwd(const BwdReq& q) {
 }  // namespace large
 
 int64_t il_attn_save_floats(int64_t B, int F, int U, int H, int L) {
-  return F > 64 ? (int64_t)L * B * large::save_stride(F, U, H) : 0;
+  if (F > 64) return (int64_t)L * B * large::save_stride(F, U, H);
+  // F <= 32, two heads of 8 (il_inst_a.hip shapes): O + softmax stats for bwd4_kernel
+  if (F <= 32 && U == 16 && H == 2) return (int64_t)L * B * small_save_stride(F, U, H);
+  return 0;
 }
 
 // F in (64, 256]: the many-field instantiations (config 3 is E = U = 8, H = 2).

@@ -95,12 +95,13 @@ RS_API int rs_il_fwd_saved(void* stream, const float* x, int64_t B, int F, int E
                      seed, y, y_ld, xsave, need > 0 ? asave : nullptr);
 }
 
-RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row_base,
-                            const int64_t* bucket, int hash_mode, const float* table,
-                            int64_t table_rows, float* x, int32_t* rows_out, int64_t B, int F,
-                            int E, int U, int H, int L, const float* W, const float* bias,
-                            const float* gamma, const float* beta, float eps, int use_res,
-                            float drop_rate, uint64_t seed, float* y, int64_t y_ld, float* xsave) {
+static int il_fwd_gather_impl(void* stream, const int64_t* ids, const int64_t* row_base,
+                              const int64_t* bucket, int hash_mode, const float* table,
+                              int64_t table_rows, float* x, int32_t* rows_out, int64_t B, int F,
+                              int E, int U, int H, int L, const float* W, const float* bias,
+                              const float* gamma, const float* beta, float eps, int use_res,
+                              float drop_rate, uint64_t seed, float* y, int64_t y_ld,
+                              float* xsave, float* asave) {
   if (!ids || !row_base || !bucket || !table || !x || !W || !bias || !gamma || !beta || !y ||
       B < 0 || F <= 0 || L <= 0 || H <= 0 || (hash_mode != RS_HASH_MOD && hash_mode != RS_HASH_SPLITMIX))
     return RS_ERR_ARG;
@@ -118,10 +119,36 @@ RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row
   q.gather_rows = rows_out;
   q.gather_hash = hash_mode;
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  q.asave = asave;
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
   return r;
+}
+
+RS_API int rs_il_fwd_gather(void* stream, const int64_t* ids, const int64_t* row_base,
+                            const int64_t* bucket, int hash_mode, const float* table,
+                            int64_t table_rows, float* x, int32_t* rows_out, int64_t B, int F,
+                            int E, int U, int H, int L, const float* W, const float* bias,
+                            const float* gamma, const float* beta, float eps, int use_res,
+                            float drop_rate, uint64_t seed, float* y, int64_t y_ld, float* xsave) {
+  return il_fwd_gather_impl(stream, ids, row_base, bucket, hash_mode, table, table_rows, x,
+                            rows_out, B, F, E, U, H, L, W, bias, gamma, beta, eps, use_res,
+                            drop_rate, seed, y, y_ld, xsave, nullptr);
+}
+
+RS_API int rs_il_fwd_gather_saved(void* stream, const int64_t* ids, const int64_t* row_base,
+                                  const int64_t* bucket, int hash_mode, const float* table,
+                                  int64_t table_rows, float* x, int32_t* rows_out, int64_t B,
+                                  int F, int E, int U, int H, int L, const float* W,
+                                  const float* bias, const float* gamma, const float* beta,
+                                  float eps, int use_res, float drop_rate, uint64_t seed, float* y,
+                                  int64_t y_ld, float* xsave, float* asave, int64_t asave_floats) {
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need > 0 && (!asave || asave_floats < need)) return RS_ERR_ARG;
+  return il_fwd_gather_impl(stream, ids, row_base, bucket, hash_mode, table, table_rows, x,
+                            rows_out, B, F, E, U, H, L, W, bias, gamma, beta, eps, use_res,
+                            drop_rate, seed, y, y_ld, xsave, need > 0 ? asave : nullptr);
 }
 
 static int bwd_small(const rs_il::BwdReq& q) {
@@ -176,13 +203,14 @@ RS_API int rs_il_bwd_saved(void* stream, const float* x, const float* xsave, con
                      workspace, workspace_floats, need > 0 ? asave : nullptr);
 }
 
-RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,
-                          int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
-                          const float* W, const float* bias, const float* gamma,
-                          const float* beta, float eps, int use_res, float drop_rate,
-                          uint64_t seed, const float* dx_base, const int32_t* rows,
-                          float* grad_table, int32_t* flag, float* dparams,
-                          int dparams_accumulate, float* workspace, int64_t workspace_floats) {
+static int il_bwd_push_impl(void* stream, const float* x, const float* xsave, const float* dy,
+                            int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                            const float* W, const float* bias, const float* gamma,
+                            const float* beta, float eps, int use_res, float drop_rate,
+                            uint64_t seed, const float* dx_base, const int32_t* rows,
+                            float* grad_table, int32_t* flag, float* dparams,
+                            int dparams_accumulate, float* workspace, int64_t workspace_floats,
+                            const float* asave) {
   if (!x || !dy || !W || !bias || !gamma || !beta || !rows || !grad_table || !flag || !workspace)
     return RS_ERR_ARG;
   if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
@@ -196,7 +224,37 @@ RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, cons
   q.push_table = grad_table;
   q.push_flag = flag;
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  q.asave = asave;
   return bwd_small(q);
+}
+
+RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,
+                          int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                          const float* W, const float* bias, const float* gamma,
+                          const float* beta, float eps, int use_res, float drop_rate,
+                          uint64_t seed, const float* dx_base, const int32_t* rows,
+                          float* grad_table, int32_t* flag, float* dparams,
+                          int dparams_accumulate, float* workspace, int64_t workspace_floats) {
+  return il_bwd_push_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta,
+                          eps, use_res, drop_rate, seed, dx_base, rows, grad_table, flag, dparams,
+                          dparams_accumulate, workspace, workspace_floats, nullptr);
+}
+
+RS_API int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave, const float* dy,
+                                int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                                const float* W, const float* bias, const float* gamma,
+                                const float* beta, float eps, int use_res, float drop_rate,
+                                uint64_t seed, const float* dx_base, const int32_t* rows,
+                                float* grad_table, int32_t* flag, float* dparams,
+                                int dparams_accumulate, float* workspace,
+                                int64_t workspace_floats, const float* asave,
+                                int64_t asave_floats) {
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need > 0 && (!asave || asave_floats < need)) return RS_ERR_ARG;
+  return il_bwd_push_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta,
+                          eps, use_res, drop_rate, seed, dx_base, rows, grad_table, flag, dparams,
+                          dparams_accumulate, workspace, workspace_floats,
+                          need > 0 ? asave : nullptr);
 }
 
 RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,

@@ -454,6 +454,74 @@ def test_interacting_saved_pair_equals_recompute(F, E, U, H, L, drop):
     assert rc == -1
 
 
+@pytest.mark.parametrize("F,L,drop", [(26, 3, 0.0), (26, 1, 0.2), (20, 2, 0.0), (31, 3, 0.1)])
+@pytest.mark.parametrize("push", [False, True])
+def test_interacting_small_saved_pair(F, L, drop, push):
+    """F <= 32, U = 16, H = 2 (config 2): rs_il_fwd_saved writes O + softmax stats, and
+    rs_il_bwd_saved / rs_il_bwd_push_saved (bwd4_kernel: LN backward first, two key sweeps) match
+    the recomputing pair -- y bit-identical, dx / pushed rows and parameter gradients within the
+    gradient tolerance (the softmax weights come from the saved stats, not a re-run max / sum)."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    lib = _lib.load()
+    B, E, U, H = 67, 16, 16, 2
+    g = torch.Generator(device=DEV).manual_seed(F * 10 + L)
+    x = torch.rand(B, F, E, device=DEV, generator=g) - 0.5
+    W = (torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.6
+    b = (torch.rand(4 * U, device=DEV, generator=g) - 0.5) * 0.2
+    gm = torch.rand(U, device=DEV, generator=g) + 0.5
+    bt = (torch.rand(U, device=DEV, generator=g) - 0.5) * 0.2
+    dy = torch.randn(B, F * U, device=DEV, generator=g)
+    base = torch.randn(B, F * E, device=DEV, generator=g)
+    rows = torch.randint(-1, 300, (B * F,), device=DEV, dtype=torch.int32, generator=g)
+    s = stream_handle()
+    n_save = int(lib.rs_il_attn_save_floats(B, F, U, H, L))
+    stride = F * U + 2 * H * F
+    assert n_save == L * B * (stride + (-stride) % 4)
+    asave = torch.full((n_save,), float("nan"), device=DEV)
+    ws_n = int(lib.rs_il_bwd_workspace_floats(B, E, U))
+    npar = E * 4 * U + 4 * U + 2 * U
+    outs = []
+    for saved in (False, True):
+        y = torch.empty(B, F * U, device=DEV)
+        xs = torch.empty(max(L - 1, 1), B, F, U, device=DEV)
+        dx = base.clone()
+        dp = torch.empty(npar, device=DEV)
+        ws = torch.empty(ws_n, device=DEV)
+        table = torch.zeros(300, E, device=DEV)
+        flag = torch.full((300,), -1, dtype=torch.int32, device=DEV)
+        common = (ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77, ptr(y), F * U,
+                  ptr(xs) if L > 1 else None)
+        xsp = ptr(xs) if L > 1 else None
+        wargs = (ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77)
+        if saved:
+            call("rs_il_fwd_saved", s, ptr(x), B, F, E, U, H, L, *common, ptr(asave), n_save)
+        else:
+            call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, *common)
+        if push:
+            name = "rs_il_bwd_push_saved" if saved else "rs_il_bwd_push"
+            tail = (ptr(asave), n_save) if saved else ()
+            call(name, s, ptr(x), xsp, ptr(dy), F * U, B, F, E, U, H, L, *wargs, ptr(base),
+                 ptr(rows), ptr(table), ptr(flag), ptr(dp), 0, ptr(ws), ws_n, *tail)
+        elif saved:
+            call("rs_il_bwd_saved", s, ptr(x), xsp, ptr(dy), F * U, B, F, E, U, H, L, *wargs,
+                 ptr(dx), 1, ptr(dp), 0, ptr(ws), ws_n, ptr(asave), n_save)
+        else:
+            call("rs_il_bwd", s, ptr(x), xsp, ptr(dy), F * U, B, F, E, U, H, L, *wargs,
+                 ptr(dx), 1, ptr(dp), 0, ptr(ws), ws_n)
+        torch.cuda.synchronize()
+        outs.append((y, table if push else dx, dp, flag))
+    assert torch.isfinite(asave).all()  # every (iteration, sample) slot written
+    assert torch.equal(outs[0][0], outs[1][0]), "y: the save changed the forward"
+    assert_grad_close(_np(outs[1][1]), _np(outs[0][1]), what="pushed rows" if push else "dx")
+    assert_grad_close(_np(outs[1][2]), _np(outs[0][2]), what="dparams")
+    assert torch.equal(outs[0][3], outs[1][3])  # the same rows marked
+    rc = lib.rs_il_bwd_saved(s, ptr(x), ptr(xs) if L > 1 else None, ptr(dy), F * U, B, F, E, U,
+                             H, L, ptr(W), ptr(b), ptr(gm), ptr(bt), 1e-14, 1, drop, 77, ptr(dx), 0,
+                             None, 0, ptr(ws), ws_n, ptr(asave), n_save - 1)
+    assert rc == -1
+
+
 def test_interacting_rank_error():
     from recommendsystem_amd.layers import InteractingLayer
     il = InteractingLayer(1, 16, 2, device=DEV)

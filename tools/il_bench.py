@@ -30,10 +30,18 @@ def main(B=4096, F=26, E=16, U=16, H=2, L=3, reps=50):
     base = torch.randn(B, F * E, device=dev, generator=g)
     def push(rows, bp):
         return lambda: call("rs_il_bwd_push", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(bp), ptr(rows), ptr(table), ptr(flag), None, 0, ptr(ws), wsn)
+    ns = int(lib.rs_il_attn_save_floats(B, F, U, H, L))
+    asave = torch.empty(max(ns, 1), device=dev)
+    fwd_s = lambda: call("rs_il_fwd_saved", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs), ptr(asave), ns)
+    bwd_s = lambda: call("rs_il_bwd_saved", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn, ptr(asave), ns)
+    def push_s(rows, bp):
+        return lambda: call("rs_il_bwd_push_saved", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), 1e-14, 1, 0.0, 0, ptr(bp), ptr(rows), ptr(table), ptr(flag), None, 0, ptr(ws), wsn, ptr(asave), ns)
+    fwd_s(); torch.cuda.synchronize()
     out = {}
     only = os.environ.get("IL_BENCH_ONLY")  # one variant (PMC passes: one kernel per dispatch kind)
     for name, fn in (("fwd", fwd), ("bwd", bwd), ("bwd+reduce", red), ("push_uniform", push(rows_u, None)),
-                     ("push_uniform_base", push(rows_u, base)), ("push_hot_base", push(rows_z, base))):
+                     ("push_uniform_base", push(rows_u, base)), ("push_hot_base", push(rows_z, base)),
+                     ("fwd_saved", fwd_s), ("bwd_saved", bwd_s), ("push_hot_base_saved", push_s(rows_z, base))):
         if only and name != only:
             continue
         fn(); torch.cuda.synchronize()
