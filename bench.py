@@ -146,6 +146,59 @@ def cpu_baseline(cfg, model, batches_cpu, seconds):
                       f"{n_single} steps on 1 thread"}
 
 
+def config1_leg(seconds, dev):
+    """configs[0]: InteractingLayer.py's forward on the host CPU --
+    x ~ U(-0.05, 0.05) [256, 26, 16] (seed 0), glorot-uniform weights (seed 1), no dropout -- with
+    the constructor defaults (layer_num 1, unit_num 128, head_num 1, use_res) and the AutoInt
+    setting (3, 16, 2, use_res).  "For config 1 the CPU path is the measurement": the fp32
+    TF-op-order restatement (oracle/torch_ref.py::interacting_layer, kind "port") timed on the
+    box's host cores (all threads, median of 3 bounded runs) and on 1 thread; beside it, the same
+    forward through rs_il_fwd on the GPU (HIP events, for reference)."""
+    from oracle import torch_ref as tr
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    B, F, E = 256, 26, 16
+    x = np.random.default_rng(0).uniform(-0.05, 0.05, size=(B, F, E)).astype(np.float32)
+    out = {"workload": "configs[0]: InteractingLayer forward, 26 fields x emb 16, batch 256 "
+                       "(x ~ U(-0.05, 0.05) seed 0, glorot-uniform weights seed 1, no dropout)",
+           "unit": "samples/sec", "kind": "port", "cores": threads}
+    per = max(seconds / 12.0, 0.25)
+    for name, (L, U, H) in (("ctor_defaults", (1, 128, 1)), ("autoint", (3, 16, 2))):
+        lim = (6.0 / (E + U)) ** 0.5
+        w = np.random.default_rng(1).uniform(-lim, lim, size=(E, 4 * U)).astype(np.float32)
+        args = (torch.from_numpy(w), torch.zeros(4 * U), torch.ones(U), torch.zeros(U), L, H, True)
+        xt = torch.from_numpy(x)
+
+        def rate(n_threads):
+            torch.set_num_threads(n_threads)
+            with torch.no_grad():
+                tr.interacting_layer(xt, *args)
+                rs = []
+                for _ in range(3):
+                    t0, k = time.perf_counter(), 0
+                    while k < 2 or time.perf_counter() - t0 < per:
+                        tr.interacting_layer(xt, *args)
+                        k += 1
+                    rs.append(B * k / (time.perf_counter() - t0))
+            return float(np.median(rs))
+
+        multi, single = rate(threads), rate(1)
+        torch.set_num_threads(threads)
+        # the same forward on the GPU (fp32, one launch)
+        xd = torch.from_numpy(x).to(dev)
+        wd, bd = torch.from_numpy(w).to(dev), torch.zeros(4 * U, device=dev)
+        gd, bed = torch.ones(U, device=dev), torch.zeros(U, device=dev)
+        y = torch.empty(B, F * U, device=dev)
+        xs = torch.empty(max(L - 1, 1), B, F, U, device=dev)
+        t = time_kernel(lambda: call("rs_il_fwd", stream_handle(), ptr(xd), B, F, E, U, H, L,
+                                     ptr(wd), ptr(bd), ptr(gd), ptr(bed), 1e-14, 1, 0.0, 0,
+                                     ptr(y), F * U, ptr(xs) if L > 1 else None), 50)
+        out[name] = {"layer": f"IL(layer_num={L}, unit_num={U}, head_num={H}, use_res=True)",
+                     "cpu_value": round(multi, 1), "cpu_single_thread": round(single, 1),
+                     "gpu_value": round(B / t, 1), "gpu_us_per_forward": round(t * 1e6, 2)}
+    return out
+
+
 WORKLOADS = {
     # name: (config index, per-GPU batch, description)
     "multi_head": (2, 4096, "configs[2]: rank/multi_head AUTOINT train (200 fields x dim 8 multi-hot, "
@@ -303,7 +356,8 @@ def run_workload(args, world, rank, dev, pg):
     else:
         shard = pg if (world > 1 and args.shard_table) else None  # N2 owner-sharded 10M table
         model = W.StaytimeRoughRank(device=dev, seed=0, shard_group=shard)
-        trainer = Trainer(model, 5e-4, [model.table], process_group=pg)
+        trainer = Trainer(model, 5e-4, [model.table], process_group=pg,
+                          lr_groups=[(model.dssm, model.rr_cfg.lr_dense)])
         pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
     graphed = world == 1 and not args.eager
     if graphed:  # one HIP graph per pool batch (forward + autograd backward + optimizers)
@@ -559,6 +613,7 @@ def main():
                                "accumulation and master weights; accuracy in tests/test_gpu_bf16.py")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(cfg, model, pool_cpu, args.cpu_baseline_seconds)
+        out["config1"] = config1_leg(args.cpu_baseline_seconds, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -2228,6 +2228,9 @@ template <class C>
 constexpr bool kSaved4 = kLnPair<C> && C::H * C::FMAX <= 64;
 // unroll of the two key sweeps (a full unroll of 26 keys lets the scheduler hoist every LDS row
 // read and spills)
+#ifndef RS_IL4_EXP
+#define RS_IL4_EXP 0
+#endif
 #ifndef RS_IL4_UNROLL_Q
 #define RS_IL4_UNROLL_Q 2
 #endif
@@ -2268,6 +2271,22 @@ __device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b
   for (int d = 0; d < N; d += 2)
     acc = __builtin_elementwise_fma(f32x2v{a[d], a[d + 1]}, f32x2v{b[d], b[d + 1]}, acc);
   return acc.x + acc.y;
+}
+
+// two independent dot products, their packed-fma chains interleaved (back-to-back dependent
+// v_pk_fma_f32 need a wait state between them)
+template <int N>
+__device__ __forceinline__ void dot2_reg_pk(const float (&a)[N], const float (&b)[N],
+                                            const float (&c)[N], const float (&d)[N], float& ab,
+                                            float& cd) {
+  f32x2v x = {0.f, 0.f}, y = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < N; k += 2) {
+    x = __builtin_elementwise_fma(f32x2v{a[k], a[k + 1]}, f32x2v{b[k], b[k + 1]}, x);
+    y = __builtin_elementwise_fma(f32x2v{c[k], c[k + 1]}, f32x2v{d[k], d[k + 1]}, y);
+  }
+  ab = x.x + x.y;
+  cd = y.x + y.y;
 }
 
 template <int N>
@@ -2402,14 +2421,17 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
   const bool push = a.push_table != nullptr;
   const bool with_base = push && dx_accumulate;
 
+  IL_STAMP_DECL
   for (int64_t b = b_first; b < a.B; b += b_step) {
     for (int it = a.L - 1; it >= 0; --it) {
+      IL_STAMP(0)
       const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       const int64_t bn = it > 0 ? b : b + b_step;  // the next iteration's sample
       const int itn = it > 0 ? it - 1 : a.L - 1;
       const bool has_next = bn < a.B;
       vm_wait_all();  // X, the save (and dy) of this iteration, and the previous push's atomics
       wave_lds_sync();
+      IL_STAMP(1)
       const bool push_now = it == 0 && push;
       float bv[NRT][M::ET][4];
       if (push_now) {
@@ -2430,7 +2452,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         }
       }
       // ---- P1: projections (MFMA); dW's X operand into registers ----
-      {
+      if (RS_IL4_EXP != 5) {
         MfmaW<C> mw;
         mw.load_proj_lds(WL, BL);
         for (int rt = 0; rt < nrt; ++rt) mfma_project<C>(XB, PR, F, rt, mw);
@@ -2450,9 +2472,10 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
       }
       wave_lds_sync();  // X dead: the next iteration's save streams into its buffer
       if (has_next) glds_copy_wave(XB, s_src(bn, itn), ns4);
+      IL_STAMP(2)
       // ---- P3: z = relu(O + R), LN + ReLU backward (lane = (row, head)): SB <- dO, R <- gR,
       //      D_{h,f} = dO_f . O_f over head h ----
-      {
+      if (RS_IL4_EXP != 6) {
         const int f = lane >> 1, h = lane & 1;
         const bool act = f < F;
         const int fr = act ? f : 0;
@@ -2508,8 +2531,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         }
       }
       wave_lds_sync();
+      IL_STAMP(3)
       // ---- Q-pass (lane = (h, i)): P -> PM, dq -> DY ----
-      {
+      if (RS_IL4_EXP != 3) {
         const bool act = lane < HF;
         const int h = act ? lane / F : 0, i = act ? lane - h * F : 0;
         float qv[DH], dO[DH], dq[DH];
@@ -2520,24 +2544,40 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         const float* kb = PR + U + h * DH;
         const float* vb = PR + 2 * U + h * DH;
         float* pm_row = PM + (h * F + i) * C::PMS;
+        const float nm = -stt.x;
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] = 0.f;
         const int nj = C::EXACT ? C::FMAX : F;
-RS_UNROLL(RS_IL4_UNROLL_Q)
-        for (int j = 0; j < nj; ++j) {
-          const float s = dot_row_pk(qv, kb + j * C::PRS) * a.sc2;
-          const float p = __builtin_amdgcn_exp2f(s - stt.x) * stt.y;
+        // software-pipelined by one key: the next key's K / V rows are in flight while this
+        // key's products run (two register sets, unrolled by two)
+        float k0[DH], v0[DH], k1[DH], v1[DH];
+        auto ld = [&](float (&k)[DH], float (&v)[DH], int j) {
+          load_row(k, kb + j * C::PRS);
+          load_row(v, vb + j * C::PRS);
+        };
+        auto key = [&](int j, const float (&k)[DH], const float (&v)[DH]) {
+          float sv, dp;
+          dot2_reg_pk(qv, k, dO, v, sv, dp);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sv, a.sc2, nm)) * stt.y;
           if (act) pm_row[j] = p;
-          float dp = dot_row_pk(dO, vb + j * C::PRS);
           if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          const float ds = p * (dp - D) * a.inv_sdh;
-          axpy_row_pk(dq, ds, kb + j * C::PRS);
+          axpy_reg_pk(dq, p * (dp - D) * a.inv_sdh, k);
+        };
+        ld(k0, v0, 0);
+RS_UNROLL(RS_IL4_UNROLL_Q)
+        for (int j = 0; j < nj; j += 2) {
+          const bool two = (C::EXACT && C::FMAX % 2 == 0) || j + 1 < nj;
+          ld(k1, v1, two ? j + 1 : j);
+          key(j, k0, v0);
+          ld(k0, v0, j + 2 < nj ? j + 2 : nj - 1);  // (the last one re-reads a row: unused)
+          if (two) key(j + 1, k1, v1);
         }
         if (act) store_row(DY + i * U + h * DH, dq);
       }
       wave_lds_sync();
+      IL_STAMP(4)
       // ---- K-pass (lane = (h, j)): dV, dK -> V, K slots as gV, gK ----
-      {
+      if (RS_IL4_EXP != 4) {
         const bool act = lane < HF;
         const int h = act ? lane / F : 0, j = act ? lane - h * F : 0;
         float vj[DH], dv[DH], dk[DH];
@@ -2547,12 +2587,16 @@ RS_UNROLL(RS_IL4_UNROLL_Q)
         const float* pcol = PM + h * F * C::PMS + j;
         const float* dl = DL + h * F;
         const int ni = C::EXACT ? C::FMAX : F;
-RS_UNROLL(RS_IL4_UNROLL_K)
-        for (int i = 0; i < ni; ++i) {
-          const float P = pcol[i * C::PMS];
-          const float D = dl[i];
-          float dOi[DH];
-          load_row(dOi, SB + i * U + h * DH);
+        // pipelined by one query like the Q-pass: P_ij, D_i, dO_i and Q_i of the next query in
+        // flight while this one's products run
+        float o0[DH], q0[DH], o1[DH], q1[DH], p0, p1, d0, d1;
+        auto ld = [&](float (&o)[DH], float (&qq)[DH], float& P, float& D, int i) {
+          load_row(o, SB + i * U + h * DH);
+          load_row(qq, PR + i * C::PRS + h * DH);
+          P = pcol[i * C::PMS];
+          D = dl[i];
+        };
+        auto query = [&](int i, const float (&dOi)[DH], const float (&qi)[DH], float P, float D) {
           float pd = P;
           float dp = dot_reg_pk(dOi, vj);
           if (DROP) {
@@ -2561,8 +2605,16 @@ RS_UNROLL(RS_IL4_UNROLL_K)
             dp = keep ? dp * a.drop_scale : 0.f;
           }
           axpy_reg_pk(dv, pd, dOi);
-          const float ds = P * (dp - D) * a.inv_sdh;
-          axpy_row_pk(dk, ds, PR + i * C::PRS + h * DH);
+          axpy_reg_pk(dk, P * (dp - D) * a.inv_sdh, qi);
+        };
+        ld(o0, q0, p0, d0, 0);
+RS_UNROLL(RS_IL4_UNROLL_K)
+        for (int i = 0; i < ni; i += 2) {
+          const bool two = (C::EXACT && C::FMAX % 2 == 0) || i + 1 < ni;
+          ld(o1, q1, p1, d1, two ? i + 1 : i);
+          query(i, o0, q0, p0, d0);
+          ld(o0, q0, p0, d0, i + 2 < ni ? i + 2 : ni - 1);
+          if (two) query(i + 1, o1, q1, p1, d1);
         }
         float kj[DH];
         load_row(kj, PR + j * C::PRS + U + h * DH);
@@ -2578,6 +2630,7 @@ RS_UNROLL(RS_IL4_UNROLL_K)
         }
       }
       wave_lds_sync();  // every lane's Q-row reads are done
+      IL_STAMP(5)
       for (int k = lane; k < F * U; k += 64) {  // Q <- gQ (dq in DY)
         const int f = k / U, c = k - f * U;
         float* qq = PR + f * C::PRS + c;
@@ -2586,18 +2639,29 @@ RS_UNROLL(RS_IL4_UNROLL_K)
       wave_lds_sync();
       // dO (SB) and dq (DY) are dead: the next iteration's input (and the next sample's dy)
       if (has_next) {
+#if RS_IL4_EXP == 2
+        if (it > 0)
+#endif
         glds_copy_wave(SB, x_src(bn, itn), nx4);
+#if RS_IL4_EXP != 2
         if (it == 0) glds_copy_wave(DY, dy + bn * dy_ld, ny4);
+#endif
       }
+      IL_STAMP(6)
       // ---- P7: dW += X^T G, db += colsum G; dx = G W^T ----
 #pragma unroll
       for (int rt = 0; rt < NRT; ++rt)
-        if (rt < nrt) mfma_dw_xreg<C>(xa[rt], PR, F, rt, dwacc, dbp);
+        if (rt < nrt && RS_IL4_EXP != 7) mfma_dw_xreg<C>(xa[rt], PR, F, rt, dwacc, dbp);
       __builtin_amdgcn_sched_barrier(0);
+      IL_STAMP(7)
       {
         MfmaW<C> mw;
         mw.load_dx_lds(WL);
+#if RS_IL4_EXP == 1
+        if (true) {
+#else
         if (it > 0) {
+#endif
           mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { DY[f * U + e] = v; });
         } else if (push) {
           // the rows (and the head's share) were fetched at the start of this iteration; the
@@ -2644,12 +2708,14 @@ RS_UNROLL(RS_IL4_UNROLL_K)
         }
       }
       wave_lds_sync();
+      if (it > 0) { IL_STAMP(8) } else { IL_STAMP(9) }
       float* const t = XB;  // XB holds the next save, SB the next input
       XB = SB;
       SB = t;
     }
   }
 
+  IL_STAMP_FLUSH(a.stamps)
   // ---- lanes -> wave -> block (wave order 0..kWpb3-1): deterministic ----
 #pragma unroll
   for (int nt = 0; nt < M::NT; ++nt) {

@@ -38,8 +38,14 @@ def exchange_sparse(table, pg, world, x_rows, x_grads):
 
 
 class Trainer:
+    """lr_groups: [(module, lr), ...] -- dense parameters of a sub-model with their own Adam
+    learning rate (a joint workload whose towers the reference trains with separate
+    tn.optimizer.Optimizer instances, e.g. config 5: staytime lr 5e-4 (staytime/model.py:72) and
+    the DSSM lr 1e-4 (rough_rank/model.py:209)); every other parameter uses lr_dense.  Each group
+    is a contiguous range of the arena with its own step counter (same count every step)."""
+
     def __init__(self, model, lr_dense: float, tables=(), process_group=None, beta1=0.9,
-                 beta2=0.999, eps=1e-8):
+                 beta2=0.999, eps=1e-8, lr_groups=()):
         self.model = model
         self.arena = ParamArena(model.parameters())
         dev = self.arena.data.device
@@ -47,6 +53,7 @@ class Trainer:
         self.v = torch.zeros_like(self.arena.data)
         self.step_count = torch.zeros(1, device=dev, dtype=torch.int64)
         self.lr, self.b1, self.b2, self.eps = float(lr_dense), beta1, beta2, eps
+        self.segments = self._lr_segments(lr_groups)
         self.tables = list(tables)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
@@ -61,6 +68,32 @@ class Trainer:
                     continue
                 self.xbuf[id(t)] = (torch.empty(t.touched_cap, device=dev, dtype=torch.int32),
                                     torch.empty(t.touched_cap, t.dim, device=dev))
+
+    def _lr_segments(self, lr_groups):
+        """[(offset, n, lr, step counter)] covering the arena in order."""
+        base = self.arena.data.data_ptr()
+        ranges = []
+        for mod, lr in lr_groups:
+            offs = sorted(((p.data_ptr() - base) // 4, p.numel()) for p in mod.parameters())
+            o0, end = offs[0][0], offs[0][0]
+            for o, n in offs:
+                if o != end:
+                    raise ValueError("an lr group's parameters must be contiguous in the arena")
+                end += n
+            ranges.append((o0, end, float(lr)))
+        ranges.sort()
+        spans, k = [], 0
+        for o0, o1, lr in ranges:
+            if o0 < k:
+                raise ValueError("lr groups overlap")
+            if o0 > k:
+                spans.append((k, o0, self.lr))
+            spans.append((o0, o1, lr))
+            k = o1
+        if k < self.arena.n:
+            spans.append((k, self.arena.n, self.lr))
+        return [(o0, o1 - o0, lr, self.step_count if i == 0 else torch.zeros_like(self.step_count))
+                for i, (o0, o1, lr) in enumerate(spans)]
 
     def step(self, *batch):
         # dropout masks: per-step host seeds restart at 0 each step and the device step counter
@@ -86,15 +119,19 @@ class Trainer:
         scale = 1.0 / self.world
         if self.on_dense_grad is not None:
             self.on_dense_grad(self.arena.grad, scale)
-        call("rs_dense_adam", s, ptr(self.arena.data), ptr(self.arena.grad), ptr(self.m), ptr(self.v),
-             self.arena.n, ptr(self.step_count), self.lr, self.b1, self.b2, self.eps, scale, 1)
+        for off, n, lr, cnt in self.segments:
+            a = 4 * off
+            call("rs_dense_adam", s, self.arena.data.data_ptr() + a, self.arena.grad.data_ptr() + a,
+                 self.m.data_ptr() + a, self.v.data_ptr() + a, n, ptr(cnt), lr, self.b1, self.b2,
+                 self.eps, scale, 1)
         for t in self.tables:
             t.step(grad_scale=scale)
         return loss
 
     # ---- HIP-graph replay of whole steps (single GPU) --------------------------------------
     def _state(self):
-        out = [self.arena.data, self.arena.grad, self.m, self.v, self.step_count]
+        out = [self.arena.data, self.arena.grad, self.m, self.v]
+        out += [cnt for *_, cnt in self.segments]
         for t in self.tables:
             out += [t.weight, t.grad, t.flag, t.n_touched, t.touched]
             out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]

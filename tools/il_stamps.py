@@ -17,12 +17,20 @@ xs = torch.empty(L - 1, B, F, U, device=dev); y = torch.empty(B, F * U, device=d
 dy = torch.randn(B, F * U, device=dev); dx = torch.empty_like(x)
 wsn = int(lib.rs_il_bwd_workspace_floats(B, E, U)); ws = torch.empty(wsn, device=dev)
 s = stream_handle()
-call("rs_il_fwd", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs))
+SAVED = os.environ.get("IL_STAMPS_SAVED", "1") == "1"   # bwd4 (saved pair) or bwd3
+ns = int(lib.rs_il_attn_save_floats(B, F, U, H, L))
+asave = torch.empty(max(ns, 1), device=dev)
+call("rs_il_fwd_saved", s, ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs), ptr(asave), ns)
 for _ in range(3):
-    call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
+    if SAVED:
+        call("rs_il_bwd_saved", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn, ptr(asave), ns)
+    else:
+        call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
 torch.cuda.synchronize()
 v = st.cpu().tolist()[:10]
-names = ["x load/prefetch", "projection(MFMA)", "attn recompute", "LN bwd", "dV", "dS/dQ", "dK + G", "dW (MFMA)", "dx (MFMA) it>0", "dx+push it=0"]
+names = (["wait x/save", "P1 proj + xa", "P3 LN bwd", "Q-pass", "K-pass", "G-Q", "dW (MFMA)",
+          "dx it>0", "dx+push it=0", "-"] if SAVED else
+         ["x load/prefetch", "projection(MFMA)", "attn recompute", "LN bwd", "dV", "dS/dQ", "dK + G", "dW (MFMA)", "dx (MFMA) it>0", "dx+push it=0"])
 tot = sum(v)
 for n, c in zip(names, v):
     print(f"{n:18s} {100.0 * c / tot:6.1f}%")
