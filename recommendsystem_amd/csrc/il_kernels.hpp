@@ -464,7 +464,7 @@ struct MfmaW {
 };
 
 // PR[f][c] = relu(X[f] . W[:, c] + b[c]) for the 16 rows of row tile rt (rows >= F skipped)
-template <class C>
+template <class C, bool ALL_ROWS = false>
 __device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, int rt,
                                              const MfmaW<C>& w) {
   const int q = lane_id() >> 4, j = lane_id() & 15;
@@ -499,7 +499,9 @@ __device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 16 * rt + 4 * q + r;
-      if (f < F) PR[f * C::PRS + c] = fmaxf(acc[nt][r] + bc, 0.f);
+      // ALL_ROWS: the caller's layout has dead space for rows F .. 16 * ceil(F / 16) - 1 (no
+      // per-element branch)
+      if (ALL_ROWS || f < F) PR[f * C::PRS + c] = fmaxf(acc[nt][r] + bc, 0.f);
     }
   }
 }
@@ -673,7 +675,7 @@ __device__ __forceinline__ void mfma_dx_push(const float* G, int F, int rt, cons
 // result goes to `emit(rt, et, r, f, e, value)`
 // (rt, et, r compile-time after unrolling: per-lane arrays indexed by them stay in registers).
 // Summation per k part in c order, parts added in order -- fixed, deterministic.
-template <class C, class Emit>
+template <class C, class Emit, bool ALL_ROWS = false>
 __device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C>& w, Emit emit) {
   using M = MfmaW<C>;
   constexpr int NRT = (C::FMAX + 15) / 16;
@@ -739,7 +741,7 @@ __device__ __forceinline__ void mfma_dx_all(const float* G, int F, const MfmaW<C
         float v = acc[rt][0][et][r];
 #pragma unroll
         for (int kh = 1; kh < KH; ++kh) v += acc[rt][kh][et][r];
-        if (f < F && e < C::E) emit(rt, et, r, f, e, v);
+        if ((ALL_ROWS || f < F) && e < C::E) emit(rt, et, r, f, e, v);
       }
     }
 }
@@ -2231,6 +2233,9 @@ constexpr bool kSaved4 = kLnPair<C> && C::H * C::FMAX <= 64;
 #ifndef RS_IL4_EXP
 #define RS_IL4_EXP 0
 #endif
+#ifndef RS_IL4_WREG
+#define RS_IL4_WREG 0
+#endif
 #ifndef RS_IL4_UNROLL_Q
 #define RS_IL4_UNROLL_Q 2
 #endif
@@ -2250,11 +2255,17 @@ struct Bwd4Layout {
     int off = 0;
     ba = off; off += xo;
     bb = off; off += xo;
+    // PR's rows F .. 16 * ceil(F / 16) - 1 (written by the unguarded projection stores) land in
+    // PM, dead at the projections; DY's (the dx rows of iterations > 0) land in ST / RW / pad,
+    // dead in P7 of those iterations
+    const int f16 = (F + 15) & ~15;
     pr = off; off += (C::FMAX * C::PRS + 3) & ~3;
-    dy = off; off += (F * C::U + 3) & ~3;
     pm = off; off += (C::H * F * C::PMS + 3) & ~3;
+    dy = off; off += (F * C::U + 3) & ~3;
     st = off; off += (C::H * F + 3) & ~3;     // D_i per (head, row)
     rows = off; off += (F + 3) & ~3;          // the fused push's table rows (int32)
+    const int dy_slack = C::EXACT ? (f16 - F) * C::U - (off - dy - F * C::U) : 0;
+    if (dy_slack > 0) off += (dy_slack + 3) & ~3;
     per_wave = off;
   }
 };
@@ -2361,6 +2372,12 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
     int dx_accumulate, float* __restrict__ partials, Args a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   static_assert(kSaved4<C>, "bwd4 needs H == 2, F <= 32 (one lane per (head, row))");
+  // PR's unguarded rows up to the next multiple of 16 must fit in PM (Bwd4Layout); the
+  // non-exact instantiations (FMAX 32) have no such rows
+  static_assert(!C::EXACT ||
+                (((C::FMAX + 15) & ~15) - C::FMAX) * C::PRS <= C::H * C::FMAX * C::PMS,
+                "PM too small for PR's padded rows");
+  static_assert(C::EXACT || C::FMAX % 16 == 0, "non-exact FMAX must be a multiple of 16");
   const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);
   const int F = C::EXACT ? C::FMAX : a.F;
   const Bwd4Layout<C> lay(F);
@@ -2420,6 +2437,10 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
   // the fused push's share of the head (dx_accumulate): 4 rows x ET columns per row tile
   const bool push = a.push_table != nullptr;
   const bool with_base = push && dx_accumulate;
+#if RS_IL4_WREG
+  MfmaW<C> mwp;  // the projection fragments stay in registers for the whole kernel
+  mwp.load_proj_lds(WL, BL);
+#endif
 
   IL_STAMP_DECL
   for (int64_t b = b_first; b < a.B; b += b_step) {
@@ -2453,9 +2474,13 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
       }
       // ---- P1: projections (MFMA); dW's X operand into registers ----
       if (RS_IL4_EXP != 5) {
+#if RS_IL4_WREG
+        for (int rt = 0; rt < nrt; ++rt) mfma_project<C, true>(XB, PR, F, rt, mwp);
+#else
         MfmaW<C> mw;
         mw.load_proj_lds(WL, BL);
-        for (int rt = 0; rt < nrt; ++rt) mfma_project<C>(XB, PR, F, rt, mw);
+        for (int rt = 0; rt < nrt; ++rt) mfma_project<C, true>(XB, PR, F, rt, mw);
+#endif
       }
       float xa[NRT][4][M::ET];
       {
@@ -2662,7 +2687,10 @@ RS_UNROLL(RS_IL4_UNROLL_K)
 #else
         if (it > 0) {
 #endif
-          mfma_dx_all<C>(PR, F, mw, [&](int, int, int, int f, int e, float v) { DY[f * U + e] = v; });
+          auto to_dy = [&](int, int, int, int f, int e, float v) { DY[f * U + e] = v; };
+          // (exact F: all NRT * 16 rows, the ones past F land in DY's slack; otherwise the
+          // tiles past ceil(F / 16) would not fit it)
+          mfma_dx_all<C, decltype(to_dy), C::EXACT>(PR, F, mw, to_dy);
         } else if (push) {
           // the rows (and the head's share) were fetched at the start of this iteration; the
           // prefetches issued since (the next save, input and dy) stay in flight

@@ -58,30 +58,37 @@ def _signed(s: int) -> int:
 @custom_op("ctr::interacting_fwd", mutates_args=())
 def interacting_fwd(x: Tensor, W: Tensor, bias: Tensor, gamma: Tensor, beta: Tensor,
                     layer_num: int, head_num: int, use_res: bool, eps: float, drop_rate: float,
-                    seed: int) -> tuple[Tensor, Tensor]:
+                    seed: int) -> tuple[Tensor, Tensor, Tensor]:
+    """Returns (y, xsave, asave): asave is the saved pair's attention save (rs_il_fwd_saved;
+    empty for shapes without one), consumed by interacting_bwd."""
     _lib.require_device(x, W)
     x = x.contiguous().float()
     B, F, E = x.shape
     U = W.shape[1] // 4
     y = torch.empty(B, F, U, device=x.device)
     xsave = torch.empty(max(layer_num - 1, 0), B, F, U, device=x.device)
-    call("rs_il_fwd", stream_handle(), ptr(x), B, F, E, U, head_num, layer_num, ptr(W), ptr(bias),
-         ptr(gamma), ptr(beta), eps, int(use_res), drop_rate, _seed(seed), ptr(y), F * U,
-         ptr(xsave) if layer_num > 1 else None)
-    return y, xsave
+    n_save = int(_lib.load().rs_il_attn_save_floats(B, F, U, head_num, layer_num))
+    asave = torch.empty(n_save, device=x.device)
+    call("rs_il_fwd_saved", stream_handle(), ptr(x), B, F, E, U, head_num, layer_num, ptr(W),
+         ptr(bias), ptr(gamma), ptr(beta), eps, int(use_res), drop_rate, _seed(seed), ptr(y), F * U,
+         ptr(xsave) if layer_num > 1 else None, ptr(asave) if n_save else None, n_save)
+    return y, xsave, asave
 
 
 @interacting_fwd.register_fake
 def _(x, W, bias, gamma, beta, layer_num, head_num, use_res, eps, drop_rate, seed):
     B, F, _ = x.shape
     U = W.shape[1] // 4
-    return x.new_empty(B, F, U), x.new_empty(max(layer_num - 1, 0), B, F, U)
+    n_save = int(_lib.load().rs_il_attn_save_floats(B, F, U, head_num, layer_num))
+    return (x.new_empty(B, F, U), x.new_empty(max(layer_num - 1, 0), B, F, U),
+            x.new_empty(n_save))
 
 
 @custom_op("ctr::interacting_bwd", mutates_args=())
-def interacting_bwd(dy: Tensor, x: Tensor, xsave: Tensor, W: Tensor, bias: Tensor, gamma: Tensor,
-                    beta: Tensor, layer_num: int, head_num: int, use_res: bool, eps: float,
-                    drop_rate: float, seed: int) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+def interacting_bwd(dy: Tensor, x: Tensor, xsave: Tensor, asave: Tensor, W: Tensor, bias: Tensor,
+                    gamma: Tensor, beta: Tensor, layer_num: int, head_num: int, use_res: bool,
+                    eps: float, drop_rate: float,
+                    seed: int) -> tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     x = x.contiguous().float()
     dy = dy.contiguous().float()
     B, F, E = x.shape
@@ -91,31 +98,32 @@ def interacting_bwd(dy: Tensor, x: Tensor, xsave: Tensor, W: Tensor, bias: Tenso
     ws = torch.empty(max(ws_n, 1), device=x.device)
     n = W.numel() + bias.numel() + gamma.numel() + beta.numel()
     dp = torch.empty(n, device=x.device)
-    call("rs_il_bwd", stream_handle(), ptr(x), ptr(xsave) if layer_num > 1 else None, ptr(dy), F * U,
-         B, F, E, U, head_num, layer_num, ptr(W), ptr(bias), ptr(gamma), ptr(beta), eps,
-         int(use_res), drop_rate, _seed(seed), ptr(dx), 0, ptr(dp), 0, ptr(ws), ws_n)
+    call("rs_il_bwd_saved", stream_handle(), ptr(x), ptr(xsave) if layer_num > 1 else None, ptr(dy),
+         F * U, B, F, E, U, head_num, layer_num, ptr(W), ptr(bias), ptr(gamma), ptr(beta), eps,
+         int(use_res), drop_rate, _seed(seed), ptr(dx), 0, ptr(dp), 0, ptr(ws), ws_n,
+         ptr(asave) if asave.numel() else None, asave.numel())
     o1, o2, o3 = W.numel(), W.numel() + bias.numel(), W.numel() + bias.numel() + gamma.numel()
     return (dx, dp[:o1].view(W.shape).clone(), dp[o1:o2].clone(), dp[o2:o3].clone(),
             dp[o3:].clone())
 
 
 @interacting_bwd.register_fake
-def _(dy, x, xsave, W, bias, gamma, beta, layer_num, head_num, use_res, eps, drop_rate, seed):
+def _(dy, x, xsave, asave, W, bias, gamma, beta, layer_num, head_num, use_res, eps, drop_rate, seed):
     return (torch.empty_like(x), torch.empty_like(W), torch.empty_like(bias),
             torch.empty_like(gamma), torch.empty_like(beta))
 
 
 def _il_setup(ctx, inputs, output):
     x, W, bias, gamma, beta, L, H, res, eps, rate, seed = inputs
-    ctx.save_for_backward(x, output[1], W, bias, gamma, beta)
+    ctx.save_for_backward(x, output[1], output[2], W, bias, gamma, beta)
     ctx.cfg = (L, H, res, eps, rate, seed)
 
 
-def _il_backward(ctx, dy, _dxsave):
-    x, xsave, W, bias, gamma, beta = ctx.saved_tensors
+def _il_backward(ctx, dy, _dxsave, _dasave):
+    x, xsave, asave, W, bias, gamma, beta = ctx.saved_tensors
     L, H, res, eps, rate, seed = ctx.cfg
-    dx, dW, db, dg, dbe = torch.ops.ctr.interacting_bwd(dy, x, xsave, W, bias, gamma, beta, L, H,
-                                                        res, eps, rate, seed)
+    dx, dW, db, dg, dbe = torch.ops.ctr.interacting_bwd(dy, x, xsave, asave, W, bias, gamma, beta,
+                                                        L, H, res, eps, rate, seed)
     return dx, dW, db, dg, dbe, None, None, None, None, None, None
 
 

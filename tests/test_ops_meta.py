@@ -9,9 +9,11 @@ def test_meta_shapes():
     m = dict(device="meta")
     x, W = torch.empty(4, 26, 16, **m), torch.empty(16, 64, **m)
     b, g, be = torch.empty(64, **m), torch.empty(16, **m), torch.empty(16, **m)
-    y, xs = torch.ops.ctr.interacting_fwd(x, W, b, g, be, 3, 2, True, 1e-14, 0.0, 0)
+    y, xs, sv = torch.ops.ctr.interacting_fwd(x, W, b, g, be, 3, 2, True, 1e-14, 0.0, 0)
     assert y.shape == (4, 26, 16) and xs.shape == (2, 4, 26, 16)
-    dx, dW, db, dg, dbe = torch.ops.ctr.interacting_bwd(y, x, xs, W, b, g, be, 3, 2, True, 1e-14, 0.0, 0)
+    assert sv.shape == (3 * 4 * (26 * 16 + 2 * 2 * 26),)  # the saved pair's O + softmax stats
+    dx, dW, db, dg, dbe = torch.ops.ctr.interacting_bwd(y, x, xs, sv, W, b, g, be, 3, 2, True, 1e-14,
+                                                        0.0, 0)
     assert dx.shape == x.shape and dW.shape == W.shape and dbe.shape == be.shape
     d = torch.ops.ctr.dense(torch.empty(5, 7, **m), torch.empty(7, 3, **m), torch.empty(3, **m), 1)
     assert d.shape == (5, 3)
