@@ -63,6 +63,10 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="configs 3-5: run the autograd step eagerly instead of replaying graphs")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--trace-markers", action="store_true",
+                    help="launch a marker kernel (torch.cuda._sleep: 'spin_kernel') right before "
+                         "and right after the timed loop, outside the timed region, so a rocprofv3 "
+                         "kernel trace can be cut to the timed steps (tools/prof_steps.py)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"],
                     help="config 2 compute mode of the headline line (f32 = the reference's math)")
     ap.add_argument("--no-bf16", action="store_true",
@@ -368,6 +372,8 @@ def run_workload(args, world, rank, dev, pg):
             return trainer.step(*pool[i % len(pool)])
     for i in range(args.warmup):
         step(i)
+    if args.trace_markers:
+        torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -379,6 +385,9 @@ def run_workload(args, world, rank, dev, pg):
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
+    if args.trace_markers:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -435,6 +444,8 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     trace("captured")
     for i in range(args.warmup):
         trainer.step_pool(i)
+    if args.trace_markers:
+        torch.cuda._sleep(1000)
     torch.cuda.synchronize()
 
     def barrier():
@@ -449,6 +460,9 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    if args.trace_markers:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

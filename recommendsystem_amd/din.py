@@ -60,7 +60,7 @@ class _DINFn(torch.autograd.Function):
     def backward(ctx, dout):
         q, keys, values, lengths, m8, W1, b1, W2, b2, probs = ctx.saved_tensors
         variant = ctx.variant
-        dout = dout.contiguous()
+        dout = _rows_view(dout)
         B, T, H = keys.shape
         dev = q.device
         dq = torch.empty(B, H, device=dev, dtype=torch.float32)
@@ -75,7 +75,7 @@ class _DINFn(torch.autograd.Function):
         call("rs_din_bwd", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys), keys.stride(0),
              keys.stride(1), ptr(values), values.stride(0), values.stride(1), B, T, H,
              ptr(lengths), ptr(m8), m8.stride(0) if m8 is not None else 0, ptr(W1), ptr(b1),
-             ptr(W2), ptr(b2), ptr(probs), ptr(dout), H, ptr(dq), H, ptr(dk), ptr(dv),
+             ptr(W2), ptr(b2), ptr(probs), ptr(dout), dout.stride(0), ptr(dq), H, ptr(dk), ptr(dv),
              ptr(dparams), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
             wgrads = (None, None, None, None)

@@ -162,15 +162,64 @@ class InteractingLayer(nn.Module):
 # ============================================================================================
 # Dense / MultiLayerDense
 # ============================================================================================
+def _row_major(t: torch.Tensor) -> torch.Tensor:
+    """A 2-D view the GEMM engine reads in place (unit column stride, any row stride >= width:
+    a column slice of a concat buffer or of a split gradient); a copy only otherwise."""
+    if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] and t.dtype == torch.float32:
+        return t
+    return t.contiguous().float()
+
+
+class _GatherMultiFn(torch.autograd.Function):
+    """outs[k][b, j] = src[b, plans[k][j]] (rs_gather_columns, one launch per plan); ONE backward
+    for all of them: a zero-filled d_src and a scatter-add per plan (atomic adds: plans may
+    overlap), instead of autograd's per-output zero fill + index_add + accumulate chain."""
+
+    @staticmethod
+    def forward(ctx, src, *plans):
+        src = _row_major(src)
+        B, S = src.shape
+        outs = []
+        for cols in plans:
+            n = cols.numel()
+            out = torch.empty(B, n, device=src.device, dtype=torch.float32)
+            call("rs_gather_columns", stream_handle(), ptr(src), src.stride(0), B, ptr(cols), n,
+                 ptr(out), n)
+            outs.append(out)
+        ctx.save_for_backward(*plans)
+        ctx.shape = (B, S)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        plans = ctx.saved_tensors
+        B, S = ctx.shape
+        ref = next(d for d in douts if d is not None)
+        dsrc = torch.zeros(B, S, device=ref.device, dtype=torch.float32)
+        for cols, d in zip(plans, douts):
+            if d is None:
+                continue
+            d = _row_major(d)
+            call("rs_scatter_add_columns", stream_handle(), ptr(d), d.stride(0), B, ptr(cols),
+                 cols.numel(), ptr(dsrc), S)
+        return (dsrc,) + (None,) * len(plans)
+
+
+def gather_multi(src, plans):
+    """Column gathers of one [B, S] source (int32 column plans on the device)."""
+    return _GatherMultiFn.apply(src, *plans)
+
+
 class _DenseFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, act):
         _lib.require_device(x, W)
-        x = x.contiguous()
+        x = _row_major(x)
         M, K = x.shape
         N = W.shape[1]
         y = torch.empty(M, N, device=x.device, dtype=torch.float32)
-        call("rs_dense_fwd", stream_handle(), ptr(x), M, K, K, ptr(W), ptr(b), N, act, ptr(y), N)
+        call("rs_dense_fwd", stream_handle(), ptr(x), M, K, x.stride(0), ptr(W), ptr(b), N, act,
+             ptr(y), N)
         ctx.save_for_backward(x, y, W, b)
         ctx.act = act
         return y
@@ -178,22 +227,22 @@ class _DenseFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, y, W, b = ctx.saved_tensors
-        dy = dy.contiguous()
+        dy = _row_major(dy)
         M, K = x.shape
         N = W.shape[1]
         s = stream_handle()
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            call("rs_dense_bwd_data", s, ptr(dy), N, ptr(y), N, ctx.act, ptr(W), M, K, N, ptr(dx),
-                 K, 0)
+            dx = torch.empty(M, K, device=x.device, dtype=torch.float32)
+            call("rs_dense_bwd_data", s, ptr(dy), dy.stride(0), ptr(y), N, ctx.act, ptr(W), M, K,
+                 N, ptr(dx), K, 0)
         ws_n = int(_lib.load().rs_dense_bwd_weight_workspace_floats(M, K, N))
         ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
         in_place = W.grad is not None and b.grad is not None and W.grad.is_contiguous()
         dW = W.grad if in_place else torch.empty_like(W)
         db = b.grad if in_place else torch.empty_like(b)
-        call("rs_dense_bwd_weight", s, ptr(x), K, ptr(dy), N, ptr(y), N, ctx.act, M, K, N,
-             ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
+        call("rs_dense_bwd_weight", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N,
+             ctx.act, M, K, N, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
             return dx, None, None, None
         return dx, dW, db, None

@@ -26,7 +26,7 @@ from torch import nn
 from ._lib import call, ptr, stream_handle
 from .din import StaytimeDIN
 from .embedding import EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam, SparseTable
-from .layers import Dense, InteractingLayer, _act_code, _DenseFn
+from .layers import Dense, InteractingLayer, _act_code, _DenseFn, gather_multi
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 from . import _lib
 from .towers import (DNN, PLE, CrossNet, DeepCrossLayer, ExpertGateLayer, FFMBlock, KDLoss,
@@ -364,6 +364,7 @@ class DSSM(nn.Module):
         nu, ni, E = cfg.user_fields, cfg.item_fields, cfg.emb_dim
         self.user_idx = torch.tensor(user_idx if user_idx is not None else list(range(nu)), device=dev)
         self.item_idx = torch.tensor(item_idx if item_idx is not None else list(range(nu, nu + ni)), device=dev)
+        self._plan_key, self._plan = None, None
         self.user = UserItemTower(nu * E, 2, cfg.output_dim, seed=seed, device=dev)
         self.item = UserItemTower(ni * E, 1, cfg.output_dim, seed=seed + 100, device=dev)
         D = (nu + ni) * E
@@ -383,15 +384,33 @@ class DSSM(nn.Module):
     def regularizers(self):
         return []
 
+    def _plans(self, nf, width):
+        """Column plans over a [B, nf * width] lookup output whose first 16 columns per field are
+        this model's embedding: user fields, item fields, and all fields (the teacher's input)."""
+        key = (nf, width)
+        if self._plan_key != key:
+            dev = self.user_idx.device
+            d = self.cfg.emb_dim
+
+            def cols(fields):
+                return torch.tensor([int(f) * width + c for f in fields for c in range(d)],
+                                    dtype=torch.int32, device=dev)
+            self._plan = (cols(self.user_idx.tolist()), cols(self.item_idx.tolist()),
+                          cols(range(nf)))
+            self._plan_key = key
+        return self._plan
+
     def forward(self, emb, mask):
-        """emb [B, nu + ni, 16]; mask [B, 1] (dense feature 4575).  Returns the reference's
-        outputs {'student', 'teacher', 'distill'} plus the logits."""
-        B = emb.shape[0]
-        ux = emb.index_select(1, self.user_idx).reshape(B, -1)
-        ix = emb.index_select(1, self.item_idx).reshape(B, -1)
+        """emb [B, nu + ni, 16] (or any [B, F, >= 16] whose columns 0:16 per field are the
+        embedding -- the joint model's [B, 52, 32] lookup); mask [B, 1] (dense feature 4575).
+        Returns the reference's outputs {'student', 'teacher', 'distill'} plus the logits."""
+        B, nf, width = emb.shape
+        emb = emb.contiguous()
+        # index_select + reshape of the user / item fields and the teacher's flatten (:21-22,
+        # :145-149) as column gathers of the lookup rows: one launch each, one fused backward
+        ux, ix, wc = gather_multi(emb.reshape(B, nf * width), self._plans(nf, width))
         user_emb = self.user(ux, mask)                                           # :145-146
         item_emb = self.item(ix)                                                 # :148-149
-        wc = emb.reshape(B, -1)                                                  # :21-22
         cross = self.cross(wc)                                                   # :24
         deep = self.t2(self.t1(wc))                                              # :25-26
         t_logit = self.t4(self.t3(torch.cat([deep, cross], dim=1)))              # :27-29

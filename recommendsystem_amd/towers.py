@@ -22,7 +22,7 @@ from torch import nn
 
 from . import _lib
 from ._lib import call, ptr, stream_handle
-from .layers import Dense, _act_code, _DenseFn
+from .layers import Dense, _act_code, _DenseFn, _row_major
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 
 
@@ -290,7 +290,7 @@ class _CrossFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, W, b = ctx.saved_tensors
         L = ctx.L
-        dy = dy.contiguous()
+        dy = _row_major(dy)
         M, D = x.shape
         dx = torch.empty(M, D, device=x.device, dtype=torch.float32)
         ws_n = int(_lib.load().rs_cross_bwd_workspace_floats(M, D, L))
@@ -298,7 +298,7 @@ class _CrossFn(torch.autograd.Function):
         block = grads_contiguous((W, b))
         dpar = block if block is not None else torch.empty(2 * L * D, device=x.device)
         call("rs_cross_bwd", stream_handle(), ptr(x), x.stride(0), M, D, L, ptr(W), ptr(b), ptr(dy),
-             D, ptr(dx), D, 0, ptr(dpar), 1 if block is not None else 0, ptr(ws), ws_n)
+             dy.stride(0), ptr(dx), D, 0, ptr(dpar), 1 if block is not None else 0, ptr(ws), ws_n)
         if block is not None:
             return dx, None, None, None
         dW, db = _split_grads((W, b), dpar)
@@ -511,10 +511,11 @@ class _MulFn(torch.autograd.Function):
     def backward(ctx, dy):
         a, g = ctx.saved_tensors
         M, N = a.shape
-        dy = dy.contiguous()
-        da, dg = torch.empty_like(a), torch.empty_like(g)
+        dy = _row_major(dy)
+        da = torch.empty(M, N, device=a.device, dtype=torch.float32)
+        dg = torch.empty(M, N, device=a.device, dtype=torch.float32)
         call("rs_mul_bwd", stream_handle(), ptr(a), a.stride(0), ptr(g), g.stride(0), M, N, ctx.scale,
-             ptr(dy), N, ptr(da), N, ptr(dg), N)
+             ptr(dy), dy.stride(0), ptr(da), N, ptr(dg), N)
         return da, dg, None
 
 

@@ -138,7 +138,7 @@ class StaytimeRoughRank(nn.Module):
             seqs.append(e)
             masks.append(m)
         st_loss = self.staytime.loss(emb, seqs, masks, y_stay, y_short, y_long, sw)
-        rr = self.rr_fields(rr_ids)[:, :, 0:16]
+        rr = self.rr_fields(rr_ids)           # [B, 52, 32]: the DSSM reads columns 0:16 per field
         return st_loss + self.dssm.loss(rr, mask, y_click)
 
 
