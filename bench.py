@@ -499,11 +499,17 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
         t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
     bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
     achieved = bwd_flops / t_bwd / 1e12
-    traffic = None
+    # HBM traffic is not measurable inside this run (PMC needs its own rocprofv3 --pmc passes):
+    # the value is the committed PMC measurement of the same launch, labelled as such
+    traffic, traffic_src = None, None
     tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")  # from tools/profile_round.sh
     if compute_dtype == "f32" and os.path.exists(tf_path):
         with open(tf_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+        if "bwd4" in tj.get("kernel", ""):
+            traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = ("committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes) "
+                           "in profiles/il_bwd_traffic.json, not measured in this run")
 
     samples = B * args.steps * world
     # BASELINE.md §3 step roofline: max(sum bytes / HBM BW, sum flops / peak), per GPU
@@ -538,6 +544,7 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
                                "forward's attention save + fused sparse push)",
                      "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "launch_us": round(t_bwd * 1e6, 2),
                      "flops_per_launch": bwd_flops},
         "il_fwd_us": round(t_fwd * 1e6, 2),

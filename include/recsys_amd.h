@@ -69,6 +69,18 @@ int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* 
                               int32_t* flag, int32_t* touched, int32_t* n_touched,
                               int32_t touched_cap);
 
+/* rs_sparse_grad_accumulate with a caller workspace of >= rs_sparse_push_workspace_bytes(B, F)
+ * bytes: single-hot pushes (offsets == NULL) claim rows by election (plain flag stores + a claim
+ * kernel, no returning atomics on hot rows' flag words; csrc/embedding.hip rs_push) -- same
+ * results and semantics.  Other shapes (multi-hot, unaligned dout) and a NULL / small workspace
+ * in list mode run rs_sparse_grad_accumulate.  Graph-capturable. */
+int64_t rs_sparse_push_workspace_bytes(int64_t B, int F);
+int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const int32_t* offsets,
+                                 int64_t B, int F, const float* dout, int64_t dout_ld,
+                                 int64_t dout_fstride, int dim, int combiner, float* grad_table,
+                                 int32_t* flag, int32_t* touched, int32_t* n_touched,
+                                 int32_t touched_cap, void* workspace, int64_t workspace_bytes);
+
 /* Deterministic variant of rs_sparse_grad_accumulate: sort by row + segmented sum,
  * so each touched row receives the sum of its occurrences in ascending id order with one plain
  * read-modify-write -- bitwise reproducible run to run (the atomic push reproduces only the row

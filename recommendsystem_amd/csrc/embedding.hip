@@ -361,6 +361,248 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single-hot push with claims by ELECTION (rs_sparse_grad_accumulate_ws, offsets == NULL).
+// PMC/timing (tools/push_prof.sh, config-4 history: 53 K ids over a 1 M-row table) split the
+// atomic push's 38 us: the returning flag CASes of list mode cost most of it -- every block
+// claims its hot rows, so the Zipf-hot rows' flag words take one returning CAS per block, and
+// those serialise at the memory side.  Here claims take no atomics on flag words:
+//   push:  block (field f, tile of samples) aggregates its occurrences in an LDS hash (one lane
+//          per occurrence probes; LP lanes per occurrence add its float4s with LDS atomics; all
+//          gradient loads issued before any add), then per distinct row: one global float-atomic
+//          row add, and -- unless the row is already claimed (flag == -2) -- a PLAIN store
+//          flag[row] = block id (the last store wins: exactly one block is elected per row) and
+//          the row goes to the block's candidate list in the workspace;
+//   claim: one block per push block re-reads its candidates; the elected block (flag == its id)
+//          claims the row (flag = -2) and appends it to touched with one n_touched atomic per
+//          block.  Single-hot tiles of T samples hold <= T distinct rows, so the 2T-slot LDS
+//          table never fills (no fallback path that could claim a row twice).
+// Scan mode (touched == NULL) skips the election and marks flag = -2 with plain stores.
+// Row set exact; fp32 summation order not fixed (as the CAS push).
+// ---------------------------------------------------------------------------------------------
+RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
+                                     int64_t B, int F, const float* dout, int64_t dout_ld,
+                                     int64_t dout_fstride, int dim, int combiner,
+                                     float* grad_table, int32_t* flag, int32_t* touched,
+                                     int32_t* n_touched, int32_t touched_cap);
+
+namespace rs_push {
+constexpr int kThreads = 256;
+constexpr int kTile = 256;                    // samples (= occurrences) per block
+constexpr int kCap = 2 * kTile;               // LDS hash slots: never full
+constexpr int kChunk = 4;                     // occurrences per lane group in flight
+
+__host__ __device__ constexpr size_t lds_bytes(int dim) {
+  return (4 + (size_t)kCap * (2 + dim) + 2 * (size_t)kTile) * 4;
+}
+
+template <int LP>
+__global__ void __launch_bounds__(kThreads) push_elect_kernel(
+    const int32_t* __restrict__ rows, int64_t B, int F, const float* __restrict__ dout,
+    int64_t dout_ld, int64_t dout_fstride, int dim, float sc, int tile,
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, int32_t* __restrict__ ws_cnt,
+    int32_t* __restrict__ ws_rows) {
+  extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+  int32_t* ctl = sm;                                       // [4]
+  int32_t* keys = ctl + 4;                                 // [kCap]
+  int32_t* orow = keys + kCap;                             // [kTile]
+  int32_t* oslot = orow + kTile;                           // [kTile]
+  float* vals = reinterpret_cast<float*>(oslot + kTile);  // [kCap][dim]
+  const int tid = threadIdx.x;
+  const int cap = 2 * tile;  // tile is a power of two <= kTile
+  for (int k = tid; k < cap; k += kThreads) keys[k] = -1;
+  for (int k = tid; k < cap * dim; k += kThreads) vals[k] = 0.f;
+  if (tid == 0) ctl[0] = 0;
+  const int f = blockIdx.y;
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * tile;
+  const int n = (int)((b0 + tile < B ? b0 + tile : B) - b0);
+  for (int i = tid; i < n; i += kThreads) orow[i] = rows[(b0 + i) * F + f];
+  __syncthreads();
+  for (int i = tid; i < n; i += kThreads) {
+    const int32_t row = orow[i];
+    int slot = -1;
+    if (row >= 0) {
+      int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));
+      for (;;) {  // cap > tile >= distinct rows: terminates
+        const int32_t old = atomicCAS(&keys[h], -1, row);
+        if (old == -1 || old == row) { slot = h; break; }
+        h = (h + 1) & (cap - 1);
+      }
+    }
+    oslot[i] = slot;
+  }
+  __syncthreads();
+  const int ng = kThreads / LP, g = tid / LP, l = tid % LP;
+  const int nvec = dim >> 2;
+  for (int i0 = g; i0 < n; i0 += ng * kChunk) {
+    float4 v[kChunk];
+    int slot[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) {
+      const int i = i0 + u * ng;
+      slot[u] = i < n ? oslot[i] : -1;
+      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (slot[u] >= 0 && l < nvec)
+        v[u] = reinterpret_cast<const float4*>(dout + (b0 + i) * dout_ld +
+                                               (int64_t)f * dout_fstride)[l];
+    }
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u) {
+      if (slot[u] < 0) continue;
+      const int i = i0 + u * ng;
+      for (int e4 = l; e4 < nvec; e4 += LP) {
+        const float4 t = e4 == l ? v[u]
+                                 : reinterpret_cast<const float4*>(
+                                       dout + (b0 + i) * dout_ld + (int64_t)f * dout_fstride)[e4];
+        float* d = vals + slot[u] * dim + 4 * e4;
+        atomicAdd(d + 0, t.x * sc); atomicAdd(d + 1, t.y * sc);
+        atomicAdd(d + 2, t.z * sc); atomicAdd(d + 3, t.w * sc);
+      }
+    }
+  }
+  __syncthreads();
+  // election (list mode): every slot's flag word is loaded at once (<= 2 per lane, all in
+  // flight), then the plain election stores and the candidate list; scan mode: plain marks
+  {
+    int32_t rw[kCap / kThreads], fl[kCap / kThreads];
+#pragma unroll
+    for (int u = 0; u < kCap / kThreads; ++u) {
+      const int slot = tid + u * kThreads;
+      rw[u] = slot < cap ? keys[slot] : -1;
+      fl[u] = (rw[u] >= 0 && ws_cnt) ? flag[rw[u]] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < kCap / kThreads; ++u) {
+      if (rw[u] < 0) continue;
+      if (!ws_cnt) {
+        scan_mark(flag, rw[u]);
+      } else if (fl[u] != -2) {  // not claimed by an earlier push: stand for election
+        flag[rw[u]] = blk;
+        ws_rows[(int64_t)blk * kCap + atomicAdd(&ctl[0], 1)] = rw[u];
+      }
+    }
+  }
+  // gradient rows: G2 lanes per row, one dword each
+  int G2 = 1;
+  while (G2 < dim && G2 < 64) G2 <<= 1;
+  const int per_pass = kThreads / G2, gs = tid / G2, l2 = tid % G2;
+  for (int slot = gs; slot < cap; slot += per_pass) {
+    const int32_t row = keys[slot];
+    if (row < 0) continue;
+    float* dst = grad_table + (int64_t)row * dim;
+    for (int e = l2; e < dim; e += G2) atomicAdd(dst + e, vals[slot * dim + e]);
+  }
+  if (ws_cnt) {
+    __syncthreads();
+    if (tid == 0) ws_cnt[blk] = ctl[0];
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) push_claim_kernel(
+    const int32_t* __restrict__ ws_cnt, const int32_t* __restrict__ ws_rows,
+    int32_t* __restrict__ flag, int32_t* __restrict__ touched, int32_t* __restrict__ n_touched,
+    int32_t touched_cap) {
+  __shared__ int32_t lidx[kCap];
+  __shared__ int32_t ctl[2];
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  const int cnt = ws_cnt[blk];
+  if (cnt == 0) return;
+  if (tid == 0) ctl[0] = 0;
+  __syncthreads();
+  const int32_t* cand = ws_rows + (int64_t)blk * kCap;
+  int32_t rw[kCap / kThreads], fl[kCap / kThreads];
+#pragma unroll
+  for (int u = 0; u < kCap / kThreads; ++u) {
+    const int e = tid + u * kThreads;
+    rw[u] = e < cnt ? cand[e] : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kCap / kThreads; ++u) fl[u] = rw[u] >= 0 ? flag[rw[u]] : -1;
+#pragma unroll
+  for (int u = 0; u < kCap / kThreads; ++u) {
+    const int e = tid + u * kThreads;
+    if (e >= cnt) continue;
+    int li = -1;
+    if (fl[u] == blk) {  // elected: this block claims the row
+      flag[rw[u]] = -2;
+      li = atomicAdd(&ctl[0], 1);
+    }
+    lidx[e] = li;
+  }
+  __syncthreads();
+  if (tid == 0) ctl[1] = ctl[0] > 0 ? atomicAdd(n_touched, ctl[0]) : 0;
+  __syncthreads();
+  const int base = ctl[1];
+  for (int e = tid; e < cnt; e += kThreads) {
+    const int li = lidx[e];
+    if (li >= 0 && base + li < touched_cap) touched[base + li] = cand[e];
+  }
+}
+
+// samples per block: kTile, smaller for small launches so they still spread over >= ~256 blocks
+inline int tile_for(int64_t B, int F) {
+  int t = kTile;
+  while (t > 32 && ((B + t - 1) / t) * (int64_t)F < 256) t >>= 1;
+  return t;
+}
+inline int64_t grid_blocks(int64_t B, int F) {
+  const int t = tile_for(B, F);
+  return ((B + t - 1) / t) * (int64_t)F;
+}
+
+}  // namespace rs_push
+
+RS_API int64_t rs_sparse_push_workspace_bytes(int64_t B, int F) {
+  if (B < 0 || F <= 0) return -1;
+  return rs_push::grid_blocks(B, F) * (1 + rs_push::kCap) * 4;
+}
+
+RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const int32_t* offsets,
+                                        int64_t B, int F, const float* dout, int64_t dout_ld,
+                                        int64_t dout_fstride, int dim, int combiner,
+                                        float* grad_table, int32_t* flag, int32_t* touched,
+                                        int32_t* n_touched, int32_t touched_cap, void* workspace,
+                                        int64_t workspace_bytes) {
+  using namespace rs_push;
+  const bool ok_shape = !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
+                        ((uintptr_t)dout & 15) == 0 && lds_bytes(dim) <= 160 * 1024 &&
+                        B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;
+  if (!ok_shape || (touched && (!workspace || workspace_bytes < rs_sparse_push_workspace_bytes(B, F))))
+    return rs_sparse_grad_accumulate(stream, rows, offsets, B, F, dout, dout_ld, dout_fstride, dim,
+                                     combiner, grad_table, flag, touched, n_touched, touched_cap);
+  if (!rows || !dout || !grad_table || !flag || F <= 0 || dim <= 0) return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
+  if (B * (int64_t)F == 0) return RS_OK;
+  hipStream_t s = rs_stream(stream);
+  const int64_t nblk = grid_blocks(B, F);
+  int32_t* ws_cnt = touched ? static_cast<int32_t*>(workspace) : nullptr;
+  int32_t* ws_rows = touched ? ws_cnt + nblk : nullptr;
+  const float sc = 1.0f;  // one id per segment: every combiner scales by 1
+  (void)combiner;
+  int LP = 1;
+  while (LP < dim / 4 && LP < 64) LP <<= 1;
+  const int tile = tile_for(B, F);
+  dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
+  const size_t lds = lds_bytes(dim);
+#define RS_PUSH_E(LL)                                                                             \
+  case LL:                                                                                        \
+    push_elect_kernel<LL><<<grid, kThreads, lds, s>>>(rows, B, F, dout, dout_ld, dout_fstride,   \
+                                                      dim, sc, tile, grad_table, flag, ws_cnt,   \
+                                                      ws_rows);                                  \
+    break;
+  switch (LP) {
+    RS_PUSH_E(1) RS_PUSH_E(2) RS_PUSH_E(4) RS_PUSH_E(8) RS_PUSH_E(16) RS_PUSH_E(32) RS_PUSH_E(64)
+    default: return RS_ERR_UNSUPPORTED;
+  }
+#undef RS_PUSH_E
+  if (touched)
+    push_claim_kernel<<<(unsigned)nblk, kThreads, 0, s>>>(ws_cnt, ws_rows, flag, touched, n_touched,
+                                                          touched_cap);
+  return rs_status_after_launch();
+}
+
+
 RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
                                      int64_t B, int F, const float* dout, int64_t dout_ld,
                                      int64_t dout_fstride, int dim, int combiner,

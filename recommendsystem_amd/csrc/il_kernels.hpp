@@ -89,6 +89,7 @@ struct BwdReq {
 };
 
 constexpr int kMaxFwdWaves = 4;
+constexpr int kFwdSpreadBlocks = 512;
 constexpr int kMaxBwdWaves = 2;
 #ifndef RS_IL_BWD_GRID
 #define RS_IL_BWD_GRID 1536
@@ -1813,7 +1814,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD3_OCC) bwd3_kernel(
   auto x_src = [&](int64_t bb, int itx) -> const float* {
     return itx == 0 ? x + bb * F * C::E : xsave + ((int64_t)(itx - 1) * a.B + bb) * F * C::U;
   };
-  const int64_t b_first = (int64_t)blockIdx.x * kWpb3 + w;
+  // wave w of block k starts at sample k + w * grid: below 4 * grid samples the active waves
+  // spread over every block (every CU) instead of filling the first blocks (bwd3_grid)
+  const int64_t b_first = (int64_t)blockIdx.x + (int64_t)gridDim.x * w;
   const int64_t b_step = (int64_t)gridDim.x * kWpb3;
   if (b_first < a.B) {  // the first sample's input rows and dy (dy_vec: rows 16-B aligned)
     glds_copy_wave(X, x_src(b_first, a.L - 1), nx4);
@@ -2427,7 +2430,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
   auto s_src = [&](int64_t bb, int itx) -> const float* {
     return a.osave_in + ((int64_t)itx * a.B + bb) * sv;
   };
-  const int64_t b_first = (int64_t)blockIdx.x * kWpb3 + w;
+  // wave w of block k starts at sample k + w * grid: below 4 * grid samples the active waves
+  // spread over every block (every CU) instead of filling the first blocks (bwd3_grid)
+  const int64_t b_first = (int64_t)blockIdx.x + (int64_t)gridDim.x * w;
   const int64_t b_step = (int64_t)gridDim.x * kWpb3;
   if (b_first < a.B) {
     glds_copy_wave(XB, x_src(b_first, a.L - 1), nx4);
@@ -2797,6 +2802,10 @@ RS_UNROLL(RS_IL4_UNROLL_K)
 // one resident round of v3 blocks on MI355X (2 per CU x 256 CUs); callers size the per-block
 // partial rows with rs_il_bwd_partial_blocks, which applies the same rule
 constexpr int kBwd3Grid = 512;
+// v3 / v4 grid: one block per sample up to kBwd3Grid samples (one active wave per block, the
+// blocks spread over every CU -- B = 512 runs one wave on each of 512 SIMDs instead of four per
+// CU on 128 CUs), then kBwd3Grid blocks whose waves take every (grid)th sample
+__host__ __forceinline__ int64_t bwd3_grid(int64_t B) { return B < kBwd3Grid ? B : kBwd3Grid; }
 
 // grid-level reduction of the per-block partials, fixed order (deterministic); interacting.hip
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
@@ -2819,6 +2828,12 @@ int fwd_launch(const FwdReq& q) {
   int wpb = (int)(kLdsBytes / per_wave);
   if (wpb > kMaxFwdWaves) wpb = kMaxFwdWaves;
   if (wpb < 1) return RS_ERR_UNSUPPORTED;
+  // small batches: fewer waves per block so the samples spread over >= 512 blocks (all CUs)
+  // instead of filling B / wpb blocks
+  if (q.B < (int64_t)kFwdSpreadBlocks * wpb) {
+    const int64_t w = q.B / kFwdSpreadBlocks;
+    wpb = w < 1 ? 1 : (int)w;
+  }
   int64_t grid = (q.B + wpb - 1) / wpb;
   if (grid > 4096) grid = 4096;
   if (grid == 0) return RS_OK;
@@ -2844,7 +2859,7 @@ int bwd_launch(const BwdReq& q) {
     if (q.asave && a.dy_vec && lds3 <= kLdsBytes / 2 && lds4 <= kLdsBytes / 2 &&
         (size_t)C::NPARAM * 4 <= lds4 && q.F <= C::FMAX && q.F >= 1) {
       // same grid rule as v3 (rs_il_bwd_partial_blocks answers for both)
-      int64_t grid = (q.B + kWpb3 - 1) / kWpb3;
+      int64_t grid = bwd3_grid(q.B);
       const int64_t max_grid = q.workspace_floats / C::NPARAM;
       if (grid > kBwd3Grid) grid = kBwd3Grid;
       if (grid > max_grid) grid = max_grid;
@@ -2862,7 +2877,7 @@ int bwd_launch(const BwdReq& q) {
   {  // v3 (one wave per sample, no workgroup barriers) when its LDS gives 2 blocks per CU
     const size_t lds3 = bwd3_lds_bytes<C>(q.F);
     if (a.dy_vec && lds3 <= kLdsBytes / 2 && (size_t)C::NPARAM * 4 <= lds3) {
-      int64_t grid = (q.B + kWpb3 - 1) / kWpb3;
+      int64_t grid = bwd3_grid(q.B);
       const int64_t max_grid = q.workspace_floats / C::NPARAM;
       if (grid > kBwd3Grid) grid = kBwd3Grid;
       if (grid > max_grid) grid = max_grid;

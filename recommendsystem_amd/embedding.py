@@ -91,6 +91,7 @@ class SparseTable:
         # reproducible) instead of the LDS-hash + float-atomic push; workspace grown on demand
         self.deterministic = False
         self._sorted_ws = None
+        self._push_ws = None
         # autograd anchor: lets the lookup's backward run (it returns no dense gradient)
         self.anchor = torch.zeros((), device=device, dtype=torch.float32, requires_grad=True)
 
@@ -131,10 +132,19 @@ class SparseTable:
                  ptr(self.flag), None if scan else ptr(self.touched),
                  None if scan else ptr(self.n_touched), self.touched_cap, ptr(ws), ws.numel(), n)
             return
-        call("rs_sparse_grad_accumulate", stream_handle(), ptr(rows), ptr(offsets), B, F, ptr(dout),
-             dout_ld, dout_fstride, self.dim, combiner, ptr(self.grad), ptr(self.flag),
+        # single-hot list-mode pushes claim rows by election (csrc/embedding.hip rs_push): a
+        # workspace of candidate rows per push block, kept and grown on demand (a captured graph
+        # reuses the one its warm-up step allocated)
+        ws, wsn = None, 0
+        if offsets is None and not scan:
+            need = int(_lib.load().rs_sparse_push_workspace_bytes(B, F))
+            if self._push_ws is None or self._push_ws.numel() < need:
+                self._push_ws = torch.empty(need, device=self.weight.device, dtype=torch.uint8)
+            ws, wsn = ptr(self._push_ws), self._push_ws.numel()
+        call("rs_sparse_grad_accumulate_ws", stream_handle(), ptr(rows), ptr(offsets), B, F,
+             ptr(dout), dout_ld, dout_fstride, self.dim, combiner, ptr(self.grad), ptr(self.flag),
              None if scan else ptr(self.touched), None if scan else ptr(self.n_touched),
-             self.touched_cap)
+             self.touched_cap, ws, wsn)
 
     def sorted_workspace(self, n_ids: int) -> torch.Tensor:
         """Workspace of the deterministic push for n_ids ids (kept and reused; reserve the

@@ -100,6 +100,56 @@ def test_sparse_push_and_adam():
     assert float(table.grad.abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("mode", ["list", "scan"])
+def test_single_hot_election_push(mode):
+    """Single-hot pushes over ONE shared row space (the DIN history / config-5 shape): many push
+    blocks see the same Zipf-hot rows and claim them by election (rs_sparse_grad_accumulate_ws).
+    A multi-hot push claims some rows first (CAS path) in the same step.  The touched list holds
+    every row exactly once, the gradients equal the oracle sums, and the step leaves flags clean."""
+    from recommendsystem_amd.embedding import SparseAdam, SparseTable
+    rng = np.random.default_rng(11)
+    B, F, dim, rows_n = 700, 5, 16, 300          # 3 sample tiles x 5 fields = 15 push blocks
+    t = SparseTable(rows_n, dim, SparseAdam(1e-2), device=DEV, seed=3)
+    t.mode = mode
+    ids = np.minimum(rng.zipf(1.1, size=(B, F)) - 1, rows_n - 1).astype(np.int32)
+    ids[rng.uniform(size=(B, F)) < 0.2] = -1     # padded positions push nothing
+    lens = rng.integers(0, 3, size=40)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    mh = rng.integers(0, rows_n, size=int(offs[-1])).astype(np.int32)
+    d_mh = torch.randn(40, dim, device=DEV)
+    d_sh = torch.randn(B, F * dim, device=DEV)
+    W0 = t.weight.cpu().numpy().astype(np.float64)
+    t.accumulate(torch.from_numpy(mh).to(DEV), torch.from_numpy(offs).to(DEV), 40, 1, d_mh, dim, dim, 0)
+    t.accumulate(torch.from_numpy(ids.reshape(-1)).to(DEV), None, B, F, d_sh, F * dim, dim, 0)
+    torch.cuda.synchronize()
+    gref = {}
+    dm, ds = _np(d_mh), _np(d_sh).reshape(B, F, dim)
+    for s_ in range(40):
+        for k in range(offs[s_], offs[s_ + 1]):
+            gref[int(mh[k])] = gref.get(int(mh[k]), 0) + dm[s_]
+    for b in range(B):
+        for f in range(F):
+            if ids[b, f] >= 0:
+                gref[int(ids[b, f])] = gref.get(int(ids[b, f]), 0) + ds[b, f]
+    if mode == "list":
+        n = int(t.n_touched[0].item())
+        lst = t.touched[:n].cpu().numpy().tolist()
+        assert len(lst) == len(set(lst)), "a row was claimed twice"
+        assert set(lst) == set(gref)
+    else:
+        assert _scan_marked(t.flag, t.rows) == set(gref)
+    G = t.grad.cpu().numpy()
+    for r, g in gref.items():
+        assert_close(G[r], g, 1e-5, 1e-5, what=f"grad row {r}")
+    t.step()
+    torch.cuda.synchronize()
+    W1 = t.weight.cpu().numpy()
+    for r, g in gref.items():
+        w, _, _ = npo.adam_sparse(W0[r], g, np.zeros(dim), np.zeros(dim), 1e-2)
+        assert_close(W1[r], w, 1e-5, 1e-4, what=f"adam row {r}")
+    assert bool((t.flag == -1).all()) and float(t.grad.abs().max()) == 0.0
+
+
 def _scan_marked(flag, nrows):
     """Rows marked by a scan-mode push (flag = -2; clean = -1)."""
     f = flag.cpu().numpy()

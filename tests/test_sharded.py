@@ -78,8 +78,8 @@ def _host_call(name, *a):
         rows_out.copy_(torch.from_numpy(r.reshape(-1).astype(np.int32)))
         mask.copy_(torch.from_numpy(m.astype(np.uint8)))
         lengths.copy_(torch.from_numpy(m.sum(1).astype(np.int32)))
-    elif name == "rs_sparse_grad_accumulate":
-        _, rows, offsets, B, F, dout, ld, fs, dim, comb, grad, flag, touched, n_t, cap = a
+    elif name in ("rs_sparse_grad_accumulate", "rs_sparse_grad_accumulate_ws"):
+        _, rows, offsets, B, F, dout, ld, fs, dim, comb, grad, flag, touched, n_t, cap = a[:15]
         assert offsets is None and F == 1
         r = rows.long()
         ok = r >= 0

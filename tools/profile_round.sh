@@ -10,7 +10,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --kernel-reps 50 > gpurun_out/$R/bench_traced.log 2>&1 || exit $?
 echo traced ok
 for c in FETCH_SIZE WRITE_SIZE; do
-  IL_BENCH_ONLY=push_hot_base REPS=10 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d gpurun_out/$R/pmc_$c -o run -- \
+  IL_BENCH_ONLY=push_hot_base_saved REPS=10 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d gpurun_out/$R/pmc_$c -o run -- \
     python3 tools/il_bench.py > gpurun_out/$R/pmc_$c.log 2>&1 || exit $?
   echo pmc $c ok
 done
