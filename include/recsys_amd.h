@@ -171,6 +171,14 @@ int rs_sparse_compact(void* stream, float* grad_table, int32_t* flag, const int3
 int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* grads, int32_t count,
                          int dim, float* grad_table, int32_t* flag, int32_t* touched,
                          int32_t* n_touched, int32_t touched_cap);
+/* rs_sparse_merge_rows with the counts on the device (the graph-captured DP step of the generic
+ * trainer): every rank's compacted list was all-gathered as a prefix of nmax = max_r count_r
+ * entries (rows_all[r * nmax], grads_all[r * nmax * dim]); counts[r * counts_stride] is rank r's
+ * count; cap bounds every count (the per-rank list capacity).  Adds rank `rank`'s list. */
+int rs_sparse_merge_rows_dev(void* stream, const int32_t* rows_all, const float* grads_all,
+                             const int32_t* counts, int64_t counts_stride, int world, int rank,
+                             int32_t cap, int dim, float* grad_table, int32_t* flag,
+                             int32_t* touched, int32_t* n_touched, int32_t touched_cap);
 
 /* Packed scan-mode exchange (the graph-captured DP step of the AutoInt trainer; same role as
  * compact/merge above).  pack: every marked row becomes one record [row (int32 bits) | grad[dim]]

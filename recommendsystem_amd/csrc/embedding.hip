@@ -565,7 +565,8 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
                                         int32_t* n_touched, int32_t touched_cap, void* workspace,
                                         int64_t workspace_bytes) {
   using namespace rs_push;
-  const bool ok_shape = !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
+  static const bool elect_off = getenv("RS_PUSH_NO_ELECT") != nullptr;  // A/B: the CAS push
+  const bool ok_shape = !elect_off && !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
                         ((uintptr_t)dout & 15) == 0 && lds_bytes(dim) <= 160 * 1024 &&
                         B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;
   if (!ok_shape || (touched && (!workspace || workspace_bytes < rs_sparse_push_workspace_bytes(B, F))))

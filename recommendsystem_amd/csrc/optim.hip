@@ -452,10 +452,22 @@ __global__ void __launch_bounds__(256) sparse_compact_kernel(
 __global__ void __launch_bounds__(256) sparse_merge_kernel(
     const int32_t* __restrict__ rows, const float* __restrict__ grads, int32_t count, int dim,
     int lps, float* __restrict__ grad_table, int32_t* __restrict__ flag,
-    int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
+    int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap,
+    const int32_t* __restrict__ counts, int64_t cstride, int world, int rank) {
   // one global n_touched atomic per block (see sparse_grad_accum_kernel)
   __shared__ int32_t nclaim, base;
   __shared__ int32_t lidx[256];
+  if (counts) {
+    // device counts (rs_sparse_merge_rows_dev): every rank's list was gathered as a prefix of
+    // nmax = max_r count_r entries, count is this launch's upper bound on every count
+    int nmax = 0;
+    for (int r = 0; r < world; ++r) nmax = max(nmax, counts[r * cstride]);
+    nmax = min(nmax, count);
+    const int n = min(counts[rank * cstride], nmax);
+    rows += (int64_t)rank * nmax;
+    grads += (int64_t)rank * nmax * dim;
+    count = n;
+  }
   const int per_block = blockDim.x / lps;
   const int gi = threadIdx.x / lps;
   const int l = threadIdx.x % lps;
@@ -507,7 +519,27 @@ RS_API int rs_sparse_merge_rows(void* stream, const int32_t* rows, const float* 
   int64_t grid = ((int64_t)count * lps + 255) / 256;
   if (grid > 4096) grid = 4096;
   sparse_merge_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(
-      rows, grads, count, dim, lps, grad_table, flag, touched, n_touched, touched_cap);
+      rows, grads, count, dim, lps, grad_table, flag, touched, n_touched, touched_cap, nullptr, 0,
+      1, 0);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_merge_rows_dev(void* stream, const int32_t* rows_all, const float* grads_all,
+                                    const int32_t* counts, int64_t counts_stride, int world,
+                                    int rank, int32_t cap, int dim, float* grad_table,
+                                    int32_t* flag, int32_t* touched, int32_t* n_touched,
+                                    int32_t touched_cap) {
+  if (!rows_all || !grads_all || !counts || !grad_table || !flag || dim <= 0 || world <= 0 ||
+      rank < 0 || rank >= world || counts_stride <= 0 || cap < 0)
+    return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
+  if (cap == 0) return RS_OK;
+  const int lps = lanes_for_dim(dim);
+  int64_t grid = ((int64_t)cap * lps + 255) / 256;  // sized for the largest count; extra blocks exit
+  if (grid > 4096) grid = 4096;
+  sparse_merge_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(
+      rows_all, grads_all, cap, dim, lps, grad_table, flag, touched, n_touched, touched_cap, counts,
+      counts_stride, world, rank);
   return rs_status_after_launch();
 }
 

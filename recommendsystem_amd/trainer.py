@@ -116,16 +116,7 @@ class Trainer:
             for t in self.tables:
                 if not is_sharded(t):
                     exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])
-        scale = 1.0 / self.world
-        if self.on_dense_grad is not None:
-            self.on_dense_grad(self.arena.grad, scale)
-        for off, n, lr, cnt in self.segments:
-            a = 4 * off
-            call("rs_dense_adam", s, self.arena.data.data_ptr() + a, self.arena.grad.data_ptr() + a,
-                 self.m.data_ptr() + a, self.v.data_ptr() + a, n, ptr(cnt), lr, self.b1, self.b2,
-                 self.eps, scale, 1)
-        for t in self.tables:
-            t.step(grad_scale=scale)
+        self._optimize(1.0 / self.world)
         return loss
 
     # ---- HIP-graph replay of whole steps (single GPU) --------------------------------------
@@ -137,15 +128,97 @@ class Trainer:
             out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]
         return out
 
+    # ---- data parallel, graph-captured (capture_pool at world > 1) -----------------------
+    # per step: graph A (forward, backward, regularisers, every replicated table's touched rows
+    # compacted into its send list, the counts into dp_counts) -> eager collectives (the dense
+    # all-reduce, ONE all-gather of all tables' counts, ONE host read of the per-table maxima,
+    # one all-gather per table of nmax rows / gradient rows) -> graph B (rank-ordered merges that
+    # read the counts on the device, rs_sparse_merge_rows_dev; dense Adam; sparse optimizers).
+    def _dp_setup(self):
+        dev = self.arena.data.device
+        self._rep = [t for t in self.tables if not is_sharded(t)]
+        if len(self._rep) != len(self.tables):
+            raise NotImplementedError("graph capture under DP needs replicated tables (owner-sharded "
+                                      "tables exchange host-sized all-to-alls inside backward)")
+        T = len(self._rep)
+        self.dp_counts = torch.zeros(max(T, 1), device=dev, dtype=torch.int32)
+        self.dp_counts_all = torch.zeros(self.world * max(T, 1), device=dev, dtype=torch.int32)
+        self.dp_all = [(torch.empty(self.world * t.touched_cap, device=dev, dtype=torch.int32),
+                        torch.empty(self.world * t.touched_cap * t.dim, device=dev))
+                       for t in self._rep]
+
+    def _dp_pack(self):
+        s = stream_handle()
+        for ti, t in enumerate(self._rep):
+            rows, grads = self.xbuf[id(t)]
+            self.dp_counts[ti:ti + 1].copy_(t.n_touched[:1])
+            call("rs_sparse_compact", s, ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched),
+                 t.dim, ptr(rows), ptr(grads), t.touched_cap)
+            t.n_touched[:1].zero_()
+
+    def _dp_exchange(self):
+        from .dist import _all_gather_flat, allreduce_flat
+        allreduce_flat(self.arena.grad, self.pg)
+        if not self._rep:
+            return
+        _all_gather_flat(self.dp_counts_all, self.dp_counts, self.pg)
+        T = len(self._rep)
+        nmax = self.dp_counts_all.view(self.world, T).max(0).values.tolist()  # the host sync
+        for ti, t in enumerate(self._rep):
+            n = int(nmax[ti])
+            if n > t.touched_cap:
+                raise RuntimeError(f"sparse exchange: {n} rows > touched capacity {t.touched_cap}")
+            if n == 0:
+                continue
+            rows, grads = self.xbuf[id(t)]
+            rows_all, grads_all = self.dp_all[ti]
+            _all_gather_flat(rows_all[:self.world * n], rows[:n], self.pg)
+            _all_gather_flat(grads_all[:self.world * n * t.dim], grads[:n].reshape(-1), self.pg)
+
+    def _dp_merge_optimize(self):
+        s = stream_handle()
+        T = len(self._rep)
+        for ti, t in enumerate(self._rep):
+            rows_all, grads_all = self.dp_all[ti]
+            for r in range(self.world):  # rank order -> identical sums on every replica
+                call("rs_sparse_merge_rows_dev", s, ptr(rows_all), ptr(grads_all),
+                     self.dp_counts_all.data_ptr() + 4 * ti, T, self.world, r, t.touched_cap, t.dim,
+                     ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched), t.touched_cap)
+        self._optimize(1.0 / self.world)
+
+    def _optimize(self, scale):
+        s = stream_handle()
+        if self.on_dense_grad is not None:
+            self.on_dense_grad(self.arena.grad, scale)
+        for off, n, lr, cnt in self.segments:
+            a = 4 * off
+            call("rs_dense_adam", s, self.arena.data.data_ptr() + a, self.arena.grad.data_ptr() + a,
+                 self.m.data_ptr() + a, self.v.data_ptr() + a, n, ptr(cnt), lr, self.b1, self.b2,
+                 self.eps, scale, 1)
+        for t in self.tables:
+            t.step(grad_scale=scale)
+
+    def _forward_backward(self, *batch):
+        for mod in self._il_layers:
+            mod._calls = 0
+        with _lib.seed_offset(self.step_count):
+            loss = self.model.loss(*batch)
+            loss.backward()
+        s = stream_handle()
+        for p, l1, l2 in self.regs:
+            call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
+        return loss
+
     def capture_pool(self, batches, warmup: int = 1) -> None:
         """Record one whole training step per device-resident batch (forward, autograd backward,
         regularisers, dense Adam, sparse optimizer) into its own HIP graph; step_pool(i) replays
         batch i with no host work.  All graphs share one memory pool and are replayed in capture
         order (cyclic), which is what makes sharing it safe.  ``warmup`` eager steps run first
-        (first-call allocations) and are rolled back, so capture changes no training state."""
+        (first-call allocations) and are rolled back, so capture changes no training state.
+        Data parallel (world > 1): per batch a forward/backward graph (ending with the sparse
+        lists packed), the collectives eager, then ONE merge + optimizer graph (_dp_* above)."""
         if self.world > 1:
-            raise NotImplementedError("graph capture of the generic trainer is single-GPU (the "
-                                      "data-parallel exchange reads counts on the host)")
+            self._dp_setup()
         saved = [t.clone() for t in self._state()]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -161,11 +234,23 @@ class Trainer:
         for b in batches:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
-                loss = self.step(*b)
+                if self.world > 1:
+                    loss = self._forward_backward(*b)
+                    self._dp_pack()
+                else:
+                    loss = self.step(*b)
             self.graphs.append(g)
             self.graph_loss.append(loss.detach())
+        self.graph_opt = None
+        if self.world > 1:
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt):  # allocates nothing
+                self._dp_merge_optimize()
 
     def step_pool(self, i: int):
         k = i % len(self.graphs)
         self.graphs[k].replay()
+        if self.graph_opt is not None:
+            self._dp_exchange()
+            self.graph_opt.replay()
         return self.graph_loss[k]

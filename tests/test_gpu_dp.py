@@ -182,6 +182,8 @@ def _worker_trainer(rank, world, port, out):
     d.table.check_overflow()
     params = torch.cat([p.detach().reshape(-1).cpu() for p in d.parameters()]).numpy()
     out[rank] = (params, d.table.weight.cpu().numpy(), grads)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def _record_grads(d, trn):
@@ -201,8 +203,6 @@ def _ill(got, want):
         a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
         ill |= np.abs(a - b) > 1e-3 * np.abs(b)
     return ill
-    dist.barrier()
-    dist.destroy_process_group()
 
 
 def test_dp_generic_trainer_two_ranks():

@@ -1,0 +1,86 @@
+"""GPU, world size 2 on one device (gloo transport): the generic Trainer's graph-captured
+data-parallel step (Trainer.capture_pool at world > 1: a forward/backward graph per batch that
+ends with every table's touched rows compacted, eager collectives with one host read of the
+per-table maxima, then one graph of rank-ordered merges reading the counts on the device
+(rs_sparse_merge_rows_dev) + dense Adam + the sparse optimizer) equals the eager DP step
+(Trainer.step: host-counted compact / all-gather / rs_sparse_merge_rows), for the config-4 DIN
+harness and the config-5 staytime + rough_rank joint model.  Tables run the deterministic push
+(sorted segmented sums), so the two paths add the same numbers in the same order.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD, STEPS = 2, 3
+DEV = torch.device("cuda", 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _build(kind, rank):
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import DINPool, StaytimeRoughRank, din_batch, staytime_batch
+    rng = np.random.default_rng(70 + rank)
+    if kind == "din":
+        m = DINPool(vocab=500, T=20, device=DEV, seed=2)
+        m.table.optimizer.learning_rate = 1e-2
+        batches = [din_batch(rng, 64, 20, 500, DEV) for _ in range(2)]
+        trn = Trainer(m, 1e-2, [m.table], process_group=dist.group.WORLD)
+    else:
+        m = StaytimeRoughRank(rows=20_011, device=DEV, seed=3)
+        batches = [staytime_batch(rng, 64, m, DEV) for _ in range(2)]
+        trn = Trainer(m, 5e-4, [m.table], process_group=dist.group.WORLD)
+    m.table.deterministic = True
+    return m, trn, batches
+
+
+def _snapshot(m):
+    params = torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()]).numpy()
+    return params, m.table.weight.cpu().numpy()
+
+
+def _worker(rank, world, port, kind, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, trn, batches = _build(kind, rank)
+    eager_losses = [float(trn.step(*batches[s % 2])) for s in range(STEPS)]
+    torch.cuda.synchronize()
+    eager = _snapshot(m)
+    m, trn, batches = _build(kind, rank)
+    trn.capture_pool(batches, warmup=1)
+    assert trn.graph_opt is not None and len(trn.graphs) == 2
+    graph_losses = [float(trn.step_pool(s)) for s in range(STEPS)]
+    torch.cuda.synchronize()
+    m.table.check_overflow()
+    out[rank] = (eager_losses, eager, graph_losses, _snapshot(m))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["din", "staytime"])
+def test_dp_trainer_graph_equals_eager(kind):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(WORLD, _free_port(), kind, out), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        el, (ep, et), gl, (gp, gt) = out[r]
+        np.testing.assert_allclose(gl, el, rtol=1e-6, err_msg=f"rank {r} losses")
+        np.testing.assert_allclose(gp, ep, rtol=1e-6, atol=1e-7, err_msg=f"rank {r} dense params")
+        np.testing.assert_allclose(gt, et, rtol=1e-6, atol=1e-7, err_msg=f"rank {r} table")
+    assert np.array_equal(out[0][3][0], out[1][3][0]), "graph DP: dense replicas diverged"
+    assert np.array_equal(out[0][3][1], out[1][3][1]), "graph DP: table replicas diverged"

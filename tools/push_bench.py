@@ -7,6 +7,7 @@ the sparse optimizer run in between (flags / gradient rows reset as in a trainin
           Zipf(1.1), lengths U{1..100} (padded positions row -1), list mode
   c4_q    config 4: the query push, B = 1024 single-hot
   c2      config 2: B = 4096 x 26 single-hot fields over 26 x 100 k, dim 16, scan mode
+  c5      config 5: B = 2048 x 91 single-hot hashed fields over one 10 M x 32 table, list mode
 
 python tools/push_bench.py [--reps N] [--only c3,c4_hist]  -> one JSON line
 """
@@ -71,7 +72,19 @@ def case_c2(rng, dev):
     return t, lambda: t.accumulate(r, None, B, F, dout, F * D, D, 0), rows
 
 
-CASES = {"c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2}
+def case_c5(rng, dev):
+    """config 5: the 91 staytime fields, B = 2048, hashed Zipf(1.2) ids over one 10 M x 32 table"""
+    B, F, V, D = 2048, 91, 10_000_000, 32
+    ids = zipf(rng, (B, F), 1 << 40, 1.2).astype(np.uint64)
+    rows = ((ids * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(20)) % np.uint64(V)
+    rows = rows.astype(np.int32)
+    t = SparseTable(V, D, SparseAdam(1e-3), device=dev, max_touched=B * 400)
+    dout = torch.randn(B, F * D, device=dev)
+    r = torch.from_numpy(rows.reshape(-1)).to(dev)
+    return t, lambda: t.accumulate(r, None, B, F, dout, F * D, D, 1), rows
+
+
+CASES = {"c5": case_c5, "c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2}
 
 
 def main():
