@@ -310,6 +310,18 @@ int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, const fl
                const float* b2, const float* probs, const float* dout, int64_t dout_ld,
                float* dq, int64_t dq_ld, float* dkeys, float* dvalues, float* dparams,
                int dparams_accumulate, float* workspace, int64_t workspace_floats);
+/* rs_din_bwd with dkeys / dvalues rows at stride dkv_rs (>= H) and columns H .. dkv_width - 1 of
+ * every row written as zeros (dkv_width <= min(dkv_rs, 2H)): the gradient of a wider facts row
+ * whose first H columns the pooling reads (staytime: 32-wide sequence rows, VideoDnn.py:57-77),
+ * without a zero fill and a strided copy.  rs_din_bwd = this with dkv_rs = dkv_width = H. */
+int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
+                       int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
+                       int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
+                       int64_t mask_ld, const float* W1, const float* b1, const float* W2,
+                       const float* b2, const float* probs, const float* dout, int64_t dout_ld,
+                       float* dq, int64_t dq_ld, float* dkeys, float* dvalues, int64_t dkv_rs,
+                       int dkv_width, float* dparams, int dparams_accumulate, float* workspace,
+                       int64_t workspace_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H4/H5/H8/H9  Keras Dense(units, activation) towers (autoint:36-52 MultiLayerDense,
@@ -424,6 +436,13 @@ int rs_row_select(void* stream, const float* mask, const float* A, int64_t lda, 
  * hi = 1 - eps.  loss_rows[m] = w_m sum_t ce (nullable), dP = gscale w_m dce/dp (nullable). */
 int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, int T, float lo, float hi,
                 float log_eps, const float* W, float gscale, float* loss_rows, float* dP);
+
+/* Fused loss total (staytime/model.py:85-89 loss_weights, rough_rank/model.py:210-214):
+ * out[0] = sum_k w_k * sum_i X[k*seg + i] over nseg <= 6 back-to-back per-row loss vectors
+ * (rs_bce_rows / rs_softmax_kl / rs_mse_rows rows; w_k = loss_weight_k / batch).  One launch,
+ * fixed summation order. */
+int rs_weighted_row_sum(void* stream, const float* X, int64_t seg, int nseg, float w0, float w1,
+                        float w2, float w3, float w4, float w5, float* out);
 
 /* N1  staytime parse_input_func labels (staytime/parse.py:16-71) for a batch of B samples:
  * label [B, ld] rows = nbins Gaussian soft-label bins (sigma, width = (right - left)/(nbins - 1))
@@ -550,6 +569,12 @@ int rs_gather_columns(void* stream, const float* src, int64_t src_ld, int64_t B,
  * twice in a plan receives both gradients). */
 int rs_scatter_add_columns(void* stream, const float* dout, int64_t out_ld, int64_t B,
                            const int32_t* cols, int ncols, float* dsrc, int64_t src_ld);
+/* The backward of several column gathers from ONE source, as one gather: out[b, c] = sum_k
+ * (map[k*ncols + c] >= 0 ? srcs[k][b*src_lds[k] + map[k*ncols + c]] : 0), every out element
+ * written once.  srcs / src_lds are HOST arrays (nsrc <= 8) of device pointers / row strides;
+ * map is a device int32 [nsrc, ncols].  (staytime trunk fan-out, VideoDnn.py:45-47,57-77,127) */
+int rs_gather_sum_columns(void* stream, int nsrc, const float* const* srcs, const int64_t* src_lds,
+                          const int32_t* map, int64_t B, int ncols, float* out, int64_t out_ld);
 /* SENet squeeze tf.reduce_mean(emb, axis=1, keepdims=True) per structure field
  * (rank/ctr/model_init.py:22-24): out[b*out_ld + f] = mean(x[b, seg[f] .. seg[f+1])). */
 int rs_segment_mean(void* stream, const float* x, int64_t x_ld, int64_t B, const int32_t* seg,

@@ -85,6 +85,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_din_bwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32, _i32,
                           _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                           _vp, _i32, _vp, _i64]),
+    "rs_din_bwd_strided": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32,
+                                  _i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                  _i64, _vp, _vp, _i64, _i32, _vp, _i32, _vp, _i64]),
     "rs_gate_mix_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
                                _vp, _i64, _vp, _i64]),
     "rs_gate_mix_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
@@ -120,6 +123,7 @@ SIGNATURES: dict[str, tuple] = {
     "rs_act_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "rs_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "rs_bce_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _f32, _vp, _vp]),
+    "rs_weighted_row_sum": (_i32, [_vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _f32, _vp]),
     "rs_staytime_labels": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _f32, _f32, _f32, _vp, _i64,
                                   _vp, _vp, _vp]),
     "rs_mlp_head_param_floats": (_i64, [_i32, _i32, _i32, _i32, _i32]),
@@ -150,6 +154,7 @@ SIGNATURES: dict[str, tuple] = {
                                       _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32,
                                       _u64, _vp, _i64, _vp, _vp, _i64]),
     "rs_gather_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "rs_gather_sum_columns": (_i32, [_vp, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i64]),
     "rs_scatter_add_columns": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
     "rs_segment_mean": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64]),
     "rs_field_scale_fwd": (_i32, [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _f32, _vp, _i64]),

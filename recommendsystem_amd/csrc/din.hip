@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
     Geo geo, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ probs,
     const float* __restrict__ dout, int64_t dout_ld, float* __restrict__ dq, int64_t dq_ld,
-    float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ part) {
+    float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ part, int64_t dkv_rs,
+    int dkv_pad) {
   constexpr int NP = nparam(VAR);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int l = lane_id(), g = l >> 4, j = l & 15, w = wave_id();
@@ -313,14 +314,20 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
         const int t = t0 + 4 * g + r;
         if (t < T) {
           float* base = (float*)nullptr;
-          const int64_t off = (b * T + t) * HD + j;
+          // row stride dkv_rs >= HD; columns HD .. dkv_pad - 1 of each row are written as zeros
+          // (the gradient of a wider facts row whose first HD columns the pooling reads)
+          const int64_t off = (b * T + t) * dkv_rs + j;
+          const bool zpad = j + HD < dkv_pad;
           if (VAR == 1 || alias_d) {
             // VAR 1: keys and values are the same facts tensor -> one gradient
             base = dk ? dk : dv;
-            if (base) base[off] = DK[r] + dvv[r];
+            if (base) {
+              base[off] = DK[r] + dvv[r];
+              if (zpad) base[off + HD] = 0.f;
+            }
           } else {
-            if (dk) dk[off] = DK[r];
-            if (dv) dv[off] = dvv[r];
+            if (dk) { dk[off] = DK[r]; if (zpad) dk[off + HD] = 0.f; }
+            if (dv) { dv[off] = dvv[r]; if (zpad) dv[off + HD] = 0.f; }
           }
         }
       }
@@ -430,15 +437,18 @@ RS_API int rs_din_fwd(void* stream, int variant, const float* q, int64_t q_ld, c
   return rs_status_after_launch();
 }
 
-RS_API int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
-                      int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
-                      int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
-                      int64_t mask_ld, const float* W1, const float* b1, const float* W2,
-                      const float* b2, const float* probs, const float* dout, int64_t dout_ld,
-                      float* dq, int64_t dq_ld, float* dkeys, float* dvalues, float* dparams,
-                      int dparams_accumulate, float* workspace, int64_t workspace_floats) {
+RS_API int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t q_ld,
+                              const float* keys, int64_t k_ss, int64_t k_rs, const float* values,
+                              int64_t v_ss, int64_t v_rs, int64_t B, int T, int H,
+                              const int32_t* lengths, const uint8_t* mask, int64_t mask_ld,
+                              const float* W1, const float* b1, const float* W2, const float* b2,
+                              const float* probs, const float* dout, int64_t dout_ld, float* dq,
+                              int64_t dq_ld, float* dkeys, float* dvalues, int64_t dkv_rs,
+                              int dkv_width, float* dparams, int dparams_accumulate,
+                              float* workspace, int64_t workspace_floats) {
   int st = din_check(variant, q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T, H);
   if (st) return st;
+  if (dkv_rs < H || dkv_width < H || dkv_width > dkv_rs || dkv_width > 2 * H) return RS_ERR_ARG;
   if (!W1 || !b1 || !W2 || !b2 || !dout || !dq || dq_ld % 4 || dq_ld < H) return RS_ERR_ARG;
   if (variant == 1 && !probs) return RS_ERR_ARG;
   if (B == 0) return RS_OK;
@@ -454,12 +464,27 @@ RS_API int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, c
   if (!workspace || workspace_floats < (int64_t)grid * np) return RS_ERR_ARG;
   if (variant == 0)
     din_bwd_kernel<0><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld, dq,
-                                                  dq_ld, dkeys, dvalues, workspace);
+                                                  dq_ld, dkeys, dvalues, workspace, dkv_rs,
+                                                  dkv_width);
   else
     din_bwd_kernel<1><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld, dq,
-                                                  dq_ld, dkeys, dvalues, workspace);
+                                                  dq_ld, dkeys, dvalues, workspace, dkv_rs,
+                                                  dkv_width);
   st = rs_status_after_launch();
   if (st || !dparams) return st;
   launch_column_reduce(s, workspace, grid, np, np, np, dparams, dparams, dparams_accumulate);
   return rs_status_after_launch();
+}
+
+RS_API int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
+                      int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
+                      int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
+                      int64_t mask_ld, const float* W1, const float* b1, const float* W2,
+                      const float* b2, const float* probs, const float* dout, int64_t dout_ld,
+                      float* dq, int64_t dq_ld, float* dkeys, float* dvalues, float* dparams,
+                      int dparams_accumulate, float* workspace, int64_t workspace_floats) {
+  return rs_din_bwd_strided(stream, variant, q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T,
+                            H, lengths, mask, mask_ld, W1, b1, W2, b2, probs, dout, dout_ld, dq,
+                            dq_ld, dkeys, dvalues, H, H, dparams, dparams_accumulate, workspace,
+                            workspace_floats);
 }

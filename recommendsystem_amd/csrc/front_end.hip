@@ -466,3 +466,55 @@ RS_API int rs_fm_proj_bwd(void* stream, const float* dy, const float* x, int64_t
   launch_column_reduce(s, workspace, (int)chunks(B), J, J, J, dV, nullptr, dV_accumulate);
   return rs_status_after_launch();
 }
+
+// ---- the backward of several column gathers from one source, as one gather ------------------
+// out[b, c] = sum_k (map[k][c] >= 0 ? src_k[b * ld_k + map[k][c]] : 0) for c < ncols: every output
+// element written once (no zero fill, no atomics, no accumulate chain).  The staytime trunk reads
+// general = emb[:, :, 0:16], the DIN queries general[:, q] and the gate input emb[:, bias, 16:32]
+// from the field embeddings (VideoDnn.py:45-47, 57-77, 127); their gradients meet in d_emb here.
+namespace {
+constexpr int kMaxSumSrc = 8;
+struct SumSrc {
+  const float* p[kMaxSumSrc];
+  int64_t ld[kMaxSumSrc];
+};
+
+__global__ void __launch_bounds__(kBlk) gather_sum_cols_kernel(SumSrc src, int nsrc,
+                                                               const int32_t* __restrict__ map,
+                                                               int64_t B, int ncols,
+                                                               float* __restrict__ out,
+                                                               int64_t out_ld) {
+  const int64_t n = B * ncols;
+  for (int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlk) {
+    const int64_t b = i / ncols;
+    const int c = (int)(i - b * ncols);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxSumSrc; ++k) {
+      if (k < nsrc) {
+        const int32_t sc = map[(int64_t)k * ncols + c];
+        if (sc >= 0) v += src.p[k][b * src.ld[k] + sc];
+      }
+    }
+    out[b * out_ld + c] = v;
+  }
+}
+}  // namespace
+
+RS_API int rs_gather_sum_columns(void* stream, int nsrc, const float* const* srcs,
+                                 const int64_t* src_lds, const int32_t* map, int64_t B, int ncols,
+                                 float* out, int64_t out_ld) {
+  if (nsrc < 1 || nsrc > kMaxSumSrc || !srcs || !src_lds || !map || !out || B < 0 || ncols < 0 ||
+      out_ld < ncols)
+    return RS_ERR_ARG;
+  SumSrc s{};
+  for (int k = 0; k < nsrc; ++k) {  // host arrays of device pointers / strides
+    if (!srcs[k]) return RS_ERR_ARG;
+    s.p[k] = srcs[k];
+    s.ld[k] = src_lds[k];
+  }
+  if (B * ncols == 0) return RS_OK;
+  gather_sum_cols_kernel<<<grid_for(B * ncols), kBlk, 0, rs_stream(stream)>>>(s, nsrc, map, B,
+                                                                              ncols, out, out_ld);
+  return rs_status_after_launch();
+}

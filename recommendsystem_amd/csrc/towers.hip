@@ -1238,3 +1238,42 @@ RS_API int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, 
                                                           loss_rows, dP);
   return rs_status_after_launch();
 }
+
+// ------------------------------- fused loss total ------------------------------------------------
+// The compiled Keras loss of a multi-output model is sum_k loss_weight_k * mean_batch(rows_k):
+// the per-row loss vectors of every output (rs_softmax_kl / rs_bce_rows / rs_mse_rows rows, laid
+// out back to back, seg floats each) are reduced with their weights in ONE launch instead of a
+// reduction, a scale and an add per output (staytime/model.py:85-89, rough_rank/model.py:210-214).
+// One workgroup, fixed summation order (deterministic).
+namespace rs_tw {
+constexpr int kWsumThreads = 1024;
+__global__ void __launch_bounds__(kWsumThreads) weighted_row_sum_kernel(
+    const float* __restrict__ X, int64_t seg, int nseg, float w0, float w1, float w2, float w3,
+    float w4, float w5, float* __restrict__ out) {
+  __shared__ float red[kWsumThreads / 64];
+  const float ws[6] = {w0, w1, w2, w3, w4, w5};
+  float acc = 0.f;
+  for (int k = 0; k < nseg; ++k) {
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < seg; i += kWsumThreads) s += X[k * seg + i];
+    acc = fmaf(ws[k], s, acc);
+  }
+  acc = group_sum<64>(acc);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < kWsumThreads / 64; ++k) t += red[k];
+    out[0] = t;
+  }
+}
+}  // namespace rs_tw
+
+RS_API int rs_weighted_row_sum(void* stream, const float* X, int64_t seg, int nseg, float w0,
+                               float w1, float w2, float w3, float w4, float w5, float* out) {
+  if (!X || !out || seg < 0 || nseg < 1 || nseg > 6) return RS_ERR_ARG;
+  rs_tw::weighted_row_sum_kernel<<<1, rs_tw::kWsumThreads, 0, rs_stream(stream)>>>(
+      X, seg, nseg, w0, w1, w2, w3, w4, w5, out);
+  return rs_status_after_launch();
+}

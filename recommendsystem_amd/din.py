@@ -38,10 +38,15 @@ def _rows_view(t: torch.Tensor) -> torch.Tensor:
 
 class _DINFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, keys, values, lengths, mask, W1, b1, W2, b2, variant):
+    def forward(ctx, q, keys, values, lengths, mask, W1, b1, W2, b2, variant, wide=False):
         _lib.require_device(q, keys, values, W1)
         q = _rows_view(q)
         keys = _rows_view(keys)
+        # wide: keys [B, T, W > H] whose first H columns are the facts; the backward returns the
+        # [B, T, W] gradient (zeros past H) straight from the kernel (rs_din_bwd_strided)
+        ctx.wide_w = keys.shape[2] if wide else 0
+        if wide:
+            keys = keys[:, :, :q.shape[1]]
         same = values is None or values.data_ptr() == keys.data_ptr() and values.shape == keys.shape
         values = keys if same else _rows_view(values)
         B, T, H = keys.shape
@@ -64,7 +69,8 @@ class _DINFn(torch.autograd.Function):
         B, T, H = keys.shape
         dev = q.device
         dq = torch.empty(B, H, device=dev, dtype=torch.float32)
-        dk = torch.empty(B, T, H, device=dev, dtype=torch.float32)
+        Wd = ctx.wide_w or H
+        dk = torch.empty(B, T, Wd, device=dev, dtype=torch.float32)
         dv = dk if (ctx.same or variant == 1) else torch.empty(B, T, H, device=dev, dtype=torch.float32)
         ws_n = int(_lib.load().rs_din_bwd_workspace_floats(variant, B, T, H))
         ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
@@ -72,11 +78,13 @@ class _DINFn(torch.autograd.Function):
         block = grads_contiguous(params)
         in_place = block is not None
         dparams = block if in_place else torch.empty(sum(p.numel() for p in params), device=dev)
-        call("rs_din_bwd", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys), keys.stride(0),
-             keys.stride(1), ptr(values), values.stride(0), values.stride(1), B, T, H,
-             ptr(lengths), ptr(m8), m8.stride(0) if m8 is not None else 0, ptr(W1), ptr(b1),
+        if ctx.wide_w and not (ctx.same or variant == 1):
+            raise NotImplementedError("wide facts need keys == values")
+        call("rs_din_bwd_strided", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys),
+             keys.stride(0), keys.stride(1), ptr(values), values.stride(0), values.stride(1), B, T,
+             H, ptr(lengths), ptr(m8), m8.stride(0) if m8 is not None else 0, ptr(W1), ptr(b1),
              ptr(W2), ptr(b2), ptr(probs), ptr(dout), dout.stride(0), ptr(dq), H, ptr(dk), ptr(dv),
-             ptr(dparams), 1 if in_place else 0, ptr(ws), ws_n)
+             Wd, Wd, ptr(dparams), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
             wgrads = (None, None, None, None)
         else:
@@ -86,8 +94,8 @@ class _DINFn(torch.autograd.Function):
                 off += p.numel()
             wgrads = tuple(outs)
         if ctx.same or variant == 1:
-            return (dq, dk, None, None, None, *wgrads, None)
-        return (dq, dk, dv, None, None, *wgrads, None)
+            return (dq, dk, None, None, None, *wgrads, None, None)
+        return (dq, dk, dv, None, None, *wgrads, None, None)
 
 
 class _DINBase(nn.Module):
@@ -151,7 +159,9 @@ class StaytimeDIN(_DINBase):
     fully masked row pools the facts uniformly."""
     VARIANT, BLOCKS = VAR_SOFTMAX, 4
 
-    def forward(self, query, facts, mask=None):
+    def forward(self, query, facts, mask=None, wide=False):
+        """``wide``: facts [B, T, W] (W <= 2 * H) whose first H = query width columns are the
+        sequence embedding (the staytime 32-wide sequence rows, VideoDnn.py:57-77); no slice."""
         m = None
         if mask is not None:
             if mask.dim() != 2 or mask.shape[0] != facts.shape[0] or mask.shape[1] < facts.shape[1]:
@@ -159,4 +169,9 @@ class StaytimeDIN(_DINBase):
             m = mask.to(device=facts.device, dtype=torch.bool)
             if m.stride(-1) != 1:
                 m = m.contiguous()
+        if wide:
+            if not self.built:
+                self.build((1, facts.shape[1], query.shape[1]), device=facts.device)
+            return _DINFn.apply(query, facts, None, None, m, self.W1, self.b1, self.W2, self.b2,
+                                self.VARIANT, True)
         return self._pool(query, facts, None, None, m)

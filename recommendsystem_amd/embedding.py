@@ -378,10 +378,13 @@ class _ShardedSeqLookupFn(torch.autograd.Function):
         E, plan = t.gather(rows)
         ctx.layer, ctx.B, ctx.plan = layer, B, plan
         ctx.mark_non_differentiable(mask, lengths)
+        ctx.set_materialize_grads(False)  # no zero-filled grads for mask / lengths
         return E.view(B, T, d), mask.view(torch.bool), lengths
 
     @staticmethod
     def backward(ctx, dout, _dmask, _dlen):
+        if dout is None:
+            return None, None, None, None
         d = ctx.layer.table.dim
         ctx.layer.table.push(dout.contiguous().view(-1, d), ctx.plan)
         return None, None, None, None
@@ -482,10 +485,13 @@ class _SeqLookupFn(torch.autograd.Function):
         ctx.layer, ctx.B = layer, B
         ctx.save_for_backward(rows)
         ctx.mark_non_differentiable(mask, lengths)
+        ctx.set_materialize_grads(False)  # no zero-filled grads for mask / lengths
         return out, mask.view(torch.bool), lengths
 
     @staticmethod
     def backward(ctx, dout, _dmask, _dlen):
+        if dout is None:
+            return None, None, None, None
         (rows,) = ctx.saved_tensors
         layer = ctx.layer
         T, dim = layer.seq_max_len, layer.table.dim

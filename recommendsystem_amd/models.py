@@ -17,6 +17,7 @@ three staytime experts' first layers plus the three MMoE gate nets' first layers
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -26,11 +27,12 @@ from torch import nn
 from ._lib import call, ptr, stream_handle
 from .din import StaytimeDIN
 from .embedding import EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam, SparseTable
-from .layers import Dense, InteractingLayer, _act_code, _DenseFn, gather_multi
+from .layers import Dense, InteractingLayer, _act_code, _DenseFn, _row_major, gather_multi
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 from . import _lib
 from .towers import (DNN, PLE, CrossNet, DeepCrossLayer, ExpertGateLayer, FFMBlock, KDLoss,
-                     SENetFM, StaytimeHead, _rows, cross_entropy_sum, gated, keras_bce)
+                     SENetFM, StaytimeHead, _rows, _split_grads, bce_term, cross_entropy_sum, fused_loss, gated,
+                     kd_mean_term, keras_bce, keras_bce_term)
 
 
 # ============================================================================================
@@ -54,35 +56,72 @@ class _SplitColsFn(torch.autograd.Function):
         return torch.cat(parts, dim=1), None
 
 
-class _EmbFanoutFn(torch.autograd.Function):
-    """staytime trunk inputs read from the field embeddings emb [B, F, 32] (VideoDnn.py:45-47,
-    57-77): general = emb[:, :, 0:16], the bias-field gate input emb[:, bias, 16:32] flattened,
-    and the DIN queries general[:, q, :].  One backward builds d_emb once (autograd's per-view
-    backward zero-fills an emb-sized gradient per view and adds them)."""
+class _StaytimeFrontFn(torch.autograd.Function):
+    """The staytime trunk's reads of the field embeddings emb [B, F, 32] in one Function
+    (VideoDnn.py:11-25, 45-47, 57-77, 99-105, 127): general = emb[:, :, 0:16] and the DIN queries
+    general[:, q] (views), the gate input emb[:, bias, 16:32] (one column gather) and the fused
+    FFM + user x item multiply over the user / item fields.  Backward: ONE gather-sum kernel
+    writes every element of d_emb from the general, gate and query gradients, then the FFM
+    backward adds its share in place -- instead of a zero fill, a copy, an add + copy per query, an
+    index_add, the FFM's own zero-filled d_emb and autograd's add of the two."""
 
     @staticmethod
-    def forward(ctx, emb, bias_idx, qidx):
+    def forward(ctx, emb, Wx, bx, Wy, by, front):
         B, F, W = emb.shape
-        ctx.shape, ctx.qidx = (B, F, W), qidx
-        ctx.save_for_backward(bias_idx)
+        emb = emb.contiguous()
+        x2 = emb.view(B, F * W)
+        ffm = front["ffm"]
+        gate = torch.empty(B, front["gate_cols"].numel(), device=emb.device)
+        call("rs_gather_columns", stream_handle(), ptr(x2), F * W, B, ptr(front["gate_cols"]),
+             gate.shape[1], ptr(gate), gate.shape[1])
+        P = ffm.NU * ffm.NI
+        y = torch.empty(B, P * ffm.dim, device=emb.device)
+        mu = torch.empty(B, ffm.NU * 16, device=emb.device)
+        call("rs_ffm_fwd", stream_handle(), ptr(x2), F * W, B, ffm.NU, ffm.NI, 16, ffm.dim,
+             ptr(ffm.cols), ptr(Wx), ptr(bx), ptr(Wy), ptr(by), ptr(y), P * ffm.dim, ptr(mu),
+             ffm.NU * 16)
+        ctx.save_for_backward(emb, Wx, bx, Wy, by)
+        ctx.front = front
         general = emb[:, :, 0:16]
-        gate = emb.index_select(1, bias_idx)[:, :, 16:32].reshape(B, -1)
-        return (general, gate, *[emb[:, q, 0:16] for q in qidx])
+        return (general, gate, *[emb[:, q, 0:16] for q in front["qidx"]], y, mu)
 
     @staticmethod
-    def backward(ctx, dgen, dgate, *dqs):
-        (bias_idx,) = ctx.saved_tensors
-        B, F, W = ctx.shape
-        ref = next(g for g in (dgen, dgate, *dqs) if g is not None)
-        d = ref.new_zeros(B, F, W)
-        if dgen is not None:
-            d[:, :, 0:16] = dgen
-        for q, dq in zip(ctx.qidx, dqs):
-            if dq is not None:
-                d[:, q, 0:16] += dq
-        if dgate is not None:
-            d[:, :, 16:32].index_add_(1, bias_idx, dgate.reshape(B, -1, 16))
-        return d, None, None
+    def backward(ctx, dgen, dgate, *rest):
+        emb, Wx, bx, Wy, by = ctx.saved_tensors
+        front = ctx.front
+        nq = len(front["qidx"])
+        dqs, dy, dmu = rest[:nq], rest[nq], rest[nq + 1]
+        B, F, W = emb.shape
+        dev = emb.device
+        srcs = []
+        for g, width in [(dgen, F * 16), (dgate, front["gate_cols"].numel())] + [(d, 16) for d in dqs]:
+            if g is None:
+                g = torch.zeros(B, width, device=dev)
+            g = g.reshape(B, width) if g.is_contiguous() else g.contiguous().reshape(B, width)
+            srcs.append(g)
+        d_emb = torch.empty(B, F, W, device=dev)
+        ptrs = (ctypes.c_void_p * len(srcs))(*[g.data_ptr() for g in srcs])
+        lds = (ctypes.c_int64 * len(srcs))(*[g.stride(0) for g in srcs])
+        call("rs_gather_sum_columns", stream_handle(), len(srcs), ctypes.addressof(ptrs),
+             ctypes.addressof(lds), ptr(front["fanout_map"]), B, F * W, ptr(d_emb), F * W)
+        ffm = front["ffm"]
+        params = (Wx, bx, Wy, by)
+        if dy is None and dmu is None:
+            return (d_emb, None, None, None, None, None)
+        P = ffm.NU * ffm.NI
+        dy = _row_major(dy) if dy is not None else torch.zeros(B, P * ffm.dim, device=dev)
+        dmu = _row_major(dmu) if dmu is not None else None
+        lib = _lib.load()
+        ws_n = int(lib.rs_ffm_bwd_workspace_floats(B, ffm.NU, ffm.NI, 16, ffm.dim))
+        ws = torch.empty(max(ws_n, 1), device=dev)
+        block = grads_contiguous(params)
+        dpar = block if block is not None else torch.empty(sum(p.numel() for p in params), device=dev)
+        call("rs_ffm_bwd", stream_handle(), ptr(emb), F * W, B, ffm.NU, ffm.NI, 16, ffm.dim,
+             ptr(ffm.cols), ptr(Wx), ptr(bx), ptr(Wy), ptr(by), ptr(dy), dy.stride(0), ptr(dmu),
+             dmu.stride(0) if dmu is not None else ffm.NU * 16, ptr(d_emb), F * W, 1, ptr(dpar),
+             1 if block is not None else 0, ptr(ws), ws_n)
+        g = (None,) * 4 if block is not None else tuple(_split_grads(params, dpar))
+        return (d_emb, *g, None)
 
 
 def split_cols(y, sizes):
@@ -400,7 +439,7 @@ class DSSM(nn.Module):
             self._plan_key = key
         return self._plan
 
-    def forward(self, emb, mask):
+    def forward(self, emb, mask, with_kd=True):
         """emb [B, nu + ni, 16] (or any [B, F, >= 16] whose columns 0:16 per field are the
         embedding -- the joint model's [B, 52, 32] lookup); mask [B, 1] (dense feature 4575).
         Returns the reference's outputs {'student', 'teacher', 'distill'} plus the logits."""
@@ -415,16 +454,19 @@ class DSSM(nn.Module):
         deep = self.t2(self.t1(wc))                                              # :25-26
         t_logit = self.t4(self.t3(torch.cat([deep, cross], dim=1)))              # :27-29
         s_logit = self.s2(self.s1(torch.cat([user_emb, item_emb], dim=1)))       # :73-81
-        distill = self.kd(s_logit, t_logit.detach())                             # :175-176
+        distill = self.kd(s_logit, t_logit.detach()) if with_kd else None        # :175-176
         return {"student": sigmoid(s_logit), "teacher": sigmoid(t_logit), "distill": distill,
                 "student_logit": s_logit, "teacher_logit": t_logit}
 
+    def loss_terms(self, emb, mask, labels):
+        """create_model losses (rough_rank/model.py:210-214) as fused LossTerms: BCE(student) +
+        BCE(teacher) + y_pred_loss(distill) = mean of the per-sample KD loss."""
+        out = self.forward(emb, mask, with_kd=False)
+        return [keras_bce_term(labels, out["student"]), keras_bce_term(labels, out["teacher"]),
+                kd_mean_term(out["student_logit"], out["teacher_logit"])]
+
     def loss(self, emb, mask, labels):
-        """create_model losses (rough_rank/model.py:210-214): BCE(student) + BCE(teacher) +
-        y_pred_loss(distill) = mean of the per-sample KD loss."""
-        out = self.forward(emb, mask)
-        return (keras_bce(labels, out["student"]) + keras_bce(labels, out["teacher"])
-                + out["distill"].mean())
+        return fused_loss(self.loss_terms(emb, mask, labels), emb.shape[0])
 
 
 # ============================================================================================
@@ -526,16 +568,49 @@ class StaytimeMTL(nn.Module):
     def regularizers(self):
         return []
 
+    def _front(self, F, W):
+        """Device plans of _StaytimeFrontFn for emb [B, F, W]: the gate gather columns and the
+        fan-out map [2 + len(query_fields), F * W] (general, gate, queries -> emb columns)."""
+        key = (F, W)
+        if getattr(self, "_front_key", None) != key:
+            dev = self.bias_idx.device
+            bias = [int(f) for f in self.cfg.bias_fields]
+            gate_cols = [f * W + 16 + c for f in bias for c in range(16)]
+            nsrc = 2 + len(self.query_idx)
+            mp = [[-1] * (F * W) for _ in range(nsrc)]
+            for f in range(F):
+                for c in range(16):
+                    mp[0][f * W + c] = f * 16 + c
+            for slot, f in enumerate(bias):
+                if mp[1][f * W + 16] != -1:
+                    raise ValueError("bias fields must be distinct")
+                for c in range(16):
+                    mp[1][f * W + 16 + c] = slot * 16 + c
+            for k, q in enumerate(self.query_idx):
+                for c in range(16):
+                    mp[2 + k][int(q) * W + c] = c
+            self._front_plan = {
+                "gate_cols": torch.tensor(gate_cols, dtype=torch.int32, device=dev),
+                "fanout_map": torch.tensor(mp, dtype=torch.int32, device=dev),
+                "qidx": [int(q) for q in self.query_idx], "ffm": self.ffm}
+            self._front_key = key
+        return self._front_plan
+
     def _trunk(self, emb, seqs, masks):
         cfg = self.cfg
         B, F, _ = emb.shape
         # general = emb[:, :, 0:16] (:47); gate input = bias fields' [16:32] (:45-46,127); DIN
         # queries = general of the query fields (:57-77)
-        general, gate_input, *queries = _EmbFanoutFn.apply(emb, self.bias_idx, list(self.query_idx))
-        din = [self.dins[s](queries[s], seqs[s][:, :, 0:16], masks[s])
+        nq = len(self.query_idx)
+        general, gate_input, *rest = _StaytimeFrontFn.apply(emb, self.ffm.Wx, self.ffm.bx,
+                                                            self.ffm.Wy, self.ffm.by,
+                                                            self._front(F, emb.shape[2]))
+        queries, (ffm, mult) = rest[:nq], rest[nq:]
+        # the DIN reads columns 0:16 of the 32-wide sequence rows in place and its backward writes
+        # the full-width gradient (no autograd slice: zero fill + strided copy per sequence)
+        din = [self.dins[s](queries[s], seqs[s], masks[s], wide=True)
                for s in range(len(self.query_idx))]
         rew, cross_term, fm_logit = self.senet(general)                            # :81-115
-        ffm, mult = self.ffm(emb.reshape(B, -1))       # fields read in place (field stride 32)
         concated = torch.cat([rew, cross_term, mult, ffm] + din, dim=1)            # :122-123
         H, NE = list(cfg.hidden_units), cfg.num_experts
         firsts = self.first(concated)
@@ -554,12 +629,17 @@ class StaytimeMTL(nn.Module):
         return concated, fm_logit, experts, gates
 
     def forward(self, emb, seqs, masks, with_loss=False, labels=None):
+        """Named outputs, or with ``with_loss`` (loss, outputs)."""
+        if with_loss:
+            terms, outs = self._outputs(emb, seqs, masks, True, labels)
+            return fused_loss(terms, emb.shape[0]), outs   # fills outs["staytime"] (P)
+        return self._outputs(emb, seqs, masks)
+
+    def _outputs(self, emb, seqs, masks, with_loss=False, labels=None):
         cfg = self.cfg
         concated, fm_logit, experts, gates = self._trunk(emb, seqs, masks)
         from .towers import _MixFn
-        E = torch.cat(experts, dim=1)                                               # :150
-        Gl = torch.cat(gates, dim=1)
-        Z = torch.cat([E, Gl], dim=1)
+        Z = torch.cat(experts + gates, dim=1)           # [experts (:150) | gate logits]: one copy
         mm = _MixFn.apply(Z, self.sel, cfg.num_experts, cfg.hidden_units[-1], cfg.num_tasks,
                           cfg.num_experts, 0)                                       # :153-164
         Hh = cfg.hidden_units[-1]
@@ -572,35 +652,15 @@ class StaytimeMTL(nn.Module):
             return {"staytime": self.head(ext), "shortplay": short, "longplay": long_}
         y_stay, y_short, y_long, sw = labels
         w = cfg.loss_weights
-        kl, P = self.head.loss(ext, y_stay, sw, loss_weight=w[0])                    # model.py:20-30
-        loss = kl + w[1] * _weighted_ce(y_short, short, sw) + w[2] * _weighted_ce(y_long, long_, sw)
-        return loss, {"staytime": P, "shortplay": short, "longplay": long_}
+        # custom_kl_loss + 2 x cross_entropy with loss_weights and sample weights (model.py:20-36,
+        # 85-89) as fused LossTerms: one launch per output + one for the weighted total
+        kl, P = self.head.loss_term(ext, y_stay, sw, loss_weight=w[0])
+        terms = [kl, bce_term(y_short, short, w[1], sample_weight=sw),
+                 bce_term(y_long, long_, w[2], sample_weight=sw)]
+        return terms, {"staytime": P, "shortplay": short, "longplay": long_}
+
+    def loss_terms(self, emb, seqs, masks, y_stay, y_short, y_long, sample_weight=None):
+        return self._outputs(emb, seqs, masks, True, (y_stay, y_short, y_long, sample_weight))[0]
 
     def loss(self, emb, seqs, masks, y_stay, y_short, y_long, sample_weight=None):
         return self.forward(emb, seqs, masks, True, (y_stay, y_short, y_long, sample_weight))[0]
-
-
-def _weighted_ce(y, p, sw):
-    """staytime/model.py:33-36 cross_entropy per element, Keras sample-weighted batch mean."""
-    return _WeightedCEFn.apply(p, y, sw)
-
-
-class _WeightedCEFn(torch.autograd.Function):
-    """mean_b w_b * [-y log(p + 1e-6) - (1 - y) log(1 - p + 1e-6)] (rs_bce_rows)."""
-
-    @staticmethod
-    def forward(ctx, p, y, w):
-        p, y = _rows(p).contiguous(), _rows(y.float()).contiguous()
-        M, T = p.shape
-        w = w.reshape(-1).float().contiguous() if w is not None else None
-        rows = torch.empty(M, device=p.device)
-        dp = torch.empty_like(p)
-        call("rs_bce_rows", stream_handle(), ptr(p), ptr(y), M, T, -3.0e38, 3.0e38, 1e-6, ptr(w),
-             1.0 / M, ptr(rows), ptr(dp))
-        ctx.save_for_backward(dp)
-        return rows.sum() / M
-
-    @staticmethod
-    def backward(ctx, dl):
-        (dp,) = ctx.saved_tensors
-        return dp * dl, None, None

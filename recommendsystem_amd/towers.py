@@ -382,12 +382,14 @@ class _FMFn(torch.autograd.Function):
         dev = x.device
         dx = torch.empty(M, F, E, device=dev)
         da = torch.empty(M, F, device=dev) if (a is not None and ctx.needs_input_grad[1]) else None
-        dy = dy.contiguous() if (ctx.want_y and dy is not None and dy.numel()) else None
-        dc = dc.contiguous() if dc is not None else None
-        dfm = dfm.contiguous() if dfm is not None else None
+        # column slices of a concat gradient are read in place (row strides), not copied
+        dy = _row_major(dy) if (ctx.want_y and dy is not None and dy.numel()) else None
+        dc = _row_major(dc) if dc is not None else None
+        dfm = _row_major(dfm) if dfm is not None else None
         call("rs_fm_bwd", stream_handle(), ptr(x), x.stride(0), x.stride(1), M, F, E, ptr(a),
-             F if a is not None else 0, ctx.a_scale, ptr(dy), F * E, ptr(dc), E, ptr(dfm), 1, ptr(dx),
-             F * E, E, 0, ptr(da), F)
+             F if a is not None else 0, ctx.a_scale, ptr(dy), dy.stride(0) if dy is not None else 0,
+             ptr(dc), dc.stride(0) if dc is not None else 0, ptr(dfm),
+             dfm.stride(0) if dfm is not None else 1, ptr(dx), F * E, E, 0, ptr(da), F)
         return dx, da, None, None
 
 
@@ -445,8 +447,8 @@ class _FFMFn(torch.autograd.Function):
         x, Wx, bx, Wy, by, cols = ctx.saved_tensors
         NU, NI, Dff, with_mult = ctx.cfg
         M = x.shape[0]
-        dy = dy.contiguous()
-        dmu = dmu.contiguous() if (with_mult and dmu is not None) else None
+        dy = _row_major(dy)
+        dmu = _row_major(dmu) if (with_mult and dmu is not None and dmu.numel()) else None
         dx = torch.zeros_like(x)
         lib = _lib.load()
         ws_n = int(lib.rs_ffm_bwd_workspace_floats(M, NU, NI, 16, Dff))
@@ -455,7 +457,8 @@ class _FFMFn(torch.autograd.Function):
         block = grads_contiguous(params)
         dpar = block if block is not None else torch.empty(sum(p.numel() for p in params), device=x.device)
         call("rs_ffm_bwd", stream_handle(), ptr(x), x.stride(0), M, NU, NI, 16, Dff, ptr(cols), ptr(Wx),
-             ptr(bx), ptr(Wy), ptr(by), ptr(dy), NU * NI * Dff, ptr(dmu), NU * 16, ptr(dx),
+             ptr(bx), ptr(Wy), ptr(by), ptr(dy), dy.stride(0), ptr(dmu),
+             dmu.stride(0) if dmu is not None else NU * 16, ptr(dx),
              x.stride(0), 1, ptr(dpar), 1 if block is not None else 0, ptr(ws), ws_n)
         g = (None,) * 4 if block is not None else tuple(_split_grads(params, dpar))
         return (dx, *g, None, None, None, None, None)
@@ -568,6 +571,7 @@ class _SoftmaxKLFn(torch.autograd.Function):
              ptr(yt), yt.stride(0), ptr(sw), float(loss_weight) / M, 1e-7, ptr(rows), ptr(dz), C)
         ctx.save_for_backward(dz)
         ctx.mark_non_differentiable(P)
+        ctx.set_materialize_grads(False)  # no zero-filled grad for P
         return rows.sum() * (float(loss_weight) / M), P
 
     @staticmethod
@@ -605,6 +609,21 @@ class StaytimeHead(nn.Module):
     def loss(self, x, y_true, sample_weight=None, loss_weight=1.0):
         z = self.dense(x)
         return _SoftmaxKLFn.apply(z, y_true, sample_weight, self._bins(z.device), loss_weight)
+
+    def loss_term(self, x, y_true, sample_weight=None, loss_weight=1.0):
+        """(LossTerm of custom_kl_loss for fused_loss, final_y_pred [B, 401]); P is written by
+        the term's launch (softmax, expected watch time and the KL rows + dZ: one kernel)."""
+        z = _rows(self.dense(x))
+        M, C = z.shape
+        P = torch.empty(M, C + 1, device=z.device)
+        yt = _rows(y_true)
+        sw = sample_weight.reshape(-1).float().contiguous() if sample_weight is not None else None
+        bins = self._bins(z.device)
+
+        def launch(rows, grad, gscale):
+            call("rs_softmax_kl", stream_handle(), ptr(z), z.stride(0), M, C, ptr(bins), ptr(P), C + 1,
+                 ptr(yt), yt.stride(0), ptr(sw), gscale, 1e-7, ptr(rows), ptr(grad), C)
+        return LossTerm(z, loss_weight, launch), P
 
 
 class _RowDotFn(torch.autograd.Function):
@@ -709,3 +728,93 @@ def cross_entropy_sum(y_true, y_pred):
     """rank/multi_head/model.py:18-22 (and rank/ctr/base_model.py:7-12): -y log(p + 1e-6) -
     (1 - y) log(1 - p + 1e-6) summed over the last axis, mean over the batch; p unclipped."""
     return _BCEFn.apply(y_pred, y_true, -3.0e38, 3.0e38, 1e-6)
+
+
+# ============================================================================================
+# Fused multi-output loss total
+# ============================================================================================
+class LossTerm:
+    """One output's share of a compiled Keras loss ``sum_k loss_weight_k * mean_batch(rows_k)``.
+    ``launch(rows, grad, gscale)`` writes the output's per-row losses into ``rows`` [M] and the
+    gradient of ``gscale * sum(rows)`` with respect to ``pred`` into ``grad`` (pred's shape,
+    contiguous); every kernel used here (rs_bce_rows, rs_softmax_kl, rs_mse_rows) computes both in
+    one launch."""
+
+    __slots__ = ("pred", "weight", "launch")
+
+    def __init__(self, pred, weight, launch):
+        self.pred, self.weight, self.launch = pred, float(weight), launch
+
+
+class _FusedLossFn(torch.autograd.Function):
+    """Total of several LossTerms: one launch per term (rows + pre-scaled gradient), ONE
+    rs_weighted_row_sum for the scalar; the backward scales every term's gradient by the incoming
+    one in a single elementwise launch.  Replaces a reduction, a scale, an add and a backward
+    multiply per output (staytime/model.py:85-89, rough_rank/model.py:210-214)."""
+
+    @staticmethod
+    def forward(ctx, terms, M, *preds):
+        dev = preds[0].device
+        K = len(terms)
+        if not 1 <= K <= 6:
+            raise ValueError("fused_loss takes 1 to 6 terms")
+        R = torch.empty(K, M, device=dev)
+        sizes = [p.numel() for p in preds]
+        G = torch.empty(sum(sizes), device=dev)
+        off = 0
+        for k, (t, n) in enumerate(zip(terms, sizes)):
+            t.launch(R[k], G[off:off + n], t.weight / M)
+            off += n
+        ws = [t.weight / M for t in terms] + [0.0] * (6 - K)
+        out = torch.empty((), device=dev)
+        call("rs_weighted_row_sum", stream_handle(), ptr(R), M, K, *ws, ptr(out))
+        ctx.save_for_backward(G)
+        ctx.sizes, ctx.shapes = sizes, [p.shape for p in preds]
+        return out
+
+    @staticmethod
+    def backward(ctx, dl):
+        (G,) = ctx.saved_tensors
+        G = G * dl
+        grads, off = [], 0
+        for n, shp in zip(ctx.sizes, ctx.shapes):
+            grads.append(G[off:off + n].view(shp))
+            off += n
+        return (None, None, *grads)
+
+
+def fused_loss(terms, M):
+    """Scalar loss = sum_k terms[k].weight * mean_M(rows_k) (see LossTerm)."""
+    return _FusedLossFn.apply(list(terms), int(M), *[t.pred for t in terms])
+
+
+def bce_term(y_true, y_pred, weight=1.0, lo=-3.0e38, hi=3.0e38, log_eps=1e-6, sample_weight=None):
+    """rs_bce_rows term: per row w_m sum_t [-y log(clip(p) + log_eps) - (1 - y) log(1 - clip(p) +
+    log_eps)]; the defaults are staytime/model.py:33-36 cross_entropy, (eps, 1 - eps, eps) is
+    tf.keras BinaryCrossentropy on probabilities (rough_rank/model.py:211-212)."""
+    p = _rows(y_pred).contiguous()
+    y = _rows(y_true.float()).contiguous()
+    M, T = p.shape
+    sw = sample_weight.reshape(-1).float().contiguous() if sample_weight is not None else None
+
+    def launch(rows, grad, gscale):
+        call("rs_bce_rows", stream_handle(), ptr(p), ptr(y), M, T, lo, hi, log_eps, ptr(sw), gscale,
+             ptr(rows), ptr(grad))
+    return LossTerm(p, weight, launch)
+
+
+def keras_bce_term(y_true, y_pred, eps=1e-7, weight=1.0):
+    return bce_term(y_true, y_pred, weight, eps, 1.0 - eps, eps)
+
+
+def kd_mean_term(student, teacher, weight=1.0):
+    """mean over the batch of KDLoss rows (rough_rank/layer.py:272-279, model.py:214: the
+    'distill' output's y_pred_loss) with the teacher stop-gradient (model.py:166)."""
+    s = _rows(student)
+    t = _rows(teacher.detach())
+    M, N = s.shape
+
+    def launch(rows, grad, gscale):
+        call("rs_mse_rows", stream_handle(), ptr(s), s.stride(0), ptr(t), t.stride(0), M, N, gscale,
+             ptr(rows), ptr(grad), N)
+    return LossTerm(s, weight, launch)

@@ -27,7 +27,7 @@ from .layers import Dense
 from .models import (DSSM, STAYTIME_BINS, DSSMConfig, MultiHeadConfig, MultiHeadRanker,
                      StaytimeConfig, StaytimeMTL)
 from .parse import staytime_labels as device_staytime_labels
-from .towers import cross_entropy_sum
+from .towers import cross_entropy_sum, fused_loss
 
 
 def zipf_ids(rng, shape, vocab, a):
@@ -137,9 +137,10 @@ class StaytimeRoughRank(nn.Module):
             e, m = self.seqs[s](seq_ids[s], seq_offs[s])
             seqs.append(e)
             masks.append(m)
-        st_loss = self.staytime.loss(emb, seqs, masks, y_stay, y_short, y_long, sw)
+        st_terms = self.staytime.loss_terms(emb, seqs, masks, y_stay, y_short, y_long, sw)
         rr = self.rr_fields(rr_ids)           # [B, 52, 32]: the DSSM reads columns 0:16 per field
-        return st_loss + self.dssm.loss(rr, mask, y_click)
+        # the joint total (staytime loss + DSSM loss) as ONE fused loss over the six outputs
+        return fused_loss(st_terms + self.dssm.loss_terms(rr, mask, y_click), emb.shape[0])
 
 
 def staytime_labels(rng, B):
