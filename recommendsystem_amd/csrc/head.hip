@@ -50,6 +50,17 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// diagnostic builds only (-DRS_HEAD_SKIP=bits, tools/head_bench.py): 1 = no W1 staging, 2 = no
+// layer-1 backward, 4 = no dW1 partial stores, 8 = no x0 / il staging
+#ifndef RS_HEAD_SKIP
+#define RS_HEAD_SKIP 0
+#endif
+#ifdef RS_HEAD_STAMPS  // diagnostic build: block 0's phase times (s_memtime) -> d il row 0
+#define HEAD_STAMP(k) \
+  if (tid == 0) { uint64_t t_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)); st_[k] = t_; }
+#else
+#define HEAD_STAMP(k)
+#endif
 constexpr int RB = 16;   // samples per workgroup (one MFMA row tile)
 constexpr int NTH = 1024; // 16 waves: 4 per SIMD at one block per CU (the LDS footprint)
 constexpr int NW = NTH / 64;
@@ -96,29 +107,37 @@ struct Lay {
 };
 
 // rows x (n4 float4) of a row-major global matrix (row stride ld floats) -> LDS (row stride
-// lds_stride); rows >= valid are zero-filled.  BATCH float4 loads per thread are in flight
-// before their LDS stores.
+// lds_stride); rows >= valid are zero-filled.  Split into issue (first BATCH * NTH float4 into
+// registers) and commit (LDS stores, then any remainder synchronously), so the caller can put the
+// loads of every source in flight before the first store: ONE memory round trip for the whole
+// prologue instead of one per source.
 template <int BATCH>
-__device__ __forceinline__ void stage_rows(float* dst, int lds_stride, const float* src,
-                                           int64_t ld, int rows, int n4, int valid, int tid) {
-  const int total = rows * n4;
-  for (int base = 0; base < total; base += BATCH * NTH) {
-    float4 v[BATCH];
-#pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int idx = base + u * NTH + tid;
-      const int r = idx / n4, c = (idx - r * n4) * 4;
-      v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < total && r < valid) v[u] = *reinterpret_cast<const float4*>(src + r * ld + c);
-    }
-#pragma unroll
-    for (int u = 0; u < BATCH; ++u) {
-      const int idx = base + u * NTH + tid;
-      const int r = idx / n4, c = (idx - r * n4) * 4;
-      if (idx < total) *reinterpret_cast<float4*>(dst + r * lds_stride + c) = v[u];
-    }
+struct StageRows {
+  float4 v[BATCH];
+  float* dst; int lds_stride; const float* src; int64_t ld; int rows, n4, valid;
+  __device__ __forceinline__ StageRows(float* d, int ls, const float* sp, int64_t l, int r, int n,
+                                       int va)
+      : dst(d), lds_stride(ls), src(sp), ld(l), rows(r), n4(n), valid(va) {}
+  __device__ __forceinline__ float4 ld4(int idx) const {
+    const int r = idx / n4, c = (idx - r * n4) * 4;
+    float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (idx < rows * n4 && r < valid) z = *reinterpret_cast<const float4*>(src + r * ld + c);
+    return z;
   }
-}
+  __device__ __forceinline__ void st4(int idx, float4 x) const {
+    const int r = idx / n4, c = (idx - r * n4) * 4;
+    if (idx < rows * n4) *reinterpret_cast<float4*>(dst + r * lds_stride + c) = x;
+  }
+  __device__ __forceinline__ void issue(int tid) {
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) v[u] = ld4(u * NTH + tid);
+  }
+  __device__ __forceinline__ void commit(int tid) {
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) st4(u * NTH + tid, v[u]);
+    for (int base = BATCH * NTH; base < rows * n4; base += NTH) st4(base + tid, ld4(base + tid));
+  }
+};
 
 // BF: bf16 math mode (rs_set_math_mode): the layer-1/2 and dx0/dW1 MFMAs take bf16-rounded
 // operands (mfma_bf16, one instruction per 16-deep k chunk, fp32 accumulate); the logits dot,
@@ -146,23 +165,50 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   float* W3s = sm + lay.w3;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, q = l >> 4, j = l & 15;
   const int64_t b0 = (int64_t)blockIdx.x * RB;
+#ifdef RS_HEAD_STAMPS
+  uint64_t st_[16] = {};
+#endif
+  HEAD_STAMP(0)
   const int nrow = (int)(a.B - b0 < RB ? a.B - b0 : RB);
   const int K0 = a.K0, S = a.S, T = a.T, C = D + S;
   const int xs = lay.xs, is = lay.is;
 
   // ---- weights (L2-resident, shared by every block) and the x0 / interacting tiles -> LDS
   //      (rows >= nrow are zero): every MFMA / dot operand below comes from LDS ----
-  {
-    // batched: every thread issues its loads of a batch before the first LDS store, so the
-    // block waits for ~one L2/HBM round trip per batch (a load -> store loop waits per element)
-    constexpr int n4 = N1 / 4;
-    stage_rows<8>(W1s, L::W1S, a.W1, N1, K0, n4, K0, tid);
-    stage_rows<4>(Xs, xs, a.x0 + b0 * a.ldx, a.ldx, RB, K0 >> 2, nrow, tid);
-    stage_rows<4>(Is, is, a.il + b0 * a.ld_il, a.ld_il, RB, S >> 2, nrow, tid);
-    for (int idx = tid; idx < N1 * N2; idx += NTH) W2s[idx] = a.W2[idx];
-    for (int idx = tid; idx < C * T; idx += NTH) W3s[idx] = a.W3[idx];
+  // the per-phase scalars (biases, labels) are loaded into registers with the staging batch:
+  // no global round trip inside the phases below
+  const int h1n = tid % N1;
+  const float b1v = tid < RB * N1 ? a.b1[h1n] : 0.f;
+  const float b2v = (N2 > 0 && w < N2 / 16) ? a.b2[16 * w + j] : 0.f;
+  float b3v[TMAX], ylv[TMAX];
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    const bool ok = t < T && l == 0 && w < nrow;
+    b3v[t] = ok ? a.b3[t] : 0.f;
+    ylv[t] = ok ? a.labels[(b0 + w) * T + t] : 0.f;
   }
-  __syncthreads();
+  {
+    // every source's first batch is in flight before the first LDS store: the block waits for
+    // ~one L2/HBM round trip for the whole prologue (a load -> store loop waits per element)
+    constexpr int n4 = N1 / 4;
+    StageRows<4> sw1(W1s, L::W1S, a.W1, N1, K0, n4, K0);
+    StageRows<2> sx(Xs, xs, a.x0 + b0 * a.ldx, a.ldx, RB, K0 >> 2, nrow);
+    StageRows<2> si(Is, is, a.il + b0 * a.ld_il, a.ld_il, RB, S >> 2, nrow);
+    if (!(RS_HEAD_SKIP & 1)) sw1.issue(tid);
+    if (!(RS_HEAD_SKIP & 8)) { sx.issue(tid); si.issue(tid); }
+    float w2v = tid < N1 * N2 ? a.W2[tid] : 0.f;
+    float w3v = tid < C * T ? a.W3[tid] : 0.f;
+    if (!(RS_HEAD_SKIP & 1)) sw1.commit(tid);
+    if (!(RS_HEAD_SKIP & 8)) { sx.commit(tid); si.commit(tid); }
+    if (tid < N1 * N2) W2s[tid] = w2v;
+    if (tid < C * T) W3s[tid] = w3v;
+    for (int idx = tid + NTH; idx < N1 * N2; idx += NTH) W2s[idx] = a.W2[idx];
+    for (int idx = tid + NTH; idx < C * T; idx += NTH) W3s[idx] = a.W3[idx];
+  }
+  // LDS-only barriers from here on: no wave reads another wave's global writes (d il, dx0 and
+  // the partial rows), so no phase boundary waits for the stores in flight (__syncthreads would)
+  lds_barrier();
+  HEAD_STAMP(1)
 
   // ---- layer 1: h1 = act1(x0 W1 + b1); wave w -> column tile w % NT1, K chunks w / NT1 :: KSPLIT
   //      (16-wide chunks; one ds_read_b128 of x0 feeds 4 k-steps; k permuted consistently) ----
@@ -209,15 +255,18 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) RED[w * 256 + (4 * q + r) * 16 + j] = acc0[r] + acc1[r];
   }
-  __syncthreads();
-  for (int idx = tid; idx < RB * N1; idx += NTH) {
-    const int r = idx / N1, n = idx - r * N1, nt = n >> 4, jj = n & 15;
+  lds_barrier();
+  HEAD_STAMP(2)
+  static_assert(RB * N1 <= NTH, "one H1 element per thread");
+  if (tid < RB * N1) {
+    const int r = tid / N1, n = h1n, nt = n >> 4, jj = n & 15;
     float v = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KSPLIT; ++ks) v += RED[(ks * NT1 + nt) * 256 + r * 16 + jj];
-    H1[r * L::H1S + n] = act_f(v + a.b1[n], a.act1);
+    H1[r * L::H1S + n] = act_f(v + b1v, a.act1);
   }
-  __syncthreads();
+  lds_barrier();
+  HEAD_STAMP(3)
 
   // ---- layer 2: h2 = act2(h1 W2 + b2) (K = N1), wave w < N2/16 owns column tile w ----
   if (N2 > 0) {
@@ -237,11 +286,12 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
           acc = mfma(x4.w, wk[3 * N2], acc);
         }
       }
-      const float bb = a.b2[16 * w + j];
+      const float bb = b2v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) H2[(4 * q + r) * L::H2S + 16 * w + j] = act_f(acc[r] + bb, a.act2);
     }
-    __syncthreads();
+    lds_barrier();
+  HEAD_STAMP(4)
   }
   const float* HD = N2 > 0 ? H2 : H1;
   constexpr int HDS = N2 > 0 ? L::H2S : L::H1S;
@@ -251,7 +301,9 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   float lsum = 0.f;
   {
     const int r = w, c0 = l;
-    for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) {  // unrolled: b3v / ylv stay registers
+      if (t >= T) break;
       float acc = 0.f;
       for (int c = c0; c < C; c += 64) {
         const float xv = c < D ? HD[r * HDS + c] : Is[r * is + (c - D)];
@@ -261,9 +313,9 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
       if (c0 == 0) {
         float dz = 0.f;
         if (r < nrow) {
-          const float y = act_f(acc + a.b3[t], a.act3);
+          const float y = act_f(acc + b3v[t], a.act3);
           const float p = fminf(fmaxf(y, a.lo), a.hi);
-          const float yl = a.labels[(b0 + r) * T + t];
+          const float yl = ylv[t];
           lsum += -yl * logf(p + a.log_eps) - (1.0f - yl) * logf(1.0f - p + a.log_eps);
           if (a.p_out) a.p_out[(b0 + r) * T + t] = p;
           const float dp = (-yl / (p + a.log_eps) + (1.0f - yl) / (1.0f - p + a.log_eps)) * a.inv_batch;
@@ -274,7 +326,8 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
     }
   }
   if (l == 0) LRED[w] = lsum;  // lane 0 of each wave holds its row's loss terms
-  __syncthreads();
+  lds_barrier();
+  HEAD_STAMP(5)
 
   float* part = a.part + (int64_t)blockIdx.x * a.np;
   const int o_b1 = K0 * N1, o_w2 = o_b1 + N1, o_b2 = o_w2 + N1 * N2, o_w3 = o_b2 + N2;
@@ -308,7 +361,8 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
       a.dil[(b0 + r) * a.ld_dil + (c - D)] = g;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  HEAD_STAMP(6)
 
   // ---- layer 2 backward: dW2 = h1^T dz2, db2, dz1 = act1'(dz2 W2^T) ----
   if (N2 > 0) {
@@ -338,7 +392,8 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
       DZ1[r * L::H1S + k] = DZD[r * (D + 4) + k];
     }
   }
-  __syncthreads();
+  lds_barrier();
+  HEAD_STAMP(7)
   if (tid < N1) {
     float g = 0.f;
 #pragma unroll
@@ -349,7 +404,7 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   // ---- layer 1 backward (MFMA), e tiles of 16 spread over the waves:
   //      dx0[r][e] = sum_n dz1[r][n] W1[e][n]    (A = dz1, B = W1 rows, both from LDS)
   //      dW1[e][n] = sum_r x0[r][e] dz1[r][n]    (A = x0^T from LDS, B = dz1 from LDS) ----
-  {
+  if (!(RS_HEAD_SKIP & 2)) {
     const int net = K0 >> 4;
     float4 dzf[N1 / 16];
 #pragma unroll
@@ -399,10 +454,16 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
         }
         // D[4q + r][j] = dW1[16 et + 4q + r][16 nt + j]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) part[(16 * et + 4 * q + r) * N1 + 16 * nt + j] = g[r];
+        for (int r = 0; r < 4; ++r)
+          if (!(RS_HEAD_SKIP & 4)) part[(16 * et + 4 * q + r) * N1 + 16 * nt + j] = g[r];
       }
     }
   }
+  HEAD_STAMP(8)
+#ifdef RS_HEAD_STAMPS
+  if (tid == 0 && blockIdx.x == 0)
+    for (int q2 = 1; q2 <= 8; ++q2) a.dil[q2 - 1] = (float)(st_[q2] - st_[q2 - 1]);
+#endif
 }
 
 template <int N1, int N2, bool BF16_OK = false>
