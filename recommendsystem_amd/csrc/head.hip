@@ -142,7 +142,10 @@ struct StageRows {
 // BF: bf16 math mode (rs_set_math_mode): the layer-1/2 and dx0/dW1 MFMAs take bf16-rounded
 // operands (mfma_bf16, one instruction per 16-deep k chunk, fp32 accumulate); the logits dot,
 // the loss and every stored value stay fp32.
-template <int N1, int N2, bool BF>
+// TT: the logits width T at compile time (1: every reference head -- AutoInt's Dense(1), the
+// multi_head towers), 0: runtime T <= TMAX.  With T known the per-row / per-column T loops unroll
+// into straight-line code (the runtime form measured 9.2 K cycles for the logits backward phase).
+template <int N1, int N2, bool BF, int TT = 0>
 __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   using L = Lay<N1, N2>;
   constexpr int D = L::D;
@@ -170,7 +173,7 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #endif
   HEAD_STAMP(0)
   const int nrow = (int)(a.B - b0 < RB ? a.B - b0 : RB);
-  const int K0 = a.K0, S = a.S, T = a.T, C = D + S;
+  const int K0 = a.K0, S = a.S, T = TT > 0 ? TT : a.T, C = D + S;
   const int xs = lay.xs, is = lay.is;
 
   // ---- weights (L2-resident, shared by every block) and the x0 / interacting tiles -> LDS
@@ -466,16 +469,17 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #endif
 }
 
-template <int N1, int N2, bool BF16_OK = false>
+template <int N1, int N2, bool BF16_OK = false, int TT = 0>
 int launch(hipStream_t s, const Args& a, int64_t grid) {
   const Lay<N1, N2> lay(a.K0, a.S, a.T);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (lds > 160 * 1024) return RS_ERR_UNSUPPORTED;
+  if (TT > 0 && a.T != TT) return RS_ERR_ARG;
   if (rs_math_mode_now() == RS_MATH_BF16) {
     if constexpr (!BF16_OK) return RS_ERR_UNSUPPORTED;  // never a silent fp32 run
-    else head_train_kernel<N1, N2, true><<<(unsigned)grid, NTH, lds, s>>>(a);
+    else head_train_kernel<N1, N2, true, TT><<<(unsigned)grid, NTH, lds, s>>>(a);
   } else {
-    head_train_kernel<N1, N2, false><<<(unsigned)grid, NTH, lds, s>>>(a);
+    head_train_kernel<N1, N2, false, TT><<<(unsigned)grid, NTH, lds, s>>>(a);
   }
   return rs_status_after_launch();
 }
@@ -525,7 +529,8 @@ RS_API int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const f
          dx_accumulate, workspace, np};
   hipStream_t s = rs_stream(stream);
 #define RS_HEAD(A, Bn) if (N1 == A && N2 == Bn) return launch<A, Bn>(s, a, grid);
-  if (N1 == 32 && N2 == 16) return launch<32, 16, true>(s, a, grid);  // config 2 (bf16 too)
+  if (N1 == 32 && N2 == 16)  // config 2 (bf16 too)
+    return T == 1 ? launch<32, 16, true, 1>(s, a, grid) : launch<32, 16, true>(s, a, grid);
   RS_HEAD(64, 32) RS_HEAD(16, 0) RS_HEAD(32, 0) RS_HEAD(64, 0)
   RS_HEAD(16, 16) RS_HEAD(32, 32) RS_HEAD(64, 16) RS_HEAD(64, 64)
 #undef RS_HEAD
