@@ -2573,7 +2573,10 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         const float D = DL[h * F + i];
         const float* kb = PR + U + h * DH;
         const float* vb = PR + 2 * U + h * DH;
-        float* pm_row = PM + (h * F + i) * C::PMS;
+        // lanes past H * F store their P values into DY (dead until this pass's dq stores,
+        // which come after the loop in program order and cover DY[0 .. 2U)): an unconditional
+        // ds_write per key instead of an exec-mask save / restore around each
+        float* pm_row = act ? PM + (h * F + i) * C::PMS : DY;
         const float nm = -stt.x;
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] = 0.f;
@@ -2589,9 +2592,9 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
           float sv, dp;
           dot2_reg_pk(qv, k, dO, v, sv, dp);
           const float p = __builtin_amdgcn_exp2f(fmaf(sv, a.sc2, nm)) * stt.y;
-          if (act) pm_row[j] = p;
+          pm_row[j] = p;
           if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          axpy_reg_pk(dq, p * (dp - D) * a.inv_sdh, k);
+          axpy_reg_pk(dq, p * (dp - D), k);  // (x 1/sqrt(dh) once, after the loop)
         };
         ld(k0, v0, 0);
 RS_UNROLL(RS_IL4_UNROLL_Q)
@@ -2602,6 +2605,8 @@ RS_UNROLL(RS_IL4_UNROLL_Q)
           ld(k0, v0, j + 2 < nj ? j + 2 : nj - 1);  // (the last one re-reads a row: unused)
           if (two) key(j + 1, k1, v1);
         }
+#pragma unroll
+        for (int d = 0; d < DH; ++d) dq[d] *= a.inv_sdh;
         if (act) store_row(DY + i * U + h * DH, dq);
       }
       wave_lds_sync();
@@ -2635,7 +2640,7 @@ RS_UNROLL(RS_IL4_UNROLL_Q)
             dp = keep ? dp * a.drop_scale : 0.f;
           }
           axpy_reg_pk(dv, pd, dOi);
-          axpy_reg_pk(dk, P * (dp - D) * a.inv_sdh, qi);
+          axpy_reg_pk(dk, P * (dp - D), qi);  // (x 1/sqrt(dh) once, after the loop)
         };
         ld(o0, q0, p0, d0, 0);
 RS_UNROLL(RS_IL4_UNROLL_K)
@@ -2651,7 +2656,7 @@ RS_UNROLL(RS_IL4_UNROLL_K)
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
           dv[d] = vj[d] > 0.f ? dv[d] : 0.f;
-          dk[d] = kj[d] > 0.f ? dk[d] : 0.f;
+          dk[d] = kj[d] > 0.f ? dk[d] * a.inv_sdh : 0.f;
         }
         // row j's K / V are read only by this lane in this pass
         if (act) {

@@ -87,6 +87,8 @@ class SparseTable:
         # mark flag[] and the optimizer sweeps it (no returning atomics in the push; best when
         # the table is not much larger than ~100x the rows a step touches)
         self.mode = "list"
+        # a single-GPU Trainer switches tables with prefer_scan to scan mode (trainer.py)
+        self.prefer_scan = False
         # deterministic pushes (rs_sparse_grad_accumulate_sorted: sort + segmented sum, bitwise
         # reproducible) instead of the LDS-hash + float-atomic push; workspace grown on demand
         self.deterministic = False

@@ -62,6 +62,13 @@ class Trainer:
         self.on_dense_grad = None  # test hook: called with the exchanged flat dense gradient
         self._il_layers = [mod for mod in model.modules() if isinstance(mod, InteractingLayer)] \
             if hasattr(model, "modules") else []
+        if self.world == 1:
+            # single-GPU: tables that ask for it run in scan mode (pushes mark flags with plain
+            # stores, no claims; the optimizer sweeps the flags) -- the DP exchange below needs
+            # list mode's touched lists
+            for t in self.tables:
+                if getattr(t, "prefer_scan", False) and not t.deterministic:
+                    t.mode = "scan"
         if self.world > 1:
             for t in self.tables:
                 if is_sharded(t):

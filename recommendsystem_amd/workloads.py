@@ -62,6 +62,9 @@ class DINPool(nn.Module):
         self.T = T
         self.table = SparseTable(vocab, dim, SparseAdam(5e-5), device=dev, seed=seed,
                                  max_touched=max_touched)
+        # 1 M rows, ~20 K touched per step at B = 1024: a 4 MB flag sweep is cheaper than the
+        # pushes' row claims (Trainer applies it at world 1)
+        self.table.prefer_scan = True
         self.query = EmbeddingFeatures(self.table, [vocab], combiner="sum")
         self.hist = SequenceEmbedding(self.table, vocab, T)
         self.din = DIN(seed=seed + 1, device=dev)
