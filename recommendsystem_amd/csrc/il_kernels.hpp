@@ -471,8 +471,14 @@ __device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, i
   const int q = lane_id() >> 4, j = lane_id() & 15;
   using M = MfmaW<C>;
   f32x4 acc[M::NT];
+  // the bias is the accumulator's initial value (column 16nt + j in every row): no add per
+  // output.  Every IL kernel (forward and the recomputing backwards) projects through this one
+  // function, so the backward's Q / K / V / R equal the forward's bit for bit.
 #pragma unroll
-  for (int nt = 0; nt < M::NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < M::NT; ++nt) {
+    const float bc = w.bp[nt];
+    acc[nt] = f32x4{bc, bc, bc, bc};
+  }
   const int arow = 16 * rt + j;  // A row of this lane (rows >= F give discarded outputs)
 #pragma unroll
   for (int ks = 0; ks < M::KS; ++ks) {
@@ -496,13 +502,12 @@ __device__ __forceinline__ void mfma_project(const float* X, float* PR, int F, i
 #pragma unroll
   for (int nt = 0; nt < M::NT; ++nt) {
     const int c = 16 * nt + j;
-    const float bc = w.bp[nt];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 16 * rt + 4 * q + r;
       // ALL_ROWS: the caller's layout has dead space for rows F .. 16 * ceil(F / 16) - 1 (no
       // per-element branch)
-      if (ALL_ROWS || f < F) PR[f * C::PRS + c] = fmaxf(acc[nt][r] + bc, 0.f);
+      if (ALL_ROWS || f < F) PR[f * C::PRS + c] = fmaxf(acc[nt][r], 0.f);
     }
   }
 }
