@@ -263,30 +263,36 @@ __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
     __builtin_amdgcn_wave_barrier();  // list reuse
     n = 0;
   };
-  int64_t c = gw;
-  int32_t fl = -1;
-  if (c < nchunks && c * 64 + lane < nrows) fl = flag[c * 64 + lane];
-  while (c < nchunks) {
-    const int64_t row0 = c * 64;
-    // prefetch the next chunk's flags
-    const int64_t cn = c + nwaves;
-    int32_t fn = -1;
-    if (cn < nchunks && cn * 64 + lane < nrows) fn = flag[cn * 64 + lane];
-    const bool hit = fl != -1;
-    const uint64_t mask = __ballot(hit);
-    if (mask) {
-      const int cnt = __popcll(mask);
-      if (n + cnt > LCAP) flush();
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-      if (hit) {
-        list[n + rank] = (uint32_t)(row0 + lane);
-        flag[row0 + lane] = -1;
-      }
-      n += cnt;
+  // the flag words of PF chunks per lane are loaded at once (a chip-full grid gives each wave
+  // ~5 chunks of a 2.6 M-row table: one memory round trip for all of them instead of one per
+  // chunk -- the sweep was a chain of dependent flag loads)
+  constexpr int PF = 8;
+  for (int64_t cb = gw; cb < nchunks; cb += PF * nwaves) {
+    int32_t fl[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int64_t c = cb + u * nwaves;
+      fl[u] = (c < nchunks && c * 64 + lane < nrows) ? flag[c * 64 + lane] : -1;
     }
-    fl = fn;
-    c = cn;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int64_t c = cb + u * nwaves;
+      if (c >= nchunks) break;  // wave-uniform
+      const int64_t row0 = c * 64;
+      const bool hit = fl[u] != -1;
+      const uint64_t mask = __ballot(hit);
+      if (mask) {
+        const int cnt = __popcll(mask);
+        if (n + cnt > LCAP) flush();
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (hit) {
+          list[n + rank] = (uint32_t)(row0 + lane);
+          flag[row0 + lane] = -1;
+        }
+        n += cnt;
+      }
+    }
   }
   if (n) flush();
 }
