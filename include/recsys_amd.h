@@ -522,6 +522,18 @@ int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
                             float* params, float* m, float* v, int64_t* step, int32_t* done,
                             float lr, float beta1, float beta2, float eps, float grad_scale,
                             int adam);
+/* rs_partials_reduce_adam with the scan-mode sparse Adam of one table (rs_sparse_adam_scan:
+ * table / m / v / grad_table / flag, lr / betas / eps / grad_scale) run by extra blocks of the
+ * SAME launch: the dense reduction + Adam and the sparse flag sweep are independent, so they
+ * share the chip instead of running back to back (the AutoInt step's optimizer tail). */
+int rs_partials_reduce_adam_scan(void* stream, int nseg, const float* const* parts,
+                                 const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
+                                 float* const* outs, const float* scales, const int64_t* adam_offs,
+                                 float* params, float* m, float* v, int64_t* step, int32_t* done,
+                                 float lr, float beta1, float beta2, float eps, float grad_scale,
+                                 int adam, float* table, float* tm, float* tv, float* grad_table,
+                                 int32_t* flag, int64_t table_rows, int dim, float slr,
+                                 float sbeta1, float sbeta2, float seps, float sgrad_scale);
 
 /* rs_il_bwd with the sparse push fused into its last pass (F <= 64): dL/dx of the layer input
  * is not stored; instead grad_table[rows[b * F + f]] += dL/dx[b, f] (+ dx_base[b, f] when

@@ -328,9 +328,19 @@ class AutoIntTrainer:
              1, None, 0, ptr(self.il_ws), self.il_ws_n, *tail)
         t.accumulate(self.rows, None, B, F, self.dx0, F * E, E, emb.combiner)
 
-    def _reduce_dense(self, adam: bool):
+    def _scan_tail(self, table):
+        """The table when its sparse optimizer can run inside the dense reduce + Adam launch
+        (scan mode, sparse Adam; rs_partials_reduce_adam_scan), else None."""
+        import os
+        from .embedding import SparseAdam
+        ok = (not os.environ.get("RS_NO_FUSED_TAIL")  # A/B switch (two launches)
+              and getattr(table, "mode", None) == "scan" and isinstance(table.optimizer, SparseAdam)
+              and not getattr(table, "deterministic", False) and hasattr(table, "m"))
+        return table if ok else None
+
+    def _reduce_dense(self, adam: bool, scan_table=None):
         """Sum the IL and head partials (fixed order) into the arena gradient and the loss; with
-        adam, apply the dense Adam in the same launch."""
+        adam, apply the dense Adam in the same launch (and, with scan_table, its sparse Adam)."""
         m, hd, cfg = self.model, self.head, self.model.cfg
         ar = m.arena
         # data parallel: the local gradient goes to the exchange bucket, not the arena
@@ -345,7 +355,7 @@ class AutoIntTrainer:
         ]
         _lib.partials_reduce_adam(stream_handle(), segs, ar.data, self.adam_m, self.adam_v,
                                   self.step_count, hd["done"], cfg.lr_dense, 0.9, 0.999, 1e-8,
-                                  1.0 / self.world, adam)
+                                  1.0 / self.world, adam, scan_table=scan_table)
 
     def _forward_backward(self):
         # math mode of the step; dropout seeds offset by the device step counter (fresh masks on
@@ -458,8 +468,12 @@ class AutoIntTrainer:
         m, cfg = self.model, self.model.cfg
         ar = m.arena
         if self.head is not None and self.world == 1:
-            self._reduce_dense(adam=True)   # partials -> grads -> Adam, one launch
-            m.table.step(grad_scale=1.0)
+            # partials -> grads -> Adam, one launch; a scan-mode table's sparse Adam runs in the
+            # same launch on blocks of its own
+            tail = self._scan_tail(m.table)
+            self._reduce_dense(adam=True, scan_table=tail)
+            if tail is None:
+                m.table.step(grad_scale=1.0)
             return
         scale = 1.0 / self.world
         if self.packed_dp:
@@ -469,11 +483,14 @@ class AutoIntTrainer:
                 call("rs_sparse_merge_packed", s, ptr(self.dp_recs_all), counts, self.dp_ld,
                      self.world, r, t.dim, ptr(t.grad), ptr(t.flag), t.rows, self.dp_cap)
             # dense: rank-ordered sum of the gathered buckets -> arena grad -> Adam, one launch
+            tail = self._scan_tail(t)
             _lib.partials_reduce_adam(s, [(ptr(self.dp_recv), self.dp_ld, self.world, self.dp_n,
                                            ptr(ar.grad), 1.0, 0)], ar.data, self.adam_m,
                                       self.adam_v, self.step_count, self.head["done"],
-                                      cfg.lr_dense, 0.9, 0.999, 1e-8, scale, True)
-            t.step(grad_scale=scale)
+                                      cfg.lr_dense, 0.9, 0.999, 1e-8, scale, True,
+                                      scan_table=tail, scan_grad_scale=scale)
+            if tail is None:
+                t.step(grad_scale=scale)
             return
         call("rs_dense_adam", stream_handle(), ptr(ar.data), ptr(ar.grad), ptr(self.adam_m),
              ptr(self.adam_v), ar.n, ptr(self.step_count), cfg.lr_dense, 0.9, 0.999, 1e-8, scale, 0)

@@ -225,19 +225,19 @@ struct ScanRow {
 // when the list is full or its chunks are done -- at ~1 % touched rows a chunk holds about one
 // marked row, so batching turns one dependent HBM round trip per chunk into one per list.  The
 // list is processed two passes at a time (both passes' loads issued before either's stores).
+// The sweep of one wave: gw = the wave's global index, nwaves = waves in the sweep, list = its
+// LCAP-entry LDS list (the standalone kernel and the fused optimizer tail share it).
+constexpr int kScanLcap = 256;  // rows per wave list
 template <bool ADAM>
-__global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
-    float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
-    float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
-    float lr, float b1, float b2, float eps, float grad_scale, const int32_t* __restrict__ gate) {
-  if (gate && *gate == 0) return;  // overflow-recovery sweep with nothing to recover
-  constexpr int LCAP = 256;  // rows per wave list
-  __shared__ uint32_t lists[(kScanBlock / 64) * LCAP];
-  uint32_t* list = lists + (threadIdx.x >> 6) * LCAP;
+__device__ __forceinline__ void scan_opt_wave(float* __restrict__ table, float* __restrict__ m,
+                                              float* __restrict__ v, float* __restrict__ grad_table,
+                                              int32_t* __restrict__ flag, int64_t nrows, int dim,
+                                              float lr, float b1, float b2, float eps,
+                                              float grad_scale, int64_t gw, int64_t nwaves,
+                                              uint32_t* list) {
+  constexpr int LCAP = kScanLcap;
   const int lane = threadIdx.x & 63;
   const int64_t nchunks = (nrows + 63) / 64;
-  const int64_t nwaves = (int64_t)gridDim.x * (kScanBlock / 64);
-  const int64_t gw = (int64_t)blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6);
   const int nv = dim >> 2;             // float4 per row
   const int lpr = nv < 64 ? nv : 64;   // lanes per row
   const int rpp = 64 / lpr;            // rows per pass
@@ -295,6 +295,19 @@ __global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
     }
   }
   if (n) flush();
+}
+
+template <bool ADAM>
+__global__ void __launch_bounds__(kScanBlock) sparse_scan_opt_kernel(
+    float* __restrict__ table, float* __restrict__ m, float* __restrict__ v,
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, int64_t nrows, int dim,
+    float lr, float b1, float b2, float eps, float grad_scale, const int32_t* __restrict__ gate) {
+  if (gate && *gate == 0) return;  // overflow-recovery sweep with nothing to recover
+  __shared__ uint32_t lists[(kScanBlock / 64) * kScanLcap];
+  const int64_t nwaves = (int64_t)gridDim.x * (kScanBlock / 64);
+  const int64_t gw = (int64_t)blockIdx.x * (kScanBlock / 64) + (threadIdx.x >> 6);
+  scan_opt_wave<ADAM>(table, m, v, grad_table, flag, nrows, dim, lr, b1, b2, eps, grad_scale, gw,
+                      nwaves, lists + (threadIdx.x >> 6) * kScanLcap);
 }
 
 static int64_t scan_grid(int64_t nrows) {
@@ -607,6 +620,14 @@ struct RedArgs {
   int32_t* done;
   float lr, b1, b2, eps, grad_scale;
   int adam;
+  int32_t nblk_red;  // blocks of the partial reduction; blocks past it run the sparse sweep
+  // fused sparse optimizer tail (rs_partials_reduce_adam_scan): the scan-mode sparse Adam of one
+  // table, run by blocks nblk_red .. gridDim.x - 1 beside the dense reduction
+  float *st_table, *st_m, *st_v, *st_grad;
+  int32_t* st_flag;
+  int64_t st_rows;
+  int st_dim;
+  float st_lr, st_b1, st_b2, st_eps, st_gscale;
 };
 
 // Block shape per segment (host-chosen): G row groups x (1024 / G) columns, G the smallest power
@@ -614,6 +635,15 @@ struct RedArgs {
 // blocks; head partials: 256 rows -> 16 x 64 over 224 blocks: the whole launch is one round).  Spreading deep segments over many CUs matters:
 // one CU keeps only ~72 KB of loads in flight, so 1024 rows x 32 columns on one CU took ~11 us.
 __global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
+  if ((int)blockIdx.x >= a.nblk_red) {  // the fused sparse sweep (independent of the dense part)
+    __shared__ uint32_t lists[16 * kScanLcap];
+    const int64_t nwaves = (int64_t)(gridDim.x - a.nblk_red) * 16;
+    const int64_t gw = (int64_t)(blockIdx.x - a.nblk_red) * 16 + (threadIdx.x >> 6);
+    scan_opt_wave<true>(a.st_table, a.st_m, a.st_v, a.st_grad, a.st_flag, a.st_rows, a.st_dim,
+                        a.st_lr, a.st_b1, a.st_b2, a.st_eps, a.st_gscale, gw, nwaves,
+                        lists + (threadIdx.x >> 6) * kScanLcap);
+    return;
+  }
   __shared__ float red[1024];
   int si = 0;
 #pragma unroll
@@ -673,16 +703,16 @@ __global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
   }
   if (a.adam && a.step) {
     // every block has consumed step_in (the Adam reads above) before it arrives
-    if (rs_last_block(a.done)) a.step[0] = a.step_in[0] + 1;
+    if (rs_last_block(a.done, a.nblk_red)) a.step[0] = a.step_in[0] + 1;
   }
 }
 
-RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
-                                   const int64_t* lds, const int32_t* nrows,
-                                   const int64_t* ncols, float* const* outs, const float* scales,
-                                   const int64_t* adam_offs, float* params, float* m, float* v,
-                                   int64_t* step, int32_t* done, float lr, float beta1,
-                                   float beta2, float eps, float grad_scale, int adam) {
+static int reduce_adam_impl(void* stream, int nseg, const float* const* parts,
+                            const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
+                            float* const* outs, const float* scales, const int64_t* adam_offs,
+                            float* params, float* m, float* v, int64_t* step, int32_t* done,
+                            float lr, float beta1, float beta2, float eps, float grad_scale,
+                            int adam, const RedArgs* tail, int64_t tail_blocks) {
   if (nseg <= 0 || nseg > RS_RED_MAXSEG || !parts || !lds || !nrows || !ncols || !outs || !scales ||
       !adam_offs)
     return RS_ERR_ARG;
@@ -703,7 +733,48 @@ RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* p
   a.params = params; a.m = m; a.v = v;
   a.step_in = step; a.step = step; a.done = done;
   a.lr = lr; a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.grad_scale = grad_scale; a.adam = adam;
-  if (nblk == 0) return RS_OK;
-  partials_reduce_adam_kernel<<<(unsigned)nblk, 1024, 0, rs_stream(stream)>>>(a);
+  a.nblk_red = (int32_t)nblk;
+  if (tail) {
+    a.st_table = tail->st_table; a.st_m = tail->st_m; a.st_v = tail->st_v;
+    a.st_grad = tail->st_grad; a.st_flag = tail->st_flag; a.st_rows = tail->st_rows;
+    a.st_dim = tail->st_dim; a.st_lr = tail->st_lr; a.st_b1 = tail->st_b1; a.st_b2 = tail->st_b2;
+    a.st_eps = tail->st_eps; a.st_gscale = tail->st_gscale;
+  }
+  const int64_t total = nblk + (tail ? tail_blocks : 0);
+  if (total == 0) return RS_OK;
+  partials_reduce_adam_kernel<<<(unsigned)total, 1024, 0, rs_stream(stream)>>>(a);
   return rs_status_after_launch();
+}
+
+RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
+                                   const int64_t* lds, const int32_t* nrows,
+                                   const int64_t* ncols, float* const* outs, const float* scales,
+                                   const int64_t* adam_offs, float* params, float* m, float* v,
+                                   int64_t* step, int32_t* done, float lr, float beta1,
+                                   float beta2, float eps, float grad_scale, int adam) {
+  return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
+                          m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, nullptr, 0);
+}
+
+RS_API int rs_partials_reduce_adam_scan(
+    void* stream, int nseg, const float* const* parts, const int64_t* lds, const int32_t* nrows,
+    const int64_t* ncols, float* const* outs, const float* scales, const int64_t* adam_offs,
+    float* params, float* m, float* v, int64_t* step, int32_t* done, float lr, float beta1,
+    float beta2, float eps, float grad_scale, int adam, float* table, float* tm, float* tv,
+    float* grad_table, int32_t* flag, int64_t table_rows, int dim, float slr, float sbeta1,
+    float sbeta2, float seps, float sgrad_scale) {
+  if (!table || !tm || !tv || !grad_table || !flag || dim <= 0 || dim % 4 || table_rows < 0 ||
+      table_rows > (int64_t)UINT32_MAX)
+    return RS_ERR_ARG;
+  RedArgs t{};
+  t.st_table = table; t.st_m = tm; t.st_v = tv; t.st_grad = grad_table; t.st_flag = flag;
+  t.st_rows = table_rows; t.st_dim = dim; t.st_lr = slr; t.st_b1 = sbeta1; t.st_b2 = sbeta2;
+  t.st_eps = seps; t.st_gscale = sgrad_scale;
+  // at most 256 16-wave blocks (4096 waves, ~10 chunks each at 2.6 M rows): with the ~300
+  // reduction blocks the launch stays about one resident round (2 such blocks per CU)
+  int64_t tail_blocks = table_rows ? (scan_grid(table_rows) * (kScanBlock / 64) + 15) / 16 : 0;
+  if (tail_blocks > 256) tail_blocks = 256;
+  return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
+                          m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, &t,
+                          tail_blocks);
 }
