@@ -477,6 +477,11 @@ int rs_bce_clip_loss(void* stream, const float* s, const float* y, int64_t M, in
 int rs_dense_adam(void* stream, float* params, float* grads, float* m, float* v, int64_t n,
                   int64_t* step, float lr, float beta1, float beta2, float eps, float grad_scale,
                   int zero_grad);
+/* rs_dense_adam with the step counter advanced by the kernel's last block (done: caller-owned
+ * int32[RS_DONE_WORDS = 288], zero between launches) instead of a second launch. */
+int rs_dense_adam_done(void* stream, float* params, float* grads, float* m, float* v, int64_t n,
+                       int64_t* step, float lr, float beta1, float beta2, float eps,
+                       float grad_scale, int zero_grad, int32_t* done);
 
 /* Keras kernel regularisers as a gradient term (L1L2 at rank/multi_head/multidnn.py:62-63,
  * L2 at :85,103 and rough_rank/layer.py:77): grads += l1 * sign(w) + 2 * l2 * w. */

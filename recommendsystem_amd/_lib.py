@@ -78,6 +78,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_bce_clip_loss": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _vp, _vp, _vp]),
     "rs_dense_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
                              _i32]),
+    "rs_dense_adam_done": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
+                             _i32, _vp]),
     "rs_din_param_count": (_i32, [_i32, _i32]),
     "rs_din_bwd_workspace_floats": (_i64, [_i32, _i64, _i32, _i32]),
     "rs_din_fwd": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32, _i32,

@@ -850,6 +850,9 @@ __device__ __forceinline__ void epilogue(float* O, const float* PR, float* ST, f
 }
 
 // ============================== forward kernel ===============================================
+#ifndef RS_IL_FWD_PK
+#define RS_IL_FWD_PK 0  // packed-fp32 (v_pk_fma_f32) score dots / PV axpys in the forward
+#endif
 template <class C, bool DROP>
 __global__ void __launch_bounds__(256, 4) fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
@@ -901,7 +904,7 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
       // O_i overwrites Q_i in place (only lane (h, i) ever reads Q_i, before writing O_i)
       float* gsave = a.osave ? a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, C::U, C::H)
                              : nullptr;
-      attention_fwd<C, false, DROP, C::PRS>(PR, PR, nullptr, a, b, lseed, gsave);
+      attention_fwd<C, false, DROP, C::PRS, RS_IL_FWD_PK != 0>(PR, PR, nullptr, a, b, lseed, gsave);
       wave_lds_sync();
       if (it == a.L - 1) {
         epilogue<C, 0, C::PRS>(PR, PR, nullptr, y + b * y_ld, C::U, a, gam, bet);

@@ -21,9 +21,10 @@
 __global__ void __launch_bounds__(256) dense_adam_kernel(float* __restrict__ p,
                                                         float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
-                                                        int64_t n, const int64_t* __restrict__ step,
+                                                        int64_t n, int64_t* __restrict__ step,
                                                         float lr, float b1, float b2, float eps,
-                                                        float grad_scale, int zero_grad) {
+                                                        float grad_scale, int zero_grad,
+                                                        int32_t* __restrict__ done) {
   const int64_t t = step[0] + 1;
   const float bc1 = 1.0f - powf(b1, (float)t);
   const float bc2 = 1.0f - powf(b2, (float)t);
@@ -38,6 +39,9 @@ __global__ void __launch_bounds__(256) dense_adam_kernel(float* __restrict__ p,
     v[i] = vi;
     p[i] -= lr_t * mi / (sqrtf(vi) + eps);
   }
+  // fused step counter: every block has read step[0] above; the last block to finish advances it
+  // (no separate increment launch)
+  if (done && rs_last_block(done)) step[0] = t;
 }
 
 __global__ void step_increment_kernel(int64_t* step) { step[0] += 1; }
@@ -51,9 +55,22 @@ RS_API int rs_dense_adam(void* stream, float* params, float* grads, float* m, fl
     int64_t grid = (n + 255) / 256;
     if (grid > 2048) grid = 2048;
     dense_adam_kernel<<<(int)grid, 256, 0, s>>>(params, grads, m, v, n, step, lr, beta1, beta2,
-                                                eps, grad_scale, zero_grad);
+                                                eps, grad_scale, zero_grad, nullptr);
   }
   step_increment_kernel<<<1, 1, 0, s>>>(step);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_dense_adam_done(void* stream, float* params, float* grads, float* m, float* v,
+                              int64_t n, int64_t* step, float lr, float beta1, float beta2,
+                              float eps, float grad_scale, int zero_grad, int32_t* done) {
+  if (!params || !grads || !m || !v || !step || !done || n < 0) return RS_ERR_ARG;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;  // n == 0: one block still advances the step
+  dense_adam_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(params, grads, m, v, n, step, lr,
+                                                              beta1, beta2, eps, grad_scale,
+                                                              zero_grad, done);
   return rs_status_after_launch();
 }
 

@@ -54,6 +54,10 @@ class Trainer:
         self.step_count = torch.zeros(1, device=dev, dtype=torch.int64)
         self.lr, self.b1, self.b2, self.eps = float(lr_dense), beta1, beta2, eps
         self.segments = self._lr_segments(lr_groups)
+        # per segment: the completion counter of rs_dense_adam_done (its last block advances
+        # the step counter) and the backward's seed (no ones_like fill launch per step)
+        self._adam_done = [torch.zeros(288, device=dev, dtype=torch.int32) for _ in self.segments]
+        self._seed = torch.ones((), device=dev)
         self.tables = list(tables)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
@@ -113,7 +117,7 @@ class Trainer:
 
     def _step(self, *batch):
         loss = self.model.loss(*batch)
-        loss.backward()
+        loss.backward(self._seed)
         s = stream_handle()
         for p, l1, l2 in self.regs:
             call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
@@ -197,11 +201,11 @@ class Trainer:
         s = stream_handle()
         if self.on_dense_grad is not None:
             self.on_dense_grad(self.arena.grad, scale)
-        for off, n, lr, cnt in self.segments:
+        for (off, n, lr, cnt), done in zip(self.segments, self._adam_done):
             a = 4 * off
-            call("rs_dense_adam", s, self.arena.data.data_ptr() + a, self.arena.grad.data_ptr() + a,
-                 self.m.data_ptr() + a, self.v.data_ptr() + a, n, ptr(cnt), lr, self.b1, self.b2,
-                 self.eps, scale, 1)
+            call("rs_dense_adam_done", s, self.arena.data.data_ptr() + a,
+                 self.arena.grad.data_ptr() + a, self.m.data_ptr() + a, self.v.data_ptr() + a, n,
+                 ptr(cnt), lr, self.b1, self.b2, self.eps, scale, 1, ptr(done))
         for t in self.tables:
             t.step(grad_scale=scale)
 
@@ -210,7 +214,7 @@ class Trainer:
             mod._calls = 0
         with _lib.seed_offset(self.step_count):
             loss = self.model.loss(*batch)
-            loss.backward()
+            loss.backward(self._seed)
         s = stream_handle()
         for p, l1, l2 in self.regs:
             call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
