@@ -339,10 +339,13 @@ __device__ __forceinline__ int64_t hash_row(int64_t id, int64_t base, int64_t bu
 #define RS_DONE_STRIDE 32
 #define RS_DONE_WORDS (9 * RS_DONE_STRIDE)
 // nblocks: the blocks taking part (blocks 0 .. nblocks - 1; default the whole grid)
-__device__ __forceinline__ bool rs_last_block(int32_t* ctr, int nblocks = -1) {
+// nblocks / bid: the blocks taking part and this block's index among them (default: the whole
+// grid, blockIdx.x)
+__device__ __forceinline__ bool rs_last_block(int32_t* ctr, int nblocks = -1, int bid = -1) {
   __syncthreads();
   if (threadIdx.x != 0) return false;
-  const unsigned G = nblocks < 0 ? gridDim.x : (unsigned)nblocks, k = blockIdx.x & 7u;
+  const unsigned G = nblocks < 0 ? gridDim.x : (unsigned)nblocks;
+  const unsigned k = (bid < 0 ? blockIdx.x : (unsigned)bid) & 7u;
   const int nk = (int)((G - k + 7u) / 8u);
   const int nsub = (int)(G < 8u ? G : 8u);
   int32_t* sub = ctr + k * RS_DONE_STRIDE;
