@@ -196,6 +196,13 @@ int rs_sparse_pack_scan(void* stream, float* grad_table, int32_t* flag, int64_t 
 int rs_sparse_merge_packed(void* stream, const float* records, const int32_t* counts,
                            int64_t counts_stride, int world, int rank, int dim, float* grad_table,
                            int32_t* flag, int64_t table_rows, int32_t cap);
+/* rs_sparse_merge_packed over a FIXED record layout: rank r's records start at r * stride (the
+ * host all-gathered every rank's whole stride-record buffer, so it never read the counts: no host
+ * synchronisation in the data-parallel step). */
+int rs_sparse_merge_packed_stride(void* stream, const float* records, const int32_t* counts,
+                                  int64_t counts_stride, int world, int rank, int dim,
+                                  float* grad_table, int32_t* flag, int64_t table_rows,
+                                  int32_t cap, int32_t stride);
 
 /* ---------------------------------------------------------------------------------------
  * Math mode (config 2's "bf16" compute mode: BASELINE.json configs[1]).

@@ -149,6 +149,7 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_compact_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _i32]),
     "rs_sparse_pack_scan": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32]),
     "rs_sparse_merge_packed": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i64, _i32]),
+    "rs_sparse_merge_packed_stride": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _i64, _i32, _i32]),
     "rs_il_bwd_push": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                               _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp, _vp,
                               _i32, _vp, _i64]),

@@ -223,6 +223,10 @@ class AutoIntTrainer:
             self.dp_recs = torch.empty(self.dp_cap * self.dp_rs, **f32)
             self.dp_recs_all = torch.empty(self.world * self.dp_cap * self.dp_rs, **f32)
             self.dp_nmax = 0
+            # exchange without a host read (dist.exchange_packed_fixed); RS_DP_SYNC=1 restores
+            # the count-sized exchange with one host synchronisation per step (A/B)
+            import os
+            self.dp_sync_free = not os.environ.get("RS_DP_SYNC")
         elif self.world > 1:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
@@ -439,9 +443,13 @@ class AutoIntTrainer:
 
     def _exchange(self):
         """Data-parallel gradient exchange (recommendsystem_amd/dist.py)."""
-        from .dist import allreduce_flat, exchange_packed, gather_sparse_lists
+        from .dist import allreduce_flat, exchange_packed, exchange_packed_fixed, gather_sparse_lists
         m, t = self.model, self.model.table
         if self.packed_dp:
+            if self.dp_sync_free:
+                exchange_packed_fixed(self.dp_send, self.dp_recv, self.dp_recs, self.dp_recs_all,
+                                      self.dp_cap, self.dp_rs, self.pg)
+                return
             self.dp_nmax = exchange_packed(self.dp_send, self.dp_recv, self.dp_n, self.dp_recs,
                                            self.dp_recs_all, self.dp_rs, self.pg)
             if self.dp_nmax > self.dp_cap:
@@ -480,8 +488,9 @@ class AutoIntTrainer:
             s, t = stream_handle(), m.table
             counts = self.dp_recv.data_ptr() + 4 * self.dp_n
             for r in range(self.world):  # rank order: identical sums on every replica
-                call("rs_sparse_merge_packed", s, ptr(self.dp_recs_all), counts, self.dp_ld,
-                     self.world, r, t.dim, ptr(t.grad), ptr(t.flag), t.rows, self.dp_cap)
+                call("rs_sparse_merge_packed_stride", s, ptr(self.dp_recs_all), counts,
+                     self.dp_ld, self.world, r, t.dim, ptr(t.grad), ptr(t.flag), t.rows,
+                     self.dp_cap, self.dp_cap if self.dp_sync_free else 0)
             # dense: rank-ordered sum of the gathered buckets -> arena grad -> Adam, one launch
             tail = self._scan_tail(t)
             _lib.partials_reduce_adam(s, [(ptr(self.dp_recv), self.dp_ld, self.world, self.dp_n,

@@ -76,13 +76,14 @@ __global__ void __launch_bounds__(kBlock) pack_scan_kernel(
 __global__ void __launch_bounds__(kBlock) merge_packed_kernel(
     const float* __restrict__ recs, const int32_t* __restrict__ counts, int64_t cstride, int world,
     int rank, int dim, int lps, float* __restrict__ grad_table, int32_t* __restrict__ flag,
-    int64_t nrows, int32_t cap) {
+    int64_t nrows, int32_t cap, int32_t stride) {
   int nmax = 0;
   for (int r = 0; r < world; ++r) nmax = max(nmax, counts[r * cstride]);
   nmax = min(nmax, cap);  // the host refuses counts past cap; never read past the buffer
+  if (stride > 0) nmax = min(nmax, stride);  // fixed layout: rank r's records at r * stride
   const int n = min(counts[rank * cstride], nmax);
   const int rs = dim + 1;
-  const float* rec = recs + (int64_t)rank * nmax * rs;
+  const float* rec = recs + (int64_t)rank * (stride > 0 ? stride : nmax) * rs;
   const int per_block = kBlock / lps;
   const int gi = threadIdx.x / lps, l = threadIdx.x % lps;
   for (int u = blockIdx.x * per_block + gi; u < n; u += gridDim.x * per_block) {
@@ -109,15 +110,24 @@ RS_API int rs_sparse_pack_scan(void* stream, float* grad_table, int32_t* flag, i
   return rs_status_after_launch();
 }
 
+RS_API int rs_sparse_merge_packed_stride(void* stream, const float* records,
+                                         const int32_t* counts, int64_t counts_stride, int world,
+                                         int rank, int dim, float* grad_table, int32_t* flag,
+                                         int64_t table_rows, int32_t cap, int32_t stride) {
+  if (!records || !counts || !grad_table || !flag || dim <= 0 || world <= 0 || rank < 0 ||
+      rank >= world || counts_stride <= 0 || table_rows < 0 || cap < 0 || stride < 0)
+    return RS_ERR_ARG;
+  const int lps = dim < 64 ? dim : 64;
+  merge_packed_kernel<<<1024, kBlock, 0, rs_stream(stream)>>>(
+      records, counts, counts_stride, world, rank, dim, lps, grad_table, flag, table_rows, cap,
+      stride);
+  return rs_status_after_launch();
+}
+
 RS_API int rs_sparse_merge_packed(void* stream, const float* records, const int32_t* counts,
                                   int64_t counts_stride, int world, int rank, int dim,
                                   float* grad_table, int32_t* flag, int64_t table_rows,
                                   int32_t cap) {
-  if (!records || !counts || !grad_table || !flag || dim <= 0 || world <= 0 || rank < 0 ||
-      rank >= world || counts_stride <= 0 || table_rows < 0 || cap < 0)
-    return RS_ERR_ARG;
-  const int lps = dim < 64 ? dim : 64;
-  merge_packed_kernel<<<1024, kBlock, 0, rs_stream(stream)>>>(
-      records, counts, counts_stride, world, rank, dim, lps, grad_table, flag, table_rows, cap);
-  return rs_status_after_launch();
+  return rs_sparse_merge_packed_stride(stream, records, counts, counts_stride, world, rank, dim,
+                                       grad_table, flag, table_rows, cap, 0);
 }

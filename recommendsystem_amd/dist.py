@@ -88,14 +88,28 @@ def exchange_packed(send: torch.Tensor, recv: torch.Tensor, n_dense: int, recs: 
     return nmax
 
 
-def merge_packed_reference(recv, ld, n_dense, recs_all, rec_floats, table_grad):
-    """Host restatement of rs_sparse_merge_packed over every rank in order (CPU tests)."""
+def exchange_packed_fixed(send: torch.Tensor, recv: torch.Tensor, recs: torch.Tensor,
+                          recs_all: torch.Tensor, cap: int, rec_floats: int, group=None) -> None:
+    """exchange_packed without the host synchronisation: every rank's WHOLE record buffer (cap
+    records, cap = the most rows one rank can touch per step, so it never overflows) is
+    all-gathered, rank r's at r * cap * rec_floats, and the merge (rs_sparse_merge_packed_stride)
+    reads each rank's count on the device.  More bytes on the links (cap instead of the largest
+    count), no host read: the CPU enqueues the next step while this one runs."""
+    world = dist.get_world_size(group)
+    k = cap * rec_floats
+    _all_gather_flat(recv, send, group)
+    _all_gather_flat(recs_all[:world * k], recs[:k], group)
+
+
+def merge_packed_reference(recv, ld, n_dense, recs_all, rec_floats, table_grad, stride=0):
+    """Host restatement of rs_sparse_merge_packed (stride 0: rank r's records at r * nmax) /
+    rs_sparse_merge_packed_stride (at r * stride) over every rank in order (CPU tests)."""
     world = recv.numel() // ld
     counts = recv.view(torch.int32).view(world, ld)[:, n_dense].tolist()
     nmax = max(counts)
     touched = []
     for r in range(world):
-        base = r * nmax * rec_floats
+        base = r * (stride if stride > 0 else nmax) * rec_floats
         for u in range(counts[r]):
             rec = recs_all[base + u * rec_floats: base + (u + 1) * rec_floats]
             row = int(rec[:1].view(torch.int32)[0])

@@ -123,3 +123,36 @@ def test_dp_packed_exchange_two_ranks():
             ref[r[k]] += g[k]
     assert np.allclose(t0, ref, atol=1e-6)
     assert tc0 == sorted(set(int(v) for rank in range(world) for v in _local_lists(rank)[0] if v >= 0))
+
+
+def _packed_fixed_worker(rank, world, port, out):
+    from recommendsystem_amd.dist import exchange_packed_fixed, merge_packed_reference
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    send, recs, ld = _packed_local(rank)
+    recv = torch.zeros(world * ld)
+    recs_all = torch.full((world * CAP * REC,), float("nan"))
+    exchange_packed_fixed(send, recv, recs, recs_all, CAP, REC)  # no count read on the host
+    table = np.zeros((ROWS, DIM), np.float32)
+    touched = merge_packed_reference(recv, ld, N_DENSE, recs_all, REC, table, stride=CAP)
+    out[rank] = (table.copy(), sorted(touched))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_packed_exchange_fixed_layout_two_ranks():
+    """The sync-free exchange (every rank's whole capacity-sized record buffer, merged at stride
+    cap) gives the same merged gradients as the count-sized one."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_packed_fixed_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    (t0, tc0), (t1, tc1) = out[0], out[1]
+    assert np.array_equal(t0, t1) and tc0 == tc1
+    ref = np.zeros((ROWS, DIM), np.float64)
+    for rank in range(world):
+        r, g, n = _local_lists(rank)
+        for k in range(n):
+            ref[r[k]] += g[k]
+    assert np.allclose(t0, ref, atol=1e-6)
