@@ -387,10 +387,21 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
                                      int32_t* n_touched, int32_t touched_cap);
 
 namespace rs_push {
-constexpr int kThreads = 256;
-constexpr int kTile = 256;                    // samples (= occurrences) per block
+#ifndef RS_PUSH_THREADS  // tuning builds only (tools/push_bench.py variants)
+// 512: same-box push_bench medians vs 256 -- config-4 history (scan) 24.2 -> 22.7 us, config-5
+// 91-field push 94.3 -> 85.6 us; a deeper chunk (8) measured no better
+#define RS_PUSH_THREADS 512
+#endif
+#ifndef RS_PUSH_TILE
+#define RS_PUSH_TILE 256
+#endif
+#ifndef RS_PUSH_CHUNK
+#define RS_PUSH_CHUNK 4
+#endif
+constexpr int kThreads = RS_PUSH_THREADS;
+constexpr int kTile = RS_PUSH_TILE;           // samples (= occurrences) per block
 constexpr int kCap = 2 * kTile;               // LDS hash slots: never full
-constexpr int kChunk = 4;                     // occurrences per lane group in flight
+constexpr int kChunk = RS_PUSH_CHUNK;         // occurrences per lane group in flight
 
 __host__ __device__ constexpr size_t lds_bytes(int dim) {
   return (4 + (size_t)kCap * (2 + dim) + 2 * (size_t)kTile) * 4;

@@ -84,7 +84,15 @@ def case_c5(rng, dev):
     return t, lambda: t.accumulate(r, None, B, F, dout, F * D, D, 1), rows
 
 
-CASES = {"c5": case_c5, "c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2}
+def case_c4_hist_scan(rng, dev):
+    """the config-4 history push as the single-GPU Trainer runs it (scan mode, prefer_scan)"""
+    t, fn, ids = case_c4_hist(rng, dev)
+    t.mode = "scan"
+    return t, fn, ids
+
+
+CASES = {"c5": case_c5, "c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2,
+         "c4_hist_scan": case_c4_hist_scan}
 
 
 def main():
