@@ -552,9 +552,12 @@ __global__ void __launch_bounds__(kThreads) push_claim_kernel(
 }
 
 // samples per block: kTile, smaller for small launches so they still spread over >= ~256 blocks
+#ifndef RS_PUSH_MIN_BLOCKS  // tuning builds only
+#define RS_PUSH_MIN_BLOCKS 256
+#endif
 inline int tile_for(int64_t B, int F) {
   int t = kTile;
-  while (t > 32 && ((B + t - 1) / t) * (int64_t)F < 256) t >>= 1;
+  while (t > 32 && ((B + t - 1) / t) * (int64_t)F < RS_PUSH_MIN_BLOCKS) t >>= 1;
   return t;
 }
 inline int64_t grid_blocks(int64_t B, int F) {
