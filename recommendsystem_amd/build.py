@@ -52,7 +52,12 @@ def _tag(extra: list[str]) -> str:
     return hashlib.sha1(" ".join(extra).encode()).hexdigest()[:8]
 
 
+# per-unit flags (measured choices, see the unit's header comment)
+PER_SOURCE_FLAGS = {"il_inst_a_fwd.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile(src: str, headers: list[str], extra: list[str]) -> str:
+    extra = list(extra) + PER_SOURCE_FLAGS.get(os.path.basename(src), [])
     obj = os.path.join(BUILD_DIR, f"{os.path.basename(src)}.{_tag(extra)}.o")
     if _newer(obj, [src] + headers):
         cmd = [_hipcc(), *COMMON_FLAGS, *extra, "-c", src, "-o", obj]

@@ -2286,8 +2286,17 @@ __host__ __forceinline__ size_t bwd4_lds_bytes(int F) {
   return ((size_t)Bwd3Layout<C>::shared_floats() + (size_t)kWpb3 * Bwd4Layout<C>(F).per_wave) * 4;
 }
 
+#ifndef RS_IL4_PK  // 0: the same even / odd accumulator pairs as scalar v_fma_f32 (tuning builds)
+#define RS_IL4_PK 1
+#endif
 template <int N>
 __device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b)[N]) {
+  if constexpr (!RS_IL4_PK) {
+    float e = 0.f, o = 0.f;
+#pragma unroll
+    for (int d = 0; d < N; d += 2) { e = fmaf(a[d], b[d], e); o = fmaf(a[d + 1], b[d + 1], o); }
+    return e + o;
+  }
   f32x2v acc = {0.f, 0.f};
 #pragma unroll
   for (int d = 0; d < N; d += 2)
@@ -2301,6 +2310,11 @@ template <int N>
 __device__ __forceinline__ void dot2_reg_pk(const float (&a)[N], const float (&b)[N],
                                             const float (&c)[N], const float (&d)[N], float& ab,
                                             float& cd) {
+  if constexpr (!RS_IL4_PK) {
+    ab = dot_reg_pk(a, b);
+    cd = dot_reg_pk(c, d);
+    return;
+  }
   f32x2v x = {0.f, 0.f}, y = {0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < N; k += 2) {
@@ -2313,6 +2327,11 @@ __device__ __forceinline__ void dot2_reg_pk(const float (&a)[N], const float (&b
 
 template <int N>
 __device__ __forceinline__ void axpy_reg_pk(float (&o)[N], float p, const float (&v)[N]) {
+  if constexpr (!RS_IL4_PK) {
+#pragma unroll
+    for (int d = 0; d < N; ++d) o[d] = fmaf(p, v[d], o[d]);
+    return;
+  }
   const f32x2v pp = {p, p};
 #pragma unroll
   for (int d = 0; d < N; d += 2) {
