@@ -226,6 +226,15 @@ int rs_get_math_mode(void);
  * at launch (a captured graph keeps the pointer it was captured with). */
 int rs_set_seed_offset(const int64_t* dev_offset);
 
+/* InteractingLayer kernel variant for the AutoInt shape family (E = U = 16, H = 2, F <= 32):
+ * 0 = auto (default), 1 = one wave per sample (fwd_kernel / bwd4_kernel), 2 = one 4-wave
+ * workgroup per sample (il_wide.hpp: the latency-bound small-batch case and the default).  Same
+ * math and outputs within fp32 summation order; the partial-row count the backward leaves for
+ * rs_partials_reduce_adam follows the variant (ask rs_il_bwd_partial_blocks under the same
+ * setting).  Process-wide, read when a launch is issued.  No reference counterpart. */
+int rs_il_set_variant(int variant);
+int rs_il_get_variant(void);
+
 /* ---------------------------------------------------------------------------------------
  * H3  InteractingLayer (InteractingLayer.py:7-61; rank/multi_head/interacting_layer.py:7-61).
  * x [B, F, E]; W [E, 4U] = [Wq | Wk | Wv | Wr] (Keras Dense kernels), bias [4U],
@@ -579,6 +588,10 @@ int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave, const
 /* Grid (= number of per-block partial rows) rs_il_bwd / rs_il_bwd_push use for this shape and
  * workspace when dy rows are 16-B aligned (dy_ld % 4 == 0); 0 for an unsupported shape. */
 int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t workspace_floats);
+/* The same for the saved entry points (rs_il_bwd_saved / rs_il_bwd_push_saved with the forward's
+ * attention save): shapes that have a save run other kernels with their own grid. */
+int rs_il_bwd_saved_partial_blocks(int64_t B, int F, int E, int U, int H,
+                                   int64_t workspace_floats);
 
 
 /* ---------------------------------------------------------------------------------------

@@ -54,6 +54,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_set_math_mode": (_i32, [_i32]),
     "rs_get_math_mode": (_i32, []),
     "rs_set_seed_offset": (_i32, [_vp]),
+    "rs_il_set_variant": (_i32, [_i32]),
+    "rs_il_get_variant": (_i32, []),
     "rs_il_param_count": (_i32, [_i32, _i32]),
     "rs_il_fwd": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32,
                          _i32, _f32, _u64, _vp, _i64, _vp]),
@@ -140,6 +142,7 @@ SIGNATURES: dict[str, tuple] = {
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32,
                                        _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _f32, _f32]),
     "rs_il_bwd_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i32, _i64]),
+    "rs_il_bwd_saved_partial_blocks": (_i32, [_i64, _i32, _i32, _i32, _i32, _i64]),
     "rs_sparse_adam_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
                                    _f32, _f32]),
     "rs_sparse_adagrad_scan": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32]),
@@ -203,6 +206,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     _LIB = lib
+    v = os.environ.get("RS_IL_VARIANT")  # A/B runs: auto | wave | wide
+    if v:
+        lib.rs_il_set_variant(IL_VARIANTS[v])
     return lib
 
 
@@ -287,6 +293,22 @@ def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=Non
 
 
 MATH_MODES = {"f32": 0, "bf16": 1}
+# rs_il_set_variant: which InteractingLayer kernels run the E = U = 16, H = 2, F <= 32 shapes
+IL_VARIANTS = {"auto": 0, "wave": 1, "wide": 2}
+
+
+@contextlib.contextmanager
+def il_variant(name: str):
+    """rs_il_set_variant for the duration of the block ("auto" | "wave" = one wave per sample |
+    "wide" = one 4-wave workgroup per sample; include/recsys_amd.h)."""
+    if name not in IL_VARIANTS:
+        raise ValueError(f"IL variant must be one of {sorted(IL_VARIANTS)}, got {name!r}")
+    prev = load().rs_il_get_variant()
+    call("rs_il_set_variant", IL_VARIANTS[name])
+    try:
+        yield
+    finally:
+        call("rs_il_set_variant", prev)
 
 
 @contextlib.contextmanager

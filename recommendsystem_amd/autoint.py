@@ -278,8 +278,11 @@ class AutoIntTrainer:
         return dict(N1=N1, N2=N2, T=T, K0=K0, S=S, off=off, npar=npar, ws=ws,
                     blocks=int(lib.rs_mlp_head_partial_blocks(self.B)),
                     il_off=il_off, il_n=il_n,
-                    il_blocks=int(lib.rs_il_bwd_partial_blocks(self.B, self.F, self.E, self.U,
-                                                               self.H, self.il_ws_n)),
+                    # the step's backward reads the forward's attention save when the shape
+                    # has one (rs_il_bwd_push_saved / rs_il_bwd_saved): its kernels' grid
+                    il_blocks=int((lib.rs_il_bwd_saved_partial_blocks if self.asave_n > 0
+                                   else lib.rs_il_bwd_partial_blocks)(
+                        self.B, self.F, self.E, self.U, self.H, self.il_ws_n)),
                     done=torch.zeros(288, device=dev, dtype=torch.int32))
 
     def _forward_backward_fused(self):

@@ -99,11 +99,21 @@ __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)
 // an s_waitcnt vmcnt(0) in front of the next LDS read -- the prefetch would complete
 // synchronously.  The compiler does not see these loads at all, so every vmcnt wait it emits
 // for its own global loads is still correct (in-order return: it may only wait longer).
+// The 32-bit LDS offset of a generic pointer into LDS, wave-uniform (readfirstlane).  The value
+// goes through an empty asm first: otherwise the compiler folds the truncation past the
+// readfirstlane into a 64-bit flat-pointer readfirstlane whose aperture half (src_shared_base)
+// the gfx950 backend rejects ("Operand has incorrect register class") when the pointer is a
+// loop-carried LDS buffer swap.
+__device__ __forceinline__ uint32_t lds_addr_u32(const void* p) {
+  uint32_t v = (uint32_t)(uintptr_t)p;
+  asm volatile("" : "+v"(v));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 __device__ __forceinline__ void glds_copy(float* dst, const float* src, int n4) {
   for (int k = threadIdx.x; k < n4; k += blockDim.x) {
     const int wbase = k - (int)(threadIdx.x & 63);  // wave-uniform
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(dst + 4 * wbase));  // generic -> LDS offset (low 32 bits)
+    const uint32_t lds = lds_addr_u32(dst + 4 * wbase);  // generic -> LDS offset
     const float* g = src + 4 * k;
     uint32_t keep;
     asm volatile(
@@ -123,8 +133,7 @@ __device__ __forceinline__ void glds_copy(float* dst, const float* src, int n4) 
 __device__ __forceinline__ void glds_copy_wave(float* dst, const float* src, int n4) {
   const int lane = (int)(threadIdx.x & 63);
   for (int k = lane; k < n4; k += 64) {
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(dst + 4 * (k - lane)));  // wave-uniform LDS base of this slot
+    const uint32_t lds = lds_addr_u32(dst + 4 * (k - lane));  // wave-uniform LDS base of this slot
     const float* g = src + 4 * k;
     uint32_t keep;
     asm volatile(
@@ -144,8 +153,7 @@ __device__ __forceinline__ void glds_copy_wave(float* dst, const float* src, int
 __device__ __forceinline__ void glds_copy_wave_u32(void* dst, const void* src, int n) {
   const int lane = (int)(threadIdx.x & 63);
   for (int k = lane; k < n; k += 64) {
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(static_cast<uint32_t*>(dst) + (k - lane)));
+    const uint32_t lds = lds_addr_u32(static_cast<uint32_t*>(dst) + (k - lane));
     const uint32_t* g = static_cast<const uint32_t*>(src) + k;
     uint32_t keep;
     asm volatile(

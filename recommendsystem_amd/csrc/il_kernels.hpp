@@ -2831,6 +2831,20 @@ RS_UNROLL(RS_IL4_UNROLL_K)
     partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
 }
 
+// ---- one workgroup per sample (il_wide.hpp) -------------------------------------------------
+// Kernel variant (rs_il_set_variant, process-wide like the math mode, read when a launch is
+// issued): 0 = auto, 1 = the per-sample-wave kernels (fwd_kernel / bwd4_kernel), 2 = the wide
+// kernels wherever they apply.
+enum { RS_IL_VARIANT_AUTO = 0, RS_IL_VARIANT_WAVE = 1, RS_IL_VARIANT_WIDE = 2 };
+int rs_il_variant_now();
+}  // namespace rs_il
+#include "il_wide.hpp"
+namespace rs_il {
+// grids: one workgroup per sample up to these, then persistent workgroups looping over samples
+// (the backward's grid is also the number of per-block partial rows)
+constexpr int kWideFwdGrid = 2048;
+constexpr int kWideBwdGrid = 1024;
+
 // one resident round of v3 blocks on MI355X (2 per CU x 256 CUs); callers size the per-block
 // partial rows with rs_il_bwd_partial_blocks, which applies the same rule
 constexpr int kBwd3Grid = 512;
@@ -2856,6 +2870,16 @@ int fwd_launch(const FwdReq& q) {
   a.g_rows = q.gather_rows;
   a.g_hash = q.gather_hash;
   if constexpr (kSaved4<C>) a.osave = q.asave;  // the saved path's O + softmax stats
+  if constexpr (kWide<C>) {
+    if (rs_il_variant_now() != RS_IL_VARIANT_WAVE) {
+      const size_t lds = (size_t)WideFwdLayout<C>().total * sizeof(float);
+      const int64_t grid = q.B < kWideFwdGrid ? q.B : kWideFwdGrid;
+      if (grid == 0) return RS_OK;
+      wfwd_kernel<C, DROP><<<(int)grid, kWideThreads, lds, q.stream>>>(
+          q.x, q.W, q.bias, q.gamma, q.beta, q.y, q.y_ld, q.xsave, a);
+      return rs_status_after_launch();
+    }
+  }
   const size_t per_wave = (size_t)a.per_wave * sizeof(float);
   int wpb = (int)(kLdsBytes / per_wave);
   if (wpb > kMaxFwdWaves) wpb = kMaxFwdWaves;
@@ -2886,6 +2910,22 @@ int bwd_launch(const BwdReq& q) {
   // x / xsave rows are copied 16 B at a time
   if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
 #ifndef RS_IL_BWD_NO_V3
+  if constexpr (kWide<C>) {  // one workgroup per sample over the forward's save (il_wide.hpp)
+    if (rs_il_variant_now() != RS_IL_VARIANT_WAVE && q.asave && a.dy_vec && q.F >= 1) {
+      int64_t grid = q.B < kWideBwdGrid ? q.B : kWideBwdGrid;
+      const int64_t max_grid = q.workspace_floats / C::NPARAM;
+      if (grid > max_grid) grid = max_grid;
+      if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
+      if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
+      a.osave_in = q.asave;
+      wbwd_kernel<C, DROP><<<(int)grid, kWideThreads, wbwd_lds_bytes<C>(q.F), q.stream>>>(
+          q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
+          q.workspace, a);
+      if (q.dparams)
+        reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
+      return rs_status_after_launch();
+    }
+  }
   if constexpr (kSaved4<C>) {  // v4: the forward's O + softmax stats (rs_il_bwd_saved)
     const size_t lds3 = bwd3_lds_bytes<C>(q.F), lds4 = bwd4_lds_bytes<C>(q.F);
     if (q.asave && a.dy_vec && lds3 <= kLdsBytes / 2 && lds4 <= kLdsBytes / 2 &&

@@ -36,6 +36,20 @@ RS_API int rs_set_math_mode(int mode) {
 
 RS_API int rs_get_math_mode(void) { return rs_math_mode_now(); }
 
+// InteractingLayer kernel variant (il_kernels.hpp: RS_IL_VARIANT_*), process-wide like the math mode
+static int g_il_variant = rs_il::RS_IL_VARIANT_AUTO;
+namespace rs_il {
+int rs_il_variant_now() { return __atomic_load_n(&g_il_variant, __ATOMIC_RELAXED); }
+}  // namespace rs_il
+
+RS_API int rs_il_set_variant(int variant) {
+  if (variant < rs_il::RS_IL_VARIANT_AUTO || variant > rs_il::RS_IL_VARIANT_WIDE) return RS_ERR_ARG;
+  __atomic_store_n(&g_il_variant, variant, __ATOMIC_RELAXED);
+  return RS_OK;
+}
+
+RS_API int rs_il_get_variant(void) { return rs_il::rs_il_variant_now(); }
+
 static const int64_t* g_seed_offset = nullptr;
 const int64_t* rs_seed_offset_now() { return __atomic_load_n(&g_seed_offset, __ATOMIC_RELAXED); }
 
@@ -257,16 +271,18 @@ RS_API int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave
                           need > 0 ? asave : nullptr);
 }
 
-RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
-                                    int64_t workspace_floats) {
+static int il_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t workspace_floats,
+                             bool saved) {
   if (F > 64) {  // il_large.hip's grid rule
     int64_t grid = B < rs_il::kMaxBwdGrid ? B : rs_il::kMaxBwdGrid;
     const int64_t by_ws = workspace_floats / rs_il_param_count(E, U);
     if (grid > by_ws) grid = by_ws;
     return (int)(grid < 0 ? 0 : grid);
   }
-  // the F <= 64 kernels pick v3 or v2 per shape: ask the dispatch (dry run, nothing launched).
-  // Pointers only need the alignment the real call has (the fused trainer's dy is 16-B aligned).
+  // the F <= 64 kernels pick a variant per shape: ask the dispatch (dry run, nothing launched).
+  // Pointers only need the alignment the real call has (the fused trainer's dy is 16-B aligned);
+  // saved: the entry points that read the forward's attention save (another kernel pair for the
+  // shapes that have one)
   static const float kDummy[4] __attribute__((aligned(16))) = {0.f, 0.f, 0.f, 0.f};
   int grid = 0;
   rs_il::BwdReq q{nullptr, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy,
@@ -274,6 +290,17 @@ RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
                   nullptr, workspace_floats};
   q.grid_out = &grid;
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  if (saved && rs_il_attn_save_floats(B < 1 ? 1 : B, F, U, H, 1) > 0) q.asave = kDummy;
   if (bwd_small(q) != RS_OK) return 0;
   return grid;
+}
+
+RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
+                                    int64_t workspace_floats) {
+  return il_partial_blocks(B, F, E, U, H, workspace_floats, false);
+}
+
+RS_API int rs_il_bwd_saved_partial_blocks(int64_t B, int F, int E, int U, int H,
+                                          int64_t workspace_floats) {
+  return il_partial_blocks(B, F, E, U, H, workspace_floats, true);
 }
