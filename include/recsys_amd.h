@@ -659,6 +659,22 @@ int rs_fm_proj_bwd(void* stream, const float* dy, const float* x, int64_t x_ld, 
                    int dx_accumulate, float* dV, int dV_accumulate, float* workspace,
                    int64_t workspace_floats);
 
+/* ---------------------------------------------------------------------------------------
+ * Training metrics: Keras 'acc' / BinaryAccuracy(), tf.keras.metrics.AUC() and
+ * tensornet tn.metric.COPC() / CTR() of the reference's model.compile calls
+ * (rank/ctr/base_model.py:183-190, rough_rank/model.py:215-219, rank/multi_head/model.py:55,
+ * staytime/model.py:81-82).  state: fp64 [rs_ctr_metrics_state_doubles(nthr)], zeroed by the
+ * caller; rs_ctr_metrics_accumulate adds one batch (p / y / w columns with row strides; w
+ * nullable = unit weights; AUC positives are y != 0, Keras's bool cast); rs_ctr_metrics_result
+ * writes out[6] = {AUC (Keras: nthr thresholds, ROC, interpolation), binary accuracy (p > 0.5),
+ * COPC = sum(w y) / sum(w p), CTR = sum(w y) / sum(w), mean prediction, total weight}.
+ * ------------------------------------------------------------------------------------- */
+int64_t rs_ctr_metrics_state_doubles(int nthr);
+int rs_ctr_metrics_accumulate(void* stream, const float* p, int64_t p_ld, const float* y,
+                              int64_t y_ld, const float* w, int64_t w_ld, int64_t B, int nthr,
+                              double* state);
+int rs_ctr_metrics_result(void* stream, const double* state, int nthr, float* out);
+
 #ifdef __cplusplus
 }
 #endif

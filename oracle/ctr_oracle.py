@@ -419,3 +419,36 @@ def staytime_parse_labels(watch_ms, extra_info, bins, sigma=4, left=-19, right=1
     pat = re.compile(STAYTIME_LANDING_RE)
     sw = np.array([5.0 if pat.fullmatch(s) else 1.0 for s in extra_info], dtype=f32)  # :64
     return stay, short, long_, sw
+
+
+def keras_auc(p, y, w=None, num_thresholds=200):
+    """tf.keras.metrics.AUC() (defaults: ROC, summation 'interpolation') as its update_state /
+    result compute it, in numpy (Keras thresholds: [-1e-7, i / (n - 1) for i = 1 .. n - 2,
+    1 + 1e-7] as fp32; a prediction is positive at t when p > t; y cast to bool); the metric sites
+    are rank/ctr/base_model.py:183-190, rough_rank/model.py:215-219, rank/multi_head/model.py:55.
+    Accumulated in float64 (Keras keeps fp32 variables; equal for unit weights below 2^24)."""
+    p = np.asarray(p, dtype=np.float32).reshape(-1)
+    y = np.asarray(y).reshape(-1) != 0
+    w = np.ones_like(p, dtype=np.float64) if w is None else np.asarray(w, dtype=np.float64).reshape(-1)
+    n = num_thresholds
+    thr = np.array([-1e-7] + [(i + 1) / (n - 1) for i in range(n - 2)] + [1.0 + 1e-7],
+                   dtype=np.float32)
+    above = p[None, :] > thr[:, None]                     # [n, B]
+    tp = (above & y[None, :]).astype(np.float64) @ w
+    fp = (above & ~y[None, :]).astype(np.float64) @ w
+    P, N = float(w[y].sum()), float(w[~y].sum())
+    tpr = tp / P if P > 0 else np.zeros(n)
+    fpr = fp / N if N > 0 else np.zeros(n)
+    return float(np.sum((fpr[:-1] - fpr[1:]) * (tpr[:-1] + tpr[1:]) / 2.0))
+
+
+def ctr_metrics(p, y, w=None):
+    """Binary accuracy (threshold 0.5, Keras 'acc' on a one-unit output), COPC = sum(w y) / sum(w p)
+    and CTR = sum(w y) / sum(w) (tensornet tn.metric.COPC / CTR: not vendored, pinned forms)."""
+    p = np.asarray(p, dtype=np.float64).reshape(-1)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    w = np.ones_like(p) if w is None else np.asarray(w, dtype=np.float64).reshape(-1)
+    correct = (y == (p.astype(np.float32) > np.float32(0.5)).astype(np.float64))
+    return {"auc": keras_auc(p, y, w), "acc": float((w * correct).sum() / w.sum()),
+            "copc": float((w * y).sum() / (w * p).sum()), "ctr": float((w * y).sum() / w.sum()),
+            "pctr": float((w * p).sum() / w.sum())}

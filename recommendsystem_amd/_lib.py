@@ -55,6 +55,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_get_math_mode": (_i32, []),
     "rs_set_seed_offset": (_i32, [_vp]),
     "rs_il_set_variant": (_i32, [_i32]),
+    "rs_ctr_metrics_state_doubles": (_i64, [_i32]),
+    "rs_ctr_metrics_accumulate": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _vp]),
+    "rs_ctr_metrics_result": (_i32, [_vp, _vp, _i32, _vp]),
     "rs_il_get_variant": (_i32, []),
     "rs_il_param_count": (_i32, [_i32, _i32]),
     "rs_il_fwd": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32,

@@ -468,7 +468,7 @@ class AutoIntTrainer:
             cnt = t.n_touched[:1].clone()
             call("rs_sparse_compact", stream_handle(), ptr(t.grad), ptr(t.flag), ptr(t.touched),
                  ptr(t.n_touched), t.dim, ptr(self.x_rows), ptr(self.x_grads), t.touched_cap)
-            t.n_touched.zero_()
+            t.n_touched[:1].zero_()  # (the sticky overflow word stays for check_overflow)
         rows_all, grads_all, n = gather_sparse_lists(self.x_rows, self.x_grads, cnt, self.pg)
         for r in range(self.world if n else 0):  # rank order -> identical sums on every replica
             call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,

@@ -580,8 +580,17 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
                                         int64_t workspace_bytes) {
   using namespace rs_push;
   static const bool elect_off = getenv("RS_PUSH_NO_ELECT") != nullptr;  // A/B: the CAS push
+  // the election push's LDS hash must fit this device's per-block LDS (queried once): larger
+  // shapes, or a part with less LDS, take the CAS push
+  static const int64_t lds_max = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+      return (int64_t)64 * 1024;
+    return (int64_t)v;
+  }();
   const bool ok_shape = !elect_off && !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
-                        ((uintptr_t)dout & 15) == 0 && lds_bytes(dim) <= 160 * 1024 &&
+                        ((uintptr_t)dout & 15) == 0 && (int64_t)lds_bytes(dim) <= lds_max &&
                         B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;
   if (!ok_shape || (touched && (!workspace || workspace_bytes < rs_sparse_push_workspace_bytes(B, F))))
     return rs_sparse_grad_accumulate(stream, rows, offsets, B, F, dout, dout_ld, dout_fstride, dim,

@@ -192,6 +192,10 @@ def load_checkpoint(path: str, model, trainer=None, tables=None) -> None:
                     raise ValueError("checkpoint holds no dense optimizer state")
                 for dst, k in zip(st, ("adam/m", "adam/v", "adam/step")):
                     dst.copy_(f.get_tensor(k))
+                # Trainer lr groups: every dense segment has its own Adam step counter, all
+                # advanced once per step (trainer._lr_segments), so they all resume at the step
+                for *_, cnt in getattr(trainer, "segments", ()):
+                    cnt.copy_(trainer.step_count)
         tmeta = json.loads(meta["tables"])
     tabs = _tables(model, trainer, tables)
     if len(tabs) != len(tmeta):

@@ -29,7 +29,8 @@ def exchange_sparse(table, pg, world, x_rows, x_grads):
     cnt = table.n_touched[:1].clone()
     call("rs_sparse_compact", stream_handle(), ptr(table.grad), ptr(table.flag), ptr(table.touched),
          ptr(table.n_touched), table.dim, ptr(x_rows), ptr(x_grads), table.touched_cap)
-    table.n_touched.zero_()
+    table.n_touched[:1].zero_()  # the count only: the completion words reset themselves and the
+    # sticky overflow word n_touched[288] stays set until check_overflow reports it
     rows_all, grads_all, n = gather_sparse_lists(x_rows, x_grads, cnt, pg)
     for r in range(world if n else 0):
         call("rs_sparse_merge_rows", stream_handle(), ptr(rows_all[r]), ptr(grads_all[r]), n,

@@ -53,7 +53,9 @@ def _trainer(seed):
     from recommendsystem_amd.workloads import StaytimeRoughRank
     j = StaytimeRoughRank(rows=20_000, device=DEV, seed=seed)
     j.table.deterministic = True
-    return j, Trainer(j, 5e-4, [j.table])
+    # the DSSM at its own lr (rough_rank/model.py:209): a second dense segment with its own Adam
+    # step counter, which a resume must restore too
+    return j, Trainer(j, 5e-4, [j.table], lr_groups=[(j.dssm, j.rr_cfg.lr_dense)])
 
 
 def test_checkpoint_resume_matches_uninterrupted(tmp_path):
@@ -70,6 +72,7 @@ def test_checkpoint_resume_matches_uninterrupted(tmp_path):
     c, tc = _trainer(99)
     export.load_checkpoint(str(tmp_path), c, tc)
     assert int(tc.step_count) == 2
+    assert all(int(cnt) == 2 for *_, cnt in tc.segments) and len(tc.segments) > 1
     lc = float(tc.step(*batches[2]))
     np.testing.assert_allclose(lc, la[2], rtol=1e-6)
     torch.cuda.synchronize()

@@ -1,0 +1,55 @@
+"""Device training metrics (recommendsystem_amd/metrics.py, csrc/metrics.hip) against the numpy
+restatement of tf.keras.metrics.AUC / binary accuracy / COPC / CTR (oracle/ctr_oracle.py):
+accumulated over several batches, with and without sample weights, predictions placed exactly on
+the fp32 thresholds and at the clip bounds (rank/ctr/base_model.py:183-190)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctr_oracle as npo
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_ctr_metrics_match_oracle(weighted):
+    from recommendsystem_amd.metrics import CtrMetrics
+    rng = np.random.default_rng(3 + weighted)
+    m = CtrMetrics(device=DEV)
+    ps, ys, ws = [], [], []
+    thr = (np.arange(1, 199) / 199.0).astype(np.float32)
+    for k in range(3):
+        B = 4096 if k < 2 else 1000
+        y = (rng.uniform(size=B) < 0.25).astype(np.float32)
+        p = np.clip(rng.beta(2, 5, size=B) + 0.2 * y, 1e-6, 1.0).astype(np.float32)
+        p[:200] = rng.choice(thr, 200)            # exactly on thresholds (p > t is false there)
+        p[200:210] = 1.0
+        p[210:220] = 1e-6
+        w = rng.uniform(0.5, 2.0, size=B).astype(np.float32) if weighted else None
+        pt = torch.from_numpy(p).to(DEV).reshape(B, 1)
+        yt = torch.from_numpy(y).to(DEV)
+        m.update(pt, yt, torch.from_numpy(w).to(DEV) if weighted else None)
+        ps.append(p); ys.append(y); ws.append(w)
+    got = m.result()
+    want = npo.ctr_metrics(np.concatenate(ps), np.concatenate(ys),
+                           np.concatenate(ws) if weighted else None)
+    for k in ("auc", "acc", "copc", "ctr", "pctr"):
+        assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k])), (k, got[k], want[k])
+    m.reset_states()
+    assert m.result()["weight"] == 0.0
+
+
+def test_ctr_metrics_strided_column():
+    """A column of a wider output (the multi-task heads' [B, T] predictions)."""
+    from recommendsystem_amd.metrics import CtrMetrics
+    g = torch.Generator(device=DEV).manual_seed(4)
+    P = torch.rand(512, 7, device=DEV, generator=g)
+    Y = (torch.rand(512, 7, device=DEV, generator=g) < 0.3).float()
+    m = CtrMetrics(device=DEV)
+    m.update(P[:, 3:4], Y[:, 3:4])
+    got = m.result()
+    want = npo.ctr_metrics(P[:, 3].cpu().numpy(), Y[:, 3].cpu().numpy())
+    assert abs(got["auc"] - want["auc"]) <= 1e-6 and abs(got["acc"] - want["acc"]) <= 1e-6

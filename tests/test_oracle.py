@@ -234,3 +234,19 @@ def test_din_twin_matches_numpy_and_finite_differences(variant):
     ts = [torch.tensor(x, requires_grad=True) for x in args]
     assert np.max(np.abs(fn(*ts).detach().numpy() - a)) < 1e-12
     assert torch.autograd.gradcheck(fn, tuple(ts), eps=1e-6, atol=1e-5)
+
+
+def test_keras_auc_restatement():
+    """oracle keras_auc: 1 for separable scores, 0.5 for constant ones, within the 200-threshold
+    binning error of the exact ROC AUC (scikit-learn) on random scores."""
+    from sklearn.metrics import roc_auc_score
+    rng = np.random.default_rng(0)
+    y = (rng.uniform(size=5000) < 0.3).astype(np.float32)
+    assert npo.keras_auc(np.where(y > 0, 0.9, 0.1), y) == pytest.approx(1.0)
+    assert npo.keras_auc(np.full(5000, 0.4), y) == pytest.approx(0.5)
+    p = np.clip(rng.beta(2, 5, size=5000) + 0.15 * y, 0, 1)
+    assert abs(npo.keras_auc(p, y) - roc_auc_score(y, p)) < 3e-3
+    w = rng.uniform(0.5, 2, size=5000)
+    assert abs(npo.keras_auc(p, y, w) - roc_auc_score(y, p, sample_weight=w)) < 3e-3
+    m = npo.ctr_metrics(p, y)
+    assert m["ctr"] == pytest.approx(y.mean()) and m["copc"] == pytest.approx(y.sum() / p.sum())

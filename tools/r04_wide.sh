@@ -6,7 +6,7 @@ D=${OUT:-gpurun_out/r04_wide}
 mkdir -p $D
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_gpu_il_wide.py tests/test_gpu_golden.py tests/test_gpu_fullsize.py \
+  tests/test_gpu_il_wide.py tests/test_gpu_metrics.py tests/test_gpu_export.py tests/test_gpu_golden.py tests/test_gpu_fullsize.py \
   "tests/test_gpu_parity.py::test_interacting_small_saved_pair" \
   "tests/test_gpu_parity.py::test_interacting_forward" "tests/test_gpu_parity.py::test_interacting_backward" \
   "tests/test_gpu_parity.py::test_autoint_train_steps_match_oracle" tests/test_gpu_bf16.py > $D/pytest.log 2>&1
