@@ -2844,6 +2844,11 @@ namespace rs_il {
 // (the backward's grid is also the number of per-block partial rows)
 constexpr int kWideFwdGrid = 2048;
 constexpr int kWideBwdGrid = 1024;
+// auto: the wide forward everywhere (B = 512: 10.1 vs 19.9 us, 4096: 34.6 vs 34.1 us, same-box
+// HIP events); the wide backward up to this batch (512: 22.7 vs 31.2 us, 1024: 36 vs 40.5 us; at
+// 4096 it is throughput-bound at 111 vs 78 us: the one-wave kernel keeps its sweeps' key
+// addresses wave-uniform and needs no cross-wave exchange), profiles/r04_wide_sb
+constexpr int64_t kWideBwdAutoMaxB = 1536;
 
 // one resident round of v3 blocks on MI355X (2 per CU x 256 CUs); callers size the per-block
 // partial rows with rs_il_bwd_partial_blocks, which applies the same rule
@@ -2911,7 +2916,9 @@ int bwd_launch(const BwdReq& q) {
   if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
 #ifndef RS_IL_BWD_NO_V3
   if constexpr (kWide<C>) {  // one workgroup per sample over the forward's save (il_wide.hpp)
-    if (rs_il_variant_now() != RS_IL_VARIANT_WAVE && q.asave && a.dy_vec && q.F >= 1) {
+    const int var = rs_il_variant_now();
+    if ((var == RS_IL_VARIANT_WIDE || (var == RS_IL_VARIANT_AUTO && q.B <= kWideBwdAutoMaxB)) &&
+        q.asave && a.dy_vec && q.F >= 1) {
       int64_t grid = q.B < kWideBwdGrid ? q.B : kWideBwdGrid;
       const int64_t max_grid = q.workspace_floats / C::NPARAM;
       if (grid > max_grid) grid = max_grid;

@@ -151,7 +151,9 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   // X rows F .. 31 stay zero (the projection reads both row tiles unguarded)
   for (int k = F * C::E + tid; k < kWideRows * C::E; k += kWideThreads) X[k] = 0.f;
 
+  IL_STAMP_DECL
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    IL_STAMP(0)
     // ---- the sample's field embeddings -> X ----
     constexpr int QV = C::E / 4;
     if (a.g_table) {
@@ -171,11 +173,13 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
       reinterpret_cast<float4*>(X)[tid] = reinterpret_cast<const float4*>(x + b * F * C::E)[tid];
     }
     lds_barrier();
+    IL_STAMP(1)
     for (int it = 0; it < a.L; ++it) {
       const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       // ---- projections (wave w: columns 16w..16w+15) ----
       wide_project<C>(X, PR, wp, bp, w);
       lds_barrier();
+      IL_STAMP(2)
       // ---- attention: (head, query) quad, keys qq + 4m ----
       {
         float qv[DH];
@@ -235,6 +239,7 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
         }
       }
       lds_barrier();
+      IL_STAMP(3)
       // ---- z = relu(O + R); y = LN(z): 8 lanes per row, two columns each ----
       {
         const bool act = lf < F;
@@ -259,8 +264,10 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
         }
       }
       lds_barrier();
+      IL_STAMP(4)
     }
   }
+  IL_STAMP_FLUSH(a.stamps)
 }
 
 // ============================== backward (saved path) =========================================
@@ -355,8 +362,10 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
     glds_copy(SB, s_src(b0, a.L - 1), ns4);
     glds_copy(DY, dy + b0 * dy_ld, ny4);
   }
+  IL_STAMP_DECL
   for (int64_t b = b0; b < a.B; b += bstep) {
     for (int it = a.L - 1; it >= 0; --it) {
+      IL_STAMP(0)
       const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       const int64_t bn = it > 0 ? b : b + bstep;  // the next iteration's sample
       const int itn = it > 0 ? it - 1 : a.L - 1;
@@ -378,6 +387,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
       }
       vm_wait_all();  // this wave's prefetches of X / save (/ dy) for this iteration
       lds_barrier();
+      IL_STAMP(1)
       // ---- P1: projections (wave w: columns 16w..) and dW's X operand into registers ----
       wide_project<C>(XB, PR, wp, bp, w);
       float xa[2][4];
@@ -392,6 +402,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         glds_copy(SN, s_src(bn, itn), ns4);
       }
       lds_barrier();
+      IL_STAMP(2)
       // ---- P3: z = relu(O + R); LN + ReLU backward -> dO (SB), gR (PR's R slot), D ----
       {
         const int t_ = tid_v();
@@ -428,6 +439,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         }
       }
       lds_barrier();
+      IL_STAMP(3)
       // ---- Q-pass: (head, query) quad, keys qq + 4m: P, dS -> PM, PD; dq -> DY ----
       {
         RS_W_ATTN_IDX
@@ -488,6 +500,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         if (aact) *reinterpret_cast<float2*>(DY + ai * U + ah * DH + 2 * qq) = mine;
       }
       lds_barrier();
+      IL_STAMP(4)
       // ---- K-pass: (head, key) quad, queries qq + 4m: dV, dK -> PR's V, K slots ----
       {
         RS_W_ATTN_IDX
@@ -540,6 +553,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         }
       }
       lds_barrier();
+      IL_STAMP(5)
       // dO (SB) is dead: at the last iteration of the sample the next sample's dy streams into
       // DY once P7 has read dq (below, after the dx exchange barrier)
       // ---- P7: G = [gQ | gK | gV | gR] column tile w; dW += X^T G, db; dx partial = G W_w^T ----
@@ -595,6 +609,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
           for (int r = 0; r < 4; ++r) XS[((w * 2 + rt) * 4 + r) * 64 + lane] = acc[rt][r];
       }
       lds_barrier();
+      IL_STAMP(6)
       if (it == 0 && has_next) glds_copy(DY, dy + bn * dy_ld, ny4);  // the next sample's dy
       // ---- dx = sum of the 4 partial tiles (wave order), cells (pf, pe) and (pf + 16, pe):
       //      -> DY (the next iteration's dy), or the fused push, or dx ----
@@ -627,6 +642,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
           if (pf + 16 < F) d[(pf + 16) * E + pe] = dx_accumulate ? d[(pf + 16) * E + pe] + v[1] : v[1];
         }
       }
+      if (it > 0) { IL_STAMP(7) } else { IL_STAMP(8) }
       float* t = XB; XB = XN; XN = t;
       t = SB; SB = SN; SN = t;
     }
@@ -634,6 +650,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
   // ---- block partials: dW tiles are disjoint per wave (no reduction), db over q, dgamma / dbeta
   //      over rows (lanes) then waves, fixed order ----
 #undef RS_W_ATTN_IDX
+  IL_STAMP_FLUSH(a.stamps)
   const int tid = threadIdx.x, lane = lane_id(), q = lane >> 4, jx = lane & 15;
   dbp += __shfl_xor(dbp, 16, 64);
   dbp += __shfl_xor(dbp, 32, 64);
