@@ -131,8 +131,12 @@ class AutoIntTrainer:
     """
 
     def __init__(self, model: AutoInt, batch_size: int, process_group=None,
-                 deterministic: bool = False):
+                 deterministic: bool = False, metrics=None):
+        """metrics: a metrics.CtrMetrics updated with (p, labels) inside every step (the Keras
+        'acc' / AUC() / tn.metric.COPC() of rank/ctr/base_model.py:183-190; one more launch per
+        step, captured with the rest).  None (the benchmark) skips it."""
         self.model = m = model
+        self.metrics = metrics
         cfg = m.cfg
         self.B = B = int(batch_size)
         self.F, self.E, self.U = F, E, U = cfg.num_fields, cfg.embed_dim, cfg.unit_num
@@ -371,6 +375,11 @@ class AutoIntTrainer:
             self._forward_backward_modal()
 
     def _forward_backward_modal(self):
+        self._forward_backward_core()
+        if self.metrics is not None:
+            self.metrics.update(self.p, self.labels)
+
+    def _forward_backward_core(self):
         if self.head is not None:
             self._forward_backward_fused()
             if self.world > 1:
@@ -528,6 +537,8 @@ class AutoIntTrainer:
         out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]
         if self.head is not None:
             out.append(self.head["done"])
+        if self.metrics is not None:
+            out.append(self.metrics.state)  # warm-up steps leave the metric totals untouched
         return out
 
     def _warmup(self, steps: int) -> None:

@@ -921,374 +921,12 @@ __global__ void __launch_bounds__(256, 4) fwd_kernel(
   }
 }
 
-// ============================== backward kernel ==============================================
-// One workgroup = one sample at a time, TWO waves sharing the sample's LDS (the per-sample state
-// is ~25 KB, so one wave per sample would cap occupancy at 1 wave/SIMD; two waves per sample give
-// ~10 waves/CU).  Row-parallel phases (projection, LN, dW, dx) split rows between the waves;
-// attention phases keep the lane = (head, row) mapping and split the inner loop (keys for the
-// row-oriented softmax / dS / dQ passes, queries for the column-oriented dV / dK passes), the
-// two partials meeting in LDS regions that are dead during that phase:
-//   fwd recompute : GPR region holds (m_w, l_w, o_w) per row
-//   dV / dQ / dK  : DY region holds the second wave's partial row vector, ST the partial D_i.
-// Every sum combines the partials in a fixed order (wave 0 + wave 1): deterministic.
-template <class C, bool DROP>
-#ifndef RS_IL_BWD_OCC
-#define RS_IL_BWD_OCC 2
-#endif
-__global__ void __launch_bounds__(128, RS_IL_BWD_OCC) bwd_kernel(
-    const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
-    int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
-    int dx_accumulate, float* __restrict__ partials, Args a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);  // dropout seed of this launch
-  constexpr int JH = (C::FMAX + 1) / 2;  // keys per wave in the split-j passes
-  float* base = smem;
-  float* X = base + a.l_x;
-  float* PR = base + a.l_pr;
-  float* GPR = base + a.l_gpr;
-  float* O = base + a.l_o;
-  float* DY = base + a.l_dy;
-  float* PM = base + a.l_pm;
-  float* ST = base + a.l_st;
-  const int lane = lane_id();
-  const int w = wave_id();  // 0 or 1
-  const int F = a.F;
-  const int HF = C::H * F;
-  const int j0 = w * JH;    // this wave's key (or query) half
-
-  for (int k = F * C::PRS + threadIdx.x; k < C::FMAX * C::PRS; k += blockDim.x) PR[k] = 0.f;
-  __syncthreads();
-
-  using M = MfmaW<C>;
-  MfmaW<C> mw;
-  mw.load(W, bias);
-  f32x4 dwacc[M::ET][M::NT];
-  float dbp[M::NT];
-#pragma unroll
-  for (int et = 0; et < M::ET; ++et)
-#pragma unroll
-    for (int nt = 0; nt < M::NT; ++nt) dwacc[et][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int nt = 0; nt < M::NT; ++nt) dbp[nt] = 0.f;
-  float dg[C::CPLN], dbt[C::CPLN], gam[C::CPLN];
-  const int u0 = lane % C::LPR;
-#pragma unroll
-  for (int c = 0; c < C::CPLN; ++c) { dg[c] = 0.f; dbt[c] = 0.f; gam[c] = gamma[u0 + c * C::LPR]; }
-  const int nrt = (F + 15) / 16;  // 16-row tiles; wave w takes tiles w, w + 2, ...
-
-  IL_STAMP_DECL
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    {
-      const float* src = dy + b * dy_ld;
-      for (int k = threadIdx.x; k < F * C::U; k += blockDim.x) DY[k] = src[k];
-    }
-    for (int it = a.L - 1; it >= 0; --it) {
-      IL_STAMP(0)
-      const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
-      {
-        const float* xin = (it == 0) ? (x + b * F * C::E)
-                                     : (xsave + ((int64_t)(it - 1) * a.B + b) * F * C::U);
-        const float4* src = reinterpret_cast<const float4*>(xin);
-        for (int k = threadIdx.x; k < F * C::E / 4; k += blockDim.x)
-          reinterpret_cast<float4*>(X)[k] = src[k];
-      }
-      __syncthreads();
-      IL_STAMP(1)
-      // ---- recompute: projections (row tiles split between the waves; MFMA) ----
-      for (int rt = w; rt < nrt; rt += 2) mfma_project<C>(X, PR, F, rt, mw);
-      __syncthreads();
-      IL_STAMP(2)
-      // ---- recompute: attention, keys split between the waves ----
-      for (int r0 = 0; r0 < HF; r0 += 64) {
-        const int r = r0 + lane;
-        const bool act = r < HF;
-        const int h = act ? r / F : 0, i = act ? r % F : 0;
-        float q[C::DH];
-        load_row(q, PR + i * C::PRS + h * C::DH);
-        const float* kb = PR + C::U + h * C::DH;
-        float s[JH];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int j = j0 + jj;
-          const float acc = (j < C::FMAX) ? dot_row(q, kb + j * C::PRS) : 0.f;
-          s[jj] = (j < F) ? acc * a.sc2 : -INFINITY;
-          mx = fmaxf(mx, s[jj]);
-        }
-        float* xch = GPR + r * (5 + 2 * C::DH);  // [m0 m1 l0 l1 | o0[DH] | o1[DH]], odd stride
-        if (act) xch[w] = mx;
-        __syncthreads();
-        const float m = act ? fmaxf(xch[0], xch[1]) : 0.f;
-        float l = 0.f;
-        float o[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) o[d] = 0.f;
-        const float* vb = PR + 2 * C::U + h * C::DH;
-#pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int j = j0 + jj;
-          s[jj] = __builtin_amdgcn_exp2f(s[jj] - m);
-          l += s[jj];
-          float e = s[jj];
-          if (DROP && j < F) e = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? e * a.drop_scale : 0.f;
-          if (j < C::FMAX) axpy_row(o, e, vb + j * C::PRS);
-        }
-        if (act) {
-          xch[2 + w] = l;
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) xch[4 + w * C::DH + d] = o[d];
-        }
-        __syncthreads();
-        if (act) {
-          const float inv = 1.0f / (xch[2] + xch[3]);
-          float* pm_row = PM + (h * F + i) * C::PMS;
-#pragma unroll
-          for (int jj = 0; jj < JH; ++jj)
-            if (j0 + jj < C::FMAX) pm_row[j0 + jj] = s[jj] * inv;
-          if (w == 0) {
-            float ov[C::DH];
-#pragma unroll
-            for (int d = 0; d < C::DH; ++d) ov[d] = (xch[4 + d] + xch[4 + C::DH + d]) * inv;
-            store_row(O + i * C::OS + h * C::DH, ov);
-          }
-        }
-        __syncthreads();
-      }
-      IL_STAMP(3)
-      // ---- recompute: z = relu(O + R), LN stats (rows split) ----
-      for (int f0 = w * C::RG; f0 < F; f0 += 2 * C::RG) {
-        const int f = f0 + lane / C::LPR;
-        const bool act = f < F;
-        float z[C::CPLN];
-        float sum = 0.f;
-#pragma unroll
-        for (int c = 0; c < C::CPLN; ++c) {
-          const int u = u0 + c * C::LPR;
-          float t = act ? O[f * C::OS + u] : 0.f;
-          if (a.use_res && act) t += PR[f * C::PRS + 3 * C::U + u];
-          z[c] = fmaxf(t, 0.f);
-          sum += z[c];
-        }
-        const float mean = group_sum<C::LPR>(sum) * (1.0f / (float)C::U);
-        float sq = 0.f;
-#pragma unroll
-        for (int c = 0; c < C::CPLN; ++c) { const float d = z[c] - mean; sq += d * d; }
-        const float var = group_sum<C::LPR>(sq) * (1.0f / (float)C::U);
-        const float rstd = 1.0f / sqrtf(var + a.eps);
-        // ---- LN + ReLU backward, fused: O <- dt; GPR[R] <- dt * (R > 0) ----
-        float zh[C::CPLN], g[C::CPLN];
-        float sg = 0.f, sgz = 0.f;
-#pragma unroll
-        for (int c = 0; c < C::CPLN; ++c) {
-          const int u = u0 + c * C::LPR;
-          zh[c] = (z[c] - mean) * rstd;
-          const float dyv = act ? DY[f * C::U + u] : 0.f;
-          dg[c] = fmaf(dyv, zh[c], dg[c]);
-          dbt[c] += dyv;
-          g[c] = dyv * gam[c];
-          sg += g[c];
-          sgz += g[c] * zh[c];
-        }
-        sg = group_sum<C::LPR>(sg) * (1.0f / (float)C::U);
-        sgz = group_sum<C::LPR>(sgz) * (1.0f / (float)C::U);
-        if (act) {
-#pragma unroll
-          for (int c = 0; c < C::CPLN; ++c) {
-            const int u = u0 + c * C::LPR;
-            const float dz = (g[c] - sg - zh[c] * sgz) * rstd;
-            const float dt = z[c] > 0.f ? dz : 0.f;  // TF ReluGrad: x > 0
-            O[f * C::OS + u] = dt;
-            GPR[f * C::PRS + 3 * C::U + u] =
-                (a.use_res && PR[f * C::PRS + 3 * C::U + u] > 0.f) ? dt : 0.f;
-          }
-        }
-      }
-      __syncthreads();
-      IL_STAMP(4)
-      // ---- dV_j = sum_i Pd_ij dO_i   (lane = (h, j); queries split between the waves) ----
-      for (int r0 = 0; r0 < HF; r0 += 64) {
-        const int r = r0 + lane;
-        const bool act = r < HF;
-        const int h = act ? r / F : 0, j = act ? r % F : 0;
-        float dv[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) dv[d] = 0.f;
-#pragma unroll
-        for (int ii = 0; ii < JH; ++ii) {
-          const int i = j0 + ii;
-          if (C::EXACT ? (i < C::FMAX) : (i < F)) {  // compile-time for exact-F shapes
-            float p = PM[(h * F + i) * C::PMS + j];
-            if (DROP) p = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? p * a.drop_scale : 0.f;
-            axpy_row(dv, p, O + i * C::OS + h * C::DH);
-          }
-        }
-        float* part = DY + r;  // [d][row]: element d at part[d * HF]
-        if (act && w == 1) {
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d * HF] = dv[d];
-        }
-        __syncthreads();
-        if (act && w == 0) {
-          float vr[C::DH];
-          load_row(vr, PR + j * C::PRS + 2 * C::U + h * C::DH);
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) vr[d] = vr[d] > 0.f ? dv[d] + part[d * HF] : 0.f;
-          store_row(GPR + j * C::PRS + 2 * C::U + h * C::DH, vr);
-        }
-        __syncthreads();
-      }
-      IL_STAMP(5)
-      // ---- dS (in place of P) and dQ   (lane = (h, i); keys split between the waves) ----
-      for (int r0 = 0; r0 < HF; r0 += 64) {
-        const int r = r0 + lane;
-        const bool act = r < HF;
-        const int h = act ? r / F : 0, i = act ? r % F : 0;
-        float dO[C::DH];
-        load_row(dO, O + i * C::OS + h * C::DH);
-        const float* vb = PR + 2 * C::U + h * C::DH;
-        const float* kb = PR + C::U + h * C::DH;
-        float* pm_row = PM + (h * F + i) * C::PMS;
-        float s[JH];
-        float Dw = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int j = j0 + jj;
-          float dp = (j < C::FMAX) ? dot_row(dO, vb + j * C::PRS) : 0.f;  // padded V rows: 0
-          if (DROP && j < F) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          const float p = (j < C::FMAX) ? pm_row[j] : 0.f;                // padded keys: p = 0
-          Dw = fmaf(p, dp, Dw);
-          s[jj] = dp;
-        }
-        if (act) ST[w * HF + r] = Dw;
-        __syncthreads();
-        const float D = act ? ST[r] + ST[HF + r] : 0.f;
-        float dq[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) dq[d] = 0.f;
-#pragma unroll
-        for (int jj = 0; jj < JH; ++jj) {
-          const int j = j0 + jj;
-          if (j < C::FMAX) {
-            const float ds = pm_row[j] * (s[jj] - D) * a.inv_sdh;
-            axpy_row(dq, ds, kb + j * C::PRS);
-            if (act) pm_row[j] = ds;
-          }
-        }
-        float* part = DY + r;
-        if (act && w == 1) {
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d * HF] = dq[d];
-        }
-        __syncthreads();
-        if (act && w == 0) {
-          float qr[C::DH];
-          load_row(qr, PR + i * C::PRS + h * C::DH);
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) qr[d] = qr[d] > 0.f ? dq[d] + part[d * HF] : 0.f;
-          store_row(GPR + i * C::PRS + h * C::DH, qr);
-        }
-        __syncthreads();
-      }
-      IL_STAMP(6)
-      // ---- dK_j = sum_i dS_ij Q_i   (lane = (h, j); queries split between the waves) ----
-      for (int r0 = 0; r0 < HF; r0 += 64) {
-        const int r = r0 + lane;
-        const bool act = r < HF;
-        const int h = act ? r / F : 0, j = act ? r % F : 0;
-        float dk[C::DH];
-#pragma unroll
-        for (int d = 0; d < C::DH; ++d) dk[d] = 0.f;
-#pragma unroll
-        for (int ii = 0; ii < JH; ++ii) {
-          const int i = j0 + ii;
-          if (C::EXACT ? (i < C::FMAX) : (i < F))
-            axpy_row(dk, PM[(h * F + i) * C::PMS + j], PR + i * C::PRS + h * C::DH);
-        }
-        float* part = DY + r;
-        if (act && w == 1) {
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) part[d * HF] = dk[d];
-        }
-        __syncthreads();
-        if (act && w == 0) {
-          float kr[C::DH];
-          load_row(kr, PR + j * C::PRS + C::U + h * C::DH);
-#pragma unroll
-          for (int d = 0; d < C::DH; ++d) kr[d] = kr[d] > 0.f ? dk[d] + part[d * HF] : 0.f;
-          store_row(GPR + j * C::PRS + C::U + h * C::DH, kr);
-        }
-        __syncthreads();
-      }
-      IL_STAMP(7)
-      // ---- dW += X^T G, db += colsum G; dx = G W^T  (row tiles split between the waves; MFMA) ----
-      for (int rt = w; rt < nrt; rt += 2) {
-        mfma_dw<C>(X, GPR, F, rt, dwacc, dbp);
-        if (it > 0) mfma_dx<C>(GPR, F, rt, mw, DY, C::U, false);  // dL/d(previous output)
-        else if (a.push_table)
-          mfma_dx_push<C>(GPR, F, rt, mw, dx_accumulate ? dx + b * F * C::E : nullptr,
-                          a.push_rows + b * F, a.push_table, a.push_flag);
-        else mfma_dx<C>(GPR, F, rt, mw, dx + b * F * C::E, C::E, dx_accumulate != 0);
-      }
-      __syncthreads();
-      IL_STAMP(8)
-    }
-  }
-  IL_STAMP_FLUSH(a.stamps)
-
-  // ---- lanes -> wave -> block (wave order): dW from the MFMA accumulators (D row = e,
-  //      col = c), db partials summed over the 4 lane groups, LN grads over the row groups ----
-#pragma unroll
-  for (int nt = 0; nt < M::NT; ++nt) {
-    dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
-    dbp[nt] += __shfl_xor(dbp[nt], 32, 64);
-  }
-#pragma unroll
-  for (int c = 0; c < C::CPLN; ++c) {
-#pragma unroll
-    for (int o = C::LPR; o < 64; o <<= 1) {
-      dg[c] += __shfl_xor(dg[c], o, 64);
-      dbt[c] += __shfl_xor(dbt[c], o, 64);
-    }
-  }
-  float* RED = base;  // the sample region is dead now
-  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x) RED[k] = 0.f;
-  __syncthreads();
-  {
-    const int q = lane >> 4, j = lane & 15;
-    for (int ww = 0; ww < 2; ++ww) {
-      if (w == ww) {
-#pragma unroll
-        for (int et = 0; et < M::ET; ++et)
-#pragma unroll
-          for (int nt = 0; nt < M::NT; ++nt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int e = 16 * et + 4 * q + r;
-              if (e < C::E) RED[e * C::NC + 16 * nt + j] += dwacc[et][nt][r];
-            }
-        if (q == 0) {
-#pragma unroll
-          for (int nt = 0; nt < M::NT; ++nt) RED[C::E * C::NC + 16 * nt + j] += dbp[nt];
-        }
-        if (lane < C::LPR) {
-#pragma unroll
-          for (int c = 0; c < C::CPLN; ++c) {
-            const int u = u0 + c * C::LPR;
-            RED[C::E * C::NC + C::NC + u] += dg[c];
-            RED[C::E * C::NC + C::NC + C::U + u] += dbt[c];
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int k = threadIdx.x; k < C::NPARAM; k += blockDim.x)
-    partials[(int64_t)blockIdx.x * C::NPARAM + k] = RED[k];
-}
-
 // ============================== backward kernel, v2 ===========================================
-// Same math and the same two-waves-per-sample split as bwd_kernel, re-laid out for occupancy:
+// One workgroup = one sample at a time, TWO waves sharing the sample's LDS (row-parallel phases
+// split rows between the waves; attention phases keep lane = (head, row) and split the inner
+// loop -- keys for the softmax / dS / dQ passes, queries for dV / dK -- the partials meeting in
+// LDS regions dead in that phase; round 1's first backward, since removed, had this split with a
+// separate gradient region), laid out for occupancy:
 //   * no gradient region: the projection gradients overwrite Q, K, V, R in place as each input
 //     dies (R after the LN backward; V after dS; K after dQ; Q after dK), dV / dQ wait in
 //     TMP / DY / O meanwhile -> ~20 KB of LDS per sample instead of ~26 KB;
@@ -1648,7 +1286,7 @@ __global__ void __launch_bounds__(128, RS_IL_BWD2_OCC) bwd2_kernel(
   vm_wait_all();
   IL_STAMP_FLUSH(a.stamps)
 
-  // ---- lanes -> wave -> block (wave order), as bwd_kernel ----
+  // ---- lanes -> wave -> block (wave order) ----
 #pragma unroll
   for (int nt = 0; nt < M::NT; ++nt) {
     dbp[nt] += __shfl_xor(dbp[nt], 16, 64);
@@ -2903,7 +2541,6 @@ int fwd_launch(const FwdReq& q) {
   return rs_status_after_launch();
 }
 
-#ifndef RS_IL_BWD_V1
 template <class C, bool DROP>
 int bwd_launch(const BwdReq& q) {
   if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
@@ -2990,31 +2627,6 @@ int bwd_launch(const BwdReq& q) {
     reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
   return rs_status_after_launch();
 }
-#else
-template <class C, bool DROP>
-int bwd_launch(const BwdReq& q) {
-  if (q.F > C::FMAX) return RS_ERR_UNSUPPORTED;
-  Args a = make_args<C>(q.B, q.F, q.L, q.use_res, q.eps, q.drop_rate, q.seed, true);
-  a.push_rows = q.push_rows;
-  a.push_table = q.push_table;
-  a.push_flag = q.push_flag;
-  // exchange scratch fits: fwd partials (4 + 2*DH per row) in GPR, D partials in ST
-  if (C::H * q.F * (5 + 2 * C::DH) > q.F * C::PRS) return RS_ERR_UNSUPPORTED;
-  const size_t lds = (size_t)a.per_wave * sizeof(float);
-  if (lds > kLdsBytes || (size_t)C::NPARAM > (size_t)a.per_wave) return RS_ERR_UNSUPPORTED;
-  int64_t grid = q.B;
-  const int64_t max_grid = q.workspace_floats / C::NPARAM;
-  if (grid > kMaxBwdGrid) grid = kMaxBwdGrid;
-  if (grid > max_grid) grid = max_grid;
-  if (grid <= 0) return q.B == 0 ? RS_OK : RS_ERR_ARG;
-  bwd_kernel<C, DROP><<<(int)grid, 128, lds, q.stream>>>(
-      q.x, q.xsave, q.dy, q.dy_ld, q.W, q.bias, q.gamma, q.beta, q.dx, q.dx_accumulate,
-      q.workspace, a);
-  if (q.dparams)  // NULL: leave the per-block partials in the workspace (kernel timing)
-    reduce_params(q.stream, q.workspace, (int)grid, C::NPARAM, q.dparams, q.dparams_accumulate);
-  return rs_status_after_launch();
-}
-#endif
 
 // EXACT instantiations (F == FMAX) drop the padded-key mask entirely.
 // BF16: this shape also has bf16-math-mode instantiations (only the shapes a bf16 benchmark

@@ -13,20 +13,24 @@
 //     (Q, K, V, R for w = 0..3), the matching dW tile (no cross-wave reduction: the tiles are
 //     disjoint) and the k-chunk 16w.. of dx = G W^T (4 partial tiles summed in wave order in
 //     LDS).  Each wave's weight fragments (4 + 4 floats + bias) stay in VGPRs for the kernel.
-//   * attention by (head, row, quarter): lane group g = tid / 4 is (head g / 32, row g % 32)
-//     and its 4 lanes take keys (or queries) j = quarter + 4m; the quarter partials meet by DPP
-//     quad sums (no LDS, no barrier).
+//   * attention sweeps by KEY (or query) across the waves: lane = (head, row) = h F + i as in
+//     the one-wave kernels, wave w takes keys j = w, w + 4, ... -- the key rows are wave-uniform
+//     (broadcast LDS reads, scalar loop control, no per-lane address math), so each wave runs
+//     the lean bwd4-style sweep over a quarter of the keys.  The waves' partials meet in LDS:
+//     forward (m_w, l_w, o_w) combined flash-style in the LN epilogue; backward dq partials
+//     (Q-pass, 4 waves) and dv (waves 0, 1) / dk (waves 2, 3) partials (K-pass, queries split
+//     in two) summed in wave order by a combine phase that also applies the ReLU masks.
 //   * LN (forward epilogue / backward) by (row, column pair): 8 lanes per row, DPP row sums.
 // Per sample-iteration the backward stores P (dropout-applied) and dS = P (dP - D) in LDS in the
-// Q-pass, so the K-pass (dV, dK) does no dP recompute.  A workgroup needs ~31 KB of LDS
-// (F = 26) and few VGPRs, so 4-5 workgroups (16-20 waves) share a CU.
+// Q-pass, so the K-pass (dV, dK) does no dP recompute.  A workgroup needs ~49 KB of LDS in the
+// backward (3 per CU, 135 VGPRs) and ~23 KB in the forward.
 //
 // Numerics: fp32 everywhere (bf16 math mode: the same bf16 MFMA operand rounding as the
 // per-sample-wave kernels); the projections use mfma tiles identical to mfma_project (bitwise the
 // same Q/K/V/R); scores q . k in even/odd fma pairs (dot_reg_pk) in the forward and the backward
-// (bitwise the same S, so P recomputed from the saved (max, 1/sum) matches the forward's);
-// softmax, attention output and LN sums use 4-way / 8-way partial sums (a different, fixed order
-// than the per-sample-wave kernels: deterministic, within fp32 rounding of them).
+// (bitwise the same S); softmax / attention / LN sums in a different fixed order than the
+// per-sample-wave kernels (partials per wave, combined in wave order): deterministic, within fp32
+// rounding of them.
 #pragma once
 
 namespace rs_il {
@@ -114,15 +118,19 @@ __device__ __forceinline__ void wide_load_w(const float* __restrict__ W, const f
 // ============================== forward =======================================================
 template <class C>
 struct WideFwdLayout {
-  int xb, pr, total;
+  int xb, pr, fp, total;
   __host__ __device__ WideFwdLayout() {
     xb = 0;
     pr = xb + kWideRows * C::E;
-    total = pr + kWideRows * C::PRS;
+    fp = pr + kWideRows * C::PRS;
+    total = fp + 4 * 64 * 12;
   }
 };
 
-template <class C, bool DROP>
+// SKIP (diagnostic instantiations only, tools/il_variants.hip; 0 in the library): bits drop phases
+// to time them by elimination (results are wrong).  Forward: 1 projection, 2 attention, 4 LN
+// epilogue, 8 input load.  Backward: 1 P1, 2 P3, 4 Q-pass, 8 K-pass, 16 P7, 32 dx sum / push.
+template <class C, bool DROP, int SKIP = 0>
 __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
     const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y,
@@ -134,6 +142,7 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   const WideFwdLayout<C> lay;
   float* const X = smem + lay.xb;
   float* const PR = smem + lay.pr;
+  float* const FP = smem + lay.fp;  // attention partials [wave][lane][12]
   const int tid = threadIdx.x;
   const int w = wave_id();
   const int F = C::EXACT ? C::FMAX : a.F;
@@ -144,10 +153,6 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   // LN lanes: row lf, columns u0, u0 + 1
   const int lf = tid >> 3, u0 = 2 * (tid & 7);
   const float gm0 = gamma[u0], gm1 = gamma[u0 + 1], bt0 = beta[u0], bt1 = beta[u0 + 1];
-  // attention lanes: (head ah, query row ai), keys qq + 4m
-  const int ag = tid >> 2, ah = ag >> 5, ai0 = ag & 31, qq = tid & 3;
-  const bool aact = ai0 < F;
-  const int ai = aact ? ai0 : 0;
   // X rows F .. 31 stay zero (the projection reads both row tiles unguarded)
   for (int k = F * C::E + tid; k < kWideRows * C::E; k += kWideThreads) X[k] = 0.f;
 
@@ -156,7 +161,8 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
     IL_STAMP(0)
     // ---- the sample's field embeddings -> X ----
     constexpr int QV = C::E / 4;
-    if (a.g_table) {
+    if (SKIP & 8) {
+    } else if (a.g_table) {
       // fused single-hot gather (as fwd_kernel): float4 k = quarter k % 4 of field k / 4's row
       float4* xo = reinterpret_cast<float4*>(const_cast<float*>(x) + b * F * C::E);
       if (tid < F * QV) {
@@ -177,82 +183,97 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
     for (int it = 0; it < a.L; ++it) {
       const uint64_t lseed = splitmix64(seed0 + (uint64_t)it);
       // ---- projections (wave w: columns 16w..16w+15) ----
-      wide_project<C>(X, PR, wp, bp, w);
+      if constexpr (!(SKIP & 1)) wide_project<C>(X, PR, wp, bp, w);
       lds_barrier();
       IL_STAMP(2)
-      // ---- attention: (head, query) quad, keys qq + 4m ----
-      {
+      // ---- attention partials: lane = (head, query i) (lane = h F + i), wave w takes keys
+      //      j = w, w + 4, ... (wave-uniform key rows): its running max m_w, sum l_w and
+      //      unnormalised output o_w -> FP[w][lane] ----
+      if constexpr (!(SKIP & 2)) {
+        const int lane = lane_id();
+        const bool act = lane < C::H * F;
+        const int h = act ? (lane >= F ? 1 : 0) : 0;
+        const int i = act ? lane - h * F : 0;
         float qv[DH];
-        ld8(qv, PR + ai * C::PRS + ah * DH);
-        const float* kb = PR + U + ah * DH;
-        const float* vb = PR + 2 * U + ah * DH;
+        ld8(qv, PR + i * C::PRS + h * DH);
+        const float* kb = PR + U + h * DH;
+        const float* vb = PR + 2 * U + h * DH;
         float s[MQ];
         float mx = -INFINITY;
 #pragma unroll
         for (int m = 0; m < MQ; ++m) {
-          const int j = qq + 4 * m;
-          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
-          float kv[DH];
-          ld8(kv, kb + (ok ? j : 0) * C::PRS);
-          s[m] = dot_reg_pk(qv, kv);  // raw q . k; scaled into the exp2 domain below
-          mx = ok ? fmaxf(mx, s[m] * a.sc2) : mx;
+          const int j = w + 4 * m;
+          s[m] = 0.f;
+          if (j < F) {  // wave-uniform
+            float kv[DH];
+            ld8(kv, kb + j * C::PRS);
+            s[m] = dot_reg_pk(qv, kv);  // raw q . k; scaled into the exp2 domain below
+            mx = fmaxf(mx, s[m] * a.sc2);
+          }
         }
-        mx = quad_max(mx);
-        float sum = 0.f;
-#pragma unroll
-        for (int m = 0; m < MQ; ++m) {
-          const int j = qq + 4 * m;
-          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
-          s[m] = ok ? __builtin_amdgcn_exp2f(fmaf(s[m], a.sc2, -mx)) : 0.f;
-          sum += s[m];
-        }
-        sum = quad_sum(sum);
-        const float inv = 1.0f / sum;
-        float o[DH];
+        float l = 0.f, o[DH];
 #pragma unroll
         for (int d = 0; d < DH; ++d) o[d] = 0.f;
         const uint32_t kb_drop = DROP ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
 #pragma unroll
         for (int m = 0; m < MQ; ++m) {
-          const int j = qq + 4 * m;
-          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
-          float p = s[m] * inv;
-          if (DROP) p = dropout_keep_k(kb_drop, ah, ai, j, a.drop_rate) ? p * a.drop_scale : 0.f;
-          float vv[DH];
-          ld8(vv, vb + (ok ? j : 0) * C::PRS);
-          axpy_reg_pk(o, p, vv);
-        }
-#pragma unroll
-        for (int d = 0; d < DH; ++d) o[d] = quad_sum(o[d]);
-        // O_i over Q_i in place (only this quad read Q_i, all four lanes before the sums)
-        float2 mine = make_float2(o[0], o[1]);
-        if (qq == 1) mine = make_float2(o[2], o[3]);
-        if (qq == 2) mine = make_float2(o[4], o[5]);
-        if (qq == 3) mine = make_float2(o[6], o[7]);
-        if (aact) {
-          *reinterpret_cast<float2*>(PR + ai * C::PRS + ah * DH + 2 * qq) = mine;
-          if (a.osave) {  // the saved path: O row and (max, 1 / sum) for the backward
-            float* gs = a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, U, C::H);
-            *reinterpret_cast<float2*>(gs + ai * U + ah * DH + 2 * qq) = mine;
-            if (qq == 0) *reinterpret_cast<float2*>(gs + F * U + 2 * (ah * F + ai)) = make_float2(mx, inv);
+          const int j = w + 4 * m;
+          if (j < F) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(s[m], a.sc2, -mx));
+            l += e;
+            float p = e;
+            if (DROP) p = dropout_keep_k(kb_drop, h, i, j, a.drop_rate) ? e * a.drop_scale : 0.f;
+            float vv[DH];
+            ld8(vv, vb + j * C::PRS);
+            axpy_reg_pk(o, p, vv);
           }
         }
+        float4* fp = reinterpret_cast<float4*>(FP + (w * 64 + lane) * 12);
+        fp[0] = make_float4(mx, l, o[0], o[1]);
+        fp[1] = make_float4(o[2], o[3], o[4], o[5]);
+        fp[2] = make_float4(o[6], o[7], 0.f, 0.f);
       }
       lds_barrier();
       IL_STAMP(3)
-      // ---- z = relu(O + R); y = LN(z): 8 lanes per row, two columns each ----
-      {
+      // ---- combine the waves' partials (flash-style: M = max m_w, L = sum l_w 2^(m_w - M),
+      //      O = sum o_w 2^(m_w - M) / L, wave order), then z = relu(O + R); y = LN(z): 8 lanes
+      //      per row, two columns each; the saved path stores O and (M, 1 / L) ----
+      if constexpr (!(SKIP & 4)) {
         const bool act = lf < F;
         const int f = act ? lf : 0;
-        const float2 o2 = *reinterpret_cast<const float2*>(PR + f * C::PRS + u0);
+        const int hh = u0 >> 3, d0 = u0 & 7;
+        const float* fp = FP + (hh * F + f) * 12;
+        float mw[4], lw[4], ow0[4], ow1[4];
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const float2 ml = *reinterpret_cast<const float2*>(fp + w2 * 768);
+          const float2 ov = *reinterpret_cast<const float2*>(fp + w2 * 768 + 2 + d0);
+          mw[w2] = ml.x; lw[w2] = ml.y; ow0[w2] = ov.x; ow1[w2] = ov.y;
+        }
+        const float M = fmaxf(fmaxf(mw[0], mw[1]), fmaxf(mw[2], mw[3]));
+        float L = 0.f, oa = 0.f, ob = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) {
+          const float sc = mw[w2] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw[w2] - M);
+          L = fmaf(lw[w2], sc, L);
+          oa = fmaf(ow0[w2], sc, oa);
+          ob = fmaf(ow1[w2], sc, ob);
+        }
+        const float inv = 1.0f / L;
+        const float2 o2 = make_float2(oa * inv, ob * inv);
+        if (act && a.osave) {  // the saved path: O row and (max, 1 / sum) for the backward
+          float* gs = a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, U, C::H);
+          *reinterpret_cast<float2*>(gs + f * U + u0) = o2;
+          if ((u0 & 7) == 0) *reinterpret_cast<float2*>(gs + F * U + 2 * (hh * F + f)) = make_float2(M, inv);
+        }
         float2 r2 = *reinterpret_cast<const float2*>(PR + f * C::PRS + 3 * U + u0);
         if (!a.use_res) r2 = make_float2(0.f, 0.f);
         const float z0 = fmaxf(o2.x + r2.x, 0.f), z1 = fmaxf(o2.y + r2.y, 0.f);
         const float mean = group_sum<8>(z0 + z1) * (1.0f / (float)U);
-        const float d0 = z0 - mean, d1 = z1 - mean;
-        const float var = group_sum<8>(d0 * d0 + d1 * d1) * (1.0f / (float)U);
+        const float c0 = z0 - mean, c1 = z1 - mean;
+        const float var = group_sum<8>(c0 * c0 + c1 * c1) * (1.0f / (float)U);
         const float rstd = 1.0f / sqrtf(var + a.eps);
-        const float2 yv = make_float2(d0 * rstd * gm0 + bt0, d1 * rstd * gm1 + bt1);
+        const float2 yv = make_float2(c0 * rstd * gm0 + bt0, c1 * rstd * gm1 + bt1);
         if (it == a.L - 1) {
           if (act) *reinterpret_cast<float2*>(y + b * y_ld + f * U + u0) = yv;
         } else {  // (X is its own buffer: no barrier between these reads and the X stores)
@@ -273,7 +294,7 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
 // ============================== backward (saved path) =========================================
 template <class C>
 struct WideBwdLayout {
-  int xb0, xb1, sb0, sb1, dy, pr, pm, pd, dl, total;
+  int xb0, xb1, sb0, sb1, dy, pr, pm, pd, dl, qp, kvp, total;
   __host__ __device__ WideBwdLayout(int F) {
     const int sv = (int)small_save_stride(F, C::U, C::H);
     int off = 0;
@@ -283,11 +304,13 @@ struct WideBwdLayout {
     sb1 = off; off += (sv + 3) & ~3;
     dy = off; off += kWideRows * C::U;
     pr = off; off += kWideRows * C::PRS;
+    // P and dS: one row per attention lane (row = h F + i; the lanes >= H F own dummy rows);
     // PM + PD also hold P7's 4 x 2 x 4 x 64 dx partials (2 048 floats)
-    const int pmn = (C::H * F * C::PMS + 3) & ~3;
-    pm = off; off += pmn > 1024 ? pmn : 1024;
-    pd = off; off += pmn > 1024 ? pmn : 1024;
+    pm = off; off += (64 * C::PMS + 3) & ~3;
+    pd = off; off += (64 * C::PMS + 3) & ~3;
     dl = off; off += (C::H * kWideRows + 3) & ~3;
+    qp = off; off += 4 * 64 * 8;   // the Q-pass's dq partials [wave][lane][8]
+    kvp = off; off += 4 * 64 * 8;  // the K-pass's dv (waves 0, 1) / dk (2, 3) partials
     total = off;
   }
 };
@@ -297,8 +320,8 @@ __host__ __forceinline__ size_t wbwd_lds_bytes(int F) {
   return (size_t)WideBwdLayout<C>(F).total * 4;
 }
 
-template <class C, bool DROP>
-__global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
+template <class C, bool DROP, int SKIP = 0>
+__global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
     const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
     int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
@@ -318,7 +341,10 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
   float* const PM = smem + lay.pm;  // P (dropout applied)  [h][i][j]
   float* const PD = smem + lay.pd;  // dS = P (dP - D)       [h][i][j]
   float* const DL = smem + lay.dl;  // D_{h,i} = dO_i . O_i
+  float* const QP = smem + lay.qp;
+  float* const KVP = smem + lay.kvp;
   float* const XS = PM;             // P7: the 4 waves' dx partial tiles (PM / PD are dead)
+  static_assert(2 * 64 * C::PMS >= 2048, "PM + PD hold the dx partial tiles");
   const int w = wave_id();
   const int sv = (int)small_save_stride(F, U, C::H);
   const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);
@@ -389,7 +415,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
       lds_barrier();
       IL_STAMP(1)
       // ---- P1: projections (wave w: columns 16w..) and dW's X operand into registers ----
-      wide_project<C>(XB, PR, wp, bp, w);
+      if constexpr (!(SKIP & 1)) wide_project<C>(XB, PR, wp, bp, w);
       float xa[2][4];
       const int q = lane_id() >> 4, jx = lane_id() & 15;
 #pragma unroll
@@ -404,7 +430,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
       lds_barrier();
       IL_STAMP(2)
       // ---- P3: z = relu(O + R); LN + ReLU backward -> dO (SB), gR (PR's R slot), D ----
-      {
+      if constexpr (!(SKIP & 2)) {
         const int t_ = tid_v();
         const int lf = t_ >> 3, u0 = 2 * (t_ & 7);
         const bool act = lf < F;
@@ -440,126 +466,143 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
       }
       lds_barrier();
       IL_STAMP(3)
-      // ---- Q-pass: (head, query) quad, keys qq + 4m: P, dS -> PM, PD; dq -> DY ----
-      {
-        RS_W_ATTN_IDX
+      // ---- Q-pass: lane = (head, query i) (lane = h F + i), wave w takes keys j = w, w + 4, ...
+      //      (wave-uniform key rows: broadcast LDS reads, scalar loop): P, dS -> PM / PD row
+      //      `lane`; this wave's dq partial -> QP[w][lane] ----
+      if constexpr (!(SKIP & 4)) {
+        const int lane = lane_id();
+        const bool act = lane < C::H * F;
+        const int h = act ? (lane >= F ? 1 : 0) : 0;
+        const int i = act ? lane - h * F : 0;
         float qv[DH], dO[DH], dq[DH];
-        ld8(qv, PR + ai * C::PRS + ah * DH);
-        ld8(dO, SB + ai * U + ah * DH);
-        const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (ah * F + ai));
-        const float D = DL[ah * F + ai];
-        const float* kb = PR + U + ah * DH;
-        const float* vb = PR + 2 * U + ah * DH;
-        float* const pm_row = PM + (ah * F + ai) * C::PMS;
-        float* const pd_row = PD + (ah * F + ai) * C::PMS;
+        ld8(qv, PR + i * C::PRS + h * DH);
+        ld8(dO, SB + i * U + h * DH);
+        const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (h * F + i));
+        const float D = DL[h * F + i];
+        const float* kb = PR + U + h * DH;
+        const float* vb = PR + 2 * U + h * DH;
+        // rows = lanes: the inactive lanes (>= H F) write rows of their own (never read)
+        float* const pm_row = PM + lane * C::PMS;
+        float* const pd_row = PD + lane * C::PMS;
         const uint32_t kb_drop = DROP ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] = 0.f;
-        // software-pipelined by one key (two register sets, the loop unrolled by two by hand):
-        // the next key's K / V rows are in flight while this key's products run
+        const int nk = (F - w + 3) >> 2;  // keys w + 4m < F
         auto ld = [&](float (&kv)[DH], float (&vv)[DH], int m) {
-          const int j = qq + 4 * m;
-          const int jc = j < F ? j : 0;
-          ld8(kv, kb + jc * C::PRS);
-          ld8(vv, vb + jc * C::PRS);
+          const int mm = m < nk ? m : (nk > 0 ? nk - 1 : 0);
+          const int j = w + 4 * mm;
+          ld8(kv, kb + j * C::PRS);
+          ld8(vv, vb + j * C::PRS);
         };
         auto key = [&](int m, const float (&kv)[DH], const float (&vv)[DH]) {
-          const int j = qq + 4 * m;
-          const bool ok = j < F;
+          const int j = w + 4 * m;
           float sv_, dp;
           dot2_reg_pk(qv, kv, dO, vv, sv_, dp);
           const float p = __builtin_amdgcn_exp2f(fmaf(sv_, a.sc2, -stt.x)) * stt.y;
           float pdrop = p;
           if (DROP) {
-            const bool keep = dropout_keep_k(kb_drop, ah, ai, j, a.drop_rate);
+            const bool keep = dropout_keep_k(kb_drop, h, i, j, a.drop_rate);
             pdrop = keep ? p * a.drop_scale : 0.f;
             dp = keep ? dp * a.drop_scale : 0.f;
           }
-          const float ds = ok ? p * (dp - D) : 0.f;
-          if (aact && ok) {
-            pm_row[j] = pdrop;
-            pd_row[j] = ds;
-          }
+          const float ds = p * (dp - D);
+          pm_row[j] = pdrop;
+          pd_row[j] = ds;
           axpy_reg_pk(dq, ds, kv);
         };
+        // software-pipelined by one key (two register sets), as bwd4's sweeps
         float k0[DH], v0[DH], k1[DH], v1[DH];
         ld(k0, v0, 0);
-#pragma unroll 1
-        for (int m = 0; m < MQ; m += 2) {
+        for (int m = 0; m < nk; m += 2) {
           ld(k1, v1, m + 1);
           key(m, k0, v0);
           ld(k0, v0, m + 2);
-          key(m + 1, k1, v1);  // (m + 1 >= MQ: a key past F, contributes nothing)
+          if (m + 1 < nk) key(m + 1, k1, v1);
         }
-#pragma unroll
-        for (int d = 0; d < DH; ++d) dq[d] = quad_sum(dq[d]) * a.inv_sdh;
-        float2 mine = make_float2(dq[0], dq[1]);
-        if (qq == 1) mine = make_float2(dq[2], dq[3]);
-        if (qq == 2) mine = make_float2(dq[4], dq[5]);
-        if (qq == 3) mine = make_float2(dq[6], dq[7]);
-        if (aact) *reinterpret_cast<float2*>(DY + ai * U + ah * DH + 2 * qq) = mine;
+        float4* qp = reinterpret_cast<float4*>(QP + (w * 64 + lane) * 8);
+        qp[0] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        qp[1] = make_float4(dq[4], dq[5], dq[6], dq[7]);
       }
       lds_barrier();
       IL_STAMP(4)
-      // ---- K-pass: (head, key) quad, queries qq + 4m: dV, dK -> PR's V, K slots ----
-      {
-        RS_W_ATTN_IDX
-        float dv[DH], dk[DH];
+      // ---- K-pass: lane = (head, key j); waves 0, 1: dv_j = sum_i Pd_ij dO_i over queries
+      //      i = w, w + 2, ...; waves 2, 3: dk_j = sum_i dS_ij q_i over i = w - 2, w, ... ->
+      //      KVP[w][lane] ----
+      if constexpr (!(SKIP & 8)) {
+        const int lane = lane_id();
+        const bool act = lane < C::H * F;
+        const int h = act ? (lane >= F ? 1 : 0) : 0;
+        const int j = act ? lane - h * F : 0;
+        const bool isv = w < 2;  // wave-uniform
+        const int i0 = w & 1;
+        const int ni = (F - i0 + 1) >> 1;
+        const float* col = (isv ? PM : PD) + h * F * C::PMS + j;
+        const float* vec = (isv ? SB : PR) + h * DH;
+        const int vs = isv ? U : C::PRS;
+        float acc[DH];
 #pragma unroll
-        for (int d = 0; d < DH; ++d) { dv[d] = 0.f; dk[d] = 0.f; }
-        const float* pcol = PM + ah * F * C::PMS + ai;
-        const float* dcol = PD + ah * F * C::PMS + ai;
-        auto ld = [&](float (&oi)[DH], float (&qi)[DH], float& P, float& S, int m) {
-          const int i = qq + 4 * m;
-          const bool ok = i < F;
-          const int ic = ok ? i : 0;
-          ld8(oi, SB + ic * U + ah * DH);
-          ld8(qi, PR + ic * C::PRS + ah * DH);
-          P = pcol[ic * C::PMS];
-          S = dcol[ic * C::PMS];
-          if (!ok) { P = 0.f; S = 0.f; }
+        for (int d = 0; d < DH; ++d) acc[d] = 0.f;
+        auto ld = [&](float (&v)[DH], float& c, int m) {
+          const int mm = m < ni ? m : (ni > 0 ? ni - 1 : 0);
+          const int i = i0 + 2 * mm;
+          ld8(v, vec + i * vs);
+          c = col[i * C::PMS];
         };
-        float o0[DH], q0[DH], o1[DH], q1[DH], P0, S0, P1, S1;
-        ld(o0, q0, P0, S0, 0);
-#pragma unroll 1
-        for (int m = 0; m < MQ; m += 2) {
-          ld(o1, q1, P1, S1, m + 1);
-          axpy_reg_pk(dv, P0, o0);
-          axpy_reg_pk(dk, S0, q0);
-          ld(o0, q0, P0, S0, m + 2);
-          axpy_reg_pk(dv, P1, o1);
-          axpy_reg_pk(dk, S1, q1);
+        float v0[DH], v1[DH], c0, c1;
+        ld(v0, c0, 0);
+        for (int m = 0; m < ni; m += 2) {
+          ld(v1, c1, m + 1);
+          axpy_reg_pk(acc, c0, v0);
+          ld(v0, c0, m + 2);
+          if (m + 1 < ni) axpy_reg_pk(acc, c1, v1);
         }
-#pragma unroll
-        for (int d = 0; d < DH; ++d) {
-          dv[d] = quad_sum(dv[d]);
-          dk[d] = quad_sum(dk[d]);
-        }
-        // this lane's two columns of row ai's V and K (read before this lane overwrites them;
-        // no other lane touches them in this pass)
-        float* vrow = PR + ai * C::PRS + 2 * U + ah * DH + 2 * qq;
-        float* krow = PR + ai * C::PRS + U + ah * DH + 2 * qq;
-        const float2 v2 = *reinterpret_cast<const float2*>(vrow);
-        const float2 k2 = *reinterpret_cast<const float2*>(krow);
-        float2 gv = make_float2(dv[0], dv[1]), gk = make_float2(dk[0], dk[1]);
-        if (qq == 1) { gv = make_float2(dv[2], dv[3]); gk = make_float2(dk[2], dk[3]); }
-        if (qq == 2) { gv = make_float2(dv[4], dv[5]); gk = make_float2(dk[4], dk[5]); }
-        if (qq == 3) { gv = make_float2(dv[6], dv[7]); gk = make_float2(dk[6], dk[7]); }
-        if (aact) {
-          *reinterpret_cast<float2*>(vrow) =
-              make_float2(v2.x > 0.f ? gv.x : 0.f, v2.y > 0.f ? gv.y : 0.f);
-          *reinterpret_cast<float2*>(krow) = make_float2(
-              k2.x > 0.f ? gk.x * a.inv_sdh : 0.f, k2.y > 0.f ? gk.y * a.inv_sdh : 0.f);
-        }
+        float4* kp = reinterpret_cast<float4*>(KVP + (w * 64 + lane) * 8);
+        kp[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        kp[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
       }
       lds_barrier();
       IL_STAMP(5)
-      // dO (SB) is dead: at the last iteration of the sample the next sample's dy streams into
-      // DY once P7 has read dq (below, after the dx exchange barrier)
-      // ---- P7: G = [gQ | gK | gV | gR] column tile w; dW += X^T G, db; dx partial = G W_w^T ----
+      // ---- combine (wave order, fixed): gQ = relu'(Q) sum_w dq_w / sqrt(dh), gK = relu'(K)
+      //      (dk_2 + dk_3) / sqrt(dh), gV = relu'(V) (dv_0 + dv_1) -> PR's Q, K, V slots ----
       {
+        const int n4 = 12 * F;  // (slot Q / K / V, row f, head, half) float4 items
+        for (int t4 = tid_v(); t4 < n4; t4 += kWideThreads) {
+          const int half = t4 & 1, hh = (t4 >> 1) & 1, rest = t4 >> 2;
+          const int sl = rest >= 2 * F ? 2 : (rest >= F ? 1 : 0);
+          const int f = rest - sl * F;
+          const int l = hh * F + f;
+          float* g = PR + f * C::PRS + sl * U + hh * DH + 4 * half;
+          const float4 cur = *reinterpret_cast<const float4*>(g);
+          float4 sum;
+          float sc = a.inv_sdh;
+          if (sl == 0) {
+            const float* qp = QP + l * 8 + 4 * half;
+            const float4 p0 = *reinterpret_cast<const float4*>(qp);
+            const float4 p1 = *reinterpret_cast<const float4*>(qp + 512);
+            const float4 p2 = *reinterpret_cast<const float4*>(qp + 1024);
+            const float4 p3 = *reinterpret_cast<const float4*>(qp + 1536);
+            sum = make_float4(((p0.x + p1.x) + p2.x) + p3.x, ((p0.y + p1.y) + p2.y) + p3.y,
+                              ((p0.z + p1.z) + p2.z) + p3.z, ((p0.w + p1.w) + p2.w) + p3.w);
+          } else {
+            const float* kp = KVP + (sl == 1 ? 1024 : 0) + l * 8 + 4 * half;
+            const float4 p0 = *reinterpret_cast<const float4*>(kp);
+            const float4 p1 = *reinterpret_cast<const float4*>(kp + 512);
+            sum = make_float4(p0.x + p1.x, p0.y + p1.y, p0.z + p1.z, p0.w + p1.w);
+            if (sl == 2) sc = 1.f;
+          }
+          *reinterpret_cast<float4*>(g) =
+              make_float4(cur.x > 0.f ? sum.x * sc : 0.f, cur.y > 0.f ? sum.y * sc : 0.f,
+                          cur.z > 0.f ? sum.z * sc : 0.f, cur.w > 0.f ? sum.w * sc : 0.f);
+        }
+      }
+      lds_barrier();
+      IL_STAMP(6)
+      // dO (SB) is dead: at the last iteration of the sample the next sample's dy streams into
+      // DY once P7's barrier has passed (below)
+      // ---- P7: G = [gQ | gK | gV | gR] column tile w; dW += X^T G, db; dx partial = G W_w^T ----
+      if constexpr (!(SKIP & 16)) {
         // G rows of this lane for dW (B operand: k = f = 16rt + 4q + t, n = 16w + jx) and for dx
-        // (A operand: m = f = 16rt + jx, k = 16w + 4q + t); the Q tile is relu'(Q) * dq (DY)
+        // (A operand: m = f = 16rt + jx, k = 16w + 4q + t)
         const int q = lane_id() >> 4, jx = lane_id() & 15;
         const int lane = lane_id();
         float gb[2][4], ga[2][4];
@@ -568,18 +611,12 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int f = 16 * rt + 4 * q + t;
-            float g = PR[f * C::PRS + 16 * w + jx];
-            if (w == 0) g = g > 0.f ? DY[f * U + jx] : 0.f;
+            const float g = PR[f * C::PRS + 16 * w + jx];
             gb[rt][t] = f < F ? g : 0.f;
             dbp += gb[rt][t];
           }
           const int fa = 16 * rt + jx;
-          float4 g4 = *reinterpret_cast<const float4*>(PR + fa * C::PRS + 16 * w + 4 * q);
-          if (w == 0) {
-            const float4 d4 = *reinterpret_cast<const float4*>(DY + fa * U + 4 * q);
-            g4 = make_float4(g4.x > 0.f ? d4.x : 0.f, g4.y > 0.f ? d4.y : 0.f,
-                             g4.z > 0.f ? d4.z : 0.f, g4.w > 0.f ? d4.w : 0.f);
-          }
+          const float4 g4 = *reinterpret_cast<const float4*>(PR + fa * C::PRS + 16 * w + 4 * q);
           ga[rt][0] = g4.x; ga[rt][1] = g4.y; ga[rt][2] = g4.z; ga[rt][3] = g4.w;
         }
         f32x4 acc[2];
@@ -609,11 +646,11 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
           for (int r = 0; r < 4; ++r) XS[((w * 2 + rt) * 4 + r) * 64 + lane] = acc[rt][r];
       }
       lds_barrier();
-      IL_STAMP(6)
+      IL_STAMP(7)
       if (it == 0 && has_next) glds_copy(DY, dy + bn * dy_ld, ny4);  // the next sample's dy
       // ---- dx = sum of the 4 partial tiles (wave order), cells (pf, pe) and (pf + 16, pe):
       //      -> DY (the next iteration's dy), or the fused push, or dx ----
-      {
+      if constexpr (!(SKIP & 32)) {
         // cell (f, e): row tile f / 16, r = f % 4, q = (f % 16) / 4, lane = 16 q + e
         float v[2];
 #pragma unroll
@@ -642,7 +679,7 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
           if (pf + 16 < F) d[(pf + 16) * E + pe] = dx_accumulate ? d[(pf + 16) * E + pe] + v[1] : v[1];
         }
       }
-      if (it > 0) { IL_STAMP(7) } else { IL_STAMP(8) }
+      if (it > 0) { IL_STAMP(8) } else { IL_STAMP(9) }
       float* t = XB; XB = XN; XN = t;
       t = SB; SB = SN; SN = t;
     }

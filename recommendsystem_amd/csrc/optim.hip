@@ -801,7 +801,19 @@ RS_API int rs_partials_reduce_adam_scan(
   // at most 256 16-wave blocks (4096 waves, ~10 chunks each at 2.6 M rows): with the ~300
   // reduction blocks the launch stays about one resident round (2 such blocks per CU)
   int64_t tail_blocks = table_rows ? (scan_grid(table_rows) * (kScanBlock / 64) + 15) / 16 : 0;
-  if (tail_blocks > 256) tail_blocks = 256;
+  // the sweep takes the resident round's blocks the reduction leaves (2 x 1024-thread blocks per
+  // CU x 256 CUs), at least 256: each wave's flag chunks then load in one or two PF batches
+  // (small batches leave few reduction blocks: B = 512 per GPU -> ~450 sweep blocks)
+  int64_t nblk_red = 0;
+  for (int k = 0; nrows && ncols && k < nseg && k < RS_RED_MAXSEG; ++k) {
+    int lg = 0;
+    while (lg < RS_RED_MAXLG && ((int64_t)16 << lg) < nrows[k]) ++lg;
+    const int64_t nc = 1024 >> lg;
+    nblk_red += (ncols[k] + nc - 1) / nc;
+  }
+  int64_t cap_blocks = 512 - nblk_red;
+  if (cap_blocks < 256) cap_blocks = 256;
+  if (tail_blocks > cap_blocks) tail_blocks = cap_blocks;
   return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
                           m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, &t,
                           tail_blocks);

@@ -2,8 +2,11 @@
 'nccl' backend (= RCCL over xGMI on ROCm).  Replaces tensornet's dense MPI all-reduce
 (tn.optimizer.Optimizer) and its PS sparse push (tn.layers.EmbeddingFeatures) for DP training.
 
-  dense  : the model's flat gradient arena is ONE all-reduce bucket (AutoInt: 15.4 K floats,
-           latency-bound; staytime+rough_rank: ~3.5 M floats = 14 MB, still one bucket).
+  dense  : the model's flat gradient arena.  AutoInt: the packed exchange below (all-gathered
+           buckets summed in rank order, 15.4 K floats).  The generic Trainer's eager DP step:
+           BucketedAllReduce -- arena ranges of <= 25 MB issued as async all-reduces from
+           autograd post-hooks while the rest of backward runs; its graph-captured DP step: one
+           all-reduce of the whole arena after the captured forward / backward.
   sharded: owner-sharded tables (embedding.ShardedSparseTable, row owner = row % world) move
            lookups and gradients with two variable-split all-to-alls each way instead
            (all_to_all_v; counts first).
@@ -153,3 +156,153 @@ def exchange_counts(counts: torch.Tensor, group=None):
     recv = torch.empty_like(counts)
     all_to_all_v(recv, counts, [1] * world, [1] * world, group)
     return counts.tolist(), recv.tolist()
+
+
+class BucketedAllReduce:
+    """The flat dense gradient all-reduced in buckets issued DURING backward (SURVEY §8(e):
+    "buckets of <= 25 MB, launched as backward produces the grads"; the reference's
+    tn.optimizer.Optimizer(dense_opt) at staytime/model.py:89, rough_rank/model.py:220 syncs the
+    dense gradients through tensornet's MPI allreduce after the whole backward).
+
+    Buckets are contiguous ranges of the parameter arena, built from its END (the parameters a
+    model registers last produce their gradients first in backward), each <= bucket_bytes.
+    ``arm(loss)`` walks loss's autograd graph once per step and registers a post-hook on every
+    node that produces an arena parameter's gradient: its AccumulateGrad node, and every custom
+    kernel Function node that saved the parameter (the fused kernels write weight gradients in
+    place and return None for them).  A parameter is ready when all its producer nodes have run;
+    a bucket is issued (async all_reduce, SUM, in place) once its parameters are ready AND every
+    earlier bucket has been issued -- the same collective order on every rank.  The hooks run on
+    the host as the autograd engine finishes each node, i.e. after that node's kernels are
+    enqueued: the collective is ordered after them on the device and overlaps the backward
+    kernels enqueued later.  ``late`` parameters (regularised ones: rs_l1l2_grad completes their
+    gradient after backward) go to the final bucket, issued by ``finish`` after the caller's
+    completion step; ``finish`` also issues buckets whose parameters got no gradient this step
+    (their zeros still take part) and waits for everything."""
+
+    def __init__(self, arena, group=None, bucket_bytes: int = 25 << 20, late=()):
+        self.arena, self.group = arena, group
+        base = arena.data.data_ptr()
+        late_ids = {id(p) for p in late}
+        spans = []  # (offset, numel, param)
+        for p in arena.params:
+            spans.append(((p.data_ptr() - base) // 4, p.numel(), p))
+        spans.sort(key=lambda t: t[0])
+        cap = max(1, int(bucket_bytes) // 4)
+        self.buckets = []   # [(off, n, [params])] in issue order
+        cur, cur_lo, cur_hi = [], None, None
+        for off, n, p in reversed(spans):
+            if id(p) in late_ids:
+                continue
+            contiguous = cur_lo is None or off + n == cur_lo
+            if cur and (not contiguous or cur_hi - off > cap):
+                self.buckets.append((cur_lo, cur_hi - cur_lo, cur))
+                cur, cur_lo, cur_hi = [], None, None
+            cur.append(p)
+            cur_hi = off + n if cur_hi is None else cur_hi
+            cur_lo = off
+        if cur:
+            self.buckets.append((cur_lo, cur_hi - cur_lo, cur))
+        self.late = [(off, n, p) for off, n, p in spans if id(p) in late_ids]
+        self._param_bucket = {}
+        for k, (_, _, ps) in enumerate(self.buckets):
+            for p in ps:
+                self._param_bucket[id(p)] = k
+        self._by_ptr = {}
+        for off, n, p in spans:
+            self._by_ptr[p.data_ptr()] = p
+        self._handles = []
+        self.issued_in_backward = 0  # diagnostics / tests: buckets issued by the hooks
+
+    # -- per step ---------------------------------------------------------------------------
+    def arm(self, loss: torch.Tensor) -> None:
+        self._handles = []
+        self._next = 0
+        self.issued_in_backward = 0
+        self._pending = [0] * len(self.buckets)      # unready params per bucket
+        self._producers = {}                         # id(param) -> producer nodes left
+        seen, stack = set(), [loss.grad_fn] if loss.grad_fn is not None else []
+        node_params = []
+        while stack:
+            node = stack.pop()
+            if node is None or node in seen:
+                continue
+            seen.add(node)
+            ps = self._node_params(node)
+            if ps:
+                node_params.append((node, ps))
+            for nxt, _ in node.next_functions:
+                if nxt is not None:
+                    stack.append(nxt)
+        for node, ps in node_params:
+            for p in ps:
+                self._producers[id(p)] = self._producers.get(id(p), 0) + 1
+            node.register_hook(self._make_hook(ps))
+        for pid, _ in self._producers.items():
+            k = self._param_bucket.get(pid)
+            if k is not None:
+                self._pending[k] += 1
+
+    def _node_params(self, node):
+        out = []
+        var = getattr(node, "variable", None)  # AccumulateGrad
+        if var is not None:
+            p = self._by_ptr.get(var.data_ptr())
+            if p is not None and id(p) in self._param_bucket:
+                out.append(p)
+            return out
+        try:
+            saved = node.saved_tensors  # custom (kernel) Functions
+        except (AttributeError, RuntimeError):
+            return out
+        for t in saved:
+            if t is None:
+                continue
+            p = self._by_ptr.get(t.data_ptr())
+            if p is not None and p.numel() == t.numel() and id(p) in self._param_bucket:
+                out.append(p)
+        return out
+
+    def _make_hook(self, ps):
+        def hook(*_):
+            for p in ps:
+                pid = id(p)
+                self._producers[pid] -= 1
+                if self._producers[pid] == 0:
+                    self._pending[self._param_bucket[pid]] -= 1
+            self._issue_ready()
+        return hook
+
+    def _issue(self, k):
+        off, n, _ = self.buckets[k]
+        self._handles.append(dist.all_reduce(self.arena.grad[off:off + n], group=self.group,
+                                             async_op=True))
+
+    def _issue_ready(self):
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._issue(self._next)
+            self._next += 1
+            self.issued_in_backward += 1
+
+    def finish(self, complete_late=None) -> None:
+        """After backward: issue what is left (buckets without gradients this step), run
+        complete_late() (the regularisers) and issue the late parameters' bucket, wait."""
+        while self._next < len(self.buckets):
+            self._issue(self._next)
+            self._next += 1
+        if complete_late is not None:
+            complete_late()
+        if self.late:
+            lo = min(off for off, _, _ in self.late)
+            hi = max(off + n for off, n, _ in self.late)
+            # one range covering the late parameters (gaps belong to early buckets, already
+            # being reduced: the late range must not overlap them)
+            if hi - lo == sum(n for _, n, _ in self.late):
+                self._handles.append(dist.all_reduce(self.arena.grad[lo:hi], group=self.group,
+                                                     async_op=True))
+            else:
+                for off, n, _ in self.late:
+                    self._handles.append(dist.all_reduce(self.arena.grad[off:off + n],
+                                                         group=self.group, async_op=True))
+        for h in self._handles:
+            h.wait()
+        self._handles = []

@@ -3,8 +3,11 @@ harness): what tensornet's ``model.fit`` runs per batch (SURVEY §3 call stacks)
 
     loss = model.loss(*batch)           (forward: librecsys_amd.so kernels via autograd)
     loss.backward()                     (kernels write weight grads in place into the arena)
+                                        [DP, eager: <= 25 MB dense buckets all-reduced from
+                                         autograd hooks as their gradients complete]
     grads += l1 sign(w) + 2 l2 w        (Keras kernel regularisers, rs_l1l2_grad)
-    [DP] all-reduce the flat dense gradient (one RCCL bucket), rank-ordered sparse exchange
+    [DP] the regularised parameters' bucket (graph-captured DP: the whole flat gradient, one
+         RCCL call), rank-ordered sparse exchange
          (owner-sharded tables: none -- their backward already pushed to the owners)
     dense Adam over the arena (one launch, zero_grad fused), sparse optimizer per table
 
@@ -46,7 +49,7 @@ class Trainer:
     is a contiguous range of the arena with its own step counter (same count every step)."""
 
     def __init__(self, model, lr_dense: float, tables=(), process_group=None, beta1=0.9,
-                 beta2=0.999, eps=1e-8, lr_groups=()):
+                 beta2=0.999, eps=1e-8, lr_groups=(), bucket_mb: float = 25.0):
         self.model = model
         self.arena = ParamArena(model.parameters())
         dev = self.arena.data.device
@@ -67,6 +70,14 @@ class Trainer:
         self.on_dense_grad = None  # test hook: called with the exchanged flat dense gradient
         self._il_layers = [mod for mod in model.modules() if isinstance(mod, InteractingLayer)] \
             if hasattr(model, "modules") else []
+        # eager DP: the dense all-reduce in buckets issued during backward (dist.BucketedAllReduce;
+        # regularised parameters in the final bucket, after rs_l1l2_grad); bucket_mb <= 0: one
+        # all-reduce after backward
+        self.bucketer = None
+        if self.world > 1 and bucket_mb and bucket_mb > 0:
+            from .dist import BucketedAllReduce
+            self.bucketer = BucketedAllReduce(self.arena, process_group, int(bucket_mb * (1 << 20)),
+                                              late=[p for p, _, _ in self.regs])
         if self.world == 1:
             # single-GPU: tables that ask for it run in scan mode (pushes mark flags with plain
             # stores, no claims; the optimizer sweeps the flags) -- the DP exchange below needs
@@ -116,15 +127,24 @@ class Trainer:
         with _lib.seed_offset(self.step_count):
             return self._step(*batch)
 
-    def _step(self, *batch):
-        loss = self.model.loss(*batch)
-        loss.backward(self._seed)
+    def _regularise(self):
         s = stream_handle()
         for p, l1, l2 in self.regs:
             call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
+
+    def _step(self, *batch):
+        loss = self.model.loss(*batch)
+        if self.bucketer is not None:
+            self.bucketer.arm(loss)  # buckets go out as backward produces their gradients
+        loss.backward(self._seed)
+        if self.bucketer is not None:
+            self.bucketer.finish(self._regularise)
+        else:
+            self._regularise()
         if self.world > 1:
-            from .dist import allreduce_flat
-            allreduce_flat(self.arena.grad, self.pg)
+            if self.bucketer is None:
+                from .dist import allreduce_flat
+                allreduce_flat(self.arena.grad, self.pg)
             for t in self.tables:
                 if not is_sharded(t):
                     exchange_sparse(t, self.pg, self.world, *self.xbuf[id(t)])

@@ -156,3 +156,74 @@ def test_dp_packed_exchange_fixed_layout_two_ranks():
         for k in range(n):
             ref[r[k]] += g[k]
     assert np.allclose(t0, ref, atol=1e-6)
+
+
+class _Fn(torch.autograd.Function):
+    """A kernel-style Function: writes its weight gradient IN PLACE into the arena and returns
+    None for it (what the fused HIP kernels do), so only the node's saved W identifies it."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return x @ W
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        W.grad.add_(x.t() @ gy)
+        return gy @ W.t(), None
+
+
+def _bucket_worker(rank, world, port, out):
+    from torch import nn
+    from recommendsystem_amd.dist import BucketedAllReduce
+    from recommendsystem_amd.params import ParamArena
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)  # the same weights on every rank
+    lin = [nn.Linear(16, 16) for _ in range(4)]
+    Wk = nn.Parameter(torch.randn(16, 8) * 0.1)          # the in-place-writer's weight
+    reg = nn.Parameter(torch.randn(8, 1) * 0.1)           # a 'late' (regularised) parameter
+    params = [p for l in lin for p in l.parameters()] + [Wk, reg]
+    arena = ParamArena(params)
+    x = torch.randn(32, 16, generator=torch.Generator().manual_seed(10 + rank))
+
+    def loss_fn():
+        h = x
+        for l in lin:
+            h = torch.relu(l(h))
+        return (_Fn.apply(h, Wk) @ reg).square().mean()
+
+    # reference: whole backward, regulariser, one all-reduce of the arena
+    arena.grad.zero_()
+    loss_fn().backward()
+    reg.grad.add_(0.01 * reg.detach())
+    want = arena.grad.clone()
+    dist.all_reduce(want)
+    # bucketed: 700-B buckets (several per step), issued from the autograd hooks
+    b = BucketedAllReduce(arena, bucket_bytes=700, late=[reg])
+    arena.grad.zero_()
+    loss = loss_fn()
+    b.arm(loss)
+    loss.backward()
+    issued = b.issued_in_backward
+    b.finish(lambda: reg.grad.add_(0.01 * reg.detach()))
+    out[rank] = (arena.grad.numpy().copy(), want.numpy().copy(), issued, len(b.buckets))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_during_backward_two_ranks():
+    """dist.BucketedAllReduce (the generic Trainer's eager DP step): buckets issued from autograd
+    post-hooks during backward -- including a parameter whose gradient a kernel-style Function
+    writes in place -- plus a late regularised bucket give exactly the one-bucket all-reduce
+    (2 ranks: a + b either way), identical on both ranks."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    g0, w0, issued0, nb = out[0]
+    g1, w1, issued1, _ = out[1]
+    assert nb > 2 and issued0 > 0 and issued0 == issued1
+    assert np.array_equal(g0, w0) and np.array_equal(g1, w1) and np.array_equal(g0, g1)

@@ -53,3 +53,26 @@ def test_ctr_metrics_strided_column():
     got = m.result()
     want = npo.ctr_metrics(P[:, 3].cpu().numpy(), Y[:, 3].cpu().numpy())
     assert abs(got["auc"] - want["auc"]) <= 1e-6 and abs(got["acc"] - want["acc"]) <= 1e-6
+
+
+def test_autoint_trainer_metrics_match_oracle():
+    """AutoIntTrainer(metrics=CtrMetrics()) accumulates AUC / acc / COPC over the steps' clipped
+    predictions inside the captured step: equal to the oracle over the same (p, labels)."""
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
+    from recommendsystem_amd.metrics import CtrMetrics
+    cfg = AutoIntConfig(vocab_per_field=1000)
+    model = AutoInt(cfg, device=DEV, seed=1, max_batch=256)
+    m = CtrMetrics(device=DEV)
+    tr = AutoIntTrainer(model, 256, metrics=m)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    ps, ys = [], []
+    for k in range(3):
+        ids = torch.randint(0, 1000, (256, 26), device=DEV, generator=g)
+        lab = (torch.rand(256, 1, device=DEV, generator=g) < 0.25).float()
+        tr.step(ids, lab)
+        ps.append(tr.p.detach().cpu().numpy().copy())
+        ys.append(lab.cpu().numpy())
+    got = m.result()
+    want = npo.ctr_metrics(np.concatenate(ps), np.concatenate(ys))
+    for k in ("auc", "acc", "copc", "ctr"):
+        assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k])), (k, got[k], want[k])

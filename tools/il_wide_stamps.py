@@ -39,14 +39,22 @@ for B in [int(b) for b in os.environ.get("BATCHES", "512 4096").split()]:
             for name, fn, names in (("fwd", fwd, FWD), ("bwd", bwd, BWD)):
                 fn(); torch.cuda.synchronize()
                 st.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 for _ in range(REPS):
                     fn()
+                e1.record()
                 torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / REPS
                 v = st.cpu().tolist()
                 # waves per launch: wide = 4 per sample; wave variant = one wave per sample
                 waves = (4 if variant == "wide" else 1) * B
                 per = REPS * waves * L
                 tot = sum(v)
-                print(f"B={B} {variant} {name}: {tot / per:8.0f} cycles per wave per sample-iteration")
+                # per-wave wall cycles of the whole launch vs the launch time: the implied clock
+                per_wave_launch = tot / (REPS * waves)
+                print(f"B={B} {variant} {name}: {tot / per:8.0f} cycles per wave per sample-iteration; "
+                      f"launch {us:.1f} us, per-wave stamped span {per_wave_launch:.0f} cycles "
+                      f"(= {per_wave_launch / us / 1e3:.2f} GHz if the span were the launch)")
                 for n, c in zip(names, v):
                     print(f"    {n:16s} {c / per:8.0f}  {100.0 * c / max(tot, 1):5.1f}%")
