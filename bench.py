@@ -454,12 +454,24 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
 
     barrier()
     torch.cuda.synchronize()
+    step_ev = None
+    if os.environ.get("RS_BENCH_STEP_TRACE"):  # diagnostic: device time of every timed step
+        step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if step_ev is not None:
+            step_ev[i].record()
         trainer.step_pool(i)
+    if step_ev is not None:
+        step_ev[args.steps].record()
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    if step_ev is not None:
+        us = [round(step_ev[k].elapsed_time(step_ev[k + 1]) * 1e3, 1) for k in range(args.steps)]
+        print(json.dumps({"step_trace_us": us, "graph": [k % len(trainer.pool_graphs)
+                                                        for k in range(args.steps)]}),
+              file=sys.stderr, flush=True)
     if args.trace_markers:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()

@@ -179,6 +179,15 @@ int rs_sparse_merge_rows_dev(void* stream, const int32_t* rows_all, const float*
                              const int32_t* counts, int64_t counts_stride, int world, int rank,
                              int32_t cap, int dim, float* grad_table, int32_t* flag,
                              int32_t* touched, int32_t* n_touched, int32_t touched_cap);
+/* rs_sparse_merge_rows_dev over a FIXED layout: rank r's list at rows_all[r * stride] (the host
+ * all-gathered `stride` entries per rank without reading the counts: no host synchronisation in
+ * the data-parallel step).  A rank whose count exceeds stride lost rows in transit: its count
+ * is recorded in the sticky *overflow (nullable; atomicMax, never cleared by the library). */
+int rs_sparse_merge_rows_dev_stride(void* stream, const int32_t* rows_all, const float* grads_all,
+                                    const int32_t* counts, int64_t counts_stride, int world,
+                                    int rank, int32_t stride, int dim, float* grad_table,
+                                    int32_t* flag, int32_t* touched, int32_t* n_touched,
+                                    int32_t touched_cap, int32_t* overflow);
 
 /* Packed scan-mode exchange (the graph-captured DP step of the AutoInt trainer; same role as
  * compact/merge above).  pack: every marked row becomes one record [row (int32 bits) | grad[dim]]

@@ -42,6 +42,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_merge_rows": (_i32, [_vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i32]),
     "rs_sparse_merge_rows_dev": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp, _vp,
                                         _vp, _vp, _i32]),
+    "rs_sparse_merge_rows_dev_stride": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
+                                                _vp, _vp, _vp, _vp, _i32, _vp]),
     "rs_sparse_sorted_workspace_bytes": (_i64, [_i64]),
     "rs_sparse_grad_accumulate_sorted": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32,
                                                 _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _i64,

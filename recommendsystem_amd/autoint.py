@@ -617,6 +617,26 @@ class AutoIntTrainer:
             self.ids, self.labels = own
         if self.world > 1:
             self._record_opt()
+        self._prime_graphs()
+
+    def _prime_graphs(self) -> None:
+        """Replay every captured graph once and roll the training state back.  A hipGraph's
+        first launch after capture is slower than the following ones (the runtime finishes
+        setting up and uploading its executable; measured per step with RS_BENCH_STEP_TRACE):
+        done here, as part of capture, so no training step pays it.  RS_NO_GRAPH_PRIME=1
+        skips it (A/B)."""
+        import os
+        if os.environ.get("RS_NO_GRAPH_PRIME"):
+            return
+        saved = [t.clone() for t in self._state()]
+        for g in self.pool_graphs:
+            g.replay()
+        if self.world > 1 and self.graph_opt is not None:
+            self.graph_opt.replay()
+        torch.cuda.synchronize()
+        for t, v in zip(self._state(), saved):
+            t.copy_(v)
+        torch.cuda.synchronize()
 
     def step_pool(self, i: int) -> torch.Tensor:
         g = self.pool_graphs[i % len(self.pool_graphs)]

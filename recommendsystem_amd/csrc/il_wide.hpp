@@ -118,12 +118,11 @@ __device__ __forceinline__ void wide_load_w(const float* __restrict__ W, const f
 // ============================== forward =======================================================
 template <class C>
 struct WideFwdLayout {
-  int xb, pr, fp, total;
+  int xb, pr, total;
   __host__ __device__ WideFwdLayout() {
     xb = 0;
     pr = xb + kWideRows * C::E;
-    fp = pr + kWideRows * C::PRS;
-    total = fp + 4 * 64 * 12;
+    total = pr + kWideRows * C::PRS;
   }
 };
 
@@ -142,7 +141,6 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   const WideFwdLayout<C> lay;
   float* const X = smem + lay.xb;
   float* const PR = smem + lay.pr;
-  float* const FP = smem + lay.fp;  // attention partials [wave][lane][12]
   const int tid = threadIdx.x;
   const int w = wave_id();
   const int F = C::EXACT ? C::FMAX : a.F;
@@ -153,6 +151,10 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   // LN lanes: row lf, columns u0, u0 + 1
   const int lf = tid >> 3, u0 = 2 * (tid & 7);
   const float gm0 = gamma[u0], gm1 = gamma[u0 + 1], bt0 = beta[u0], bt1 = beta[u0 + 1];
+  // attention lanes: (head ah, query row ai), keys qq + 4m
+  const int ag = tid >> 2, ah = ag >> 5, ai0 = ag & 31, qq = tid & 3;
+  const bool aact = ai0 < F;
+  const int ai = aact ? ai0 : 0;
   // X rows F .. 31 stay zero (the projection reads both row tiles unguarded)
   for (int k = F * C::E + tid; k < kWideRows * C::E; k += kWideThreads) X[k] = 0.f;
 
@@ -186,94 +188,79 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
       if constexpr (!(SKIP & 1)) wide_project<C>(X, PR, wp, bp, w);
       lds_barrier();
       IL_STAMP(2)
-      // ---- attention partials: lane = (head, query i) (lane = h F + i), wave w takes keys
-      //      j = w, w + 4, ... (wave-uniform key rows): its running max m_w, sum l_w and
-      //      unnormalised output o_w -> FP[w][lane] ----
+      // ---- attention: (head, query) quad, keys qq + 4m ----
       if constexpr (!(SKIP & 2)) {
-        const int lane = lane_id();
-        const bool act = lane < C::H * F;
-        const int h = act ? (lane >= F ? 1 : 0) : 0;
-        const int i = act ? lane - h * F : 0;
         float qv[DH];
-        ld8(qv, PR + i * C::PRS + h * DH);
-        const float* kb = PR + U + h * DH;
-        const float* vb = PR + 2 * U + h * DH;
+        ld8(qv, PR + ai * C::PRS + ah * DH);
+        const float* kb = PR + U + ah * DH;
+        const float* vb = PR + 2 * U + ah * DH;
         float s[MQ];
         float mx = -INFINITY;
 #pragma unroll
         for (int m = 0; m < MQ; ++m) {
-          const int j = w + 4 * m;
-          s[m] = 0.f;
-          if (j < F) {  // wave-uniform
-            float kv[DH];
-            ld8(kv, kb + j * C::PRS);
-            s[m] = dot_reg_pk(qv, kv);  // raw q . k; scaled into the exp2 domain below
-            mx = fmaxf(mx, s[m] * a.sc2);
-          }
+          const int j = qq + 4 * m;
+          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
+          float kv[DH];
+          ld8(kv, kb + (ok ? j : 0) * C::PRS);
+          s[m] = dot_reg_pk(qv, kv);  // raw q . k; scaled into the exp2 domain below
+          mx = ok ? fmaxf(mx, s[m] * a.sc2) : mx;
         }
-        float l = 0.f, o[DH];
+        mx = quad_max(mx);
+        float sum = 0.f;
+#pragma unroll
+        for (int m = 0; m < MQ; ++m) {
+          const int j = qq + 4 * m;
+          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
+          s[m] = ok ? __builtin_amdgcn_exp2f(fmaf(s[m], a.sc2, -mx)) : 0.f;
+          sum += s[m];
+        }
+        sum = quad_sum(sum);
+        const float inv = 1.0f / sum;
+        float o[DH];
 #pragma unroll
         for (int d = 0; d < DH; ++d) o[d] = 0.f;
         const uint32_t kb_drop = DROP ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
 #pragma unroll
         for (int m = 0; m < MQ; ++m) {
-          const int j = w + 4 * m;
-          if (j < F) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(s[m], a.sc2, -mx));
-            l += e;
-            float p = e;
-            if (DROP) p = dropout_keep_k(kb_drop, h, i, j, a.drop_rate) ? e * a.drop_scale : 0.f;
-            float vv[DH];
-            ld8(vv, vb + j * C::PRS);
-            axpy_reg_pk(o, p, vv);
+          const int j = qq + 4 * m;
+          const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
+          float p = s[m] * inv;
+          if (DROP) p = dropout_keep_k(kb_drop, ah, ai, j, a.drop_rate) ? p * a.drop_scale : 0.f;
+          float vv[DH];
+          ld8(vv, vb + (ok ? j : 0) * C::PRS);
+          axpy_reg_pk(o, p, vv);
+        }
+#pragma unroll
+        for (int d = 0; d < DH; ++d) o[d] = quad_sum(o[d]);
+        // O_i over Q_i in place (only this quad read Q_i, all four lanes before the sums)
+        float2 mine = make_float2(o[0], o[1]);
+        if (qq == 1) mine = make_float2(o[2], o[3]);
+        if (qq == 2) mine = make_float2(o[4], o[5]);
+        if (qq == 3) mine = make_float2(o[6], o[7]);
+        if (aact) {
+          *reinterpret_cast<float2*>(PR + ai * C::PRS + ah * DH + 2 * qq) = mine;
+          if (a.osave) {  // the saved path: O row and (max, 1 / sum) for the backward
+            float* gs = a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, U, C::H);
+            *reinterpret_cast<float2*>(gs + ai * U + ah * DH + 2 * qq) = mine;
+            if (qq == 0) *reinterpret_cast<float2*>(gs + F * U + 2 * (ah * F + ai)) = make_float2(mx, inv);
           }
         }
-        float4* fp = reinterpret_cast<float4*>(FP + (w * 64 + lane) * 12);
-        fp[0] = make_float4(mx, l, o[0], o[1]);
-        fp[1] = make_float4(o[2], o[3], o[4], o[5]);
-        fp[2] = make_float4(o[6], o[7], 0.f, 0.f);
       }
       lds_barrier();
       IL_STAMP(3)
-      // ---- combine the waves' partials (flash-style: M = max m_w, L = sum l_w 2^(m_w - M),
-      //      O = sum o_w 2^(m_w - M) / L, wave order), then z = relu(O + R); y = LN(z): 8 lanes
-      //      per row, two columns each; the saved path stores O and (M, 1 / L) ----
+      // ---- z = relu(O + R); y = LN(z): 8 lanes per row, two columns each ----
       if constexpr (!(SKIP & 4)) {
         const bool act = lf < F;
         const int f = act ? lf : 0;
-        const int hh = u0 >> 3, d0 = u0 & 7;
-        const float* fp = FP + (hh * F + f) * 12;
-        float mw[4], lw[4], ow0[4], ow1[4];
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) {
-          const float2 ml = *reinterpret_cast<const float2*>(fp + w2 * 768);
-          const float2 ov = *reinterpret_cast<const float2*>(fp + w2 * 768 + 2 + d0);
-          mw[w2] = ml.x; lw[w2] = ml.y; ow0[w2] = ov.x; ow1[w2] = ov.y;
-        }
-        const float M = fmaxf(fmaxf(mw[0], mw[1]), fmaxf(mw[2], mw[3]));
-        float L = 0.f, oa = 0.f, ob = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) {
-          const float sc = mw[w2] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw[w2] - M);
-          L = fmaf(lw[w2], sc, L);
-          oa = fmaf(ow0[w2], sc, oa);
-          ob = fmaf(ow1[w2], sc, ob);
-        }
-        const float inv = 1.0f / L;
-        const float2 o2 = make_float2(oa * inv, ob * inv);
-        if (act && a.osave) {  // the saved path: O row and (max, 1 / sum) for the backward
-          float* gs = a.osave + ((int64_t)it * a.B + b) * small_save_stride(F, U, C::H);
-          *reinterpret_cast<float2*>(gs + f * U + u0) = o2;
-          if ((u0 & 7) == 0) *reinterpret_cast<float2*>(gs + F * U + 2 * (hh * F + f)) = make_float2(M, inv);
-        }
+        const float2 o2 = *reinterpret_cast<const float2*>(PR + f * C::PRS + u0);
         float2 r2 = *reinterpret_cast<const float2*>(PR + f * C::PRS + 3 * U + u0);
         if (!a.use_res) r2 = make_float2(0.f, 0.f);
         const float z0 = fmaxf(o2.x + r2.x, 0.f), z1 = fmaxf(o2.y + r2.y, 0.f);
         const float mean = group_sum<8>(z0 + z1) * (1.0f / (float)U);
-        const float c0 = z0 - mean, c1 = z1 - mean;
-        const float var = group_sum<8>(c0 * c0 + c1 * c1) * (1.0f / (float)U);
+        const float d0 = z0 - mean, d1 = z1 - mean;
+        const float var = group_sum<8>(d0 * d0 + d1 * d1) * (1.0f / (float)U);
         const float rstd = 1.0f / sqrtf(var + a.eps);
-        const float2 yv = make_float2(c0 * rstd * gm0 + bt0, c1 * rstd * gm1 + bt1);
+        const float2 yv = make_float2(d0 * rstd * gm0 + bt0, d1 * rstd * gm1 + bt1);
         if (it == a.L - 1) {
           if (act) *reinterpret_cast<float2*>(y + b * y_ld + f * U + u0) = yv;
         } else {  // (X is its own buffer: no barrier between these reads and the X stores)
@@ -294,23 +281,26 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
 // ============================== backward (saved path) =========================================
 template <class C>
 struct WideBwdLayout {
-  int xb0, xb1, sb0, sb1, dy, pr, pm, pd, dl, qp, kvp, total;
+  int xb0, xb1, sb0, sb1, dy, pr, pm, pd, dl, qp, hf1, total;
   __host__ __device__ WideBwdLayout(int F) {
     const int sv = (int)small_save_stride(F, C::U, C::H);
+    hf1 = C::H * F + 1;  // attention rows h F + i, plus one dummy row for the idle lanes
     int off = 0;
     xb0 = off; off += kWideRows * C::E;
     xb1 = off; off += kWideRows * C::E;
     sb0 = off; off += (sv + 3) & ~3;
     sb1 = off; off += (sv + 3) & ~3;
-    dy = off; off += kWideRows * C::U;
+    dy = off; off += (F * C::U + 3) & ~3;
     pr = off; off += kWideRows * C::PRS;
-    // P and dS: one row per attention lane (row = h F + i; the lanes >= H F own dummy rows);
-    // PM + PD also hold P7's 4 x 2 x 4 x 64 dx partials (2 048 floats)
-    pm = off; off += (64 * C::PMS + 3) & ~3;
-    pd = off; off += (64 * C::PMS + 3) & ~3;
+    // P and dS, one row per attention lane.  Once the K-pass sweep is done PM + PD also hold its
+    // dv / dk partials (4 x hf1 x 8), and in P7 the 4 x 2 x 4 x 64 dx partial tiles (2 048)
+    const int pmn = (hf1 * C::PMS + 3) & ~3;
+    const int need = 4 * hf1 * 8 > 2048 ? 4 * hf1 * 8 : 2048;
+    const int pmd = 2 * pmn > need ? pmn : (need + 1) / 2 + 4;
+    pm = off; off += pmd;
+    pd = off; off += pmd;
     dl = off; off += (C::H * kWideRows + 3) & ~3;
-    qp = off; off += 4 * 64 * 8;   // the Q-pass's dq partials [wave][lane][8]
-    kvp = off; off += 4 * 64 * 8;  // the K-pass's dv (waves 0, 1) / dk (2, 3) partials
+    qp = off; off += 4 * hf1 * 8;  // the Q-pass's dq partials [wave][row][8]
     total = off;
   }
 };
@@ -321,7 +311,7 @@ __host__ __forceinline__ size_t wbwd_lds_bytes(int F) {
 }
 
 template <class C, bool DROP, int SKIP = 0>
-__global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
+__global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
     const float* __restrict__ x, const float* __restrict__ xsave, const float* __restrict__ dy,
     int64_t dy_ld, const float* __restrict__ W, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ dx,
@@ -342,9 +332,9 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
   float* const PD = smem + lay.pd;  // dS = P (dP - D)       [h][i][j]
   float* const DL = smem + lay.dl;  // D_{h,i} = dO_i . O_i
   float* const QP = smem + lay.qp;
-  float* const KVP = smem + lay.kvp;
-  float* const XS = PM;             // P7: the 4 waves' dx partial tiles (PM / PD are dead)
-  static_assert(2 * 64 * C::PMS >= 2048, "PM + PD hold the dx partial tiles");
+  float* const KVP = PM;            // K-pass partials, after its sweep (PM / PD are dead then)
+  float* const XS = PM;             // P7: the 4 waves' dx partial tiles
+  const int HF1 = lay.hf1;          // partial rows per wave
   const int w = wave_id();
   const int sv = (int)small_save_stride(F, U, C::H);
   const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);
@@ -362,12 +352,11 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
   const bool aact = ai0 < F;                                                \
   const int ai = aact ? ai0 : 0;
 
-  // zero once: X rows >= F of both buffers, DY rows >= F (read by P7's unguarded tile loads)
+  // zero once: X rows >= F of both buffers (read by the projection's unguarded row tiles)
   for (int k = F * E + (int)threadIdx.x; k < kWideRows * E; k += kWideThreads) {
     smem[lay.xb0 + k] = 0.f;
     smem[lay.xb1 + k] = 0.f;
   }
-  for (int k = F * U + (int)threadIdx.x; k < kWideRows * U; k += kWideThreads) DY[k] = 0.f;
 
   f32x4 dwacc = f32x4{0.f, 0.f, 0.f, 0.f};  // dW[4q + r][16w + jx]
   float dbp = 0.f;                           // db[16w + jx] over this lane's rows
@@ -481,9 +470,10 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
         const float D = DL[h * F + i];
         const float* kb = PR + U + h * DH;
         const float* vb = PR + 2 * U + h * DH;
-        // rows = lanes: the inactive lanes (>= H F) write rows of their own (never read)
-        float* const pm_row = PM + lane * C::PMS;
-        float* const pd_row = PD + lane * C::PMS;
+        // row = lane = h F + i; the idle lanes (>= H F) share the dummy row H F (never read)
+        const int prow = act ? lane : C::H * F;
+        float* const pm_row = PM + prow * C::PMS;
+        float* const pd_row = PD + prow * C::PMS;
         const uint32_t kb_drop = DROP ? dropout_sample_key(lseed, (uint32_t)b) : 0u;
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] = 0.f;
@@ -519,7 +509,7 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
           ld(k0, v0, m + 2);
           if (m + 1 < nk) key(m + 1, k1, v1);
         }
-        float4* qp = reinterpret_cast<float4*>(QP + (w * 64 + lane) * 8);
+        float4* qp = reinterpret_cast<float4*>(QP + (w * HF1 + prow) * 8);
         qp[0] = make_float4(dq[0], dq[1], dq[2], dq[3]);
         qp[1] = make_float4(dq[4], dq[5], dq[6], dq[7]);
       }
@@ -556,9 +546,12 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
           ld(v0, c0, m + 2);
           if (m + 1 < ni) axpy_reg_pk(acc, c1, v1);
         }
-        float4* kp = reinterpret_cast<float4*>(KVP + (w * 64 + lane) * 8);
+        lds_barrier();  // every wave's P / dS reads are done: the partials go over PM / PD
+        float4* kp = reinterpret_cast<float4*>(KVP + (w * HF1 + (act ? lane : C::H * F)) * 8);
         kp[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
         kp[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+      } else {
+        lds_barrier();
       }
       lds_barrier();
       IL_STAMP(5)
@@ -577,16 +570,18 @@ __global__ void __launch_bounds__(kWideThreads, 3) wbwd_kernel(
           float sc = a.inv_sdh;
           if (sl == 0) {
             const float* qp = QP + l * 8 + 4 * half;
+            const int ws = HF1 * 8;
             const float4 p0 = *reinterpret_cast<const float4*>(qp);
-            const float4 p1 = *reinterpret_cast<const float4*>(qp + 512);
-            const float4 p2 = *reinterpret_cast<const float4*>(qp + 1024);
-            const float4 p3 = *reinterpret_cast<const float4*>(qp + 1536);
+            const float4 p1 = *reinterpret_cast<const float4*>(qp + ws);
+            const float4 p2 = *reinterpret_cast<const float4*>(qp + 2 * ws);
+            const float4 p3 = *reinterpret_cast<const float4*>(qp + 3 * ws);
             sum = make_float4(((p0.x + p1.x) + p2.x) + p3.x, ((p0.y + p1.y) + p2.y) + p3.y,
                               ((p0.z + p1.z) + p2.z) + p3.z, ((p0.w + p1.w) + p2.w) + p3.w);
           } else {
-            const float* kp = KVP + (sl == 1 ? 1024 : 0) + l * 8 + 4 * half;
+            const int ws = HF1 * 8;
+            const float* kp = KVP + (sl == 1 ? 2 * ws : 0) + l * 8 + 4 * half;
             const float4 p0 = *reinterpret_cast<const float4*>(kp);
-            const float4 p1 = *reinterpret_cast<const float4*>(kp + 512);
+            const float4 p1 = *reinterpret_cast<const float4*>(kp + ws);
             sum = make_float4(p0.x + p1.x, p0.y + p1.y, p0.z + p1.z, p0.w + p1.w);
             if (sl == 2) sc = 1.f;
           }

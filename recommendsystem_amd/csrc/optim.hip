@@ -489,11 +489,20 @@ __global__ void __launch_bounds__(256) sparse_merge_kernel(
     const int32_t* __restrict__ rows, const float* __restrict__ grads, int32_t count, int dim,
     int lps, float* __restrict__ grad_table, int32_t* __restrict__ flag,
     int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap,
-    const int32_t* __restrict__ counts, int64_t cstride, int world, int rank) {
+    const int32_t* __restrict__ counts, int64_t cstride, int world, int rank,
+    int32_t stride = 0, int32_t* __restrict__ overflow = nullptr) {
   // one global n_touched atomic per block (see sparse_grad_accum_kernel)
   __shared__ int32_t nclaim, base;
   __shared__ int32_t lidx[256];
-  if (counts) {
+  if (counts && stride > 0) {
+    // fixed layout (rs_sparse_merge_rows_dev_stride): rank r's list at r * stride, whatever the
+    // counts; a count past stride lost rows in transit -> the sticky overflow word
+    const int c = counts[rank * cstride];
+    if (overflow && c > stride && blockIdx.x == 0 && threadIdx.x == 0) atomicMax(overflow, c);
+    rows += (int64_t)rank * stride;
+    grads += (int64_t)rank * stride * dim;
+    count = min(c, min(count, stride));
+  } else if (counts) {
     // device counts (rs_sparse_merge_rows_dev): every rank's list was gathered as a prefix of
     // nmax = max_r count_r entries, count is this launch's upper bound on every count
     int nmax = 0;
@@ -576,6 +585,25 @@ RS_API int rs_sparse_merge_rows_dev(void* stream, const int32_t* rows_all, const
   sparse_merge_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(
       rows_all, grads_all, cap, dim, lps, grad_table, flag, touched, n_touched, touched_cap, counts,
       counts_stride, world, rank);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_sparse_merge_rows_dev_stride(void* stream, const int32_t* rows_all,
+                                           const float* grads_all, const int32_t* counts,
+                                           int64_t counts_stride, int world, int rank,
+                                           int32_t stride, int dim, float* grad_table,
+                                           int32_t* flag, int32_t* touched, int32_t* n_touched,
+                                           int32_t touched_cap, int32_t* overflow) {
+  if (!rows_all || !grads_all || !counts || !grad_table || !flag || dim <= 0 || world <= 0 ||
+      rank < 0 || rank >= world || counts_stride <= 0 || stride <= 0)
+    return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
+  const int lps = lanes_for_dim(dim);
+  int64_t grid = ((int64_t)stride * lps + 255) / 256;  // sized for a full list; extra blocks exit
+  if (grid > 4096) grid = 4096;
+  sparse_merge_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(
+      rows_all, grads_all, stride, dim, lps, grad_table, flag, touched, n_touched, touched_cap,
+      counts, counts_stride, world, rank, stride, overflow);
   return rs_status_after_launch();
 }
 

@@ -164,9 +164,10 @@ class Trainer:
     # per step: graph A (forward, backward, regularisers, every replicated table's touched rows
     # compacted into its send list, the counts into dp_counts) -> eager collectives (the dense
     # all-reduce, ONE all-gather of all tables' counts, ONE host read of the per-table maxima,
-    # one all-gather per table of nmax rows / gradient rows) -> graph B (rank-ordered merges that
-    # read the counts on the device, rs_sparse_merge_rows_dev; dense Adam; sparse optimizers).
-    def _dp_setup(self):
+    # one all-gather per table of nmax rows / gradient rows -- or, with dp_caps, fixed-size
+    # all-gathers and no host read) -> graph B (rank-ordered merges that read the counts on the
+    # device, rs_sparse_merge_rows_dev[_stride]; dense Adam; sparse optimizers).
+    def _dp_setup(self, dp_caps=None):
         dev = self.arena.data.device
         self._rep = [t for t in self.tables if not is_sharded(t)]
         if len(self._rep) != len(self.tables):
@@ -175,6 +176,18 @@ class Trainer:
         T = len(self._rep)
         self.dp_counts = torch.zeros(max(T, 1), device=dev, dtype=torch.int32)
         self.dp_counts_all = torch.zeros(self.world * max(T, 1), device=dev, dtype=torch.int32)
+        # sync-free exchange (dp_caps: rows per rank per step for each replicated table, e.g. the
+        # batch's id count for that table -- a bound the caller knows): every rank's first cap
+        # compacted rows travel whatever the counts, the merge reads the counts on the device
+        # (rs_sparse_merge_rows_dev_stride) and a count past cap lands in dp_overflow
+        # (check_dp_overflow, off the hot path).  None: one host read of the counts per step,
+        # the all-gathers sized to the largest count.
+        if dp_caps is not None:
+            dp_caps = [int(min(c, t.touched_cap)) for c, t in zip(dp_caps, self._rep)]
+            if len(dp_caps) != T or min(dp_caps, default=1) <= 0:
+                raise ValueError("dp_caps: one positive row capacity per replicated table")
+        self.dp_caps = dp_caps
+        self.dp_overflow = torch.zeros(1, device=dev, dtype=torch.int32)
         self.dp_all = [(torch.empty(self.world * t.touched_cap, device=dev, dtype=torch.int32),
                         torch.empty(self.world * t.touched_cap * t.dim, device=dev))
                        for t in self._rep]
@@ -194,6 +207,14 @@ class Trainer:
         if not self._rep:
             return
         _all_gather_flat(self.dp_counts_all, self.dp_counts, self.pg)
+        if self.dp_caps is not None:  # fixed sizes: nothing read back on the host
+            for ti, t in enumerate(self._rep):
+                n = self.dp_caps[ti]
+                rows, grads = self.xbuf[id(t)]
+                rows_all, grads_all = self.dp_all[ti]
+                _all_gather_flat(rows_all[:self.world * n], rows[:n], self.pg)
+                _all_gather_flat(grads_all[:self.world * n * t.dim], grads[:n].reshape(-1), self.pg)
+            return
         T = len(self._rep)
         nmax = self.dp_counts_all.view(self.world, T).max(0).values.tolist()  # the host sync
         for ti, t in enumerate(self._rep):
@@ -213,6 +234,12 @@ class Trainer:
         for ti, t in enumerate(self._rep):
             rows_all, grads_all = self.dp_all[ti]
             for r in range(self.world):  # rank order -> identical sums on every replica
+                if self.dp_caps is not None:
+                    call("rs_sparse_merge_rows_dev_stride", s, ptr(rows_all), ptr(grads_all),
+                         self.dp_counts_all.data_ptr() + 4 * ti, T, self.world, r,
+                         self.dp_caps[ti], t.dim, ptr(t.grad), ptr(t.flag), ptr(t.touched),
+                         ptr(t.n_touched), t.touched_cap, ptr(self.dp_overflow))
+                    continue
                 call("rs_sparse_merge_rows_dev", s, ptr(rows_all), ptr(grads_all),
                      self.dp_counts_all.data_ptr() + 4 * ti, T, self.world, r, t.touched_cap, t.dim,
                      ptr(t.grad), ptr(t.flag), ptr(t.touched), ptr(t.n_touched), t.touched_cap)
@@ -241,16 +268,27 @@ class Trainer:
             call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
         return loss
 
-    def capture_pool(self, batches, warmup: int = 1) -> None:
+    def check_dp_overflow(self) -> None:
+        """Raise if a sync-free DP step (capture_pool(dp_caps=...)) saw a rank touch more rows
+        than its cap (rows lost in transit).  Reads the device: call it off the hot path."""
+        n = int(self.dp_overflow.item()) if getattr(self, "dp_overflow", None) is not None else 0
+        if n:
+            self.dp_overflow.zero_()
+            raise RuntimeError(f"sparse DP exchange overflow: a rank touched {n} rows, dp_caps "
+                               f"{self.dp_caps} (raise dp_caps)")
+
+    def capture_pool(self, batches, warmup: int = 1, dp_caps=None) -> None:
         """Record one whole training step per device-resident batch (forward, autograd backward,
         regularisers, dense Adam, sparse optimizer) into its own HIP graph; step_pool(i) replays
         batch i with no host work.  All graphs share one memory pool and are replayed in capture
         order (cyclic), which is what makes sharing it safe.  ``warmup`` eager steps run first
         (first-call allocations) and are rolled back, so capture changes no training state.
         Data parallel (world > 1): per batch a forward/backward graph (ending with the sparse
-        lists packed), the collectives eager, then ONE merge + optimizer graph (_dp_* above)."""
+        lists packed), the collectives eager, then ONE merge + optimizer graph (_dp_* above);
+        with dp_caps (per replicated table: rows one rank can touch per step) the collectives
+        have fixed sizes and the host reads nothing back (sync-free; check_dp_overflow)."""
         if self.world > 1:
-            self._dp_setup()
+            self._dp_setup(dp_caps)
         saved = [t.clone() for t in self._state()]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -278,6 +316,19 @@ class Trainer:
             self.graph_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_opt):  # allocates nothing
                 self._dp_merge_optimize()
+        # prime: replay each graph once and roll the state back (a graph's first launch after
+        # capture is slower; AutoIntTrainer._prime_graphs)
+        import os
+        if not os.environ.get("RS_NO_GRAPH_PRIME"):
+            saved = [t.clone() for t in self._state()]
+            for g in self.graphs:
+                g.replay()
+            if self.graph_opt is not None:
+                self.graph_opt.replay()
+            torch.cuda.synchronize()
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+            torch.cuda.synchronize()
 
     def step_pool(self, i: int):
         k = i % len(self.graphs)

@@ -52,7 +52,13 @@ def _snapshot(m):
     return params, m.table.weight.cpu().numpy()
 
 
-def _worker(rank, world, port, kind, out):
+def _caps(kind):
+    """rows one rank can touch per step: every id of the 64-sample batch (DIN: query + 20 history
+    ids; staytime + rough_rank: 91 fields + 3 x 50 sequence + 52 DSSM ids per sample)"""
+    return [64 * 21] if kind == "din" else [64 * (91 + 150 + 52)]
+
+
+def _worker(rank, world, port, kind, out, sync_free=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
@@ -62,21 +68,26 @@ def _worker(rank, world, port, kind, out):
     torch.cuda.synchronize()
     eager = _snapshot(m)
     m, trn, batches = _build(kind, rank)
-    trn.capture_pool(batches, warmup=1)
+    trn.capture_pool(batches, warmup=1, dp_caps=_caps(kind) if sync_free else None)
     assert trn.graph_opt is not None and len(trn.graphs) == 2
     graph_losses = [float(trn.step_pool(s)) for s in range(STEPS)]
     torch.cuda.synchronize()
     m.table.check_overflow()
+    trn.check_dp_overflow()
     out[rank] = (eager_losses, eager, graph_losses, _snapshot(m))
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("sync_free", [False, True])
 @pytest.mark.parametrize("kind", ["din", "staytime"])
-def test_dp_trainer_graph_equals_eager(kind):
+def test_dp_trainer_graph_equals_eager(kind, sync_free):
+    """sync_free: capture_pool(dp_caps=...) -- fixed-size all-gathers, no host read per step
+    (rs_sparse_merge_rows_dev_stride); the eager step all-reduces the dense gradient in buckets
+    issued during backward (dist.BucketedAllReduce)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(WORLD, _free_port(), kind, out), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(WORLD, _free_port(), kind, out, sync_free), nprocs=WORLD, join=True)
     for r in range(WORLD):
         el, (ep, et), gl, (gp, gt) = out[r]
         np.testing.assert_allclose(gl, el, rtol=1e-6, err_msg=f"rank {r} losses")
