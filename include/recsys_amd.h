@@ -537,6 +537,21 @@ int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const float* i
                       float clip_lo, float clip_hi, float log_eps, float* p_out, float* dil,
                       int64_t ld_dil, float* dx0, int64_t ld_dx, int dx_accumulate,
                       float* workspace, int64_t workspace_floats);
+/* rs_mlp_head_train with the layer-1 weight gradient deferred: instead of a 16-row dW1 partial
+ * per block (K0 x N1 floats: 57 KB per block at config 2) the kernel stores its layer-1 dz rows,
+ * dz1[b * ld_dz1 + n] = dL/d(x0 W1 + b1)[b][n] (ld_dz1 >= N1), and the partial rows start at b1:
+ * rs_mlp_head_dz_workspace_floats(...) = blocks x (rs_mlp_head_param_floats - K0 N1 + 1), arena
+ * order [b1 W2 b2 W3 b3 | loss_sum].  dW1 = x0^T dz1 is formed by the InteractingLayer backward
+ * that follows (rs_il_bwd_push_saved_xt / rs_il_bwd_saved_xt) as a few sample-range partial rows. */
+int64_t rs_mlp_head_dz_workspace_floats(int64_t B, int K0, int N1, int N2, int S, int T);
+int rs_mlp_head_train_dz(void* stream, const float* x0, int64_t ldx, const float* il,
+                         int64_t ld_il, int64_t B, int K0, int S, int N1, int act1, int N2,
+                         int act2, int T, int act3, const float* W1, const float* b1,
+                         const float* W2, const float* b2, const float* W3, const float* b3,
+                         const float* labels, float clip_lo, float clip_hi, float log_eps,
+                         float* p_out, float* dil, int64_t ld_dil, float* dx0, int64_t ld_dx,
+                         int dx_accumulate, float* workspace, int64_t workspace_floats,
+                         float* dz1, int64_t ld_dz1);
 
 /* Per-block gradient partials -> gradients (-> dense Adam), one launch (replaces the
  * column-reduce launches of the fused backward kernels plus rs_dense_adam and its step-increment
@@ -593,6 +608,36 @@ int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave, const
                          const float* dx_base, const int32_t* rows, float* grad_table,
                          int32_t* flag, float* dparams, int dparams_accumulate, float* workspace,
                          int64_t workspace_floats, const float* asave, int64_t asave_floats);
+/* rs_il_bwd_saved / rs_il_bwd_push_saved carrying a deferred weight gradient (the fused head's
+ * dW1, rs_mlp_head_train_dz): besides the InteractingLayer backward, the launch's waves first
+ * form xt_slab[sp][k][n] = sum over sample range sp of xt_x[b][k] xt_dz[b][n] for
+ * sp < rs_il_xt_splits(B) (equal ranges of the batch, a function of B alone), k < xt_K0,
+ * n < xt_N1 (xt_K0 % 16 == 0, xt_N1 % 16 == 0; row strides xt_ldx >= xt_K0, xt_lddz >= xt_N1);
+ * xt_slab holds rs_il_xt_splits(B) x xt_K0 x xt_N1 floats, summed in range order by the
+ * optimizer tail (rs_partials_reduce_adam*).  Shapes whose backward has no such kernel (no
+ * attention save, F > 32, H != 2) return RS_ERR_UNSUPPORTED. */
+int rs_il_xt_splits(int64_t B);
+/* The grid rs_il_bwd_(push_)saved_xt would use for this shape (> 0), or 0 when the shape's
+ * saved backward cannot carry the deferred weight gradient. */
+int rs_il_bwd_xt_supported(int64_t B, int F, int E, int U, int H, int64_t workspace_floats);
+int rs_il_bwd_saved_xt(void* stream, const float* x, const float* xsave, const float* dy,
+                       int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L, const float* W,
+                       const float* bias, const float* gamma, const float* beta, float eps,
+                       int use_res, float drop_rate, uint64_t seed, float* dx, int dx_accumulate,
+                       float* dparams, int dparams_accumulate, float* workspace,
+                       int64_t workspace_floats, const float* asave, int64_t asave_floats,
+                       const float* xt_x, int64_t xt_ldx, const float* xt_dz, int64_t xt_lddz,
+                       int xt_K0, int xt_N1, float* xt_slab);
+int rs_il_bwd_push_saved_xt(void* stream, const float* x, const float* xsave, const float* dy,
+                            int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                            const float* W, const float* bias, const float* gamma,
+                            const float* beta, float eps, int use_res, float drop_rate,
+                            uint64_t seed, const float* dx_base, const int32_t* rows,
+                            float* grad_table, int32_t* flag, float* dparams,
+                            int dparams_accumulate, float* workspace, int64_t workspace_floats,
+                            const float* asave, int64_t asave_floats, const float* xt_x,
+                            int64_t xt_ldx, const float* xt_dz, int64_t xt_lddz, int xt_K0,
+                            int xt_N1, float* xt_slab);
 
 /* Grid (= number of per-block partial rows) rs_il_bwd / rs_il_bwd_push use for this shape and
  * workspace when dy rows are 16-B aligned (dy_ld % 4 == 0); 0 for an unsupported shape. */

@@ -141,6 +141,10 @@ SIGNATURES: dict[str, tuple] = {
     "rs_mlp_head_train": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
                                  _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32,
                                  _f32, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
+    "rs_mlp_head_dz_workspace_floats": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32]),
+    "rs_mlp_head_train_dz": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
+                                    _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32,
+                                    _f32, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp, _i64]),
     "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
     "rs_partials_reduce_adam_scan": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -164,6 +168,15 @@ SIGNATURES: dict[str, tuple] = {
     "rs_il_bwd_push_saved": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
                                     _vp, _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp, _vp, _vp,
                                     _vp, _i32, _vp, _i64, _vp, _i64]),
+    "rs_il_xt_splits": (_i32, [_i64]),
+    "rs_il_bwd_xt_supported": (_i32, [_i64, _i32, _i32, _i32, _i32, _i64]),
+    "rs_il_bwd_saved_xt": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
+                                  _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _i32, _vp, _i32, _vp,
+                                  _i64, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i32, _vp]),
+    "rs_il_bwd_push_saved_xt": (_i32, [_vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _i32,
+                                       _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32, _u64, _vp, _vp,
+                                       _vp, _vp, _vp, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                       _i64, _i32, _i32, _vp]),
     "rs_il_fwd_gather_saved": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _i32,
                                       _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _i32, _f32,
                                       _u64, _vp, _i64, _vp, _vp, _i64]),

@@ -277,9 +277,27 @@ class AutoIntTrainer:
         if npar != o - off:
             return None
         dev = self.dev
-        ws = torch.empty(int(lib.rs_mlp_head_workspace_floats(self.B, K0, N1, N2, S, T)),
-                         device=dev, dtype=torch.float32)
-        return dict(N1=N1, N2=N2, T=T, K0=K0, S=S, off=off, npar=npar, ws=ws,
+        # deferred dW1 (rs_mlp_head_train_dz): the head stores dz1 [B, N1] and the IL backward's
+        # waves form dW1 = x0^T dz1 as rs_il_xt_splits(B) sample-range partial rows
+        # (rs_il_bwd_push_saved_xt), instead of K0 x N1 partial floats per 16-sample head block
+        # (57 KB x B / 16: 14.6 MB written and read back per B = 4096 step).  Needs a saved
+        # backward that carries it (rs_il_bwd_xt_supported); RS_HEAD_W1_PARTIALS=1 keeps the
+        # partial-row form (A/B runs)
+        import os
+        dz = (not os.environ.get("RS_HEAD_W1_PARTIALS") and self.asave_n > 0 and
+              lib.rs_il_bwd_xt_supported(self.B, self.F, self.E, self.U, self.H, self.il_ws_n) > 0)
+        w1n = K0 * N1 if dz else 0
+        nws = (lib.rs_mlp_head_dz_workspace_floats if dz else lib.rs_mlp_head_workspace_floats)(
+            self.B, K0, N1, N2, S, T)
+        ws = torch.empty(int(nws), device=dev, dtype=torch.float32)
+        xt = None
+        if dz:
+            ns = int(lib.rs_il_xt_splits(self.B))
+            xt = dict(dz1=torch.zeros(self.B, N1, device=dev, dtype=torch.float32), splits=ns,
+                      slab=torch.zeros(ns * K0 * N1, device=dev, dtype=torch.float32))
+        return dict(N1=N1, N2=N2, T=T, K0=K0, S=S, off=off, npar=npar, ws=ws, xt=xt,
+                    # the partial rows: [b1 ... b3 | loss] (deferred dW1) or [W1 b1 ... | loss]
+                    w1n=w1n, pn=npar - w1n,
                     blocks=int(lib.rs_mlp_head_partial_blocks(self.B)),
                     il_off=il_off, il_n=il_n,
                     # the step's backward reads the forward's attention save when the shape
@@ -315,24 +333,32 @@ class AutoIntTrainer:
         d = self.deep_layers
         lg = self.logit_layers[0]
         d2 = d[1] if hd["N2"] else None
-        call("rs_mlp_head_train", s, ptr(self.x0), F * E, self.cat.data_ptr() + 4 * D, CW, B,
+        xt = hd["xt"]
+        call("rs_mlp_head_train_dz" if xt else "rs_mlp_head_train", s, ptr(self.x0), F * E,
+             self.cat.data_ptr() + 4 * D, CW, B,
              hd["K0"], hd["S"], hd["N1"], d[0].act, hd["N2"], d2.act if d2 is not None else 0,
              hd["T"], lg.act, ptr(d[0].kernel), ptr(d[0].bias),
              ptr(d2.kernel) if d2 is not None else None, ptr(d2.bias) if d2 is not None else None,
              ptr(lg.kernel), ptr(lg.bias), ptr(self.labels), 1e-6, 1.0, 1e-6, ptr(self.p),
              self.dcat.data_ptr() + 4 * D, CW, ptr(self.dx0), F * E, 0, ptr(hd["ws"]),
-             hd["ws"].numel())
+             hd["ws"].numel(), *((ptr(xt["dz1"]), hd["N1"]) if xt else ()))
+        # the deferred dW1 rides on the IL backward (x0^T dz1 partial rows)
+        xa = (ptr(self.x0), F * E, ptr(xt["dz1"]), hd["N1"], hd["K0"], hd["N1"],
+              ptr(xt["slab"])) if xt else ()
         if self.push:
             # dL/dx0 = head share (dx0) + IL share, added straight into the table rows
-            call("rs_il_bwd_push_saved", s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
+            call("rs_il_bwd_push_saved_xt" if xt else "rs_il_bwd_push_saved", s, ptr(self.x0),
+                 ptr(self.xsave) if L > 1 else None,
                  self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
                  ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed,
                  ptr(self.dx0), ptr(self.rows), ptr(t.grad), ptr(t.flag), None, 0,
-                 ptr(self.il_ws), self.il_ws_n, ptr(self.asave), self.asave_n)
+                 ptr(self.il_ws), self.il_ws_n, ptr(self.asave), self.asave_n, *xa)
             return
         # (F > 64: the forward above is the plain one, no save to read)
         saved = F <= 64 and self.asave_n > 0
         name, tail = ("rs_il_bwd_saved", (ptr(self.asave), self.asave_n)) if saved else ("rs_il_bwd", ())
+        if xt:
+            name, tail = "rs_il_bwd_saved_xt", tail + xa
         call(name, s, ptr(self.x0), ptr(self.xsave) if L > 1 else None,
              self.dcat.data_ptr() + 4 * D, CW, B, F, E, U, H, L, ptr(il.kernel), ptr(il.bias),
              ptr(il.gamma), ptr(il.beta), il.epsilon, int(il.use_res), drop, il.seed, ptr(self.dx0),
@@ -356,14 +382,19 @@ class AutoIntTrainer:
         ar = m.arena
         # data parallel: the local gradient goes to the exchange bucket, not the arena
         g0 = self.dp_send.data_ptr() if self.packed_dp else ar.grad.data_ptr()
-        npl = hd["npar"] + 1
+        pn, ho = hd["pn"], hd["off"] + hd["w1n"]  # partial-row columns and their arena offset
         segs = [
             (self.il_ws.data_ptr(), hd["il_n"], hd["il_blocks"], hd["il_n"], g0 + 4 * hd["il_off"],
              1.0, hd["il_off"]),
-            (hd["ws"].data_ptr(), npl, hd["blocks"], hd["npar"], g0 + 4 * hd["off"], 1.0, hd["off"]),
-            (hd["ws"].data_ptr() + 4 * hd["npar"], npl, hd["blocks"], 1, self.loss.data_ptr(),
+            (hd["ws"].data_ptr(), pn + 1, hd["blocks"], pn, g0 + 4 * ho, 1.0, ho),
+            (hd["ws"].data_ptr() + 4 * pn, pn + 1, hd["blocks"], 1, self.loss.data_ptr(),
              1.0 / self.B, -1),
         ]
+        xt = hd["xt"]
+        if xt is not None:  # dW1's sample-range rows from the IL backward (rs_il_bwd_*_xt)
+            w1 = hd["K0"] * hd["N1"]
+            segs.insert(1, (xt["slab"].data_ptr(), w1, xt["splits"], w1, g0 + 4 * hd["off"], 1.0,
+                            hd["off"]))
         _lib.partials_reduce_adam(stream_handle(), segs, ar.data, self.adam_m, self.adam_v,
                                   self.step_count, hd["done"], cfg.lr_dense, 0.9, 0.999, 1e-8,
                                   1.0 / self.world, adam, scan_table=scan_table)

@@ -78,6 +78,7 @@ struct Args {
   float* dil; int64_t ld_dil;              // [B, S]
   float* dx0; int64_t ld_dx; int dx_accumulate;
   float* part; int64_t np;                 // [gridDim.x, np]
+  float* dz1; int64_t ld_dz1;              // deferred dW1 (rs_mlp_head_train_dz): [B, N1], else null
 };
 
 // LDS carve-up (floats).  Row strides are padded by 4 (16-byte aligned rows, staggered banks).
@@ -145,7 +146,12 @@ struct StageRows {
 // TT: the logits width T at compile time (1: every reference head -- AutoInt's Dense(1), the
 // multi_head towers), 0: runtime T <= TMAX.  With T known the per-row / per-column T loops unroll
 // into straight-line code (the runtime form measured 9.2 K cycles for the logits backward phase).
-template <int N1, int N2, bool BF, int TT = 0>
+// DZ: deferred dW1 (rs_mlp_head_train_dz): the block stores its layer-1 dz rows (dz1 [B, N1])
+// instead of a 16-row dW1 partial (K0 x N1 floats per block: 57 KB at config 2, 14.6 MB per
+// B = 4096 step, written here and read back by the reduction); the optimizer tail forms
+// dW1 = x0^T dz1 over the whole batch (rs_partials_reduce_adam_ex).  The partial row then starts
+// at b1.
+template <int N1, int N2, bool BF, int TT = 0, bool DZ = false>
 __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   using L = Lay<N1, N2>;
   constexpr int D = L::D;
@@ -299,11 +305,15 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
   const float* HD = N2 > 0 ? H2 : H1;
   constexpr int HDS = N2 > 0 ? L::H2S : L::H1S;
 
-  // ---- logits: z[r][t] = sum_c cat[r][c] W3[c][t] + b3[t]; one wave per row (RB = NW) ----
+  // ---- logits: z[r][t] = sum_c cat[r][c] W3[c][t] + b3[t]; one wave per row (RB = NW).  The
+  //      row's wave goes straight on with its share of the backward: d il[r] = dz[r] W3[D:]^T
+  //      (global) and the deep output's dz (DZD row r) -- no barrier between the loss and them;
+  //      the cross-row sums (dW3, db3, loss) wait for the layer-2 backward phase ----
   static_assert(NW == RB, "logits pass maps one wave to one row");
   float lsum = 0.f;
   {
     const int r = w, c0 = l;
+    float dzt[TMAX] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {  // unrolled: b3v / ylv stay registers
       if (t >= T) break;
@@ -313,8 +323,8 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
         acc = fmaf(xv, W3s[c * T + t], acc);
       }
       acc = group_sum<64>(acc);
+      float dz = 0.f;
       if (c0 == 0) {
-        float dz = 0.f;
         if (r < nrow) {
           const float y = act_f(acc + b3v[t], a.act3);
           const float p = fminf(fmaxf(y, a.lo), a.hi);
@@ -326,21 +336,39 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
         }
         Z3[r * TMAX + t] = dz;
       }
+      dzt[t] = __shfl(dz, 0, 64);  // the row's dz to every lane of its wave
+    }
+    // d(concat)[r][c] = sum_t dz[r][t] W3[c][t]: the interacting part -> d il (global), the deep
+    // part -> DZD (with the deep output activation's gradient)
+    for (int c = c0; c < C; c += 64) {
+      float g = 0.f;
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t)
+        if (t < T) g = fmaf(dzt[t], W3s[c * T + t], g);
+      if (c < D) {
+        DZD[r * (D + 4) + c] = act_b(g, HD[r * HDS + c], N2 > 0 ? a.act2 : a.act1);
+      } else if (r < nrow) {
+        a.dil[(b0 + r) * a.ld_dil + (c - D)] = g;
+      }
     }
   }
   if (l == 0) LRED[w] = lsum;  // lane 0 of each wave holds its row's loss terms
   lds_barrier();
   HEAD_STAMP(5)
+  HEAD_STAMP(6)
 
   float* part = a.part + (int64_t)blockIdx.x * a.np;
-  const int o_b1 = K0 * N1, o_w2 = o_b1 + N1, o_b2 = o_w2 + N1 * N2, o_w3 = o_b2 + N2;
+  const int o_b1 = DZ ? 0 : K0 * N1, o_w2 = o_b1 + N1, o_b2 = o_w2 + N1 * N2, o_w3 = o_b2 + N2;
   const int o_b3 = o_w3 + C * T, o_loss = o_b3 + T;
-  // ---- logits backward: dW3 / db3 partials, d(concat) -> d il (global) and dz of the deep out ----
+  // ---- logits' cross-row sums: dW3 / db3 partials and the block's loss ----
   for (int c = tid; c < C; c += NTH) {
     float g[TMAX] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
     for (int r = 0; r < RB; ++r) {
       const float xv = c < D ? HD[r * HDS + c] : Is[r * is + (c - D)];
-      for (int t = 0; t < T; ++t) g[t] = fmaf(xv, Z3[r * TMAX + t], g[t]);
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t)
+        if (t < T) g[t] = fmaf(xv, Z3[r * TMAX + t], g[t]);
     }
     for (int t = 0; t < T; ++t) part[o_w3 + c * T + t] = g[t];
   }
@@ -354,18 +382,6 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
     for (int k = 0; k < NW; ++k) s += LRED[k];
     part[o_loss] = s;
   }
-  for (int idx = tid; idx < RB * C; idx += NTH) {
-    const int r = idx / C, c = idx - r * C;
-    float g = 0.f;
-    for (int t = 0; t < T; ++t) g = fmaf(Z3[r * TMAX + t], W3s[c * T + t], g);
-    if (c < D) {
-      DZD[r * (D + 4) + c] = act_b(g, HD[r * HDS + c], N2 > 0 ? a.act2 : a.act1);
-    } else if (r < nrow) {
-      a.dil[(b0 + r) * a.ld_dil + (c - D)] = g;
-    }
-  }
-  lds_barrier();
-  HEAD_STAMP(6)
 
   // ---- layer 2 backward: dW2 = h1^T dz2, db2, dz1 = act1'(dz2 W2^T) ----
   if (N2 > 0) {
@@ -403,6 +419,12 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
     for (int r = 0; r < RB; ++r) g += DZ1[r * L::H1S + tid];
     part[o_b1 + tid] = g;
   }
+  if constexpr (DZ) {
+    for (int idx = tid; idx < nrow * N1; idx += NTH) {
+      const int r = idx / N1, n = idx - r * N1;
+      a.dz1[(b0 + r) * a.ld_dz1 + n] = DZ1[r * L::H1S + n];
+    }
+  }
 
   // ---- layer 1 backward (MFMA), e tiles of 16 spread over the waves:
   //      dx0[r][e] = sum_n dz1[r][n] W1[e][n]    (A = dz1, B = W1 rows, both from LDS)
@@ -417,7 +439,7 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int nt = 0; nt < NT1; ++nt) dzb[t][nt] = DZ1[(4 * q + t) * L::H1S + 16 * nt + j];
+      for (int nt = 0; nt < NT1; ++nt) dzb[t][nt] = DZ ? 0.f : DZ1[(4 * q + t) * L::H1S + 16 * nt + j];
     for (int et = w; et < net; et += NW) {
       const int e = 16 * et + j;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -442,6 +464,7 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
           *d = a.dx_accumulate ? *d + acc[r] : acc[r];
         }
       }
+      if constexpr (DZ) continue;
       float xa[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) xa[t] = Xs[(4 * q + t) * xs + e];
@@ -469,26 +492,32 @@ __global__ void __launch_bounds__(NTH) head_train_kernel(Args a) {
 #endif
 }
 
-template <int N1, int N2, bool BF16_OK = false, int TT = 0>
-int launch(hipStream_t s, const Args& a, int64_t grid) {
+template <int N1, int N2, bool BF16_OK = false, int TT = 0, bool DZ = false>
+int launch_mode(hipStream_t s, const Args& a, int64_t grid) {
   const Lay<N1, N2> lay(a.K0, a.S, a.T);
   const size_t lds = (size_t)lay.total * sizeof(float);
   if (lds > 160 * 1024) return RS_ERR_UNSUPPORTED;
   if (TT > 0 && a.T != TT) return RS_ERR_ARG;
   if (rs_math_mode_now() == RS_MATH_BF16) {
     if constexpr (!BF16_OK) return RS_ERR_UNSUPPORTED;  // never a silent fp32 run
-    else head_train_kernel<N1, N2, true, TT><<<(unsigned)grid, NTH, lds, s>>>(a);
+    else head_train_kernel<N1, N2, true, TT, DZ><<<(unsigned)grid, NTH, lds, s>>>(a);
   } else {
-    head_train_kernel<N1, N2, false, TT><<<(unsigned)grid, NTH, lds, s>>>(a);
+    head_train_kernel<N1, N2, false, TT, DZ><<<(unsigned)grid, NTH, lds, s>>>(a);
   }
   return rs_status_after_launch();
 }
 
+template <int N1, int N2, bool BF16_OK = false, int TT = 0>
+int launch(hipStream_t s, const Args& a, int64_t grid) {
+  return a.dz1 ? launch_mode<N1, N2, BF16_OK, TT, true>(s, a, grid)
+               : launch_mode<N1, N2, BF16_OK, TT, false>(s, a, grid);
+}
+
 }  // namespace rs_head
 
-static int64_t head_np(int K0, int N1, int N2, int S, int T) {
+static int64_t head_np(int K0, int N1, int N2, int S, int T, bool dz = false) {
   const int D = N2 > 0 ? N2 : N1;
-  return (int64_t)K0 * N1 + N1 + (int64_t)N1 * N2 + N2 + (int64_t)(D + S) * T + T + 1;
+  return (dz ? 0 : (int64_t)K0 * N1) + N1 + (int64_t)N1 * N2 + N2 + (int64_t)(D + S) * T + T + 1;
 }
 
 RS_API int64_t rs_mlp_head_param_floats(int K0, int N1, int N2, int S, int T) {
@@ -499,8 +528,48 @@ RS_API int64_t rs_mlp_head_workspace_floats(int64_t B, int K0, int N1, int N2, i
   return ((B + rs_head::RB - 1) / rs_head::RB) * head_np(K0, N1, N2, S, T);
 }
 
+RS_API int64_t rs_mlp_head_dz_workspace_floats(int64_t B, int K0, int N1, int N2, int S, int T) {
+  return ((B + rs_head::RB - 1) / rs_head::RB) * head_np(K0, N1, N2, S, T, true);
+}
+
 RS_API int rs_mlp_head_partial_blocks(int64_t B) {
   return (int)((B + rs_head::RB - 1) / rs_head::RB);
+}
+
+static int head_train_impl(void* stream, const float* x0, int64_t ldx, const float* il,
+                           int64_t ld_il, int64_t B, int K0, int S, int N1, int act1, int N2,
+                           int act2, int T, int act3, const float* W1, const float* b1,
+                           const float* W2, const float* b2, const float* W3, const float* b3,
+                           const float* labels, float clip_lo, float clip_hi, float log_eps,
+                           float* p_out, float* dil, int64_t ld_dil, float* dx0, int64_t ld_dx,
+                           int dx_accumulate, float* workspace, int64_t workspace_floats,
+                           float* dz1, int64_t ld_dz1) {
+  using namespace rs_head;
+  if (!x0 || !il || !W1 || !b1 || !W3 || !b3 || !labels || !dil || !dx0 || !workspace)
+    return RS_ERR_ARG;
+  if (N2 > 0 && (!W2 || !b2)) return RS_ERR_ARG;
+  if (B < 0 || K0 <= 0 || S <= 0 || T <= 0) return RS_ERR_ARG;
+  if (dz1 && ld_dz1 < N1) return RS_ERR_ARG;
+  if (B == 0) return RS_OK;
+  if (T > TMAX || K0 % 16 != 0 || S % 4 != 0 || ldx % 4 != 0 || ld_il % 4 != 0)
+    return RS_ERR_UNSUPPORTED;
+  if (((uintptr_t)x0 & 15) || ((uintptr_t)il & 15)) return RS_ERR_UNSUPPORTED;
+  for (int act : {act1, act2, act3})
+    if (act < ACT_NONE || act > ACT_SIGMOID) return RS_ERR_ARG;
+  const int64_t grid = (B + RB - 1) / RB;
+  const int64_t np = head_np(K0, N1, N2, S, T, dz1 != nullptr);
+  if (workspace_floats < grid * np) return RS_ERR_ARG;
+  Args a{x0, ldx, il, ld_il, W1, b1, W2, b2, W3, b3, labels, B, K0, S, T, act1, act2, act3,
+         clip_lo, clip_hi, log_eps, 1.0f / (float)B, p_out, dil, ld_dil, dx0, ld_dx,
+         dx_accumulate, workspace, np, dz1, ld_dz1};
+  hipStream_t s = rs_stream(stream);
+#define RS_HEAD(A, Bn) if (N1 == A && N2 == Bn) return launch<A, Bn>(s, a, grid);
+  if (N1 == 32 && N2 == 16)  // config 2 (bf16 too)
+    return T == 1 ? launch<32, 16, true, 1>(s, a, grid) : launch<32, 16, true>(s, a, grid);
+  RS_HEAD(64, 32) RS_HEAD(16, 0) RS_HEAD(32, 0) RS_HEAD(64, 0)
+  RS_HEAD(16, 16) RS_HEAD(32, 32) RS_HEAD(64, 16) RS_HEAD(64, 64)
+#undef RS_HEAD
+  return RS_ERR_UNSUPPORTED;
 }
 
 RS_API int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const float* il,
@@ -510,29 +579,21 @@ RS_API int rs_mlp_head_train(void* stream, const float* x0, int64_t ldx, const f
                              const float* labels, float clip_lo, float clip_hi, float log_eps,
                              float* p_out, float* dil, int64_t ld_dil, float* dx0, int64_t ld_dx,
                              int dx_accumulate, float* workspace, int64_t workspace_floats) {
-  using namespace rs_head;
-  if (!x0 || !il || !W1 || !b1 || !W3 || !b3 || !labels || !dil || !dx0 || !workspace)
-    return RS_ERR_ARG;
-  if (N2 > 0 && (!W2 || !b2)) return RS_ERR_ARG;
-  if (B < 0 || K0 <= 0 || S <= 0 || T <= 0) return RS_ERR_ARG;
-  if (B == 0) return RS_OK;
-  if (T > TMAX || K0 % 16 != 0 || S % 4 != 0 || ldx % 4 != 0 || ld_il % 4 != 0)
-    return RS_ERR_UNSUPPORTED;
-  if (((uintptr_t)x0 & 15) || ((uintptr_t)il & 15)) return RS_ERR_UNSUPPORTED;
-  for (int act : {act1, act2, act3})
-    if (act < ACT_NONE || act > ACT_SIGMOID) return RS_ERR_ARG;
-  const int64_t grid = (B + RB - 1) / RB;
-  const int64_t np = head_np(K0, N1, N2, S, T);
-  if (workspace_floats < grid * np) return RS_ERR_ARG;
-  Args a{x0, ldx, il, ld_il, W1, b1, W2, b2, W3, b3, labels, B, K0, S, T, act1, act2, act3,
-         clip_lo, clip_hi, log_eps, 1.0f / (float)B, p_out, dil, ld_dil, dx0, ld_dx,
-         dx_accumulate, workspace, np};
-  hipStream_t s = rs_stream(stream);
-#define RS_HEAD(A, Bn) if (N1 == A && N2 == Bn) return launch<A, Bn>(s, a, grid);
-  if (N1 == 32 && N2 == 16)  // config 2 (bf16 too)
-    return T == 1 ? launch<32, 16, true, 1>(s, a, grid) : launch<32, 16, true>(s, a, grid);
-  RS_HEAD(64, 32) RS_HEAD(16, 0) RS_HEAD(32, 0) RS_HEAD(64, 0)
-  RS_HEAD(16, 16) RS_HEAD(32, 32) RS_HEAD(64, 16) RS_HEAD(64, 64)
-#undef RS_HEAD
-  return RS_ERR_UNSUPPORTED;
+  return head_train_impl(stream, x0, ldx, il, ld_il, B, K0, S, N1, act1, N2, act2, T, act3, W1, b1,
+                         W2, b2, W3, b3, labels, clip_lo, clip_hi, log_eps, p_out, dil, ld_dil, dx0,
+                         ld_dx, dx_accumulate, workspace, workspace_floats, nullptr, 0);
+}
+
+RS_API int rs_mlp_head_train_dz(void* stream, const float* x0, int64_t ldx, const float* il,
+                                int64_t ld_il, int64_t B, int K0, int S, int N1, int act1, int N2,
+                                int act2, int T, int act3, const float* W1, const float* b1,
+                                const float* W2, const float* b2, const float* W3, const float* b3,
+                                const float* labels, float clip_lo, float clip_hi, float log_eps,
+                                float* p_out, float* dil, int64_t ld_dil, float* dx0,
+                                int64_t ld_dx, int dx_accumulate, float* workspace,
+                                int64_t workspace_floats, float* dz1, int64_t ld_dz1) {
+  if (!dz1) return RS_ERR_ARG;
+  return head_train_impl(stream, x0, ldx, il, ld_il, B, K0, S, N1, act1, N2, act2, T, act3, W1, b1,
+                         W2, b2, W3, b3, labels, clip_lo, clip_hi, log_eps, p_out, dil, ld_dil, dx0,
+                         ld_dx, dx_accumulate, workspace, workspace_floats, dz1, ld_dz1);
 }

@@ -86,6 +86,13 @@ struct BwdReq {
   // return without launching (rs_il_bwd_partial_blocks)
   int* grid_out = nullptr;
   int bf16 = 0;  // RS_MATH_BF16 (rs_set_math_mode): bf16 operands on the matrix cores
+  // a deferred weight gradient carried by this launch (rs_il_bwd_saved_xt): the fused head's
+  // dW1 = xt_x^T xt_dz over the batch, as xt_splits(B) sample-range partial rows in xt_slab
+  const float* xt_x = nullptr;
+  const float* xt_dz = nullptr;
+  int64_t xt_ldx = 0, xt_lddz = 0;
+  int xt_K0 = 0, xt_N1 = 0;
+  float* xt_slab = nullptr;
 };
 
 constexpr int kMaxFwdWaves = 4;
@@ -175,7 +182,61 @@ struct Args {
   // [H*F] x {scaled max, 1 / sum}; the backward reads them instead of re-running the softmax
   float* osave;
   const float* osave_in;
+  // deferred weight gradient (BwdReq::xt_*): slab[sp][k][n] = sum over sample range sp of
+  // x[b][k] dz[b][n]; xt_nsplit ranges, jobs = (K0 / 16) x (N1 / 16) x nsplit 16 x 16 tiles
+  const float* xt_x;
+  const float* xt_dz;
+  int64_t xt_ldx, xt_lddz;
+  int xt_K0, xt_N1, xt_nsplit;
+  float* xt_slab;
 };
+
+// sample ranges of the deferred weight gradient (a function of B alone: the partial rows, their
+// fixed-order sum and so every bit of the result depend on B only)
+__host__ __device__ inline int xt_splits(int64_t B) {
+  const int64_t n = (B + 15) / 16;
+  return (int)(n < 1 ? 1 : (n > 32 ? 32 : n));
+}
+
+// The deferred weight-gradient jobs of one wave (wave gw of nw in the grid): each job is a
+// 16 x 16 tile (k tile, n tile) of x^T dz over one sample range, v_mfma_f32_16x16x4f32 with 4
+// samples per step (A = x[b + q][16 kt + j], B = dz[b + q][16 nt + j]); eight steps' loads are
+// issued before their MFMAs.  The tile goes to slab row sp (row-major [K0][N1]): the optimizer
+// tail sums the nsplit rows in order.  Runs before the wave's first sample, while its first
+// sample's operands stream into LDS.
+__device__ __forceinline__ void xt_wave_jobs(const Args& a, int64_t gw, int64_t nw) {
+  if (!a.xt_x) return;
+  const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+  const int nkt = a.xt_K0 >> 4, nnt = a.xt_N1 >> 4, ns = a.xt_nsplit;
+  const int64_t njobs = (int64_t)nkt * nnt * ns;
+  const int64_t per = ((((int64_t)a.B + ns - 1) / ns) + 3) & ~(int64_t)3;
+  for (int64_t job = gw; job < njobs; job += nw) {
+    const int sp = (int)(job % ns);
+    const int64_t t = job / ns;
+    const int kt = (int)(t % nkt), nt = (int)(t / nkt);
+    const int64_t lo = sp * per;
+    const int64_t hi = lo + per < (int64_t)a.B ? lo + per : (int64_t)a.B;
+    const float* xp = a.xt_x + 16 * kt + j;
+    const float* dp = a.xt_dz + 16 * nt + j;
+    float __attribute__((ext_vector_type(4))) acc = {0.f, 0.f, 0.f, 0.f};
+    constexpr int KB = 8;
+    for (int64_t g = lo; g < hi; g += 4 * KB) {
+      float xv[KB], dv[KB];
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+        const int64_t b = g + 4 * u + q;
+        const bool ok = b < hi;
+        xv[u] = ok ? xp[b * a.xt_ldx] : 0.f;
+        dv[u] = ok ? dp[b * a.xt_lddz] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < KB; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[u], dv[u], acc, 0, 0, 0);
+    }
+    float* o = a.xt_slab + (int64_t)sp * a.xt_K0 * a.xt_N1 + (int64_t)(16 * kt) * a.xt_N1 + 16 * nt + j;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[(int64_t)(4 * q + r) * a.xt_N1] = acc[r];
+  }
+}
 
 static inline int r4(int v) { return (v + 3) & ~3; }
 
@@ -190,6 +251,8 @@ Args make_args(int64_t B, int F, int L, int use_res, float eps, float drop_rate,
                bool bwd) {
   Args a;
   a.B = (int)B; a.F = F; a.L = L; a.use_res = use_res;
+  a.xt_x = nullptr; a.xt_dz = nullptr; a.xt_slab = nullptr;
+  a.xt_ldx = a.xt_lddz = 0; a.xt_K0 = a.xt_N1 = 0; a.xt_nsplit = 1;
   a.ncol = use_res ? C::NC : 3 * C::U;
   a.eps = eps;
   a.sdh = (float)__builtin_sqrt((double)C::DH);   // Python float dh ** 0.5 -> fp32 constant
@@ -2104,6 +2167,7 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
     glds_copy_wave(SB, s_src(b_first, a.L - 1), ns4);
     glds_copy_wave(DY, dy + b_first * dy_ld, ny4);
   }
+  xt_wave_jobs(a, (int64_t)blockIdx.x * kWpb3 + w, (int64_t)gridDim.x * kWpb3);
   // the fused push's share of the head (dx_accumulate): 4 rows x ET columns per row tile
   const bool push = a.push_table != nullptr;
   const bool with_base = push && dx_accumulate;
@@ -2549,6 +2613,13 @@ int bwd_launch(const BwdReq& q) {
   a.push_table = q.push_table;
   a.push_flag = q.push_flag;
   a.dy_vec = (q.dy_ld % 4 == 0) && ((uintptr_t)q.dy % 16 == 0);
+  if (q.xt_x) {
+    if (!q.xt_dz || !q.xt_slab || q.xt_K0 <= 0 || q.xt_K0 % 16 || q.xt_N1 <= 0 || q.xt_N1 % 16 ||
+        q.xt_ldx < q.xt_K0 || q.xt_lddz < q.xt_N1)
+      return RS_ERR_ARG;
+    a.xt_x = q.xt_x; a.xt_dz = q.xt_dz; a.xt_ldx = q.xt_ldx; a.xt_lddz = q.xt_lddz;
+    a.xt_K0 = q.xt_K0; a.xt_N1 = q.xt_N1; a.xt_nsplit = xt_splits(q.B); a.xt_slab = q.xt_slab;
+  }
   // x / xsave rows are copied 16 B at a time
   if ((uintptr_t)q.x % 16 || (q.xsave && (uintptr_t)q.xsave % 16)) return RS_ERR_ARG;
 #ifndef RS_IL_BWD_NO_V3
@@ -2590,6 +2661,8 @@ int bwd_launch(const BwdReq& q) {
       return rs_status_after_launch();
     }
   }
+  // the deferred weight gradient rides on the wide / v4 kernels only
+  if (q.xt_x) return RS_ERR_UNSUPPORTED;
   {  // v3 (one wave per sample, no workgroup barriers) when its LDS gives 2 blocks per CU
     const size_t lds3 = bwd3_lds_bytes<C>(q.F);
     if (a.dy_vec && lds3 <= kLdsBytes / 2 && (size_t)C::NPARAM * 4 <= lds3) {

@@ -377,6 +377,8 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
     glds_copy(SB, s_src(b0, a.L - 1), ns4);
     glds_copy(DY, dy + b0 * dy_ld, ny4);
   }
+  // the deferred weight-gradient jobs, while the first sample's operands stream in
+  xt_wave_jobs(a, (int64_t)blockIdx.x * 4 + w, (int64_t)gridDim.x * 4);
   IL_STAMP_DECL
   for (int64_t b = b0; b < a.B; b += bstep) {
     for (int it = a.L - 1; it >= 0; --it) {

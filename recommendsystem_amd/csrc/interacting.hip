@@ -172,12 +172,24 @@ static int bwd_small(const rs_il::BwdReq& q) {
   return r;
 }
 
+// the deferred weight gradient a backward launch carries (rs_il_bwd_saved_xt /
+// rs_il_bwd_push_saved_xt)
+struct XtArgs {
+  const float* x; int64_t ldx; const float* dz; int64_t lddz; int K0, N1; float* slab;
+};
+static void set_xt(rs_il::BwdReq& q, const XtArgs* xt) {
+  if (!xt) return;
+  q.xt_x = xt->x; q.xt_ldx = xt->ldx; q.xt_dz = xt->dz; q.xt_lddz = xt->lddz;
+  q.xt_K0 = xt->K0; q.xt_N1 = xt->N1; q.xt_slab = xt->slab;
+}
+
 static int il_bwd_impl(void* stream, const float* x, const float* xsave, const float* dy,
                        int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
                        const float* W, const float* bias, const float* gamma, const float* beta,
                        float eps, int use_res, float drop_rate, uint64_t seed, float* dx,
                        int dx_accumulate, float* dparams, int dparams_accumulate,
-                       float* workspace, int64_t workspace_floats, const float* asave) {
+                       float* workspace, int64_t workspace_floats, const float* asave,
+                       const XtArgs* xt = nullptr) {
   if (!x || !dy || !W || !bias || !gamma || !beta || !dx || !workspace) return RS_ERR_ARG;
   if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
     return RS_ERR_ARG;
@@ -187,7 +199,8 @@ static int il_bwd_impl(void* stream, const float* x, const float* xsave, const f
                   workspace, workspace_floats};
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
-  if (F > 64) return rs_il::il_large_bwd(q);
+  set_xt(q, xt);
+  if (F > 64) return xt ? RS_ERR_UNSUPPORTED : rs_il::il_large_bwd(q);
   return bwd_small(q);
 }
 
@@ -224,7 +237,7 @@ static int il_bwd_push_impl(void* stream, const float* x, const float* xsave, co
                             uint64_t seed, const float* dx_base, const int32_t* rows,
                             float* grad_table, int32_t* flag, float* dparams,
                             int dparams_accumulate, float* workspace, int64_t workspace_floats,
-                            const float* asave) {
+                            const float* asave, const XtArgs* xt = nullptr) {
   if (!x || !dy || !W || !bias || !gamma || !beta || !rows || !grad_table || !flag || !workspace)
     return RS_ERR_ARG;
   if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
@@ -239,6 +252,7 @@ static int il_bwd_push_impl(void* stream, const float* x, const float* xsave, co
   q.push_flag = flag;
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
+  set_xt(q, xt);
   return bwd_small(q);
 }
 
@@ -269,6 +283,51 @@ RS_API int rs_il_bwd_push_saved(void* stream, const float* x, const float* xsave
                           eps, use_res, drop_rate, seed, dx_base, rows, grad_table, flag, dparams,
                           dparams_accumulate, workspace, workspace_floats,
                           need > 0 ? asave : nullptr);
+}
+
+RS_API int rs_il_xt_splits(int64_t B) { return rs_il::xt_splits(B); }
+
+static bool xt_ok(const XtArgs& t) {
+  return t.x && t.dz && t.slab && t.K0 > 0 && t.K0 % 16 == 0 && t.N1 > 0 && t.N1 % 16 == 0 &&
+         t.ldx >= t.K0 && t.lddz >= t.N1;
+}
+
+RS_API int rs_il_bwd_saved_xt(void* stream, const float* x, const float* xsave, const float* dy,
+                              int64_t dy_ld, int64_t B, int F, int E, int U, int H, int L,
+                              const float* W, const float* bias, const float* gamma,
+                              const float* beta, float eps, int use_res, float drop_rate,
+                              uint64_t seed, float* dx, int dx_accumulate, float* dparams,
+                              int dparams_accumulate, float* workspace, int64_t workspace_floats,
+                              const float* asave, int64_t asave_floats, const float* xt_x,
+                              int64_t xt_ldx, const float* xt_dz, int64_t xt_lddz, int xt_K0,
+                              int xt_N1, float* xt_slab) {
+  const XtArgs xt{xt_x, xt_ldx, xt_dz, xt_lddz, xt_K0, xt_N1, xt_slab};
+  if (!xt_ok(xt)) return RS_ERR_ARG;
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need <= 0 || !asave || asave_floats < need) return need <= 0 ? RS_ERR_UNSUPPORTED : RS_ERR_ARG;
+  return il_bwd_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta, eps,
+                     use_res, drop_rate, seed, dx, dx_accumulate, dparams, dparams_accumulate,
+                     workspace, workspace_floats, asave, &xt);
+}
+
+RS_API int rs_il_bwd_push_saved_xt(void* stream, const float* x, const float* xsave,
+                                   const float* dy, int64_t dy_ld, int64_t B, int F, int E, int U,
+                                   int H, int L, const float* W, const float* bias,
+                                   const float* gamma, const float* beta, float eps, int use_res,
+                                   float drop_rate, uint64_t seed, const float* dx_base,
+                                   const int32_t* rows, float* grad_table, int32_t* flag,
+                                   float* dparams, int dparams_accumulate, float* workspace,
+                                   int64_t workspace_floats, const float* asave,
+                                   int64_t asave_floats, const float* xt_x, int64_t xt_ldx,
+                                   const float* xt_dz, int64_t xt_lddz, int xt_K0, int xt_N1,
+                                   float* xt_slab) {
+  const XtArgs xt{xt_x, xt_ldx, xt_dz, xt_lddz, xt_K0, xt_N1, xt_slab};
+  if (!xt_ok(xt)) return RS_ERR_ARG;
+  const int64_t need = rs_il_attn_save_floats(B, F, U, H, L);
+  if (need <= 0 || !asave || asave_floats < need) return need <= 0 ? RS_ERR_UNSUPPORTED : RS_ERR_ARG;
+  return il_bwd_push_impl(stream, x, xsave, dy, dy_ld, B, F, E, U, H, L, W, bias, gamma, beta,
+                          eps, use_res, drop_rate, seed, dx_base, rows, grad_table, flag, dparams,
+                          dparams_accumulate, workspace, workspace_floats, asave, &xt);
 }
 
 static int il_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t workspace_floats,
@@ -303,4 +362,22 @@ RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,
 RS_API int rs_il_bwd_saved_partial_blocks(int64_t B, int F, int E, int U, int H,
                                           int64_t workspace_floats) {
   return il_partial_blocks(B, F, E, U, H, workspace_floats, true);
+}
+
+// whether the saved backward of this shape can carry a deferred weight gradient
+// (rs_il_bwd_saved_xt / rs_il_bwd_push_saved_xt): its grid, or 0
+RS_API int rs_il_bwd_xt_supported(int64_t B, int F, int E, int U, int H, int64_t workspace_floats) {
+  if (F > 64 || rs_il_attn_save_floats(B < 1 ? 1 : B, F, U, H, 1) <= 0) return 0;
+  static const float kDummy[16] __attribute__((aligned(16))) = {};
+  int grid = 0;
+  rs_il::BwdReq q{nullptr, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy, kDummy,
+                  (int64_t)F * U, B, F, E, U, H, 1, 1, 1e-14f, 0.f, 0, nullptr, 0, nullptr, 0,
+                  nullptr, workspace_floats};
+  q.grid_out = &grid;
+  q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
+  q.asave = kDummy;
+  q.xt_x = kDummy; q.xt_dz = kDummy; q.xt_ldx = 16; q.xt_lddz = 16; q.xt_K0 = 16; q.xt_N1 = 16;
+  q.xt_slab = const_cast<float*>(kDummy);
+  if (bwd_small(q) != RS_OK) return 0;
+  return grid;
 }
