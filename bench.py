@@ -552,8 +552,9 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
                    "global_batch": B * world, "per_gpu_batch": B, "fields": F, "emb_dim": E,
                    "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "rs_il::bwd4_kernel (InteractingLayer backward over the "
-                               "forward's attention save + fused sparse push)",
+        "roofline": {"bound": "mfma", "kernel": ("rs_il::bwd4_kernel" if B > 1536 else "rs_il::wbwd_kernel")
+                     + " (InteractingLayer backward over the forward's attention save + fused sparse "
+                       "push; the step's launch also carries the head's deferred dW1, not counted here)",
                      "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

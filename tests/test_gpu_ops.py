@@ -102,3 +102,41 @@ def test_compile_aot_eager_traces_the_ops():
     xr = x.clone().requires_grad_(True)
     cf(xr).sum().backward()
     assert xr.grad is not None and torch.isfinite(xr.grad).all()
+
+
+@pytest.mark.parametrize("M,K,N,act,acc", [
+    (2048, 64, 32, 1, 0),     # 4 tiles -> split-K, reduced inside the GEMM launch
+    (2048, 200, 48, 2, 1),    # ragged tiles, sigmoid Z operand, accumulate
+    (4099, 96, 64, 0, 0),     # ragged M (the last split short)
+    (300, 512, 256, 1, 0),    # short M: three splits
+])
+def test_dense_bwd_weight_split_k(M, K, N, act, acc):
+    """rs_dense_bwd_weight: dW = X^T dZ, db = colsum dZ (dZ = dY * act'(Y)) against float64, for
+    shapes whose plan splits the reduction (the last split of each tile sums the partials in split
+    order inside the launch); two launches are bitwise equal."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    X = torch.rand(M, K, device="cuda", generator=g) - 0.5
+    dY = torch.rand(M, N, device="cuda", generator=g) - 0.5
+    Y = torch.rand(M, N, device="cuda", generator=g) - 0.3   # relu mask ~30 % off
+    if act == 2:
+        Y = torch.rand(M, N, device="cuda", generator=g)
+    lib = _lib.load()
+    ws_n = int(lib.rs_dense_bwd_weight_workspace_floats(M, K, N))
+    outs = []
+    for _ in range(2):
+        ws = torch.full((max(ws_n, 1),), float("nan"), device="cuda")
+        dW = torch.full((K, N), 0.25, device="cuda")
+        db = torch.full((N,), 0.5, device="cuda")
+        call("rs_dense_bwd_weight", stream_handle(), ptr(X), K, ptr(dY), N, ptr(Y), N, act, M, K,
+             N, ptr(dW), ptr(db), acc, ptr(ws), ws_n)
+        torch.cuda.synchronize()
+        outs.append((dW.clone(), db.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    Yd, dYd = Y.double(), dY.double()
+    dZ = dYd * (Yd > 0) if act == 1 else dYd * Yd * (1 - Yd) if act == 2 else dYd
+    rW = X.double().T @ dZ + (0.25 if acc else 0.0)
+    rb = dZ.sum(0) + (0.5 if acc else 0.0)
+    assert_close(to_np(outs[0][0]), rW.cpu().numpy(), 1e-4, 1e-5, what="dW")
+    assert_close(to_np(outs[0][1]), rb.cpu().numpy(), 1e-4, 1e-5, what="db")
