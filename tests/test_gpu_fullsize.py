@@ -33,9 +33,11 @@ def _zipf(rng, shape, vocab, a=1.2):
     return np.minimum(rng.zipf(a, size=shape) - 1, vocab - 1).astype(np.int64)
 
 
-def test_bench_step_matches_oracle_full_size():
+@pytest.mark.parametrize("B", [4096, 512, 1000])
+def test_bench_step_matches_oracle_full_size(B):
+    """B = 4096: the one-wave IL backward (bwd4); B = 512 / 1000 (per-GPU batches of the
+    strong-scaling series): the wide IL kernels (il_wide.hpp) under the same trainer."""
     from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
-    B = 4096
     cfg = AutoIntConfig()
     model = AutoInt(cfg, device=DEV, seed=0, max_batch=B)
     trainer = AutoIntTrainer(model, B)
