@@ -571,6 +571,19 @@ int rs_partials_reduce_adam(void* stream, int nseg, const float* const* parts,
  * table / m / v / grad_table / flag, lr / betas / eps / grad_scale) run by extra blocks of the
  * SAME launch: the dense reduction + Adam and the sparse flag sweep are independent, so they
  * share the chip instead of running back to back (the AutoInt step's optimizer tail). */
+/* rs_partials_reduce_adam_scan whose sparse part walks the step's looked-up rows (rows[0 .. nlist),
+ * -1 = none) instead of sweeping flag[]: each marked row is updated once (its flag released by an
+ * atomic exchange).  Valid only when those rows are the only rows marked -- the single-GPU AutoInt
+ * step, whose own push marks exactly them; dim / 4 a power of two, dim <= 256. */
+int rs_partials_reduce_adam_rows(void* stream, int nseg, const float* const* parts,
+                                 const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
+                                 float* const* outs, const float* scales, const int64_t* adam_offs,
+                                 float* params, float* m, float* v, int64_t* step, int32_t* done,
+                                 float lr, float beta1, float beta2, float eps, float grad_scale,
+                                 int adam, float* table, float* tm, float* tv, float* grad_table,
+                                 int32_t* flag, int64_t table_rows, int dim, float slr,
+                                 float sbeta1, float sbeta2, float seps, float sgrad_scale,
+                                 const int32_t* rows, int64_t nlist);
 int rs_partials_reduce_adam_scan(void* stream, int nseg, const float* const* parts,
                                  const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
                                  float* const* outs, const float* scales, const int64_t* adam_offs,

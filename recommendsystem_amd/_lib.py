@@ -145,6 +145,10 @@ SIGNATURES: dict[str, tuple] = {
     "rs_mlp_head_train_dz": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _i32,
                                     _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32,
                                     _f32, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp, _i64]),
+    "rs_partials_reduce_adam_rows": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32,
+                                            _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
+                                            _f32, _f32, _vp, _i64]),
     "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
     "rs_partials_reduce_adam_scan": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -278,11 +282,13 @@ def c_array(ctype, values):
 
 def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=None, done=None,
                          lr=0.0, beta1=0.9, beta2=0.999, eps=1e-8, grad_scale=1.0,
-                         adam=False, scan_table=None, scan_grad_scale=1.0) -> int:
+                         adam=False, scan_table=None, scan_grad_scale=1.0, scan_rows=None) -> int:
     """rs_partials_reduce_adam over a list of segments
     (part_ptr, ld, nrows, ncols, out_ptr, scale, adam_off); with ``scan_table`` (a scan-mode
     SparseTable with a SparseAdam optimizer) its sparse Adam runs in the same launch
-    (rs_partials_reduce_adam_scan)."""
+    (rs_partials_reduce_adam_scan); with ``scan_rows`` = (rows, n) too, it walks those n looked-up
+    rows instead of sweeping the flags (rs_partials_reduce_adam_rows: valid when they are the only
+    rows marked)."""
     n = len(segments)
     keep = []
 
@@ -298,6 +304,13 @@ def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=Non
     outs = arr(ctypes.c_void_p, [s[4] for s in segments])
     scales = arr(ctypes.c_float, [s[5] for s in segments])
     offs = arr(ctypes.c_int64, [s[6] for s in segments])
+    if scan_table is not None and scan_rows is not None:
+        t, o = scan_table, scan_table.optimizer
+        return call("rs_partials_reduce_adam_rows", stream, n, parts, lds, nrows, ncols, outs,
+                    scales, offs, ptr(params), ptr(m), ptr(v), ptr(step), ptr(done), lr, beta1,
+                    beta2, eps, grad_scale, int(adam), ptr(t.weight), ptr(t.m), ptr(t.v),
+                    ptr(t.grad), ptr(t.flag), t.rows, t.dim, o.learning_rate, o.beta1, o.beta2,
+                    o.epsilon, scan_grad_scale, ptr(scan_rows[0]), int(scan_rows[1]))
     if scan_table is not None:
         t, o = scan_table, scan_table.optimizer
         return call("rs_partials_reduce_adam_scan", stream, n, parts, lds, nrows, ncols, outs,

@@ -121,6 +121,11 @@ def cross_entropy(y_true: torch.Tensor, y_pred: torch.Tensor, a: float = 1.0) ->
     return torch.mean(torch.sum(loss, dim=1), dim=0)
 
 
+# the largest B x F for which the single-GPU step's sparse Adam walks the looked-up rows instead of
+# sweeping the flag array (rows mode; measured in profiles/r04/rows_mode/)
+ROWS_MODE_MAXN = 26 * 2048
+
+
 class AutoIntTrainer:
     """Fused AutoInt train step over fixed-shape batches (ids int64 [B, F], labels fp32 [B, T]).
 
@@ -375,7 +380,7 @@ class AutoIntTrainer:
               and not getattr(table, "deterministic", False) and hasattr(table, "m"))
         return table if ok else None
 
-    def _reduce_dense(self, adam: bool, scan_table=None):
+    def _reduce_dense(self, adam: bool, scan_table=None, scan_rows=None):
         """Sum the IL and head partials (fixed order) into the arena gradient and the loss; with
         adam, apply the dense Adam in the same launch (and, with scan_table, its sparse Adam)."""
         m, hd, cfg = self.model, self.head, self.model.cfg
@@ -397,7 +402,8 @@ class AutoIntTrainer:
                             hd["off"]))
         _lib.partials_reduce_adam(stream_handle(), segs, ar.data, self.adam_m, self.adam_v,
                                   self.step_count, hd["done"], cfg.lr_dense, 0.9, 0.999, 1e-8,
-                                  1.0 / self.world, adam, scan_table=scan_table)
+                                  1.0 / self.world, adam, scan_table=scan_table,
+                                  scan_rows=scan_rows)
 
     def _forward_backward(self):
         # math mode of the step; dropout seeds offset by the device step counter (fresh masks on
@@ -522,7 +528,14 @@ class AutoIntTrainer:
             # partials -> grads -> Adam, one launch; a scan-mode table's sparse Adam runs in the
             # same launch on blocks of its own
             tail = self._scan_tail(m.table)
-            self._reduce_dense(adam=True, scan_table=tail)
+            # small batches: the sparse Adam walks the step's B x F looked-up rows (the only rows
+            # its push marked) instead of sweeping the 2.6 M flags (rs_partials_reduce_adam_rows);
+            # RS_SPARSE_ROWS_MAXN sets the largest B x F that does
+            import os
+            rows_max = int(os.environ.get("RS_SPARSE_ROWS_MAXN", str(ROWS_MODE_MAXN)))
+            rows = (self.rows, self.B * self.F) if (tail is not None and
+                                                    self.B * self.F <= rows_max) else None
+            self._reduce_dense(adam=True, scan_table=tail, scan_rows=rows)
             if tail is None:
                 m.table.step(grad_scale=1.0)
             return

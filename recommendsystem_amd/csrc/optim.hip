@@ -675,7 +675,41 @@ struct RedArgs {
   int64_t st_rows;
   int st_dim;
   float st_lr, st_b1, st_b2, st_eps, st_gscale;
+  // rows mode (rs_partials_reduce_adam_rows): the step's looked-up rows instead of the flag sweep
+  const int32_t* st_list;
+  int64_t st_nlist;
 };
+
+// Rows mode of the fused sparse Adam: the marked rows are exactly the rows the step looked up
+// (single-GPU AutoInt step: only its own push marks the table), so instead of sweeping the 2.6 M
+// flags the tail walks the B x F looked-up rows.  One dim/4-lane group per position: its leader
+// releases the flag with an atomic exchange and the group that took the -2 updates the row (each
+// marked row exactly once, whatever its multiplicity); positions of already-released rows and
+// out-of-range ids (-1) do nothing.
+__device__ __forceinline__ void rows_opt_block(const RedArgs& a, int vb, int nblk) {
+  const int nv = a.st_dim >> 2;
+  const int lpr = nv < 64 ? nv : 64;  // lanes per position (a power of two: dim / 4)
+  const int per_block = 1024 / lpr;
+  const int sub = (int)threadIdx.x % lpr;
+  const int lead = ((int)threadIdx.x & 63) - sub;
+  for (int64_t i = (int64_t)vb * per_block + threadIdx.x / lpr; i - (threadIdx.x / lpr) < a.st_nlist;
+       i += (int64_t)nblk * per_block) {
+    const bool in = i < a.st_nlist;
+    const int32_t r = in ? a.st_list[i] : -1;
+    int own = 0;
+    if (sub == 0 && r >= 0 && r < a.st_rows) own = atomicExch(a.st_flag + r, -1) == -2;
+    own = __shfl(own, lead, 64);
+    if (own) {
+      for (int e4 = sub; e4 < nv; e4 += lpr) {
+        ScanRow<true> x;
+        const int64_t o = (int64_t)r * a.st_dim + 4 * e4;
+        x.load(a.st_table, a.st_m, a.st_v, a.st_grad, o);
+        x.update_store(a.st_table, a.st_m, a.st_v, a.st_grad, o, a.st_lr, a.st_b1, a.st_b2,
+                       a.st_eps, a.st_gscale);
+      }
+    }
+  }
+}
 
 // Block shape per segment (host-chosen): G row groups x (1024 / G) columns, G the smallest power
 // of two with <= 16 rows per thread (IL partials: 1024 rows -> 64 groups x 16 columns over 70
@@ -687,6 +721,10 @@ __global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
   const bool is_scan = a.scan_first ? (int)blockIdx.x < a.nblk_scan : (int)blockIdx.x >= a.nblk_red;
   const int vb = a.scan_first ? (is_scan ? (int)blockIdx.x : (int)blockIdx.x - a.nblk_scan)
                               : (is_scan ? (int)blockIdx.x - a.nblk_red : (int)blockIdx.x);
+  if (is_scan && a.st_list) {  // rows mode
+    rows_opt_block(a, vb, a.nblk_scan);
+    return;
+  }
   if (is_scan) {  // the fused sparse sweep (independent of the dense part)
     __shared__ uint32_t lists[16 * kScanLcap];
     const int64_t nwaves = (int64_t)a.nblk_scan * 16;
@@ -795,6 +833,7 @@ static int reduce_adam_impl(void* stream, int nseg, const float* const* parts,
     a.st_grad = tail->st_grad; a.st_flag = tail->st_flag; a.st_rows = tail->st_rows;
     a.st_dim = tail->st_dim; a.st_lr = tail->st_lr; a.st_b1 = tail->st_b1; a.st_b2 = tail->st_b2;
     a.st_eps = tail->st_eps; a.st_gscale = tail->st_gscale;
+    a.st_list = tail->st_list; a.st_nlist = tail->st_nlist;
   }
   const int64_t total = nblk + (tail ? tail_blocks : 0);
   if (total == 0) return RS_OK;
@@ -810,6 +849,28 @@ RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* p
                                    float beta2, float eps, float grad_scale, int adam) {
   return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
                           m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, nullptr, 0);
+}
+
+RS_API int rs_partials_reduce_adam_rows(
+    void* stream, int nseg, const float* const* parts, const int64_t* lds, const int32_t* nrows,
+    const int64_t* ncols, float* const* outs, const float* scales, const int64_t* adam_offs,
+    float* params, float* m, float* v, int64_t* step, int32_t* done, float lr, float beta1,
+    float beta2, float eps, float grad_scale, int adam, float* table, float* tm, float* tv,
+    float* grad_table, int32_t* flag, int64_t table_rows, int dim, float slr, float sbeta1,
+    float sbeta2, float seps, float sgrad_scale, const int32_t* rows, int64_t nlist) {
+  if (!table || !tm || !tv || !grad_table || !flag || !rows || dim <= 0 || dim % 4 ||
+      (dim / 4) & (dim / 4 - 1) || dim > 256 || table_rows < 0 || nlist < 0)
+    return RS_ERR_ARG;
+  RedArgs t{};
+  t.st_table = table; t.st_m = tm; t.st_v = tv; t.st_grad = grad_table; t.st_flag = flag;
+  t.st_rows = table_rows; t.st_dim = dim; t.st_lr = slr; t.st_b1 = sbeta1; t.st_b2 = sbeta2;
+  t.st_eps = seps; t.st_gscale = sgrad_scale; t.st_list = rows; t.st_nlist = nlist;
+  const int64_t per_block = 1024 / (dim / 4 < 64 ? dim / 4 : 64);
+  int64_t blocks = (nlist + per_block - 1) / per_block;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
+                          m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, &t, blocks);
 }
 
 RS_API int rs_partials_reduce_adam_scan(
