@@ -122,8 +122,10 @@ def cross_entropy(y_true: torch.Tensor, y_pred: torch.Tensor, a: float = 1.0) ->
 
 
 # the largest B x F for which the single-GPU step's sparse Adam walks the looked-up rows instead of
-# sweeping the flag array (rows mode; measured in profiles/r04/rows_mode/)
-ROWS_MODE_MAXN = 26 * 2048
+# sweeping the flag array (rows mode).  Same box, 200 steps (profiles/r04/final/rows_mode/): B = 512
+# 0.0580 -> 0.0537 ms, 1024 0.0717 -> 0.0714, 2048 0.0972 -> 0.1041 (worse: the Zipf-hot rows'
+# flag exchanges serialise), 4096 0.1523 -> 0.1689
+ROWS_MODE_MAXN = 26 * 1024
 
 
 class AutoIntTrainer:

@@ -21,3 +21,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/step_traffic.py $D $D/step_traffic.json | tail -30
 python3 tools/traffic_json.py $D $D/il_bwd_traffic.json | cut -c1-300
+BATCHES="2048" OUT=$D/small_batch_2048 bash tools/small_batch.sh
