@@ -584,6 +584,21 @@ int rs_partials_reduce_adam_rows(void* stream, int nseg, const float* const* par
                                  int32_t* flag, int64_t table_rows, int dim, float slr,
                                  float sbeta1, float sbeta2, float seps, float sgrad_scale,
                                  const int32_t* rows, int64_t nlist);
+/* rs_partials_reduce_adam_rows over strided entries rows[i * list_stride] (i < nlist) of which,
+ * when counts != NULL, segment s = i / seg_len holds counts[s * counts_stride] valid entries (the
+ * packed DP records after the all-gather: rank r's [row | grad] records at r * cap, its count in
+ * the gathered dense bucket) -- the marked rows of a data-parallel step are exactly those. */
+int rs_partials_reduce_adam_rows_ex(void* stream, int nseg, const float* const* parts,
+                                    const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
+                                    float* const* outs, const float* scales,
+                                    const int64_t* adam_offs, float* params, float* m, float* v,
+                                    int64_t* step, int32_t* done, float lr, float beta1,
+                                    float beta2, float eps, float grad_scale, int adam,
+                                    float* table, float* tm, float* tv, float* grad_table,
+                                    int32_t* flag, int64_t table_rows, int dim, float slr,
+                                    float sbeta1, float sbeta2, float seps, float sgrad_scale,
+                                    const int32_t* rows, int64_t nlist, int64_t list_stride,
+                                    const int32_t* counts, int64_t counts_stride, int64_t seg_len);
 int rs_partials_reduce_adam_scan(void* stream, int nseg, const float* const* parts,
                                  const int64_t* lds, const int32_t* nrows, const int64_t* ncols,
                                  float* const* outs, const float* scales, const int64_t* adam_offs,

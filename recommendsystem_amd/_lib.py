@@ -149,6 +149,11 @@ SIGNATURES: dict[str, tuple] = {
                                             _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32,
                                             _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32,
                                             _f32, _f32, _vp, _i64]),
+    "rs_partials_reduce_adam_rows_ex": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                               _vp, _vp, _vp, _vp, _f32, _f32, _f32, _f32, _f32,
+                                               _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32,
+                                               _f32, _f32, _f32, _f32, _vp, _i64, _i64, _vp, _i64,
+                                               _i64]),
     "rs_partials_reduce_adam": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _f32, _f32, _f32, _f32, _f32, _i32]),
     "rs_partials_reduce_adam_scan": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -288,7 +293,9 @@ def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=Non
     SparseTable with a SparseAdam optimizer) its sparse Adam runs in the same launch
     (rs_partials_reduce_adam_scan); with ``scan_rows`` = (rows, n) too, it walks those n looked-up
     rows instead of sweeping the flags (rs_partials_reduce_adam_rows: valid when they are the only
-    rows marked)."""
+    rows marked); ``scan_rows`` = (rows_ptr, n, stride, counts_ptr, counts_stride, seg_len) walks
+    strided entries of which each seg_len-long segment holds counts[seg] valid ones (the packed DP
+    records after the exchange, rs_partials_reduce_adam_rows_ex)."""
     n = len(segments)
     keep = []
 
@@ -306,11 +313,15 @@ def partials_reduce_adam(stream, segments, params=None, m=None, v=None, step=Non
     offs = arr(ctypes.c_int64, [s[6] for s in segments])
     if scan_table is not None and scan_rows is not None:
         t, o = scan_table, scan_table.optimizer
-        return call("rs_partials_reduce_adam_rows", stream, n, parts, lds, nrows, ncols, outs,
+        rows, nr, *packed = scan_rows
+        stride, cptr, cstride, seg = packed if packed else (1, None, 0, 0)
+        return call("rs_partials_reduce_adam_rows_ex", stream, n, parts, lds, nrows, ncols, outs,
                     scales, offs, ptr(params), ptr(m), ptr(v), ptr(step), ptr(done), lr, beta1,
                     beta2, eps, grad_scale, int(adam), ptr(t.weight), ptr(t.m), ptr(t.v),
                     ptr(t.grad), ptr(t.flag), t.rows, t.dim, o.learning_rate, o.beta1, o.beta2,
-                    o.epsilon, scan_grad_scale, ptr(scan_rows[0]), int(scan_rows[1]))
+                    o.epsilon, scan_grad_scale,
+                    rows if isinstance(rows, int) else ptr(rows), int(nr), int(stride), cptr,
+                    int(cstride), int(seg))
     if scan_table is not None:
         t, o = scan_table, scan_table.optimizer
         return call("rs_partials_reduce_adam_scan", stream, n, parts, lds, nrows, ncols, outs,

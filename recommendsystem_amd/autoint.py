@@ -551,11 +551,19 @@ class AutoIntTrainer:
                      self.dp_cap, self.dp_cap if self.dp_sync_free else 0)
             # dense: rank-ordered sum of the gathered buckets -> arena grad -> Adam, one launch
             tail = self._scan_tail(t)
+            # small per-rank batches: walk the gathered records (the rows the merges marked, at
+            # most world x B_local x F) instead of sweeping the flags (rows mode, as at world 1)
+            import os
+            rows_max = int(os.environ.get("RS_SPARSE_ROWS_MAXN", str(ROWS_MODE_MAXN)))
+            rows = None
+            if tail is not None and self.dp_sync_free and self.B * self.F <= rows_max:
+                rows = (self.dp_recs_all.data_ptr(), self.world * self.dp_cap, self.dp_rs,
+                        counts, self.dp_ld, self.dp_cap)
             _lib.partials_reduce_adam(s, [(ptr(self.dp_recv), self.dp_ld, self.world, self.dp_n,
                                            ptr(ar.grad), 1.0, 0)], ar.data, self.adam_m,
                                       self.adam_v, self.step_count, self.head["done"],
                                       cfg.lr_dense, 0.9, 0.999, 1e-8, scale, True,
-                                      scan_table=tail, scan_grad_scale=scale)
+                                      scan_table=tail, scan_grad_scale=scale, scan_rows=rows)
             if tail is None:
                 t.step(grad_scale=scale)
             return

@@ -678,6 +678,9 @@ struct RedArgs {
   // rows mode (rs_partials_reduce_adam_rows): the step's looked-up rows instead of the flag sweep
   const int32_t* st_list;
   int64_t st_nlist;
+  int64_t st_list_stride;      // int32 words between entries (packed DP records: dim + 1)
+  const int32_t* st_counts;    // per-segment valid counts (packed DP: one segment per rank), or null
+  int64_t st_counts_stride, st_seg_len;
 };
 
 // Rows mode of the fused sparse Adam: the marked rows are exactly the rows the step looked up
@@ -694,8 +697,12 @@ __device__ __forceinline__ void rows_opt_block(const RedArgs& a, int vb, int nbl
   const int lead = ((int)threadIdx.x & 63) - sub;
   for (int64_t i = (int64_t)vb * per_block + threadIdx.x / lpr; i - (threadIdx.x / lpr) < a.st_nlist;
        i += (int64_t)nblk * per_block) {
-    const bool in = i < a.st_nlist;
-    const int32_t r = in ? a.st_list[i] : -1;
+    bool in = i < a.st_nlist;
+    if (in && a.st_counts) {  // packed DP records: rank segment i / seg_len holds counts[seg] valid
+      const int64_t seg = i / a.st_seg_len;
+      in = (i - seg * a.st_seg_len) < (int64_t)a.st_counts[seg * a.st_counts_stride];
+    }
+    const int32_t r = in ? a.st_list[i * a.st_list_stride] : -1;
     int own = 0;
     if (sub == 0 && r >= 0 && r < a.st_rows) own = atomicExch(a.st_flag + r, -1) == -2;
     own = __shfl(own, lead, 64);
@@ -833,7 +840,9 @@ static int reduce_adam_impl(void* stream, int nseg, const float* const* parts,
     a.st_grad = tail->st_grad; a.st_flag = tail->st_flag; a.st_rows = tail->st_rows;
     a.st_dim = tail->st_dim; a.st_lr = tail->st_lr; a.st_b1 = tail->st_b1; a.st_b2 = tail->st_b2;
     a.st_eps = tail->st_eps; a.st_gscale = tail->st_gscale;
-    a.st_list = tail->st_list; a.st_nlist = tail->st_nlist;
+    a.st_list = tail->st_list; a.st_nlist = tail->st_nlist; a.st_list_stride = tail->st_list_stride;
+    a.st_counts = tail->st_counts; a.st_counts_stride = tail->st_counts_stride;
+    a.st_seg_len = tail->st_seg_len;
   }
   const int64_t total = nblk + (tail ? tail_blocks : 0);
   if (total == 0) return RS_OK;
@@ -851,6 +860,15 @@ RS_API int rs_partials_reduce_adam(void* stream, int nseg, const float* const* p
                           m, v, step, done, lr, beta1, beta2, eps, grad_scale, adam, nullptr, 0);
 }
 
+RS_API int rs_partials_reduce_adam_rows_ex(
+    void* stream, int nseg, const float* const* parts, const int64_t* lds, const int32_t* nrows,
+    const int64_t* ncols, float* const* outs, const float* scales, const int64_t* adam_offs,
+    float* params, float* m, float* v, int64_t* step, int32_t* done, float lr, float beta1,
+    float beta2, float eps, float grad_scale, int adam, float* table, float* tm, float* tv,
+    float* grad_table, int32_t* flag, int64_t table_rows, int dim, float slr, float sbeta1,
+    float sbeta2, float seps, float sgrad_scale, const int32_t* rows, int64_t nlist,
+    int64_t list_stride, const int32_t* counts, int64_t counts_stride, int64_t seg_len);
+
 RS_API int rs_partials_reduce_adam_rows(
     void* stream, int nseg, const float* const* parts, const int64_t* lds, const int32_t* nrows,
     const int64_t* ncols, float* const* outs, const float* scales, const int64_t* adam_offs,
@@ -858,13 +876,30 @@ RS_API int rs_partials_reduce_adam_rows(
     float beta2, float eps, float grad_scale, int adam, float* table, float* tm, float* tv,
     float* grad_table, int32_t* flag, int64_t table_rows, int dim, float slr, float sbeta1,
     float sbeta2, float seps, float sgrad_scale, const int32_t* rows, int64_t nlist) {
+  return rs_partials_reduce_adam_rows_ex(
+      stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params, m, v, step, done,
+      lr, beta1, beta2, eps, grad_scale, adam, table, tm, tv, grad_table, flag, table_rows, dim, slr,
+      sbeta1, sbeta2, seps, sgrad_scale, rows, nlist, 1, nullptr, 0, 0);
+}
+
+RS_API int rs_partials_reduce_adam_rows_ex(
+    void* stream, int nseg, const float* const* parts, const int64_t* lds, const int32_t* nrows,
+    const int64_t* ncols, float* const* outs, const float* scales, const int64_t* adam_offs,
+    float* params, float* m, float* v, int64_t* step, int32_t* done, float lr, float beta1,
+    float beta2, float eps, float grad_scale, int adam, float* table, float* tm, float* tv,
+    float* grad_table, int32_t* flag, int64_t table_rows, int dim, float slr, float sbeta1,
+    float sbeta2, float seps, float sgrad_scale, const int32_t* rows, int64_t nlist,
+    int64_t list_stride, const int32_t* counts, int64_t counts_stride, int64_t seg_len) {
   if (!table || !tm || !tv || !grad_table || !flag || !rows || dim <= 0 || dim % 4 ||
-      (dim / 4) & (dim / 4 - 1) || dim > 256 || table_rows < 0 || nlist < 0)
+      (dim / 4) & (dim / 4 - 1) || dim > 256 || table_rows < 0 || nlist < 0 || list_stride < 1 ||
+      (counts && (counts_stride < 1 || seg_len < 1)))
     return RS_ERR_ARG;
   RedArgs t{};
   t.st_table = table; t.st_m = tm; t.st_v = tv; t.st_grad = grad_table; t.st_flag = flag;
   t.st_rows = table_rows; t.st_dim = dim; t.st_lr = slr; t.st_b1 = sbeta1; t.st_b2 = sbeta2;
   t.st_eps = seps; t.st_gscale = sgrad_scale; t.st_list = rows; t.st_nlist = nlist;
+  t.st_list_stride = list_stride; t.st_counts = counts; t.st_counts_stride = counts_stride;
+  t.st_seg_len = counts ? seg_len : 1;
   const int64_t per_block = 1024 / (dim / 4 < 64 ? dim / 4 : 64);
   int64_t blocks = (nlist + per_block - 1) / per_block;
   if (blocks < 1) blocks = 1;
