@@ -34,6 +34,8 @@
 #pragma once
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace rs_il {
 
 struct FwdReq {
@@ -2545,6 +2547,15 @@ namespace rs_il {
 // grids: one workgroup per sample up to these, then persistent workgroups looping over samples
 // (the backward's grid is also the number of per-block partial rows)
 constexpr int kWideFwdGrid = 2048;
+// tuning runs: RS_IL_WIDE_FWD_GRID overrides the forward's persistent grid (read once)
+inline int64_t wide_fwd_grid() {
+  static const int64_t g = [] {
+    const char* e = getenv("RS_IL_WIDE_FWD_GRID");
+    const long v = e ? atol(e) : 0L;
+    return (int64_t)(v >= 64 && v <= 65536 ? v : kWideFwdGrid);
+  }();
+  return g;
+}
 constexpr int kWideBwdGrid = 1024;
 // auto: the wide forward everywhere (B = 512: 10.1 vs 19.9 us, 4096: 34.6 vs 34.1 us, same-box
 // HIP events); the wide backward up to this batch (512: 22.7 vs 31.2 us, 1024: 36 vs 40.5 us; at
@@ -2580,7 +2591,8 @@ int fwd_launch(const FwdReq& q) {
   if constexpr (kWide<C>) {
     if (rs_il_variant_now() != RS_IL_VARIANT_WAVE) {
       const size_t lds = (size_t)WideFwdLayout<C>().total * sizeof(float);
-      const int64_t grid = q.B < kWideFwdGrid ? q.B : kWideFwdGrid;
+      const int64_t gmax = wide_fwd_grid();
+      const int64_t grid = q.B < gmax ? q.B : gmax;
       if (grid == 0) return RS_OK;
       wfwd_kernel<C, DROP><<<(int)grid, kWideThreads, lds, q.stream>>>(
           q.x, q.W, q.bias, q.gamma, q.beta, q.y, q.y_ld, q.xsave, a);
