@@ -2546,7 +2546,10 @@ int rs_il_variant_now();
 namespace rs_il {
 // grids: one workgroup per sample up to these, then persistent workgroups looping over samples
 // (the backward's grid is also the number of per-block partial rows)
-constexpr int kWideFwdGrid = 2048;
+// the forward runs one workgroup per sample up to 4096 samples: ~6 resident per CU (78 VGPRs),
+// so a 2048-workgroup grid at B = 4096 left a second round of 512 workgroups with 2 samples each
+// (same box, 200 steps: 0.1542 -> 0.1508 ms per step; 1536: 0.1535; 1024: 0.1575)
+constexpr int kWideFwdGrid = 4096;
 // tuning runs: RS_IL_WIDE_FWD_GRID overrides the forward's persistent grid (read once)
 inline int64_t wide_fwd_grid() {
   static const int64_t g = [] {

@@ -77,7 +77,8 @@ def _run(variant, B, F, L, drop, push, x, prm, dy, base, rows):
 CASES = [  # (B, F, L, drop)
     (67, 26, 3, 0.0),      # config 2 (exact-F instantiation)
     (1, 26, 3, 0.0),       # one sample: one workgroup
-    (2500, 26, 3, 0.0),    # more samples than the grids (persistent loops, 3 / 2 per block)
+    (2500, 26, 3, 0.0),    # more samples than the backward's grid (persistent loop)
+    (4500, 26, 3, 0.0),    # more samples than the forward's grid too
     (40, 20, 2, 0.0),      # padded F (FMAX 32)
     (9, 31, 3, 0.1),       # dropout, padded
     (13, 4, 1, 0.0),       # fewer fields than key quarters + the dx-exchange buffer floor
