@@ -17,6 +17,7 @@
 //                fixed-order reduce (deterministic, no float atomics)
 #include "common.hpp"
 
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 
@@ -73,92 +74,153 @@ struct GemmArgs {
   float* db;          // bwd weight: column sums of B (row m-chunk z) or NULL
 };
 
-template <bool Z>
-__device__ __forceinline__ float opval(const float* p, const float* y, int64_t i, int64_t iy, int act) {
-  if (!Z) return p[i];
-  return act_bwd(p[i], y[iy], act);
-}
-
-template <bool Z>
-__device__ __forceinline__ float4 opval4(const float* p, const float* y, int64_t i, int64_t iy, int act) {
-  float4 v = *reinterpret_cast<const float4*>(p + i);
-  if (Z) {
-    const float4 yv = *reinterpret_cast<const float4*>(y + iy);
-    v.x = act_bwd(v.x, yv.x, act); v.y = act_bwd(v.y, yv.y, act);
-    v.z = act_bwd(v.z, yv.z, act); v.w = act_bwd(v.w, yv.w, act);
-  }
-  return v;
-}
-
 // Load one operand slab (tile rows [x0, x0 + BX) x reduction [r0, r0 + GBK)) into NL = BX/32
 // float4 registers per thread.  ALONG_R: contiguous along r (A row / B col layouts), else
-// contiguous along x (A col / B row).
-template <int BX, bool ALONG_R, bool Z, bool VEC>
-__device__ __forceinline__ float4 load_one(const float* p, int64_t ld, const float* y, int64_t ldy,
-                                           int act, int64_t x0, int64_t X, int64_t r0, int64_t R,
-                                           int idx) {
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  int64_t x, r;
-  if (ALONG_R) {
-    x = x0 + idx / RQ;
-    r = r0 + 4 * (idx % RQ);
-    if (x >= X) return v;
-    if (VEC && r + 3 < R) return opval4<Z>(p, y, x * ld + r, x * ldy + r, act);
-    float e[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) e[i] = (r + i < R) ? opval<Z>(p, y, x * ld + r + i, x * ldy + r + i, act) : 0.f;
-    return make_float4(e[0], e[1], e[2], e[3]);
-  } else {
-    r = r0 + idx / (BX / 4);
-    x = x0 + 4 * (idx % (BX / 4));
-    if (r >= R) return v;
-    if (VEC && x + 3 < X) return opval4<Z>(p, y, r * ld + x, r * ldy + x, act);
-    float e[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) e[i] = (x + i < X) ? opval<Z>(p, y, r * ld + x + i, r * ldy + x + i, act) : 0.f;
-    return make_float4(e[0], e[1], e[2], e[3]);
-  }
-}
-
-template <int BX>
+// contiguous along x (A col / B row).  Z operands keep dY and Y raw in registers: dZ = dY act'(Y)
+// is formed only when the slab is stored to LDS, after the MFMAs of the current slab, so no wait
+// on the prefetch lands in front of them (out-of-range elements load as dY = Y = 0 -> dZ = 0).
+template <int BX, bool Z>
 struct Slab {
   static constexpr int NL = BX * GBK / 4 / 256;  // float4 per thread
   float4 v[NL];
+  float4 y[Z ? NL : 1];
+  unsigned ok;  // VEC loads: bit u set when float4 u is in range
 };
 
 template <int BX, bool ALONG_R, bool Z, bool VEC>
-__device__ __forceinline__ void load_slab(Slab<BX>& sl, const float* p, int64_t ld, const float* y,
-                                          int64_t ldy, int act, int64_t x0, int64_t X, int64_t r0,
-                                          int64_t R, int t) {
+__device__ __forceinline__ void load_one(float4& v, float4& yv, const float* p, int64_t ld,
+                                         const float* y, int64_t ldy, int64_t x0, int64_t X,
+                                         int64_t r0, int64_t R, int idx) {
+  v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (Z) yv = v;
+  int64_t x, r, xs, rs;  // element (x, r); strides of the four consecutive elements
+  if (ALONG_R) {
+    x = x0 + idx / RQ;
+    r = r0 + 4 * (idx % RQ);
+    if (x >= X) return;
+    if (VEC && r + 3 < R) {
+      v = *reinterpret_cast<const float4*>(p + x * ld + r);
+      if (Z) yv = *reinterpret_cast<const float4*>(y + x * ldy + r);
+      return;
+    }
+    xs = 0; rs = 1;
+  } else {
+    r = r0 + idx / (BX / 4);
+    x = x0 + 4 * (idx % (BX / 4));
+    if (r >= R) return;
+    if (VEC && x + 3 < X) {
+      v = *reinterpret_cast<const float4*>(p + r * ld + x);
+      if (Z) yv = *reinterpret_cast<const float4*>(y + r * ldy + x);
+      return;
+    }
+    xs = 1; rs = 0;
+  }
+  float e[4], f[4];
 #pragma unroll
-  for (int u = 0; u < Slab<BX>::NL; ++u)
-    sl.v[u] = load_one<BX, ALONG_R, Z, VEC>(p, ld, y, ldy, act, x0, X, r0, R, t + 256 * u);
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = x + i * xs < X && r + i * rs < R;
+    e[i] = ok ? p[(x + i * xs) * (ALONG_R ? ld : 1) + (r + i * rs) * (ALONG_R ? 1 : ld)] : 0.f;
+    f[i] = (Z && ok) ? y[(x + i * xs) * (ALONG_R ? ldy : 1) + (r + i * rs) * (ALONG_R ? 1 : ldy)] : 0.f;
+  }
+  v = make_float4(e[0], e[1], e[2], e[3]);
+  if (Z) yv = make_float4(f[0], f[1], f[2], f[3]);
 }
 
-template <int BX, bool ALONG_R>
-__device__ __forceinline__ void store_slab(float* s, const Slab<BX>& sl, int t) {
+// VEC operands (16-B aligned rows, extents along the contiguous axis multiples of 4) load every
+// float4 unconditionally: an out-of-range one reads element 0 instead and is zeroed when stored
+// (bit u of Slab::ok).  Branch-free loads let the compiler wait for exactly the older slab's loads
+// before storing it; with per-lane branches it waited for every outstanding load, which
+// serialised the slab's loads and the two-slab prefetch.
+template <int BX, bool ALONG_R, bool Z, bool VEC>
+__device__ __forceinline__ void load_slab(Slab<BX, Z>& sl, const float* p, int64_t ld, const float* y,
+                                          int64_t ldy, int64_t x0, int64_t X, int64_t r0,
+                                          int64_t R, int t) {
+  if constexpr (VEC) {
+    sl.ok = 0;
 #pragma unroll
-  for (int u = 0; u < Slab<BX>::NL; ++u) {
+    for (int u = 0; u < Slab<BX, Z>::NL; ++u) {
+      const int idx = t + 256 * u;
+      int64_t x, r;
+      if (ALONG_R) { x = x0 + idx / RQ; r = r0 + 4 * (idx % RQ); }
+      else { r = r0 + idx / (BX / 4); x = x0 + 4 * (idx % (BX / 4)); }
+      const bool ok = x < X && r < R;
+      sl.ok |= ok ? 1u << u : 0u;
+      const int64_t o = ok ? (ALONG_R ? x * ld + r : r * ld + x) : 0;
+      sl.v[u] = *reinterpret_cast<const float4*>(p + o);
+      if (Z) {
+        const int64_t oy = ok ? (ALONG_R ? x * ldy + r : r * ldy + x) : 0;
+        sl.y[u] = *reinterpret_cast<const float4*>(y + oy);
+      }
+    }
+  } else {
+    sl.ok = ~0u;
+#pragma unroll
+    for (int u = 0; u < Slab<BX, Z>::NL; ++u)
+      load_one<BX, ALONG_R, Z, VEC>(sl.v[u], sl.y[Z ? u : 0], p, ld, y, ldy, x0, X, r0, R, t + 256 * u);
+  }
+}
+
+// LDS image of one operand slab.  ALONG_R operands (contiguous along the reduction in global
+// memory) keep rows of x: [x][GBK + 4], and a lane's float4 along r covers four k-steps.  The
+// others keep the global orientation, rows of r: [GBK][BX + pad] (float4 stores, no transpose:
+// a transposing scalar store into [x][r] rows hit the same few banks from every lane), and a
+// lane reads its four k-steps as four ds_read_b32 -- pad 4 (MF 16: the four lane groups' rows
+// 4 apart land 16 banks apart) or 8 (MF 32: the two half-waves' rows land 32 banks apart).
+template <int BX, int MF, bool ALONG_R>
+struct OpLay {
+  static constexpr int LDX = BX + (MF == 32 ? 8 : 4);
+  static constexpr int SIZE = ALONG_R ? BX * LDP : GBK * LDX;
+};
+
+template <int BX, int MF, bool ALONG_R, bool Z>
+__device__ __forceinline__ void store_slab(float* s, const Slab<BX, Z>& sl, int act, int t) {
+#pragma unroll
+  for (int u = 0; u < Slab<BX, Z>::NL; ++u) {
     const int idx = t + 256 * u;
-    const float4 v = sl.v[u];
+    float4 v = sl.v[u];
+    if (!((sl.ok >> u) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (Z) {
+      const float4 yv = sl.y[u];
+      v.x = act_bwd(v.x, yv.x, act); v.y = act_bwd(v.y, yv.y, act);
+      v.z = act_bwd(v.z, yv.z, act); v.w = act_bwd(v.w, yv.w, act);
+    }
     if (ALONG_R) {
       *reinterpret_cast<float4*>(s + (idx / RQ) * LDP + 4 * (idx % RQ)) = v;
     } else {
       const int ri = idx / (BX / 4), xq = idx % (BX / 4);
-      s[(4 * xq + 0) * LDP + ri] = v.x;
-      s[(4 * xq + 1) * LDP + ri] = v.y;
-      s[(4 * xq + 2) * LDP + ri] = v.z;
-      s[(4 * xq + 3) * LDP + ri] = v.w;
+      *reinterpret_cast<float4*>(s + ri * OpLay<BX, MF, false>::LDX + 4 * xq) = v;
     }
   }
 }
 
-template <int BM, int BN, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
+// the operand values at (x, kb + j), j = 0..3 (the k-steps of four consecutive MFMAs)
+template <int BX, int MF, bool ALONG_R>
+__device__ __forceinline__ float4 frag4(const float* s, int x, int kb) {
+  if (ALONG_R) return *reinterpret_cast<const float4*>(s + x * LDP + kb);
+  constexpr int LDX = OpLay<BX, MF, false>::LDX;
+  return make_float4(s[kb * LDX + x], s[(kb + 1) * LDX + x], s[(kb + 2) * LDX + x],
+                     s[(kb + 3) * LDX + x]);
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// MF = 16: 16x16 output tiles on v_mfma_f32_16x16x4_f32 (32 x 32 / 32 x 64 / 64 x 64 blocks; small
+// and medium GEMMs).  MF = 32: 32x32 tiles on v_mfma_f32_32x32x2_f32 for the large GEMMs (64 / 128
+// square-or-oblong blocks): the four waves form a 2 x 2 grid, each owning (BM/2) x (BN/2) as
+// 32x32 tiles, so per 8 k a wave reads BM/64 A and BN/64 B fragments (one ds_read_b128 each) for
+// (BM/64)(BN/64) x 4 MFMAs -- twice the flops per operand read of the 16x16 form, and a 64 x 128 /
+// 128 x 128 block moves 2-4x less L2 traffic per flop than a 32 x 64 one.  The k index inside each
+// 8-slab is permuted as in the 16x16 form (lane half h supplies k = 4h + j to MFMA j, in A and B).
+template <int BM, int BN, int MF, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
-  constexpr int TM = BM / 16, TN = BN / 16, WT = TM * TN / 4;
-  static_assert(WT >= 1, "tile too small for 4 waves");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDP];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDP];
+  static_assert(MF == 16 || MF == 32, "MFMA tile");
+  constexpr int TM = BM / MF, TN = BN / MF;
+  constexpr int WT = MF == 16 ? TM * TN / 4 : 1;            // 16x16 tiles per wave
+  constexpr int WM = MF == 32 ? BM / 64 : 1, WN = MF == 32 ? BN / 64 : 1;  // 32x32 tiles per wave
+  static_assert(MF == 16 ? WT >= 1 : (BM % 64 == 0 && BN % 64 == 0), "tile too small for 4 waves");
+  constexpr bool A_ALONG_R = ALAY == LAY_ROW, B_ALONG_R = BLAY == LAY_COL;
+  __shared__ __attribute__((aligned(16))) float As[2][OpLay<BM, MF, A_ALONG_R>::SIZE];
+  __shared__ __attribute__((aligned(16))) float Bs[2][OpLay<BN, MF, B_ALONG_R>::SIZE];
   const int t = threadIdx.x, w = t >> 6, l = t & 63;
   const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
   const int64_t rb = (int64_t)blockIdx.z * g.rchunk;
@@ -166,69 +228,117 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   const bool do_db = g.db != nullptr && blockIdx.x == 0;
   float csum = 0.f;
   f32x4 acc[WT];
+  f32x16 acc32[WM][WN];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < WT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr bool A_ALONG_R = ALAY == LAY_ROW, B_ALONG_R = BLAY == LAY_COL;
-  Slab<BM> ra;
-  Slab<BN> rbv;
-  load_slab<BM, A_ALONG_R, AZ, VEC>(ra, g.a, g.lda, g.ay, g.lday, g.act_z, m0, g.M, rb, re, t);
-  load_slab<BN, B_ALONG_R, BZ, VEC>(rbv, g.b, g.ldb, g.by, g.ldby, g.act_z, n0, g.N, rb, re, t);
-  store_slab<BM, A_ALONG_R>(As[0], ra, t);
-  store_slab<BN, B_ALONG_R>(Bs[0], rbv, t);
+    for (int i = 0; i < WT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
+  }
+  const int wr = w >> 1, wc = w & 1;  // MF = 32: the wave's quadrant
+  // one slab in flight in registers: slab s + 1 loads while slab s feeds the MFMAs
+  Slab<BM, AZ> ra;
+  Slab<BN, BZ> rbv;
+  auto load = [&](int64_t r) {
+    load_slab<BM, A_ALONG_R, AZ, VEC>(ra, g.a, g.lda, g.ay, g.lday, m0, g.M, r, re, t);
+    load_slab<BN, B_ALONG_R, BZ, VEC>(rbv, g.b, g.ldb, g.by, g.ldby, n0, g.N, r, re, t);
+  };
+  auto store = [&](int sbuf) {
+    store_slab<BM, MF, A_ALONG_R, AZ>(As[sbuf], ra, g.act_z, t);
+    store_slab<BN, MF, B_ALONG_R, BZ>(Bs[sbuf], rbv, g.act_z, t);
+  };
+  auto compute = [&](int cb) {
+    if (do_db && t < BN) {
+#pragma unroll
+      for (int k = 0; k < GBK; ++k)
+        csum += B_ALONG_R ? Bs[cb][t * LDP + k] : Bs[cb][k * OpLay<BN, MF, false>::LDX + t];
+    }
+    if constexpr (MF == 16) {
+#pragma unroll
+      for (int kg = 0; kg < GBK / 16; ++kg) {
+#pragma unroll
+        for (int i = 0; i < WT; ++i) {
+          const int q = w * WT + i, rt = q / TN, ct = q % TN;
+          const float4 af = frag4<BM, MF, A_ALONG_R>(As[cb], rt * 16 + (l & 15), kg * 16 + 4 * (l >> 4));
+          const float4 bf = frag4<BN, MF, B_ALONG_R>(Bs[cb], ct * 16 + (l & 15), kg * 16 + 4 * (l >> 4));
+          acc[i] = mfma4(af.x, bf.x, acc[i]);
+          acc[i] = mfma4(af.y, bf.y, acc[i]);
+          acc[i] = mfma4(af.z, bf.z, acc[i]);
+          acc[i] = mfma4(af.w, bf.w, acc[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kg = 0; kg < GBK / 8; ++kg) {
+        float4 af[WM], bf[WN];
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+          af[i] = frag4<BM, MF, A_ALONG_R>(As[cb], wr * (BM / 2) + i * 32 + (l & 31), kg * 8 + 4 * (l >> 5));
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          bf[j] = frag4<BN, MF, B_ALONG_R>(Bs[cb], wc * (BN / 2) + j * 32 + (l & 31), kg * 8 + 4 * (l >> 5));
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].x, bf[j].x, acc32[i][j], 0, 0, 0);
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].y, bf[j].y, acc32[i][j], 0, 0, 0);
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].z, bf[j].z, acc32[i][j], 0, 0, 0);
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i].w, bf[j].w, acc32[i][j], 0, 0, 0);
+          }
+      }
+    }
+  };
+  load(rb);
+  store(0);
   __syncthreads();
   int buf = 0;
   for (int64_t r0 = rb; r0 < re; r0 += GBK) {
-    const bool more = r0 + GBK < re;
-    if (more) {
-      load_slab<BM, A_ALONG_R, AZ, VEC>(ra, g.a, g.lda, g.ay, g.lday, g.act_z, m0, g.M, r0 + GBK, re, t);
-      load_slab<BN, B_ALONG_R, BZ, VEC>(rbv, g.b, g.ldb, g.by, g.ldby, g.act_z, n0, g.N, r0 + GBK, re, t);
-    }
-    if (do_db && t < BN) {
-#pragma unroll
-      for (int k = 0; k < GBK; ++k) csum += Bs[buf][t * LDP + k];
-    }
-#pragma unroll
-    for (int kg = 0; kg < GBK / 16; ++kg) {
-#pragma unroll
-      for (int i = 0; i < WT; ++i) {
-        const int q = w * WT + i, rt = q / TN, ct = q % TN;
-        const float4 af = *reinterpret_cast<const float4*>(
-            &As[buf][(rt * 16 + (l & 15)) * LDP + kg * 16 + 4 * (l >> 4)]);
-        const float4 bf = *reinterpret_cast<const float4*>(
-            &Bs[buf][(ct * 16 + (l & 15)) * LDP + kg * 16 + 4 * (l >> 4)]);
-        acc[i] = mfma4(af.x, bf.x, acc[i]);
-        acc[i] = mfma4(af.y, bf.y, acc[i]);
-        acc[i] = mfma4(af.z, bf.z, acc[i]);
-        acc[i] = mfma4(af.w, bf.w, acc[i]);
-      }
-    }
-    if (more) {
-      store_slab<BM, A_ALONG_R>(As[buf ^ 1], ra, t);
-      store_slab<BN, B_ALONG_R>(Bs[buf ^ 1], rbv, t);
-    }
+    load(r0 + GBK);  // (beyond re: masked loads of element 0, never stored)
+    compute(buf);
+    if (r0 + GBK < re) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
   // ---- epilogue ----
-#pragma unroll
-  for (int i = 0; i < WT; ++i) {
-    const int q = w * WT + i, rt = q / TN, ct = q % TN;
-    const int64_t n = n0 + ct * 16 + (l & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t m = m0 + rt * 16 + (l >> 4) * 4 + j;
-      if (m < g.M && n < g.N) {
-        const float v = acc[i][j];
-        if (g.epi == EPI_FWD) {
-          g.out[m * g.ldo + n] = act_fwd(v + g.bias[n], g.act);
-        } else if (g.epi == EPI_STORE) {
-          float* d = g.out + m * g.ldo + n;
-          *d = g.accumulate ? *d + v : v;
-        } else {
-          g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + m * g.N + n] = v;
-        }
+  auto emit = [&](int64_t m, int64_t n, float v) {
+    if (m < g.M && n < g.N) {
+      if (g.epi == EPI_FWD) {
+        g.out[m * g.ldo + n] = act_fwd(v + g.bias[n], g.act);
+      } else if (g.epi == EPI_STORE) {
+        float* d = g.out + m * g.ldo + n;
+        *d = g.accumulate ? *d + v : v;
+      } else {
+        g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + m * g.N + n] = v;
       }
     }
+  };
+  if constexpr (MF == 16) {
+#pragma unroll
+    for (int i = 0; i < WT; ++i) {
+      const int q = w * WT + i, rt = q / TN, ct = q % TN;
+      const int64_t n = n0 + ct * 16 + (l & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) emit(m0 + rt * 16 + (l >> 4) * 4 + j, n, acc[i][j]);
+    }
+  } else {
+    // 32x32 accumulator: register 4 i + j holds row 8 i + 4 (lane / 32) + j, column lane % 32
+#pragma unroll
+    for (int ti = 0; ti < WM; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < WN; ++tj) {
+        const int64_t n = n0 + wc * (BN / 2) + tj * 32 + (l & 31);
+        const int64_t mb = m0 + wr * (BM / 2) + ti * 32 + 4 * (l >> 5);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) emit(mb + 8 * i + j, n, acc32[ti][tj][4 * i + j]);
+      }
   }
   if (do_db && t < BN && n0 + t < g.N) {
     if (g.epi == EPI_PARTIAL) g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + g.M * g.N + n0 + t] = csum;
@@ -236,22 +346,29 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   }
 }
 
-struct GemmPlan { int bm, bn, splits; int64_t rchunk; };
+struct GemmPlan { int bm, bn, mf, splits; int64_t rchunk; };
 
 // Tile / split-K policy.  256 CUs take ~4 resident 256-thread GEMM blocks each, so a launch wants
 // ~1k blocks: 64-row tiles only when that still gives >= big_min tiles, and reductions split
 // (deterministic partials + column_reduce) while the tile count is below split_below, towards
 // split_target blocks with >= min_rows reduction rows per split; launches that cannot split
-// (forward, data gradient) take 32-column tiles below narrow_below tiles.  RS_GEMM_TUNE="a,b,c,d[,e]"
-// overrides (host-side, read once; tools/gemm_tune.sh).
-struct GemmTune { int big_min, split_below, split_target, min_rows, narrow_below; };
+// (forward, data gradient) take 32-column tiles below narrow_below tiles.  GEMMs of >= big_macs
+// multiply-adds may take the 32x32-MFMA blocks instead (64 x 64 .. 128 x 128), sized by the MFMA
+// time of the busiest CU plus any split-K round trip, larger blocks on ties -- off by default:
+// on the configs 3 / 5 shapes they measured no better than the 16x16 blocks at ~4 resident
+// blocks per CU (the loads, not the MFMAs, bound these GEMMs).
+// RS_GEMM_TUNE="a,b,c,d[,e[,f]]" overrides (host-side, read once; tools/gemm_tune.sh); f > 0
+// enables the large-GEMM blocks from f multiply-adds.
+struct GemmTune { int big_min, split_below, split_target, min_rows, narrow_below; int64_t big_macs; };
 static const GemmTune& gemm_tune() {
   static const GemmTune t = [] {
-    GemmTune v{512, 512, 1024, 128, 512};
+    GemmTune v{512, 512, 1024, 128, 512, INT64_MAX};  // 32x32 blocks opt-in (f = 2^28: DESIGN 5.6)
     if (const char* e = getenv("RS_GEMM_TUNE")) {
       GemmTune o = v;
-      const int n = sscanf(e, "%d,%d,%d,%d,%d", &o.big_min, &o.split_below, &o.split_target,
-                           &o.min_rows, &o.narrow_below);
+      long long bm = (long long)v.big_macs;
+      const int n = sscanf(e, "%d,%d,%d,%d,%d,%lld", &o.big_min, &o.split_below, &o.split_target,
+                           &o.min_rows, &o.narrow_below, &bm);
+      o.big_macs = bm > 0 ? (int64_t)bm : INT64_MAX;
       if (n >= 4 && o.split_target > 0 && o.min_rows >= GBK)
         v = o;
     }
@@ -260,9 +377,60 @@ static const GemmTune& gemm_tune() {
   return t;
 }
 
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static GemmPlan finish_plan(GemmPlan p, int64_t R) {
+  int64_t rc = cdiv(R, p.splits);
+  rc = cdiv(rc, GBK) * GBK;
+  p.rchunk = rc < GBK ? GBK : rc;
+  p.splits = (int)cdiv(R, p.rchunk);
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
 static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
   const GemmTune& tu = gemm_tune();
   GemmPlan p;
+  p.mf = 16;
+  if (M * N * R >= tu.big_macs) {
+    // large GEMM: 32x32-MFMA blocks; cost = rounds over 256 CUs x block area x rows per split
+    static const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    double best = 0;
+    for (const auto& c : cand) {
+      const int64_t tiles = cdiv(M, c[0]) * cdiv(N, c[1]);
+      int64_t s = 1;
+      if (allow_split) {  // fill one round of 256 CUs, >= 256 reduction rows per split
+        s = 256 / tiles;
+        const int64_t max_s = R / 256;
+        if (s > max_s) s = max_s;
+        if (s < 1) s = 1;
+      }
+      // us: MFMA time of the busiest CU (614 GFLOP/s per CU) + the split partials' round trip
+      // (written and re-read by column_reduce at ~4 TB/s) and the reduce launch
+      double cost = (double)cdiv(tiles * s, 256) * c[0] * c[1] * (double)cdiv(R, s) * 2.0 / 6.14e5;
+      if (s > 1) cost += (double)s * M * N * 8.0 / 4.0e6 + 3.0;
+      if (best == 0 || cost < best * 0.999) {
+        best = cost;
+        p.bm = c[0]; p.bn = c[1]; p.splits = (int)s;
+      }
+    }
+    p.mf = 32;
+    static const int forced = [] {  // tuning runs: RS_GEMM_BIG_TILE=BMxBN forces the block
+      const char* e = getenv("RS_GEMM_BIG_TILE");
+      int bm = 0, bn = 0;
+      if (e && sscanf(e, "%dx%d", &bm, &bn) == 2 && (bm == 64 || bm == 128) && (bn == 64 || bn == 128))
+        return bm * 1000 + bn;
+      return 0;
+    }();
+    if (forced) {
+      p.bm = forced / 1000; p.bn = forced % 1000;
+      const int64_t tiles = cdiv(M, p.bm) * cdiv(N, p.bn);
+      int64_t sp = allow_split ? 512 / tiles : 1;
+      if (sp > R / 256) sp = R / 256;
+      p.splits = (int)(sp < 1 ? 1 : sp);
+    }
+    return finish_plan(p, R);
+  }
   p.bn = N <= 32 ? 32 : 64;
   const int64_t tn = (N + p.bn - 1) / p.bn;
   p.bm = ((M + 63) / 64) * tn >= tu.big_min ? 64 : 32;
@@ -278,29 +446,31 @@ static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
     if (s > max_s) s = max_s;
     p.splits = (int)(s < 1 ? 1 : s);
   }
-  int64_t rc = (R + p.splits - 1) / p.splits;
-  rc = (rc + GBK - 1) / GBK * GBK;
-  p.rchunk = rc < GBK ? GBK : rc;
-  p.splits = (int)((R + p.rchunk - 1) / p.rchunk);
-  if (p.splits < 1) p.splits = 1;
-  return p;
+  return finish_plan(p, R);
 }
 
 template <int ALAY, int BLAY, bool AZ, bool BZ>
 static void launch_gemm(hipStream_t s, const GemmPlan& p, const GemmArgs& g, bool vec) {
   dim3 grid((unsigned)((g.M + p.bm - 1) / p.bm), (unsigned)((g.N + p.bn - 1) / p.bn), (unsigned)p.splits);
-#define RS_GEMM(BMM, BNN, V) gemm_kernel<BMM, BNN, ALAY, BLAY, AZ, BZ, V><<<grid, 256, 0, s>>>(g)
-  if (vec) {
-    if (p.bm == 64 && p.bn == 64) RS_GEMM(64, 64, true);
-    else if (p.bm == 64) RS_GEMM(64, 32, true);
-    else if (p.bn == 64) RS_GEMM(32, 64, true);
-    else RS_GEMM(32, 32, true);
-  } else {
-    if (p.bm == 64 && p.bn == 64) RS_GEMM(64, 64, false);
-    else if (p.bm == 64) RS_GEMM(64, 32, false);
-    else if (p.bn == 64) RS_GEMM(32, 64, false);
-    else RS_GEMM(32, 32, false);
+#define RS_GEMM(BMM, BNN, MF, V) gemm_kernel<BMM, BNN, MF, ALAY, BLAY, AZ, BZ, V><<<grid, 256, 0, s>>>(g)
+#define RS_GEMM_V(V)                                                   \
+  if (p.mf == 32) {                                                    \
+    if (p.bm == 128 && p.bn == 128) RS_GEMM(128, 128, 32, V);          \
+    else if (p.bm == 128) RS_GEMM(128, 64, 32, V);                     \
+    else if (p.bn == 128) RS_GEMM(64, 128, 32, V);                     \
+    else RS_GEMM(64, 64, 32, V);                                       \
+  } else {                                                             \
+    if (p.bm == 64 && p.bn == 64) RS_GEMM(64, 64, 16, V);              \
+    else if (p.bm == 64) RS_GEMM(64, 32, 16, V);                       \
+    else if (p.bn == 64) RS_GEMM(32, 64, 16, V);                       \
+    else RS_GEMM(32, 32, 16, V);                                       \
   }
+  if (vec) {
+    RS_GEMM_V(true)
+  } else {
+    RS_GEMM_V(false)
+  }
+#undef RS_GEMM_V
 #undef RS_GEMM
 }
 
@@ -314,7 +484,8 @@ RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t 
   GemmArgs g{X, ldx, nullptr, 0, W, N, nullptr, 0, M, N, K, 0, 0, EPI_FWD, act, bias, Y, ldy, 0, nullptr};
   GemmPlan p = plan_gemm(M, N, K, false);
   g.rchunk = p.rchunk;
-  const bool vec = aligned16(X) && aligned16(W) && ldx % 4 == 0 && N % 4 == 0;
+  // VEC: every operand float4 lies wholly inside or wholly outside its extent
+  const bool vec = aligned16(X) && aligned16(W) && ldx % 4 == 0 && N % 4 == 0 && K % 4 == 0;
   launch_gemm<LAY_ROW, LAY_ROW, false, false>(rs_stream(stream), p, g, vec);
   return rs_status_after_launch();
 }
@@ -362,7 +533,7 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
              split ? EPI_PARTIAL : EPI_STORE, 0, nullptr, split ? workspace : dW, N, accumulate,
              db};
   const bool vec = aligned16(X) && aligned16(dY) && aligned16(Y) && ldx % 4 == 0 && lddy % 4 == 0 &&
-                   ldy % 4 == 0;
+                   ldy % 4 == 0 && K % 4 == 0 && N % 4 == 0;
   launch_gemm<LAY_COL, LAY_ROW, false, true>(s, p, g, vec);
   if (split) {
     const int64_t total = (int64_t)K * N + N;

@@ -78,7 +78,11 @@ CASES = [  # (B, F, L, drop)
     (67, 26, 3, 0.0),      # config 2 (exact-F instantiation)
     (1, 26, 3, 0.0),       # one sample: one workgroup
     (2500, 26, 3, 0.0),    # more samples than the backward's grid (persistent loop)
-    (4500, 26, 3, 0.0),    # more samples than the forward's grid too
+    # more samples than the forward's grid too, at few fields and one layer: a batch has B F 64 L
+    # ReLU inputs and about one in 1e7 lies within fp32 rounding of the kink, where the float64
+    # dx itself jumps (B = 4500, F = 26, L = 3: sample 2272's dx moves by 1.6 under a 1e-7 relative
+    # change of x, tools/diag_wide2272.py) -- two fp32 kernels may then land on either side
+    (4200, 8, 1, 0.0),
     (40, 20, 2, 0.0),      # padded F (FMAX 32)
     (9, 31, 3, 0.1),       # dropout, padded
     (13, 4, 1, 0.0),       # fewer fields than key quarters + the dx-exchange buffer floor

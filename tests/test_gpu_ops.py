@@ -140,3 +140,53 @@ def test_dense_bwd_weight_split_k(M, K, N, act, acc):
     rb = dZ.sum(0) + (0.5 if acc else 0.0)
     assert_close(to_np(outs[0][0]), rW.cpu().numpy(), 1e-4, 1e-5, what="dW")
     assert_close(to_np(outs[0][1]), rb.cpu().numpy(), 1e-4, 1e-5, what="db")
+
+
+@pytest.mark.parametrize("M,K,N,act", [
+    (2048, 1712, 960, 1),     # config-5 first layer: 32x32-MFMA blocks, 128 x 64
+    (4099, 1616, 273, 0),     # config-3 trunk, ragged M / N, unaligned rows (scalar loads)
+    (1000, 1840, 400, 2),     # ragged M, sigmoid Z operand
+    (600, 1000, 700, 1),      # ragged everywhere, weight gradient split over M
+])
+def test_dense_large_gemm_blocks(M, K, N, act):
+    """The large-GEMM blocks (v_mfma_f32_32x32x2_f32, >= 2^28 multiply-adds): forward with bias +
+    activation into a strided output, data gradient accumulated into a strided dX, weight gradient
+    (+ column sums, split or not) -- each against float64."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    s = stream_handle()
+    ldx = K + 8
+    Xb = torch.rand(M, ldx, device="cuda", generator=g) - 0.5
+    X = Xb[:, :K]
+    W = (torch.rand(K, N, device="cuda", generator=g) - 0.5) * 0.1
+    b = torch.rand(N, device="cuda", generator=g) - 0.5
+    ldy = N + 4
+    Yb = torch.full((M, ldy), float("nan"), device="cuda")
+    call("rs_dense_fwd", s, ptr(Xb), M, K, ldx, ptr(W), ptr(b), N, act, ptr(Yb), ldy)
+    torch.cuda.synchronize()
+    Y = Yb[:, :N]
+    Xd, Wd = X.double(), W.double()
+    z = Xd @ Wd + b.double()
+    ry = torch.relu(z) if act == 1 else torch.sigmoid(z) if act == 2 else z
+    tol = 1e-7 * K * 0.25 * 8
+    assert_close(to_np(Y), ry.cpu().numpy(), tol, 1e-5, what="fwd")
+    dY = torch.rand(M, N, device="cuda", generator=g) - 0.5
+    Yc = Y.contiguous()
+    Yd = Yc.double()
+    dZ = dY.double() * (Yd > 0) if act == 1 else dY.double() * Yd * (1 - Yd) if act == 2 else dY.double()
+    dXb = torch.full((M, ldx), 0.25, device="cuda")
+    call("rs_dense_bwd_data", s, ptr(dY), N, ptr(Yc), N, act, ptr(W), M, K, N, ptr(dXb), ldx, 1)
+    lib = _lib.load()
+    ws_n = int(lib.rs_dense_bwd_weight_workspace_floats(M, K, N))
+    ws = torch.full((max(ws_n, 1),), float("nan"), device="cuda")
+    dW = torch.empty(K, N, device="cuda")
+    db = torch.empty(N, device="cuda")
+    call("rs_dense_bwd_weight", s, ptr(Xb), ldx, ptr(dY), N, ptr(Yc), N, act, M, K, N, ptr(dW),
+         ptr(db), 0, ptr(ws), ws_n)
+    torch.cuda.synchronize()
+    assert_close(to_np(dXb[:, :K]), (dZ @ Wd.T + 0.25).cpu().numpy(), 1e-7 * N * 0.05 * 8, 1e-5,
+                 what="dX")
+    assert torch.all(dXb[:, K:] == 0.25)
+    assert_close(to_np(dW), (Xd.T @ dZ).cpu().numpy(), 1e-7 * M * 0.25 * 8, 1e-5, what="dW")
+    assert_close(to_np(db), dZ.sum(0).cpu().numpy(), 1e-7 * M * 8, 1e-5, what="db")
