@@ -365,6 +365,19 @@ int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N);
 int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* dY, int64_t lddy,
                         const float* Y, int64_t ldy, int act, int64_t M, int K, int N, float* dW,
                         float* db, int accumulate, float* workspace, int64_t workspace_floats);
+/* Grouped Dense: G <= 8 independent layers of one kind in ONE launch (plus one grouped split-K
+ * reduce for weight gradients) -- the per-expert / per-task layers that staytime/VideoDnn.py:130-191
+ * and rough_rank/layer.py:174-233 build in Python loops.  desc: G records of int64 (pointers cast):
+ *   fwd        [M, K, N, ldx, ldy, act, X, W, bias, Y]                           (10 per layer)
+ *   bwd_data   [M, K, N, lddy, ldy, act, dY, Y, W, dX, lddx, accumulate]         (12 per layer)
+ *   bwd_weight [M, K, N, ldx, lddy, ldy, act, X, dY, Y, dW, db, accumulate]      (13 per layer;
+ *              one accumulate flag for the group)
+ * Same results as the per-layer calls up to summation order of split reductions. */
+int rs_dense_fwd_grouped(void* stream, int G, const int64_t* desc);
+int rs_dense_bwd_data_grouped(void* stream, int G, const int64_t* desc);
+int64_t rs_dense_bwd_weight_grouped_workspace_floats(int G, const int64_t* desc);
+int rs_dense_bwd_weight_grouped(void* stream, int G, const int64_t* desc, float* workspace,
+                                int64_t workspace_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H5/H8/H9  Tower ops around the Dense GEMMs (csrc/towers.hip).  act codes as rs_dense_fwd.

@@ -212,7 +212,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // 128 x 128 block moves 2-4x less L2 traffic per flop than a 32 x 64 one.  The k index inside each
 // 8-slab is permuted as in the 16x16 form (lane half h supplies k = 4h + j to MFMA j, in A and B).
 template <int BM, int BN, int MF, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_block(const GemmArgs& g, const int64_t bx, const int64_t by,
+                                           const int64_t bz) {
   static_assert(MF == 16 || MF == 32, "MFMA tile");
   constexpr int TM = BM / MF, TN = BN / MF;
   constexpr int WT = MF == 16 ? TM * TN / 4 : 1;            // 16x16 tiles per wave
@@ -222,10 +223,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[2][OpLay<BM, MF, A_ALONG_R>::SIZE];
   __shared__ __attribute__((aligned(16))) float Bs[2][OpLay<BN, MF, B_ALONG_R>::SIZE];
   const int t = threadIdx.x, w = t >> 6, l = t & 63;
-  const int64_t m0 = (int64_t)blockIdx.x * BM, n0 = (int64_t)blockIdx.y * BN;
-  const int64_t rb = (int64_t)blockIdx.z * g.rchunk;
+  const int64_t m0 = bx * BM, n0 = by * BN;
+  const int64_t rb = bz * g.rchunk;
   const int64_t re = rb + g.rchunk < g.R ? rb + g.rchunk : g.R;
-  const bool do_db = g.db != nullptr && blockIdx.x == 0;
+  const bool do_db = g.db != nullptr && bx == 0;
   float csum = 0.f;
   f32x4 acc[WT];
   f32x16 acc32[WM][WN];
@@ -314,7 +315,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
         float* d = g.out + m * g.ldo + n;
         *d = g.accumulate ? *d + v : v;
       } else {
-        g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + m * g.N + n] = v;
+        g.out[bz * (g.M * g.N + g.N) + m * g.N + n] = v;
       }
     }
   };
@@ -341,8 +342,78 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
       }
   }
   if (do_db && t < BN && n0 + t < g.N) {
-    if (g.epi == EPI_PARTIAL) g.out[(int64_t)blockIdx.z * (g.M * g.N + g.N) + g.M * g.N + n0 + t] = csum;
+    if (g.epi == EPI_PARTIAL) g.out[bz * (g.M * g.N + g.N) + g.M * g.N + n0 + t] = csum;
     else g.db[n0 + t] = g.accumulate ? g.db[n0 + t] + csum : csum;
+  }
+}
+
+template <int BM, int BN, int MF, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+  gemm_block<BM, BN, MF, ALAY, BLAY, AZ, BZ, VEC>(g, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Grouped launch: up to kMaxGroup independent GEMMs of one operand form and block shape (the
+// expert / gate / tower layers of the configs-3/5 models that a Python loop launched one by one).
+// Linear block b -> problem p (start[p] <= b < start[p + 1]) -> (split, tile row, tile column).
+// The problem index is block-uniform, so its arguments are read with scalar loads.
+constexpr int kMaxGroup = 8;
+struct GemmGroup {
+  GemmArgs g[kMaxGroup];
+  int start[kMaxGroup + 1];
+  int tx[kMaxGroup], ty[kMaxGroup];
+  int n;
+};
+
+template <int BM, int BN, int MF, int ALAY, int BLAY, bool AZ, bool BZ, bool VEC>
+__global__ void __launch_bounds__(256) gemm_group_kernel(GemmGroup gg) {
+  const int b = (int)blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxGroup; ++k) p += (k < gg.n && b >= gg.start[k]) ? 1 : 0;
+  const int local = b - gg.start[p];
+  const int per = gg.tx[p] * gg.ty[p];
+  const int bz = local / per, rem = local - bz * per;
+  gemm_block<BM, BN, MF, ALAY, BLAY, AZ, BZ, VEC>(gg.g[p], rem % gg.tx[p], rem / gg.tx[p], bz);
+}
+
+// Grouped deterministic column reduction of split-K partials: problem p's partial rows (one per
+// split, K N weights then N biases) summed in split order into dW / db, blocks of 64 columns x 16
+// row groups exactly as column_reduce_kernel.
+struct ReduceGroup {
+  const float* part[kMaxGroup];
+  float* dw[kMaxGroup];
+  float* db[kMaxGroup];
+  int64_t kn[kMaxGroup], total[kMaxGroup];
+  int nrows[kMaxGroup];
+  int start[kMaxGroup + 1];
+  int accumulate, n;
+};
+
+__global__ void __launch_bounds__(1024) column_reduce_group_kernel(ReduceGroup rg) {
+  constexpr int G = 16;
+  __shared__ float red[G][64];
+  const int b = (int)blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxGroup; ++k) p += (k < rg.n && b >= rg.start[k]) ? 1 : 0;
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t total = rg.total[p];
+  const int64_t c = (int64_t)(b - rg.start[p]) * 64 + lc;
+  const float* part = rg.part[p];
+  const int nrows = rg.nrows[p];
+  float s = 0.f;
+  if (c < total) {
+#pragma unroll 4
+    for (int r = g; r < nrows; r += G) s += part[(int64_t)r * total + c];
+  }
+  red[g][lc] = s;
+  __syncthreads();
+  if (g == 0 && c < total) {
+    float t = red[0][lc];
+#pragma unroll
+    for (int k = 1; k < G; ++k) t += red[k][lc];
+    float* d = c < rg.kn[p] ? rg.dw[p] + c : rg.db[p] + (c - rg.kn[p]);
+    *d = rg.accumulate ? (*d + t) : t;
   }
 }
 
@@ -538,6 +609,212 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
   if (split) {
     const int64_t total = (int64_t)K * N + N;
     launch_column_reduce(s, workspace, p.splits, total, total, (int64_t)K * N, dW, db, accumulate);
+  }
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped Dense launches (G <= kMaxGroup independent layers of one kind in ONE launch each): the
+// per-expert / per-task / per-tower layers of the configs-3/5 models (staytime/VideoDnn.py:130-191
+// ppnet gates and expert stacks, MMoE gate layers, task towers).  Host descriptors, int64 per
+// problem (pointers as integers):
+//   fwd         [M, K, N, ldx, ldy, act, X, W, bias, Y]
+//   bwd_data    [M, K, N, lddy, ldy, act, dY, Y, W, dX, lddx, accumulate]
+//   bwd_weight  [M, K, N, ldx, lddy, ldy, act, X, dY, Y, dW, db, accumulate]
+// One block shape for the group (the largest problem's plan); weight gradients split their
+// reduction per problem by the single-launch rule applied to the group's total tile count, and
+// the split problems' partials are reduced by ONE grouped column_reduce launch.
+// ---------------------------------------------------------------------------------------------
+enum { GD_FWD = 10, GD_BWD_DATA = 12, GD_BWD_WEIGHT = 13 };
+
+template <typename T>
+static T* dptr(int64_t v) { return reinterpret_cast<T*>((uintptr_t)v); }
+
+template <int ALAY, int BLAY, bool AZ, bool BZ>
+static void launch_group(hipStream_t s, int bm, int bn, bool vec, const GemmGroup& gg) {
+  const unsigned grid = (unsigned)gg.start[gg.n];
+#define RS_GG(BMM, BNN, V) gemm_group_kernel<BMM, BNN, 16, ALAY, BLAY, AZ, BZ, V><<<grid, 256, 0, s>>>(gg)
+#define RS_GG_V(V)                                   \
+  if (bm == 64 && bn == 64) RS_GG(64, 64, V);        \
+  else if (bm == 64) RS_GG(64, 32, V);               \
+  else if (bn == 64) RS_GG(32, 64, V);               \
+  else RS_GG(32, 32, V);
+  if (vec) {
+    RS_GG_V(true)
+  } else {
+    RS_GG_V(false)
+  }
+#undef RS_GG_V
+#undef RS_GG
+}
+
+struct GroupPlan {
+  int bm, bn;
+  int splits[kMaxGroup];
+  int64_t rchunk[kMaxGroup];
+};
+
+// (Mo, No, R) per problem: output extent and reduction length
+static bool plan_group(int G, const int64_t (*shape)[3], bool allow_split, GroupPlan& gp) {
+  if (G < 1 || G > kMaxGroup) return false;
+  int big = 0;
+  for (int p = 1; p < G; ++p)
+    if (shape[p][0] * shape[p][1] * shape[p][2] > shape[big][0] * shape[big][1] * shape[big][2]) big = p;
+  GemmPlan bp = plan_gemm(shape[big][0], shape[big][1], shape[big][2], allow_split);
+  if (bp.mf != 16) { bp.bm = 64; bp.bn = 64; }
+  gp.bm = bp.bm; gp.bn = bp.bn;
+  const GemmTune& tu = gemm_tune();
+  int64_t tiles = 0;
+  for (int p = 0; p < G; ++p) tiles += cdiv(shape[p][0], gp.bm) * cdiv(shape[p][1], gp.bn);
+  int64_t sp = 1;
+  if (allow_split && tiles < tu.split_below) sp = cdiv(tu.split_target, tiles);
+  for (int p = 0; p < G; ++p) {
+    GemmPlan q;
+    q.bm = gp.bm; q.bn = gp.bn; q.mf = 16;
+    int64_t s = sp;
+    const int64_t max_s = cdiv(shape[p][2], tu.min_rows);
+    if (s > max_s) s = max_s;
+    q.splits = (int)(s < 1 ? 1 : s);
+    q = finish_plan(q, shape[p][2]);
+    gp.splits[p] = q.splits;
+    gp.rchunk[p] = q.rchunk;
+  }
+  return true;
+}
+
+static void group_blocks(GemmGroup& gg, int G, const GroupPlan& gp) {
+  gg.n = G;
+  gg.start[0] = 0;
+  for (int p = 0; p < G; ++p) {
+    gg.tx[p] = (int)cdiv(gg.g[p].M, gp.bm);
+    gg.ty[p] = (int)cdiv(gg.g[p].N, gp.bn);
+    gg.start[p + 1] = gg.start[p] + gg.tx[p] * gg.ty[p] * gp.splits[p];
+  }
+  for (int p = G; p < kMaxGroup; ++p) gg.start[p + 1] = gg.start[G];
+}
+
+RS_API int rs_dense_fwd_grouped(void* stream, int G, const int64_t* desc) {
+  if (!desc || G < 1 || G > kMaxGroup) return RS_ERR_ARG;
+  GemmGroup gg{};
+  int64_t shape[kMaxGroup][3];
+  bool vec = true;
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + GD_FWD * p;
+    const int64_t M = d[0], K = d[1], N = d[2], ldx = d[3], ldy = d[4];
+    const float* X = dptr<const float>(d[6]);
+    const float* W = dptr<const float>(d[7]);
+    const float* bias = dptr<const float>(d[8]);
+    float* Y = dptr<float>(d[9]);
+    if (!X || !W || !bias || !Y || M <= 0 || K <= 0 || N <= 0 || ldx < K || ldy < N) return RS_ERR_ARG;
+    gg.g[p] = GemmArgs{X, ldx, nullptr, 0, W, N, nullptr, 0, M, N, K, 0, 0, EPI_FWD, (int)d[5],
+                       bias, Y, ldy, 0, nullptr};
+    shape[p][0] = M; shape[p][1] = N; shape[p][2] = K;
+    vec = vec && aligned16(X) && aligned16(W) && ldx % 4 == 0 && N % 4 == 0 && K % 4 == 0;
+  }
+  GroupPlan gp;
+  if (!plan_group(G, shape, false, gp)) return RS_ERR_ARG;
+  for (int p = 0; p < G; ++p) gg.g[p].rchunk = gp.rchunk[p];
+  group_blocks(gg, G, gp);
+  launch_group<LAY_ROW, LAY_ROW, false, false>(rs_stream(stream), gp.bm, gp.bn, vec, gg);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_dense_bwd_data_grouped(void* stream, int G, const int64_t* desc) {
+  if (!desc || G < 1 || G > kMaxGroup) return RS_ERR_ARG;
+  GemmGroup gg{};
+  int64_t shape[kMaxGroup][3];
+  bool vec = true;
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + GD_BWD_DATA * p;
+    const int64_t M = d[0], K = d[1], N = d[2], lddy = d[3], ldy = d[4], lddx = d[10];
+    const float* dY = dptr<const float>(d[6]);
+    const float* Y = dptr<const float>(d[7]);
+    const float* W = dptr<const float>(d[8]);
+    float* dX = dptr<float>(d[9]);
+    if (!dY || !Y || !W || !dX || M <= 0 || K <= 0 || N <= 0 || lddx < K) return RS_ERR_ARG;
+    gg.g[p] = GemmArgs{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, 0, (int)d[5], EPI_STORE, 0,
+                       nullptr, dX, lddx, (int)d[11], nullptr};
+    shape[p][0] = M; shape[p][1] = K; shape[p][2] = N;
+    vec = vec && aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 && ldy % 4 == 0 &&
+          N % 4 == 0;
+  }
+  GroupPlan gp;
+  if (!plan_group(G, shape, false, gp)) return RS_ERR_ARG;
+  for (int p = 0; p < G; ++p) gg.g[p].rchunk = gp.rchunk[p];
+  group_blocks(gg, G, gp);
+  launch_group<LAY_ROW, LAY_COL, true, false>(rs_stream(stream), gp.bm, gp.bn, vec, gg);
+  return rs_status_after_launch();
+}
+
+static bool weight_group_plan(int G, const int64_t* desc, GroupPlan& gp) {
+  int64_t shape[kMaxGroup][3];
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + GD_BWD_WEIGHT * p;
+    shape[p][0] = d[1]; shape[p][1] = d[2]; shape[p][2] = d[0];  // C[K, N] over M rows
+  }
+  return plan_group(G, shape, true, gp);
+}
+
+RS_API int64_t rs_dense_bwd_weight_grouped_workspace_floats(int G, const int64_t* desc) {
+  if (!desc || G < 1 || G > kMaxGroup) return -1;
+  GroupPlan gp;
+  if (!weight_group_plan(G, desc, gp)) return -1;
+  int64_t n = 0;
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + GD_BWD_WEIGHT * p;
+    if (gp.splits[p] > 1) n += (int64_t)gp.splits[p] * (d[1] * d[2] + d[2]);
+  }
+  return n;
+}
+
+RS_API int rs_dense_bwd_weight_grouped(void* stream, int G, const int64_t* desc, float* workspace,
+                                       int64_t workspace_floats) {
+  if (!desc || G < 1 || G > kMaxGroup) return RS_ERR_ARG;
+  GroupPlan gp;
+  if (!weight_group_plan(G, desc, gp)) return RS_ERR_ARG;
+  GemmGroup gg{};
+  ReduceGroup rg{};
+  int nred = 0;
+  int64_t off = 0;
+  bool vec = true;
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + GD_BWD_WEIGHT * p;
+    const int64_t M = d[0], K = d[1], N = d[2], ldx = d[3], lddy = d[4], ldy = d[5];
+    const float* X = dptr<const float>(d[7]);
+    const float* dY = dptr<const float>(d[8]);
+    const float* Y = dptr<const float>(d[9]);
+    float* dW = dptr<float>(d[10]);
+    float* db = dptr<float>(d[11]);
+    const int acc = (int)d[12];
+    if (!X || !dY || !Y || !dW || !db || M <= 0 || K <= 0 || N <= 0) return RS_ERR_ARG;
+    const bool split = gp.splits[p] > 1;
+    float* part = nullptr;
+    if (split) {
+      const int64_t need = (int64_t)gp.splits[p] * (K * N + N);
+      if (!workspace || off + need > workspace_floats) return RS_ERR_ARG;
+      part = workspace + off;
+      off += need;
+      rg.part[nred] = part; rg.dw[nred] = dW; rg.db[nred] = db;
+      rg.kn[nred] = K * N; rg.total[nred] = K * N + N; rg.nrows[nred] = gp.splits[p];
+      rg.accumulate = acc;  // (one flag per call: the Python group passes the same for every layer)
+      ++nred;
+    }
+    gg.g[p] = GemmArgs{X, ldx, nullptr, 0, dY, lddy, Y, ldy, K, N, M, gp.rchunk[p], (int)d[6],
+                       split ? EPI_PARTIAL : EPI_STORE, 0, nullptr, split ? part : dW, N, acc, db};
+    vec = vec && aligned16(X) && aligned16(dY) && aligned16(Y) && ldx % 4 == 0 && lddy % 4 == 0 &&
+          ldy % 4 == 0 && K % 4 == 0 && N % 4 == 0;
+  }
+  for (int p = 1; p < G; ++p)
+    if ((int)desc[GD_BWD_WEIGHT * p + 12] != (int)desc[12]) return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  group_blocks(gg, G, gp);
+  launch_group<LAY_COL, LAY_ROW, false, true>(s, gp.bm, gp.bn, vec, gg);
+  if (nred) {
+    rg.n = nred;
+    rg.start[0] = 0;
+    for (int q = 0; q < nred; ++q) rg.start[q + 1] = rg.start[q] + (int)cdiv(rg.total[q], 64);
+    for (int q = nred; q < kMaxGroup; ++q) rg.start[q + 1] = rg.start[nred];
+    column_reduce_group_kernel<<<rg.start[nred], 1024, 0, s>>>(rg);
   }
   return rs_status_after_launch();
 }

@@ -282,6 +282,93 @@ class Dense(nn.Module):
         return y.reshape(*lead, self.units)
 
 
+def _desc_ptr(vals):
+    """A host int64 descriptor array for the grouped Dense entries (kept alive by the caller)."""
+    import ctypes
+    arr = (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+    return arr, ctypes.cast(arr, ctypes.c_void_p)
+
+
+class _GroupedDenseFn(torch.autograd.Function):
+    """G independent Dense layers in one forward launch and two (+ one reduce) backward launches
+    (rs_dense_*_grouped).  apply(acts, x_0..x_{G-1}, W_0.., b_0..)."""
+
+    @staticmethod
+    def forward(ctx, acts, *t):
+        G = len(acts)
+        xs, Ws, bs = [_row_major(x) for x in t[:G]], t[G:2 * G], t[2 * G:]
+        _lib.require_device(*xs, *Ws)
+        ys, desc = [], []
+        for x, W, b, a in zip(xs, Ws, bs, acts):
+            M, K = x.shape
+            N = W.shape[1]
+            y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+            ys.append(y)
+            desc += [M, K, N, x.stride(0), N, a, ptr(x), ptr(W), ptr(b), ptr(y)]
+        keep, d = _desc_ptr(desc)
+        call("rs_dense_fwd_grouped", stream_handle(), G, d)
+        del keep
+        ctx.save_for_backward(*xs, *ys, *Ws, *bs)
+        ctx.acts = acts
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        acts = ctx.acts
+        G = len(acts)
+        sv = ctx.saved_tensors
+        xs, ys, Ws, bs = sv[:G], sv[G:2 * G], sv[2 * G:3 * G], sv[3 * G:]
+        dev = xs[0].device
+        s = stream_handle()
+        dys = [_row_major(d) if d is not None else torch.zeros_like(y) for d, y in zip(dys, ys)]
+        dxs = [None] * G
+        if any(ctx.needs_input_grad[1:1 + G]):
+            desc = []
+            for i in range(G):
+                M, K = xs[i].shape
+                N = Ws[i].shape[1]
+                dxs[i] = torch.empty(M, K, device=dev, dtype=torch.float32)
+                desc += [M, K, N, dys[i].stride(0), N, acts[i], ptr(dys[i]), ptr(ys[i]), ptr(Ws[i]),
+                         ptr(dxs[i]), K, 0]
+            keep, d = _desc_ptr(desc)
+            call("rs_dense_bwd_data_grouped", s, G, d)
+            del keep
+        in_place = all(W.grad is not None and b.grad is not None and W.grad.is_contiguous()
+                       for W, b in zip(Ws, bs))
+        dWs = [W.grad if in_place else torch.empty_like(W) for W in Ws]
+        dbs = [b.grad if in_place else torch.empty_like(b) for b in bs]
+        desc = []
+        for i in range(G):
+            M, K = xs[i].shape
+            N = Ws[i].shape[1]
+            desc += [M, K, N, xs[i].stride(0), dys[i].stride(0), N, acts[i], ptr(xs[i]), ptr(dys[i]),
+                     ptr(ys[i]), ptr(dWs[i]), ptr(dbs[i]), 1 if in_place else 0]
+        keep, d = _desc_ptr(desc)
+        ws_n = int(_lib.load().rs_dense_bwd_weight_grouped_workspace_floats(G, d))
+        ws = torch.empty(max(ws_n, 1), device=dev, dtype=torch.float32)
+        call("rs_dense_bwd_weight_grouped", s, G, d, ptr(ws), ws_n)
+        del keep
+        if in_place:
+            return (None, *dxs) + (None,) * (2 * G)
+        return (None, *dxs, *dWs, *dbs)
+
+
+def grouped_dense(layers, xs):
+    """[layer_i(x_i)] for built Dense layers of one input rank, as ONE grouped launch per pass
+    (same math as calling each layer; the per-expert / per-task loops of staytime/VideoDnn.py and
+    rough_rank/layer.py).  Up to 8 layers per group."""
+    layers, xs = list(layers), list(xs)
+    if len(layers) == 1 or len(layers) > 8:
+        return [l(x) for l, x in zip(layers, xs)]
+    for l, x in zip(layers, xs):
+        if not l.built:
+            l.build(tuple(x.shape), device=x.device)
+    acts = tuple(l.act for l in layers)
+    flat = [x.reshape(-1, x.shape[-1]).float() for x in xs]
+    ys = _GroupedDenseFn.apply(acts, *flat, *[l.kernel for l in layers], *[l.bias for l in layers])
+    return [y.reshape(*x.shape[:-1], l.units) for y, x, l in zip(ys, xs, layers)]
+
+
 class MultiLayerDense(nn.Module):
     """MultiLayerDense(units=[...], activation=...) (imported at autoint:9, absent from the
     reference): pinned as Dense(u, activation) for every u in order."""

@@ -27,7 +27,8 @@ from torch import nn
 from ._lib import call, ptr, stream_handle
 from .din import StaytimeDIN
 from .embedding import EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam, SparseTable
-from .layers import Dense, InteractingLayer, _act_code, _DenseFn, _row_major, gather_multi
+from .layers import (Dense, InteractingLayer, _act_code, _DenseFn, _row_major, gather_multi,
+                     grouped_dense)
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 from . import _lib
 from .towers import (DNN, PLE, CrossNet, DeepCrossLayer, ExpertGateLayer, FFMBlock, KDLoss,
@@ -612,21 +613,22 @@ class StaytimeMTL(nn.Module):
                for s in range(len(self.query_idx))]
         rew, cross_term, fm_logit = self.senet(general)                            # :81-115
         concated = torch.cat([rew, cross_term, mult, ffm] + din, dim=1)            # :122-123
-        H, NE = list(cfg.hidden_units), cfg.num_experts
+        H, NE, L = list(cfg.hidden_units), cfg.num_experts, len(cfg.hidden_units)
         firsts = self.first(concated)
         pp1 = self.pp1(gate_input)
-        experts, k = [], 0
-        for i in range(NE):
-            deep = firsts[i]
-            for j in range(len(H)):
-                g = self.pp2[i * len(H) + j](pp1[i * len(H) + j])                 # :134-138
-                if j > 0:
-                    deep = self.exp_rest[k](deep)
-                    k += 1
-                deep = gated(deep, g, 2.0)                                         # :139-146
-            experts.append(deep)
-        gates = [self.gate_out[t](self.gate_l2[t](firsts[NE + t])) for t in range(cfg.num_tasks)]
-        return concated, fm_logit, experts, gates
+        # the per-expert / per-task layers as grouped launches (one per pass for each group):
+        # expert i, layer j: gate = pp2[i L + j](pp1[i L + j]) (:134-138); deep = exp_rest[i (L-1)
+        # + j - 1](deep) for j > 0; deep = gated(deep, gate, 2) (:139-146)
+        gs = grouped_dense(self.pp2, [pp1[q] for q in range(NE * L)])
+        deeps = [firsts[i] for i in range(NE)]
+        for j in range(L):
+            if j > 0:
+                deeps = grouped_dense([self.exp_rest[i * (L - 1) + j - 1] for i in range(NE)], deeps)
+            deeps = [gated(deeps[i], gs[i * L + j], 2.0) for i in range(NE)]
+        T = cfg.num_tasks
+        gates = grouped_dense(self.gate_out,
+                              grouped_dense(self.gate_l2, [firsts[NE + t] for t in range(T)]))
+        return concated, fm_logit, deeps, gates
 
     def forward(self, emb, seqs, masks, with_loss=False, labels=None):
         """Named outputs, or with ``with_loss`` (loss, outputs)."""
@@ -646,8 +648,9 @@ class StaytimeMTL(nn.Module):
         mmoe = split_cols(mm, [Hh] * cfg.num_tasks)
         cross = self.dcn(concated)                                                  # :167
         ext = torch.cat([mmoe[0], cross], dim=1)                                    # :168
-        short = self.task_out[0](torch.cat([fm_logit, self.deep_logit[0](mmoe[1])], dim=1))  # :182-185
-        long_ = self.task_out[1](torch.cat([fm_logit, self.deep_logit[1](mmoe[2])], dim=1))  # :188-191
+        dl = grouped_dense(self.deep_logit, [mmoe[1], mmoe[2]])
+        short, long_ = grouped_dense(self.task_out, [torch.cat([fm_logit, dl[0]], dim=1),  # :182-185
+                                                     torch.cat([fm_logit, dl[1]], dim=1)])  # :188-191
         if not with_loss:
             return {"staytime": self.head(ext), "shortplay": short, "longplay": long_}
         y_stay, y_short, y_long, sw = labels

@@ -190,3 +190,40 @@ def test_dense_large_gemm_blocks(M, K, N, act):
     assert torch.all(dXb[:, K:] == 0.25)
     assert_close(to_np(dW), (Xd.T @ dZ).cpu().numpy(), 1e-7 * M * 0.25 * 8, 1e-5, what="dW")
     assert_close(to_np(db), dZ.sum(0).cpu().numpy(), 1e-7 * M * 8, 1e-5, what="db")
+
+
+@pytest.mark.parametrize("acc", [False, True])
+def test_grouped_dense_matches_layers(acc):
+    """grouped_dense (rs_dense_*_grouped: one launch per pass for up to 8 layers) == the layers
+    called one by one: mixed shapes and activations, column-slice inputs (row stride > width), a
+    weight gradient that splits its reduction, ragged N, gradients accumulated into .grad."""
+    from recommendsystem_amd.layers import Dense, grouped_dense
+    torch.manual_seed(5)
+    M = 2048
+    src = torch.randn(M, 256 + 128 + 64, device=DEV)
+    specs = [(256, "sigmoid", src[:, :256]), (128, "relu", src[:, 256:384]),
+             (3, None, src[:, 384:448]), (64, "relu", torch.randn(M, 32, device=DEV))]
+    outs = {}
+    for mode in ("single", "grouped"):
+        layers = []
+        for i, (u, a, x) in enumerate(specs):
+            l = Dense(u, a, seed=40 + i, device=DEV)
+            l.build(tuple(x.shape), device=DEV)
+            with torch.no_grad():
+                l.bias.uniform_(-0.2, 0.2, generator=torch.Generator(device=DEV).manual_seed(i))
+            if acc:
+                l.kernel.grad = torch.full_like(l.kernel, 0.5)
+                l.bias.grad = torch.full_like(l.bias, 0.25)
+            layers.append(l)
+        xs = [x.detach().clone().requires_grad_(True) for _, _, x in specs]
+        ys = grouped_dense(layers, xs) if mode == "grouped" else [l(x) for l, x in zip(layers, xs)]
+        g = torch.Generator(device=DEV).manual_seed(9)
+        loss = sum((y * torch.randn(y.shape, device=DEV, generator=g)).sum() for y in ys)
+        loss.backward()
+        torch.cuda.synchronize()
+        outs[mode] = ([y.detach() for y in ys], [x.grad for x in xs],
+                      [l.kernel.grad.clone() for l in layers], [l.bias.grad.clone() for l in layers])
+    for what, a, b in zip(("y", "dx", "dW", "db"), outs["grouped"], outs["single"]):
+        for i, (u, v) in enumerate(zip(a, b)):
+            scale = float(v.abs().max()) + 1e-6
+            assert_close(to_np(u), to_np(v), 2e-6 * scale + 1e-6, 1e-5, what=f"{what}[{i}]")
