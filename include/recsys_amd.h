@@ -437,6 +437,11 @@ int rs_mul_fwd(void* stream, const float* A, int64_t lda, const float* G, int64_
 int rs_mul_bwd(void* stream, const float* A, int64_t lda, const float* G, int64_t ldg, int64_t M,
                int N, float scale, const float* dY, int64_t lddy, float* dA, int64_t ldda,
                float* dG, int64_t lddg);
+/* Grouped gating multiplies (G <= 8, one launch): desc int64 records
+ *   fwd [M, N, lda, ldg, ldy, A, G, Y]                     Y = A * (scale G)
+ *   bwd [M, N, lda, ldg, lddy, ldda, lddg, A, G, dY, dA, dG]  (dA / dG may be 0) */
+int rs_mul_fwd_grouped(void* stream, int G, const int64_t* desc, float scale);
+int rs_mul_bwd_grouped(void* stream, int G, const int64_t* desc, float scale);
 /* H9/H10 staytime head (staytime/VideoDnn.py:168-179) + custom_kl_loss (staytime/model.py:20-30):
  * P[m, 0:C] = softmax(Z[m]), P[m, C] = max(P . bins, 0) (P, bins nullable); with y_true:
  * loss_rows[m] = w_m * sum_c yt log(yt / yp) (yt, yp clipped to [eps, 1]) and

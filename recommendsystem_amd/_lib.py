@@ -122,6 +122,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_mul_fwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _i64]),
     "rs_mul_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _f32, _vp, _i64, _vp, _i64, _vp,
                           _i64]),
+    "rs_mul_fwd_grouped": (_i32, [_vp, _i32, _vp, _f32]),
+    "rs_mul_bwd_grouped": (_i32, [_vp, _i32, _vp, _f32]),
     "rs_softmax_kl": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _i64, _vp, _i64, _vp, _f32, _f32,
                              _vp, _vp, _i64]),
     "rs_rowdot": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp, _i64, _vp,

@@ -433,7 +433,10 @@ struct GemmPlan { int bm, bn, mf, splits; int64_t rchunk; };
 struct GemmTune { int big_min, split_below, split_target, min_rows, narrow_below; int64_t big_macs; };
 static const GemmTune& gemm_tune() {
   static const GemmTune t = [] {
-    GemmTune v{512, 512, 1024, 128, 512, INT64_MAX};  // 32x32 blocks opt-in (f = 2^28: DESIGN 5.6)
+    // round 4 (after the slab-pipeline change, tools/r04_tune*.sh, 50 steps): 64-row tiles from
+    // 256 tiles, split below 256, narrow below 256 -- config 5 2.60 -> 2.53 ms, config 3 2.01 ->
+    // 2.02, config 4 unchanged; the 32x32 blocks opt-in (f = 2^28: DESIGN 5.6)
+    GemmTune v{256, 256, 1024, 128, 256, INT64_MAX};
     if (const char* e = getenv("RS_GEMM_TUNE")) {
       GemmTune o = v;
       long long bm = (long long)v.big_macs;

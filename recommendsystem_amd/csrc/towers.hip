@@ -975,6 +975,84 @@ RS_API int rs_mul_bwd(void* stream, const float* A, int64_t lda, const float* G,
   return rs_status_after_launch();
 }
 
+// Grouped ppnet gating (staytime/VideoDnn.py:139-146, one multiply per expert): G <= 8 problems,
+// one element per thread, block b -> problem p by start offsets (a block-uniform index).
+//   fwd desc [M, N, lda, ldg, ldy, A, G, Y]                    Y = A * (scale G)
+//   bwd desc [M, N, lda, ldg, lddy, ldda, lddg, A, G, dY, dA, dG]
+constexpr int kMulGroup = 8;
+struct MulGroup {
+  const float* a[kMulGroup]; const float* g[kMulGroup]; const float* dy[kMulGroup];
+  float* y[kMulGroup]; float* da[kMulGroup]; float* dg[kMulGroup];
+  int64_t lda[kMulGroup], ldg[kMulGroup], ldy[kMulGroup], ldda[kMulGroup], lddg[kMulGroup];
+  int64_t M[kMulGroup];
+  int N[kMulGroup];
+  int start[kMulGroup + 1];
+  int n;
+  float scale;
+};
+
+template <bool BWD>
+__global__ void __launch_bounds__(256) mul_group_kernel(MulGroup mg) {
+  const int b = (int)blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int k = 1; k < kMulGroup; ++k) p += (k < mg.n && b >= mg.start[k]) ? 1 : 0;
+  const int64_t i = (int64_t)(b - mg.start[p]) * 256 + threadIdx.x;
+  const int N = mg.N[p];
+  if (i >= mg.M[p] * N) return;
+  const int64_t m = i / N, c = i - m * N;
+  const float a = mg.a[p][m * mg.lda[p] + c], g = mg.g[p][m * mg.ldg[p] + c];
+  if (!BWD) {
+    mg.y[p][m * mg.ldy[p] + c] = a * (mg.scale * g);
+  } else {
+    const float d = mg.dy[p][m * mg.ldy[p] + c] * mg.scale;
+    if (mg.da[p]) mg.da[p][m * mg.ldda[p] + c] = d * g;
+    if (mg.dg[p]) mg.dg[p][m * mg.lddg[p] + c] = d * a;
+  }
+}
+
+template <typename T>
+static T* mptr(int64_t v) { return reinterpret_cast<T*>((uintptr_t)v); }
+
+static int mul_group_launch(void* stream, int G, const int64_t* desc, float scale, bool bwd) {
+  if (!desc || G < 1 || G > kMulGroup) return RS_ERR_ARG;
+  MulGroup mg{};
+  mg.n = G;
+  mg.scale = scale;
+  mg.start[0] = 0;
+  for (int p = 0; p < G; ++p) {
+    const int64_t* d = desc + (bwd ? 12 : 8) * p;
+    mg.M[p] = d[0]; mg.N[p] = (int)d[1]; mg.lda[p] = d[2]; mg.ldg[p] = d[3]; mg.ldy[p] = d[4];
+    if (bwd) {
+      mg.ldda[p] = d[5]; mg.lddg[p] = d[6];
+      mg.a[p] = mptr<const float>(d[7]); mg.g[p] = mptr<const float>(d[8]);
+      mg.dy[p] = mptr<const float>(d[9]); mg.da[p] = mptr<float>(d[10]); mg.dg[p] = mptr<float>(d[11]);
+      if (!mg.dy[p]) return RS_ERR_ARG;
+    } else {
+      mg.a[p] = mptr<const float>(d[5]); mg.g[p] = mptr<const float>(d[6]); mg.y[p] = mptr<float>(d[7]);
+      if (!mg.y[p]) return RS_ERR_ARG;
+    }
+    if (!mg.a[p] || !mg.g[p] || mg.M[p] < 0 || mg.N[p] <= 0) return RS_ERR_ARG;
+    const int64_t blocks = (mg.M[p] * mg.N[p] + 255) / 256;
+    if (mg.start[p] + blocks > (int64_t)1 << 30) return RS_ERR_ARG;
+    mg.start[p + 1] = mg.start[p] + (int)blocks;
+  }
+  for (int p = G; p < kMulGroup; ++p) mg.start[p + 1] = mg.start[G];
+  if (mg.start[G] == 0) return RS_OK;
+  hipStream_t s = rs_stream(stream);
+  if (bwd) mul_group_kernel<true><<<mg.start[G], 256, 0, s>>>(mg);
+  else mul_group_kernel<false><<<mg.start[G], 256, 0, s>>>(mg);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_mul_fwd_grouped(void* stream, int G, const int64_t* desc, float scale) {
+  return mul_group_launch(stream, G, desc, scale, false);
+}
+
+RS_API int rs_mul_bwd_grouped(void* stream, int G, const int64_t* desc, float scale) {
+  return mul_group_launch(stream, G, desc, scale, true);
+}
+
 RS_API int rs_softmax_kl(void* stream, const float* Z, int64_t ldz, int64_t M, int C,
                          const float* bins, float* P, int64_t ldp, const float* y_true,
                          int64_t ldt, const float* sample_w, float gscale, float eps,

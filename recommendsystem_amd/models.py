@@ -32,8 +32,8 @@ from .layers import (Dense, InteractingLayer, _act_code, _DenseFn, _row_major, g
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 from . import _lib
 from .towers import (DNN, PLE, CrossNet, DeepCrossLayer, ExpertGateLayer, FFMBlock, KDLoss,
-                     SENetFM, StaytimeHead, _rows, _split_grads, bce_term, cross_entropy_sum, fused_loss, gated,
-                     kd_mean_term, keras_bce, keras_bce_term)
+                     SENetFM, StaytimeHead, _rows, _split_grads, bce_term, cross_entropy_sum, fused_loss,
+                     gated, gated_group, kd_mean_term, keras_bce, keras_bce_term)
 
 
 # ============================================================================================
@@ -624,7 +624,7 @@ class StaytimeMTL(nn.Module):
         for j in range(L):
             if j > 0:
                 deeps = grouped_dense([self.exp_rest[i * (L - 1) + j - 1] for i in range(NE)], deeps)
-            deeps = [gated(deeps[i], gs[i * L + j], 2.0) for i in range(NE)]
+            deeps = gated_group(deeps, [gs[i * L + j] for i in range(NE)], 2.0)
         T = cfg.num_tasks
         gates = grouped_dense(self.gate_out,
                               grouped_dense(self.gate_l2, [firsts[NE + t] for t in range(T)]))

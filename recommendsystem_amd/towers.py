@@ -522,6 +522,56 @@ class _MulFn(torch.autograd.Function):
         return da, dg, None
 
 
+class _GroupedMulFn(torch.autograd.Function):
+    """Y_i = A_i * (scale G_i) for G <= 8 pairs in one launch each way (rs_mul_*_grouped)."""
+
+    @staticmethod
+    def forward(ctx, scale, *t):
+        from .layers import _desc_ptr
+        G = len(t) // 2
+        As, Gs = [_rows(a) for a in t[:G]], [_rows(g) for g in t[G:]]
+        ys, desc = [], []
+        for a, g in zip(As, Gs):
+            M, N = a.shape
+            y = torch.empty(M, N, device=a.device)
+            ys.append(y)
+            desc += [M, N, a.stride(0), g.stride(0), N, ptr(a), ptr(g), ptr(y)]
+        keep, d = _desc_ptr(desc)
+        call("rs_mul_fwd_grouped", stream_handle(), G, d, float(scale))
+        del keep
+        ctx.save_for_backward(*As, *Gs)
+        ctx.scale = float(scale)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        from .layers import _desc_ptr
+        sv = ctx.saved_tensors
+        G = len(sv) // 2
+        As, Gs = sv[:G], sv[G:]
+        das, dgs, desc = [], [], []
+        for a, g, dy in zip(As, Gs, dys):
+            M, N = a.shape
+            dy = _row_major(dy) if dy is not None else torch.zeros(M, N, device=a.device)
+            da = torch.empty(M, N, device=a.device)
+            dg = torch.empty(M, N, device=a.device)
+            das.append(da)
+            dgs.append(dg)
+            desc += [M, N, a.stride(0), g.stride(0), dy.stride(0), N, N, ptr(a), ptr(g), ptr(dy),
+                     ptr(da), ptr(dg)]
+        keep, d = _desc_ptr(desc)
+        call("rs_mul_bwd_grouped", stream_handle(), G, d, ctx.scale)
+        del keep
+        return (None, *das, *dgs)
+
+
+def gated_group(deeps, gates, scale=2.0):
+    """[gated(d, g, scale)] for up to 8 (deep, gate) pairs in one launch per pass."""
+    if len(deeps) == 1 or len(deeps) > 8:
+        return [gated(d, g, scale) for d, g in zip(deeps, gates)]
+    return list(_GroupedMulFn.apply(float(scale), *deeps, *gates))
+
+
 def gated(deep, gate, scale=2.0):
     """ppnet gating tf.multiply(2 * sigmoid_gate, deep) (staytime/VideoDnn.py:139-146)."""
     return _MulFn.apply(deep, gate, float(scale))

@@ -227,3 +227,23 @@ def test_grouped_dense_matches_layers(acc):
         for i, (u, v) in enumerate(zip(a, b)):
             scale = float(v.abs().max()) + 1e-6
             assert_close(to_np(u), to_np(v), 2e-6 * scale + 1e-6, 1e-5, what=f"{what}[{i}]")
+
+
+def test_gated_group_matches_gated():
+    """gated_group (rs_mul_*_grouped, one launch per pass) == gated per pair: column-slice
+    operands, outputs and both gradients bitwise (the same single multiply per element)."""
+    from recommendsystem_amd.towers import gated, gated_group
+    torch.manual_seed(3)
+    src = torch.randn(1000, 256 + 128 + 128, device=DEV)
+    gts = torch.rand(1000, 512, device=DEV)
+    pairs = [(src[:, :256], gts[:, :256]), (src[:, 256:384], gts[:, 256:384]), (src[:, 384:], gts[:, 384:])]
+    res = {}
+    for mode in ("single", "group"):
+        ds = [d.detach().clone().requires_grad_(True) for d, _ in pairs]
+        gs = [g.detach().clone().requires_grad_(True) for _, g in pairs]
+        ys = gated_group(ds, gs, 2.0) if mode == "group" else [gated(d, g, 2.0) for d, g in zip(ds, gs)]
+        gen = torch.Generator(device=DEV).manual_seed(4)
+        sum((y * torch.randn(y.shape, device=DEV, generator=gen)).sum() for y in ys).backward()
+        res[mode] = [y.detach() for y in ys] + [d.grad for d in ds] + [g.grad for g in gs]
+    for a, b in zip(res["group"], res["single"]):
+        assert torch.equal(a, b)
