@@ -365,6 +365,14 @@ int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N);
 int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* dY, int64_t lddy,
                         const float* Y, int64_t ldy, int act, int64_t M, int K, int N, float* dW,
                         float* db, int accumulate, float* workspace, int64_t workspace_floats);
+/* The whole Dense backward in one launch: dX (+)= dZ W^T and dW / db (+)= X^T dZ / colsum dZ side by
+ * side (plus the split-K reduce when the weight gradient splits; workspace as
+ * rs_dense_bwd_weight_workspace_floats).  Same results as rs_dense_bwd_data + rs_dense_bwd_weight
+ * (it falls back to them for unaligned operands). */
+int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* dY, int64_t lddy,
+                 const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K, int N,
+                 float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db, int w_accumulate,
+                 float* workspace, int64_t workspace_floats);
 /* Grouped Dense: G <= 8 independent layers of one kind in ONE launch (plus one grouped split-K
  * reduce for weight gradients) -- the per-expert / per-task layers that staytime/VideoDnn.py:130-191
  * and rough_rank/layer.py:174-233 build in Python loops.  desc: G records of int64 (pointers cast):

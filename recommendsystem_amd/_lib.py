@@ -82,6 +82,8 @@ SIGNATURES: dict[str, tuple] = {
     "rs_dense_bwd_weight_workspace_floats": (_i64, [_i64, _i32, _i32]),
     "rs_dense_bwd_weight": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _i32,
                                    _vp, _vp, _i32, _vp, _i64]),
+    "rs_dense_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp,
+                            _i64, _i32, _vp, _vp, _i32, _vp, _i64]),
     "rs_dense_fwd_grouped": (_i32, [_vp, _i32, _vp]),
     "rs_dense_bwd_data_grouped": (_i32, [_vp, _i32, _vp]),
     "rs_dense_bwd_weight_grouped_workspace_floats": (_i64, [_i32, _vp]),

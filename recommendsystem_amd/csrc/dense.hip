@@ -617,6 +617,85 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
 }
 
 // ---------------------------------------------------------------------------------------------
+// One Dense layer's backward as ONE launch: blocks [0, nd) form the data gradient dX = dZ W^T,
+// blocks [nd, ...) the weight gradient (its splits) -- two independent GEMMs of different operand
+// forms side by side instead of back to back (one kernel boundary less per layer, and the small
+// layers' two half-empty launches fill the chip together).  Both forms' LDS tiles are static, so a
+// block reserves the sum; the branch is block-uniform.
+// ---------------------------------------------------------------------------------------------
+template <int BMD, int BND, int BMW, int BNW>
+__global__ void __launch_bounds__(256) dense_bwd_dual_kernel(GemmArgs gd, GemmArgs gw, int nd,
+                                                             int txd, int txw, int tyw) {
+  const int b = (int)blockIdx.x;
+  if (b < nd) {
+    gemm_block<BMD, BND, 16, LAY_ROW, LAY_COL, true, false, true>(gd, b % txd, b / txd, 0);
+  } else {
+    const int l = b - nd, per = txw * tyw;
+    const int bz = l / per, r = l - bz * per;
+    gemm_block<BMW, BNW, 16, LAY_COL, LAY_ROW, false, true, true>(gw, r % txw, r / txw, bz);
+  }
+}
+
+template <int BMD, int BND>
+static void launch_dual_w(hipStream_t s, unsigned grid, const GemmArgs& gd, const GemmArgs& gw,
+                          int nd, int txd, int txw, int tyw, int bmw, int bnw) {
+#define RS_DUAL(BMW, BNW) \
+  dense_bwd_dual_kernel<BMD, BND, BMW, BNW><<<grid, 256, 0, s>>>(gd, gw, nd, txd, txw, tyw)
+  if (bmw == 64 && bnw == 64) RS_DUAL(64, 64);
+  else if (bmw == 64) RS_DUAL(64, 32);
+  else if (bnw == 64) RS_DUAL(32, 64);
+  else RS_DUAL(32, 32);
+#undef RS_DUAL
+}
+
+static void launch_dual(hipStream_t s, unsigned grid, const GemmArgs& gd, const GemmArgs& gw, int nd,
+                        int txd, int txw, int tyw, int bmd, int bnd, int bmw, int bnw) {
+  if (bmd == 64 && bnd == 64) launch_dual_w<64, 64>(s, grid, gd, gw, nd, txd, txw, tyw, bmw, bnw);
+  else if (bmd == 64) launch_dual_w<64, 32>(s, grid, gd, gw, nd, txd, txw, tyw, bmw, bnw);
+  else if (bnd == 64) launch_dual_w<32, 64>(s, grid, gd, gw, nd, txd, txw, tyw, bmw, bnw);
+  else launch_dual_w<32, 32>(s, grid, gd, gw, nd, txd, txw, tyw, bmw, bnw);
+}
+
+RS_API int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* dY, int64_t lddy,
+                        const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K,
+                        int N, float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db,
+                        int w_accumulate, float* workspace, int64_t workspace_floats) {
+  if (!X || !dY || !Y || !W || !dX || !dW || !db || M < 0 || K <= 0 || N <= 0 || lddx < K)
+    return RS_ERR_ARG;
+  const GemmPlan pd = plan_gemm(M, K, N, false);
+  const GemmPlan pw = plan_gemm(K, N, M, true);
+  const bool vec_d = aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 && ldy % 4 == 0 &&
+                     N % 4 == 0;
+  const bool vec_w = aligned16(X) && aligned16(dY) && aligned16(Y) && ldx % 4 == 0 && lddy % 4 == 0 &&
+                     ldy % 4 == 0 && K % 4 == 0 && N % 4 == 0;
+  const int64_t txd = cdiv(M, pd.bm), tyd = cdiv(K, pd.bn);
+  const int64_t txw = cdiv(K, pw.bm), tyw = cdiv(N, pw.bn);
+  const int64_t nd = txd * tyd, nw = txw * tyw * pw.splits;
+  if (M == 0 || pd.mf != 16 || pw.mf != 16 || !vec_d || !vec_w || nd + nw > ((int64_t)1 << 30)) {
+    int st = M == 0 ? RS_OK
+                    : rs_dense_bwd_data(stream, dY, lddy, Y, ldy, act, W, M, K, N, dX, lddx, dx_accumulate);
+    if (st) return st;
+    return rs_dense_bwd_weight(stream, X, ldx, dY, lddy, Y, ldy, act, M, K, N, dW, db, w_accumulate,
+                               workspace, workspace_floats);
+  }
+  const bool split = pw.splits > 1;
+  if (split && (!workspace || workspace_floats < (int64_t)pw.splits * ((int64_t)K * N + N)))
+    return RS_ERR_ARG;
+  GemmArgs gd{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, pd.rchunk, act, EPI_STORE, 0, nullptr, dX,
+              lddx, dx_accumulate, nullptr};
+  GemmArgs gw{X, ldx, nullptr, 0, dY, lddy, Y, ldy, K, N, M, pw.rchunk, act,
+              split ? EPI_PARTIAL : EPI_STORE, 0, nullptr, split ? workspace : dW, N, w_accumulate, db};
+  hipStream_t s = rs_stream(stream);
+  launch_dual(s, (unsigned)(nd + nw), gd, gw, (int)nd, (int)txd, (int)txw, (int)tyw, pd.bm, pd.bn,
+              pw.bm, pw.bn);
+  if (split) {
+    const int64_t total = (int64_t)K * N + N;
+    launch_column_reduce(s, workspace, pw.splits, total, total, (int64_t)K * N, dW, db, w_accumulate);
+  }
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Grouped Dense launches (G <= kMaxGroup independent layers of one kind in ONE launch each): the
 // per-expert / per-task / per-tower layers of the configs-3/5 models (staytime/VideoDnn.py:130-191
 // ppnet gates and expert stacks, MMoE gate layers, task towers).  Host descriptors, int64 per

@@ -193,7 +193,8 @@ class BucketedAllReduce:
         for off, n, p in reversed(spans):
             if id(p) in late_ids:
                 continue
-            contiguous = cur_lo is None or off + n == cur_lo
+            # adjacent in the arena up to its layer-alignment gap (< 16 floats of zeros)
+            contiguous = cur_lo is None or 0 <= cur_lo - (off + n) < 16
             if cur and (not contiguous or cur_hi - off > cap):
                 self.buckets.append((cur_lo, cur_hi - cur_lo, cur))
                 cur, cur_lo, cur_hi = [], None, None

@@ -231,18 +231,19 @@ class _DenseFn(torch.autograd.Function):
         M, K = x.shape
         N = W.shape[1]
         s = stream_handle()
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty(M, K, device=x.device, dtype=torch.float32)
-            call("rs_dense_bwd_data", s, ptr(dy), dy.stride(0), ptr(y), N, ctx.act, ptr(W), M, K,
-                 N, ptr(dx), K, 0)
         ws_n = int(_lib.load().rs_dense_bwd_weight_workspace_floats(M, K, N))
         ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
         in_place = W.grad is not None and b.grad is not None and W.grad.is_contiguous()
         dW = W.grad if in_place else torch.empty_like(W)
         db = b.grad if in_place else torch.empty_like(b)
-        call("rs_dense_bwd_weight", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N,
-             ctx.act, M, K, N, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
+        dx = None
+        if ctx.needs_input_grad[0]:  # data and weight gradients in one launch
+            dx = torch.empty(M, K, device=x.device, dtype=torch.float32)
+            call("rs_dense_bwd", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N, ctx.act,
+                 ptr(W), M, K, N, ptr(dx), K, 0, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
+        else:
+            call("rs_dense_bwd_weight", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N,
+                 ctx.act, M, K, N, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
             return dx, None, None, None
         return dx, dW, db, None

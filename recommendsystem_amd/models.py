@@ -449,12 +449,23 @@ class DSSM(nn.Module):
         # index_select + reshape of the user / item fields and the teacher's flatten (:21-22,
         # :145-149) as column gathers of the lookup rows: one launch each, one fused backward
         ux, ix, wc = gather_multi(emb.reshape(B, nf * width), self._plans(nf, width))
-        user_emb = self.user(ux, mask)                                           # :145-146
-        item_emb = self.item(ix)                                                 # :148-149
+        heads = [h.layers for h in list(self.user.heads) + list(self.item.heads)]
+        if all(len(h) == 1 for h in heads):
+            # the towers' per-task output DNNs (one Dense each) as one grouped launch per pass
+            uo, io = self.user.ple(ux), self.item.ple(ix)
+            he = grouped_dense([h[0] for h in heads], list(uo) + list(io))
+            nu_t = len(self.user.heads)
+            user_emb = row_select(mask, he[1], he[0]) if mask is not None else he[0]  # :145-146
+            item_emb = he[nu_t]                                                  # :148-149
+        else:
+            user_emb = self.user(ux, mask)
+            item_emb = self.item(ix)
         cross = self.cross(wc)                                                   # :24
         deep = self.t2(self.t1(wc))                                              # :25-26
-        t_logit = self.t4(self.t3(torch.cat([deep, cross], dim=1)))              # :27-29
-        s_logit = self.s2(self.s1(torch.cat([user_emb, item_emb], dim=1)))       # :73-81
+        # the teacher's and the student's last two layers pairwise grouped (independent chains)
+        t3o, s1o = grouped_dense([self.t3, self.s1], [torch.cat([deep, cross], dim=1),   # :27-29
+                                                      torch.cat([user_emb, item_emb], dim=1)])  # :73-81
+        t_logit, s_logit = grouped_dense([self.t4, self.s2], [t3o, s1o])
         distill = self.kd(s_logit, t_logit.detach()) if with_kd else None        # :175-176
         return {"student": sigmoid(s_logit), "teacher": sigmoid(t_logit), "distill": distill,
                 "student_logit": s_logit, "teacher_logit": t_logit}

@@ -62,22 +62,36 @@ def grads_contiguous(params: Sequence[nn.Parameter]) -> torch.Tensor | None:
 class ParamArena:
     """One flat buffer for all dense parameters of a model (+ grads + Adam moments)."""
 
-    def __init__(self, params: Iterable[nn.Parameter], device=None):
+    def __init__(self, params: Iterable[nn.Parameter], device=None, align: int = 1):
+        """align > 1: each LAYER's parameters (a run of params adjacent in one storage, e.g. one
+        FlatBlock: [kernel, bias] or a packed [W1 b1 W2 b2]) led by a weight matrix start at a
+        multiple of ``align`` floats; parameters inside a layer stay packed.  The GEMM engine takes its vectorised
+        (float4) operand path only for 16-byte aligned weights, so the generic Trainer uses 16
+        (64 B); the gaps hold zeros in data, grad and the Adam moments (a zero gradient leaves
+        them zero).  The AutoInt step keeps align = 1 (its fused kernels address the arena
+        by packed offsets)."""
         self.params = [p for p in params]
         if not self.params:
             raise ValueError("ParamArena needs at least one parameter")
         device = device or self.params[0].device
-        self.n = sum(p.numel() for p in self.params)
-        self.data = torch.empty(self.n, device=device, dtype=torch.float32)
+        offs, off, prev = [], 0, None
+        for p in self.params:
+            st = (p.untyped_storage().data_ptr(), p.storage_offset())
+            same_layer = prev is not None and st[0] == prev[0] and st[1] == prev[1]
+            if align > 1 and not same_layer and p.dim() >= 2:  # a layer led by a weight matrix
+                off = (off + align - 1) // align * align
+            offs.append(off)
+            off += p.numel()
+            prev = (st[0], st[1] + p.numel())
+        self.n = off
+        self.data = torch.zeros(self.n, device=device, dtype=torch.float32)
         self.grad = torch.zeros(self.n, device=device, dtype=torch.float32)
-        off = 0
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, offs):
                 sz = p.numel()
                 self.data[off:off + sz].copy_(p.detach().reshape(-1))
                 p.data = self.data[off:off + sz].view(p.shape)
                 p.grad = self.grad[off:off + sz].view(p.shape)
-                off += sz
 
     def zero_grad(self) -> None:
         self.grad.zero_()

@@ -24,6 +24,8 @@ from .embedding import is_sharded
 from .layers import InteractingLayer
 from .params import ParamArena
 
+ARENA_ALIGN = 16  # floats: every layer's weights start 64-B aligned (the GEMMs' float4 path)
+
 
 def exchange_sparse(table, pg, world, x_rows, x_grads):
     """Data-parallel sparse exchange of one table (dist.py protocol): compact -> all-gather ->
@@ -51,7 +53,7 @@ class Trainer:
     def __init__(self, model, lr_dense: float, tables=(), process_group=None, beta1=0.9,
                  beta2=0.999, eps=1e-8, lr_groups=(), bucket_mb: float = 25.0):
         self.model = model
-        self.arena = ParamArena(model.parameters())
+        self.arena = ParamArena(model.parameters(), align=ARENA_ALIGN)
         dev = self.arena.data.device
         self.m = torch.zeros_like(self.arena.data)
         self.v = torch.zeros_like(self.arena.data)
@@ -100,9 +102,9 @@ class Trainer:
             offs = sorted(((p.data_ptr() - base) // 4, p.numel()) for p in mod.parameters())
             o0, end = offs[0][0], offs[0][0]
             for o, n in offs:
-                if o != end:
+                if o < end or o - end >= ARENA_ALIGN:  # (alignment gaps between layers only)
                     raise ValueError("an lr group's parameters must be contiguous in the arena")
-                end += n
+                end = o + n
             ranges.append((o0, end, float(lr)))
         ranges.sort()
         spans, k = [], 0

@@ -193,7 +193,14 @@ def _record_grads(d, trn):
     """Per step: the exchanged dense gradient and the table gradient, both as the optimizers
     see them (times the 1/world scale)."""
     rec = []
-    trn.on_dense_grad = lambda g, scale: rec.append(((g * scale).cpu().numpy(),
+    # the arena leaves alignment gaps between layers (trainer.ARENA_ALIGN): pack the gradient
+    # in parameter order, as the parameters are compared
+    base = trn.arena.data.data_ptr()
+    spans = [((p.data_ptr() - base) // 4, p.numel()) for p in d.parameters()]
+
+    def packed(g):
+        return torch.cat([g[o:o + n] for o, n in spans])
+    trn.on_dense_grad = lambda g, scale: rec.append(((packed(g) * scale).cpu().numpy(),
                                                      (d.table.grad * scale).cpu().numpy()))
     return rec
 

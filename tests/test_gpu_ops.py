@@ -247,3 +247,36 @@ def test_gated_group_matches_gated():
         res[mode] = [y.detach() for y in ys] + [d.grad for d in ds] + [g.grad for g in gs]
     for a, b in zip(res["group"], res["single"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,K,N,act", [(2048, 256, 128, 1), (2048, 1712, 960, 1), (300, 64, 48, 2),
+                                       (2048, 64, 3, 0)])
+def test_dense_bwd_one_launch_equals_two(M, K, N, act):
+    """rs_dense_bwd (data + weight gradient blocks in one launch) == rs_dense_bwd_data followed by
+    rs_dense_bwd_weight, bitwise (same block plans, same summation order), with accumulation."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    s = stream_handle()
+    X = torch.rand(M, K, device="cuda", generator=g) - 0.5
+    W = torch.rand(K, N, device="cuda", generator=g) - 0.5
+    Y = torch.rand(M, N, device="cuda", generator=g) - 0.3
+    dY = torch.rand(M, N, device="cuda", generator=g) - 0.5
+    ws_n = int(_lib.load().rs_dense_bwd_weight_workspace_floats(M, K, N))
+    res = []
+    for one in (True, False):
+        ws = torch.full((max(ws_n, 1),), float("nan"), device="cuda")
+        dX = torch.full((M, K), 0.5, device="cuda")
+        dW = torch.full((K, N), 0.25, device="cuda")
+        db = torch.full((N,), 0.125, device="cuda")
+        if one:
+            call("rs_dense_bwd", s, ptr(X), K, ptr(dY), N, ptr(Y), N, act, ptr(W), M, K, N, ptr(dX), K, 1,
+                 ptr(dW), ptr(db), 1, ptr(ws), ws_n)
+        else:
+            call("rs_dense_bwd_data", s, ptr(dY), N, ptr(Y), N, act, ptr(W), M, K, N, ptr(dX), K, 1)
+            call("rs_dense_bwd_weight", s, ptr(X), K, ptr(dY), N, ptr(Y), N, act, M, K, N, ptr(dW),
+                 ptr(db), 1, ptr(ws), ws_n)
+        torch.cuda.synchronize()
+        res.append((dX, dW, db))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

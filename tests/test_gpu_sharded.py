@@ -232,7 +232,11 @@ def _train_worker(rank, world, port, out):
         j = StaytimeRoughRank(rows=ROWS, device=DEV, seed=3, shard_group=pg if kind == "sharded" else None)
         trn = Trainer(j, 5e-4, [j.table], process_group=pg)
         grads = []
-        trn.on_dense_grad = lambda g, scale: grads.append((g * scale).cpu().numpy())
+        # pack the arena gradient (layer-alignment gaps, trainer.ARENA_ALIGN) in parameter order
+        base = trn.arena.data.data_ptr()
+        spans = [((p.data_ptr() - base) // 4, p.numel()) for p in j.parameters()]
+        trn.on_dense_grad = lambda g, scale: grads.append(
+            (torch.cat([g[o:o + n] for o, n in spans]) * scale).cpu().numpy())
         rng = np.random.default_rng(90 + rank)
         batches = [staytime_batch(rng, B5, j, DEV) for _ in range(2)]
         losses = [float(trn.step(*batches[s % 2])) for s in range(STEPS)]

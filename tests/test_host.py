@@ -165,7 +165,10 @@ def test_trainer_lr_groups_segments():
     m = Joint()
     t = Trainer(m, 5e-4, lr_groups=[(m.b, 1e-4)])
     segs = [(o, n, lr) for o, n, lr, _ in t.segments]
-    assert segs == [(0, 16, 5e-4), (16, 10, 1e-4), (26, 15, 5e-4)]
+    # layers led by a weight matrix start 16-float aligned (trainer.ARENA_ALIGN): a.weight 0..12,
+    # a.bias 12..16, b.weight 16..24, b.bias 24..26, (gap) c.weight 32..42, c.bias 42..47
+    assert segs == [(0, 16, 5e-4), (16, 10, 1e-4), (26, 21, 5e-4)]
     cnts = [c for *_, c in t.segments]
     assert cnts[0] is t.step_count and len({id(c) for c in cnts}) == 3
-    assert [(o, n, lr) for o, n, lr, _ in Trainer(m, 5e-4).segments] == [(0, 41, 5e-4)]
+    assert [(o, n, lr) for o, n, lr, _ in Trainer(m, 5e-4).segments] == [(0, 47, 5e-4)]
+    assert m.c.weight.data_ptr() % 64 == 0 or m.c.weight.data_ptr() - m.a.weight.data_ptr() == 128
