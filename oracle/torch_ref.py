@@ -108,6 +108,43 @@ def interacting_layer(x, W, bias, gamma, beta, layer_num=1, head_num=1, use_res=
     return out
 
 
+def interacting_layer_kinks(x, W, bias, gamma, beta, layer_num, head_num, use_res=True,
+                            eps=1e-14, flips=()):
+    """interacting_layer (InteractingLayer.py:37-61, no dropout) with the projection ReLUs
+    written as z * mask so that single ReLU derivatives can be flipped.
+
+    Returns (y, margins): margins[it] = |z| / (sum_e |x_e W_ec| + |b_c|) per [B, F, 4U]
+    projection input of iteration it -- the distance of each ReLU input from its kink in units
+    of the magnitude of the sum that forms it (fp32 rounding of that sum is ~6e-8 of it, plus
+    the propagated fp32 difference of the iteration's input).  relu(O + R) has no kink to
+    track: O and R are post-ReLU, so O + R >= 0.
+    flips: (it, b, f, c) entries whose ReLU derivative is inverted (c indexes [Q|K|V|R])."""
+    U = W.shape[1] // 4
+    dh = U // head_num
+    out, margins = x, []
+    for it in range(layer_num):
+        z = torch.tensordot(out, W, dims=([out.dim() - 1], [0])) + bias            # [B, F, 4U]
+        scale = torch.tensordot(out.detach().abs(), W.detach().abs(),
+                                dims=([out.dim() - 1], [0])) + bias.detach().abs()
+        margins.append((z.detach().abs() / scale))
+        keep = (z.detach() > 0).to(z.dtype)
+        for (fi, b, f, c) in flips:
+            if fi == it:
+                keep[b, f, c] = 1.0 - keep[b, f, c]
+        pr = z * keep
+        q, k, v, r = (pr[..., j * U:(j + 1) * U] for j in range(4))
+        heads = []
+        for h in range(head_num):
+            sl = slice(dh * h, dh * (h + 1))
+            w = torch.softmax(q[..., sl] @ k[..., sl].transpose(1, 2) / float(dh ** 0.5), dim=-1)
+            heads.append(w @ v[..., sl])
+        o = torch.cat(heads, dim=-1)
+        if use_res:
+            o = o + r
+        out = layer_norm(torch.relu(o), gamma, beta, eps)
+    return out, margins
+
+
 def mlp(x, layers, activation, bf16=None):
     """bf16: per-layer operand-rounding modes (see dense), or None."""
     for i, (W, b) in enumerate(layers):

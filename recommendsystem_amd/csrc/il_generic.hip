@@ -1,0 +1,503 @@
+// H3 InteractingLayer for ANY (E, U, H) with U % H == 0 and F <= 256 -- the shapes no compiled-in
+// instantiation covers (il_inst_*.hip, il_large.hip).  The reference trains whatever
+// model_param['interact'] passes (autoint:30-35 -> InteractingLayer(**...)); its constructor
+// defaults are layer_num 1, unit_num 128, head_num 1 (InteractingLayer.py:9-16), so dh = 128 over
+// 16-dim embeddings.  Same math as the specialised kernels (InteractingLayer.py:37-61, tied
+// weights, keras-layer-normalization LN, the counter-based dropout mask of common.hpp), shapes
+// read at run time:
+//
+//   * one 256-thread workgroup per sample (grid-stride); the sample's x, Q|K|V|R (post-ReLU),
+//     the attention output and, in the backward, dY / dK / dV live in LDS (row strides padded to
+//     odd word counts: the thread-per-(row, key) score loops read K rows without bank conflicts);
+//   * projections: thread = (row, column) over F x 4U, W from L1/L2, one fmaf chain in a fixed
+//     order -- the backward recomputes Q/K/V/R with the SAME function, so the recomputed ReLU
+//     masks are bit-identical to the forward's;
+//   * attention per head in query tiles of QT rows (QT x F scores in LDS): scores thread =
+//     (query, key), softmax one wave per row (DPP/shuffle reductions), P.V thread = (query, d);
+//   * backward per tile: P, dP = dO.V^T and dS = P (dP - D_i) per (query, key) into LDS, then
+//     dQ thread = (query, d) and dK / dV thread = (key, d) accumulated over the tiles (each element
+//     owned by one thread: no atomics); projection backward dW / db read-modify-write into the
+//     block's partial row (column_reduce over blocks, deterministic), dX = dZ W^T thread = (row, e)
+//     -> the previous iteration's dY, dx, or the fused sparse push at iteration 0.
+//
+// LDS bounds the shape: the backward needs F (E + 8U) + 2 QT F + small floats (<= 160 KB), e.g.
+// the constructor defaults (E 16, U 128) up to F = 37 fields; larger shapes return
+// RS_ERR_UNSUPPORTED.  fp32 only (a bf16 math-mode request is RS_ERR_UNSUPPORTED).
+#include "il_kernels.hpp"
+
+namespace rs_il {
+namespace gen {
+
+constexpr int NT = 256;
+constexpr int FMAXG = 256;
+constexpr size_t kLdsMax = 160 * 1024;
+
+struct Layout {
+  int PS, OS;                            // row strides: Q|K|V|R rows, U-wide rows
+  int QT;                                // query rows per attention tile
+  int xs, P, O, G, DK, DV, S, PT, rst, hst, acc, rows, total;  // float offsets
+};
+
+__host__ __device__ inline Layout make_layout(int F, int E, int U, int H, int QT, bool bwd) {
+  Layout l;
+  l.PS = 4 * U + 1;
+  l.OS = U + 1;
+  l.QT = QT;
+  int o = 0;
+  l.xs = o; o += F * E;  // (iterations > 0 have E == U)
+  l.P = o; o += F * l.PS;
+  l.O = o; o += F * l.OS;
+  l.G = o; if (bwd) o += F * l.OS;
+  l.DK = o; if (bwd) o += F * l.OS;
+  l.DV = o; if (bwd) o += F * l.OS;
+  l.S = o; o += QT * F;
+  l.PT = o; if (bwd) o += QT * F;
+  l.rst = o; o += 4 * F;
+  l.hst = o; o += 4 * H * F;
+  l.acc = o; if (bwd) o += 2 * U;
+  l.rows = o; if (bwd) o += F;
+  l.total = o;
+  return l;
+}
+
+// the largest query tile (<= 64 rows) whose layout fits the LDS, or 0
+inline int pick_qt(int F, int E, int U, int H, bool bwd) {
+  for (int qt = F < 64 ? F : 64; qt >= 1; qt = qt > 1 ? qt / 2 : 0) {
+    if ((size_t)make_layout(F, E, U, H, qt, bwd).total * 4 <= kLdsMax) return qt;
+    if (qt == 1) break;
+  }
+  return 0;
+}
+
+struct GArgs {
+  int64_t B;
+  int F, E, U, H, L, DH, use_res, drop;
+  float eps, drop_rate, inv_keep, sc2, inv_sdh;
+  uint64_t seed, seed_off;
+  const float *x, *xsave_in, *dy, *W, *bias, *gamma, *beta;
+  int64_t dy_ld, y_ld;
+  float *y, *xsave, *dx;
+  int dx_accumulate;
+  float* part;
+  const int64_t *g_ids, *g_base, *g_bucket;
+  const float* g_table;
+  int64_t g_table_rows;
+  int32_t* g_rows;
+  int g_hash;
+  const int32_t* push_rows;
+  float* push_table;
+  int32_t* push_flag;
+  Layout lay;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// Q|K|V|R = relu(x W + b) for every (row, column); one fixed fmaf order (forward == backward)
+__device__ __forceinline__ void project(const GArgs& a, const float* xs, float* P) {
+  const int NC = 4 * a.U, XS = a.E;
+  for (int idx = threadIdx.x; idx < a.F * NC; idx += NT) {
+    const int f = idx / NC, c = idx - f * NC;
+    const float* xr = xs + f * XS;
+    float acc = a.bias[c];
+    for (int e = 0; e < a.E; ++e) acc = fmaf(xr[e], a.W[e * NC + c], acc);
+    P[f * a.lay.PS + c] = fmaxf(acc, 0.f);
+  }
+}
+
+// scaled score (base-2 domain) of query i, key j, head h
+__device__ __forceinline__ float score2(const GArgs& a, const float* P, int i, int j, int h) {
+  const float* q = P + i * a.lay.PS + h * a.DH;
+  const float* k = P + j * a.lay.PS + a.U + h * a.DH;
+  float s = 0.f;
+  for (int d = 0; d < a.DH; ++d) s = fmaf(q[d], k[d], s);
+  return s * a.sc2;
+}
+
+// attention forward of head h, query rows [i0, i0 + nq): O rows (and, with hst, the row stats
+// {scaled max, 1 / sum} into hst[(h F + i) 4 + 0..1])
+__device__ void attn_tile_fwd(const GArgs& a, float* sm, int h, int i0, int nq, uint32_t kb,
+                              bool stats) {
+  const Layout& l = a.lay;
+  const int F = a.F;
+  float* P = sm + l.P;
+  float* S = sm + l.S;
+  for (int idx = threadIdx.x; idx < nq * F; idx += NT) {
+    const int ii = idx / F, j = idx - ii * F;
+    S[idx] = score2(a, P, i0 + ii, j, h);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int ii = w; ii < nq; ii += NT / 64) {
+    float* row = S + ii * F;
+    float mx = -INFINITY;
+    for (int j = lane; j < F; j += 64) mx = fmaxf(mx, row[j]);
+    mx = wave_max(mx);
+    float sum = 0.f;
+    for (int j = lane; j < F; j += 64) {
+      const float e = __builtin_amdgcn_exp2f(row[j] - mx);
+      row[j] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.0f / sum;
+    const int i = i0 + ii;
+    for (int j = lane; j < F; j += 64) {
+      float p = row[j] * inv;
+      if (a.drop) p = dropout_keep_k(kb, (uint32_t)h, (uint32_t)i, (uint32_t)j, a.drop_rate) ? p * a.inv_keep : 0.f;
+      row[j] = p;
+    }
+    if (stats && lane == 0) {
+      sm[l.hst + (h * F + i) * 4 + 0] = mx;
+      sm[l.hst + (h * F + i) * 4 + 1] = inv;
+    }
+  }
+  __syncthreads();
+  float* O = sm + l.O;
+  for (int idx = threadIdx.x; idx < nq * a.DH; idx += NT) {
+    const int ii = idx / a.DH, d = idx - ii * a.DH;
+    const float* pr = S + ii * F;
+    const float* v = P + 2 * a.U + h * a.DH + d;
+    float o = 0.f;
+    for (int j = 0; j < F; ++j) o = fmaf(pr[j], v[j * l.PS], o);
+    O[(i0 + ii) * l.OS + h * a.DH + d] = o;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t layer_key(const GArgs& a, int it, int64_t b) {
+  return a.drop ? dropout_sample_key(splitmix64(rs_eff_seed(a.seed, a.seed_off) + (uint64_t)it), (uint32_t)b)
+                : 0u;
+}
+
+__global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const Layout& l = a.lay;
+  const int F = a.F, U = a.U, E = a.E, XS = E;
+  float* xs = sm + l.xs;
+  float* P = sm + l.P;
+  float* O = sm + l.O;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    for (int idx = threadIdx.x; idx < F * E; idx += NT) {
+      const int f = idx / E, e = idx - f * E;
+      float v;
+      if (a.g_ids) {  // fused single-hot gather (rs_il_fwd_gather)
+        const int64_t row = hash_row(a.g_ids[b * F + f], a.g_base[f], a.g_bucket[f], a.g_hash);
+        const bool ok = row >= 0 && row < a.g_table_rows;
+        v = ok ? a.g_table[row * E + e] : 0.f;
+        const_cast<float*>(a.x)[b * F * E + idx] = v;
+        if (e == 0 && a.g_rows) a.g_rows[b * F + f] = ok ? (int32_t)row : -1;
+      } else {
+        v = a.x[b * F * E + idx];
+      }
+      xs[f * XS + e] = v;
+    }
+    __syncthreads();
+    for (int it = 0; it < a.L; ++it) {
+      project(a, xs, P);
+      __syncthreads();
+      const uint32_t kb = layer_key(a, it, b);
+      for (int h = 0; h < a.H; ++h)
+        for (int i0 = 0; i0 < F; i0 += l.QT)
+          attn_tile_fwd(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, false);
+      // LN statistics per row
+      for (int f = threadIdx.x; f < F; f += NT) {
+        float mean = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const float o = O[f * l.OS + u];
+          mean += fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f);
+        }
+        mean *= 1.0f / U;
+        float var = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const float o = O[f * l.OS + u];
+          const float z = fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f) - mean;
+          var = fmaf(z, z, var);
+        }
+        var *= 1.0f / U;
+        sm[l.rst + 4 * f] = mean;
+        sm[l.rst + 4 * f + 1] = 1.0f / sqrtf(var + a.eps);
+      }
+      __syncthreads();
+      const bool last = it == a.L - 1;
+      for (int idx = threadIdx.x; idx < F * U; idx += NT) {
+        const int f = idx / U, u = idx - f * U;
+        const float o = O[f * l.OS + u];
+        const float z = fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f);
+        const float yv = fmaf((z - sm[l.rst + 4 * f]) * sm[l.rst + 4 * f + 1], a.gamma[u], a.beta[u]);
+        if (last) {
+          a.y[b * a.y_ld + idx] = yv;
+        } else {  // E == U (tied weights): the next iteration's input
+          xs[f * XS + u] = yv;
+          a.xsave[((int64_t)it * a.B + b) * F * U + idx] = yv;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const Layout& l = a.lay;
+  const int F = a.F, U = a.U, E = a.E, DH = a.DH, NC = 4 * U, XS = E;
+  const int NPARAM = E * NC + NC + 2 * U;
+  float* xs = sm + l.xs;
+  float* P = sm + l.P;
+  float* O = sm + l.O;      // O, then dQ
+  float* G = sm + l.G;      // dY -> dA (= dO) -> dY of the previous iteration
+  float* DK = sm + l.DK;
+  float* DV = sm + l.DV;
+  float* S = sm + l.S;      // scores -> dS
+  float* PT = sm + l.PT;    // P after dropout
+  float* acc = sm + l.acc;  // dgamma | dbeta over the block's samples
+  int32_t* rows = reinterpret_cast<int32_t*>(sm + l.rows);
+  float* part = a.part + (int64_t)blockIdx.x * NPARAM;
+  for (int k = threadIdx.x; k < E * NC + NC; k += NT) part[k] = 0.f;
+  for (int k = threadIdx.x; k < 2 * U; k += NT) acc[k] = 0.f;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    for (int it = a.L - 1; it >= 0; --it) {
+      const float* xin = it == 0 ? a.x + b * F * E : a.xsave_in + ((int64_t)(it - 1) * a.B + b) * F * U;
+      for (int idx = threadIdx.x; idx < F * E; idx += NT) {
+        const int f = idx / E, e = idx - f * E;
+        xs[f * XS + e] = xin[idx];
+      }
+      if (it == a.L - 1)
+        for (int idx = threadIdx.x; idx < F * U; idx += NT) {
+          const int f = idx / U, u = idx - f * U;
+          G[f * l.OS + u] = a.dy[b * a.dy_ld + idx];
+        }
+      if (it == 0 && a.push_table)
+        for (int f = threadIdx.x; f < F; f += NT) rows[f] = a.push_rows[b * F + f];
+      for (int idx = threadIdx.x; idx < F * l.OS; idx += NT) { DK[idx] = 0.f; DV[idx] = 0.f; }
+      __syncthreads();
+      project(a, xs, P);
+      __syncthreads();
+      const uint32_t kb = layer_key(a, it, b);
+      for (int h = 0; h < a.H; ++h)
+        for (int i0 = 0; i0 < F; i0 += l.QT)
+          attn_tile_fwd(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, true);
+      // ---- epilogue backward: LN, ReLU, residual ----
+      for (int f = threadIdx.x; f < F; f += NT) {
+        float mean = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const float o = O[f * l.OS + u];
+          mean += fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f);
+        }
+        mean *= 1.0f / U;
+        float var = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const float o = O[f * l.OS + u];
+          const float z = fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f) - mean;
+          var = fmaf(z, z, var);
+        }
+        var *= 1.0f / U;
+        const float rstd = 1.0f / sqrtf(var + a.eps);
+        float m1 = 0.f, m2 = 0.f;
+        for (int u = 0; u < U; ++u) {
+          const float o = O[f * l.OS + u];
+          const float z = fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f);
+          const float gd = G[f * l.OS + u] * a.gamma[u];
+          m1 += gd;
+          m2 = fmaf(gd, (z - mean) * rstd, m2);
+        }
+        sm[l.rst + 4 * f] = mean;
+        sm[l.rst + 4 * f + 1] = rstd;
+        sm[l.rst + 4 * f + 2] = m1 * (1.0f / U);
+        sm[l.rst + 4 * f + 3] = m2 * (1.0f / U);
+      }
+      __syncthreads();
+      for (int u = threadIdx.x; u < U; u += NT) {  // dgamma, dbeta (column owners)
+        float sg = 0.f, sb = 0.f;
+        for (int f = 0; f < F; ++f) {
+          const float o = O[f * l.OS + u];
+          const float z = fmaxf(a.use_res ? o + P[f * l.PS + 3 * U + u] : o, 0.f);
+          const float g = G[f * l.OS + u];
+          sg = fmaf(g, (z - sm[l.rst + 4 * f]) * sm[l.rst + 4 * f + 1], sg);
+          sb += g;
+        }
+        acc[u] += sg;
+        acc[U + u] += sb;
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < F * U; idx += NT) {
+        const int f = idx / U, u = idx - f * U;
+        const float o = O[f * l.OS + u];
+        const float r = P[f * l.PS + 3 * U + u];
+        const float z = fmaxf(a.use_res ? o + r : o, 0.f);
+        const float* rs = sm + l.rst + 4 * f;
+        const float xh = (z - rs[0]) * rs[1];
+        const float dz = rs[1] * (G[f * l.OS + u] * a.gamma[u] - rs[2] - xh * rs[3]);
+        const float da = z > 0.f ? dz : 0.f;
+        G[f * l.OS + u] = da;
+        P[f * l.PS + 3 * U + u] = (a.use_res && r > 0.f) ? da : 0.f;  // R -> dR (masked)
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < a.H * F; idx += NT) {  // D = dO . O per (head, row)
+        const int h = idx / F, i = idx - h * F;
+        float d = 0.f;
+        for (int k = 0; k < DH; ++k) d = fmaf(G[i * l.OS + h * DH + k], O[i * l.OS + h * DH + k], d);
+        sm[l.hst + idx * 4 + 2] = d;
+      }
+      __syncthreads();
+      // ---- attention backward per head and query tile ----
+      for (int h = 0; h < a.H; ++h) {
+        for (int i0 = 0; i0 < F; i0 += l.QT) {
+          const int nq = F - i0 < l.QT ? F - i0 : l.QT;
+          for (int idx = threadIdx.x; idx < nq * F; idx += NT) {
+            const int ii = idx / F, j = idx - ii * F, i = i0 + ii;
+            const float* hs = sm + l.hst + (h * F + i) * 4;
+            const float p = __builtin_amdgcn_exp2f(score2(a, P, i, j, h) - hs[0]) * hs[1];
+            const float* go = G + i * l.OS + h * DH;
+            const float* vv = P + j * l.PS + 2 * U + h * DH;
+            float dp = 0.f;
+            for (int k = 0; k < DH; ++k) dp = fmaf(go[k], vv[k], dp);
+            float pd = p;
+            if (a.drop) {
+              const bool keep = dropout_keep_k(kb, (uint32_t)h, (uint32_t)i, (uint32_t)j, a.drop_rate);
+              dp = keep ? dp * a.inv_keep : 0.f;
+              pd = keep ? p * a.inv_keep : 0.f;
+            }
+            S[idx] = p * (dp - hs[2]);
+            PT[idx] = pd;
+          }
+          __syncthreads();
+          for (int idx = threadIdx.x; idx < nq * DH; idx += NT) {  // dQ rows of the tile
+            const int ii = idx / DH, d = idx - ii * DH;
+            const float* ds = S + ii * F;
+            const float* kk = P + U + h * DH + d;
+            float s = 0.f;
+            for (int j = 0; j < F; ++j) s = fmaf(ds[j], kk[j * l.PS], s);
+            O[(i0 + ii) * l.OS + h * DH + d] = s * a.inv_sdh;
+          }
+          for (int idx = threadIdx.x; idx < F * DH; idx += NT) {  // dK, dV over the tile's rows
+            const int j = idx / DH, d = idx - j * DH;
+            float sk = 0.f, sv = 0.f;
+            for (int ii = 0; ii < nq; ++ii) {
+              sk = fmaf(S[ii * F + j], P[(i0 + ii) * l.PS + h * DH + d], sk);
+              sv = fmaf(PT[ii * F + j], G[(i0 + ii) * l.OS + h * DH + d], sv);
+            }
+            DK[j * l.OS + h * DH + d] += sk * a.inv_sdh;
+            DV[j * l.OS + h * DH + d] += sv;
+          }
+          __syncthreads();
+        }
+      }
+      // ---- dZ = [dQ | dK | dV | dR] through the projection ReLUs ----
+      for (int idx = threadIdx.x; idx < F * 3 * U; idx += NT) {
+        const int f = idx / (3 * U), c = idx - f * 3 * U;
+        float* dst = (c < U ? O : c < 2 * U ? DK : DV) + f * l.OS + (c % U);
+        if (!(P[f * l.PS + c] > 0.f)) *dst = 0.f;
+      }
+      __syncthreads();
+      auto dzp = [&](int f, int c) -> float {
+        const int g = c / U;
+        return g == 3 ? P[f * l.PS + c] : (g == 0 ? O : g == 1 ? DK : DV)[f * l.OS + c - g * U];
+      };
+      for (int idx = threadIdx.x; idx < E * NC; idx += NT) {  // dW (block partial, RMW)
+        const int e = idx / NC, c = idx - e * NC;
+        float s = 0.f;
+        for (int f = 0; f < F; ++f) s = fmaf(xs[f * XS + e], dzp(f, c), s);
+        part[idx] += s;
+      }
+      for (int c = threadIdx.x; c < NC; c += NT) {
+        float s = 0.f;
+        for (int f = 0; f < F; ++f) s += dzp(f, c);
+        part[E * NC + c] += s;
+      }
+      for (int idx = threadIdx.x; idx < F * E; idx += NT) {  // dX = dZ W^T
+        const int f = idx / E, e = idx - f * E;
+        const float* wr = a.W + e * NC;
+        float s = 0.f;
+        for (int c = 0; c < NC; ++c) s = fmaf(dzp(f, c), wr[c], s);
+        if (it > 0) {
+          G[f * l.OS + e] = s;  // E == U: dY of iteration it - 1
+        } else if (a.push_table) {
+          const int32_t row = rows[f];
+          if (row >= 0) {
+            if (a.dx_accumulate) s += a.dx[b * F * E + idx];
+            if (e == 0) scan_mark(a.push_flag, row);
+            atomicAdd(a.push_table + (int64_t)row * E + e, s);
+          }
+        } else {
+          float* d = a.dx + b * F * E + idx;
+          *d = a.dx_accumulate ? *d + s : s;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = threadIdx.x; k < 2 * U; k += NT) part[E * NC + NC + k] = acc[k];
+}
+
+GArgs make_args(int64_t B, int F, int E, int U, int H, int L, int use_res, float eps,
+                float drop_rate, uint64_t seed) {
+  GArgs a{};
+  a.B = B; a.F = F; a.E = E; a.U = U; a.H = H; a.L = L; a.DH = U / H; a.use_res = use_res;
+  a.drop = drop_rate > 0.f;
+  a.eps = eps;
+  a.drop_rate = drop_rate;
+  a.inv_keep = drop_rate > 0.f ? 1.0f / (1.0f - drop_rate) : 1.0f;
+  a.sc2 = 1.4426950408889634f / sqrtf((float)(U / H));
+  a.inv_sdh = 1.0f / sqrtf((float)(U / H));
+  a.seed = seed;
+  a.seed_off = (uint64_t)(uintptr_t)rs_seed_offset_now();
+  return a;
+}
+
+}  // namespace gen
+
+int il_generic_fwd(const FwdReq& q) {
+  using namespace gen;
+  if (q.bf16 || q.F > FMAXG || q.U % q.H != 0 || q.E <= 0 || (q.L > 1 && q.E != q.U))
+    return RS_ERR_UNSUPPORTED;
+  const int qt = pick_qt(q.F, q.E, q.U, q.H, false);
+  if (qt == 0) return RS_ERR_UNSUPPORTED;
+  if (q.B == 0) return RS_OK;
+  GArgs a = make_args(q.B, q.F, q.E, q.U, q.H, q.L, q.use_res, q.eps, q.drop_rate, q.seed);
+  a.x = q.x; a.W = q.W; a.bias = q.bias; a.gamma = q.gamma; a.beta = q.beta;
+  a.y = q.y; a.y_ld = q.y_ld; a.xsave = q.xsave;
+  a.g_ids = q.gather_ids; a.g_base = q.gather_base; a.g_bucket = q.gather_bucket;
+  a.g_table = q.gather_table; a.g_table_rows = q.gather_table_rows; a.g_rows = q.gather_rows;
+  a.g_hash = q.gather_hash;
+  a.lay = make_layout(q.F, q.E, q.U, q.H, qt, false);
+  const int64_t grid = q.B < 4096 ? q.B : 4096;
+  fwd_kernel<<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  return rs_status_after_launch();
+}
+
+int il_generic_bwd(const BwdReq& q) {
+  using namespace gen;
+  if (q.bf16 || q.xt_x || q.F > FMAXG || q.U % q.H != 0 || q.E <= 0 || (q.L > 1 && q.E != q.U))
+    return RS_ERR_UNSUPPORTED;
+  const int qt = pick_qt(q.F, q.E, q.U, q.H, true);
+  if (qt == 0) return RS_ERR_UNSUPPORTED;
+  const int nparam = q.E * 4 * q.U + 4 * q.U + 2 * q.U;
+  int64_t grid = q.B < kMaxBwdGrid ? q.B : kMaxBwdGrid;
+  const int64_t max_grid = q.workspace_floats / nparam;
+  if (grid > max_grid) grid = max_grid;
+  if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
+  if (q.B == 0) return RS_OK;
+  if (grid <= 0) return RS_ERR_ARG;
+  GArgs a = make_args(q.B, q.F, q.E, q.U, q.H, q.L, q.use_res, q.eps, q.drop_rate, q.seed);
+  a.x = q.x; a.xsave_in = q.xsave; a.dy = q.dy; a.dy_ld = q.dy_ld;
+  a.W = q.W; a.bias = q.bias; a.gamma = q.gamma; a.beta = q.beta;
+  a.dx = q.dx; a.dx_accumulate = q.dx_accumulate; a.part = q.workspace;
+  a.push_rows = q.push_rows; a.push_table = q.push_table; a.push_flag = q.push_flag;
+  a.lay = make_layout(q.F, q.E, q.U, q.H, qt, true);
+  bwd_kernel<<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  int st = rs_status_after_launch();
+  if (st || !q.dparams) return st;
+  reduce_params(q.stream, q.workspace, (int)grid, nparam, q.dparams, q.dparams_accumulate);
+  return rs_status_after_launch();
+}
+
+}  // namespace rs_il

@@ -9,6 +9,8 @@ RS_IL_DECLARE_UNIT(il_unit_b)
 RS_IL_DECLARE_UNIT(il_unit_c)
 int il_large_fwd(const FwdReq& q);  // il_large.hip: F in (64, 256]
 int il_large_bwd(const BwdReq& q);
+int il_generic_fwd(const FwdReq& q);  // il_generic.hip: any (E, U, H), F <= 256, LDS-bounded
+int il_generic_bwd(const BwdReq& q);
 int64_t il_attn_save_floats(int64_t B, int F, int U, int H, int L);
 
 void reduce_params(hipStream_t s, const float* partials, int nblocks, int nparam, float* out,
@@ -78,10 +80,10 @@ static int il_fwd_impl(void* stream, const float* x, int64_t B, int F, int E, in
                   eps, drop_rate, seed, y, xsave, y_ld};
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
-  if (F > 64) return rs_il::il_large_fwd(q);
-  int r = rs_il::il_unit_a_fwd(q);
-  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
-  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
+  int r = F > 64 ? rs_il::il_large_fwd(q) : rs_il::il_unit_a_fwd(q);
+  if (F <= 64 && r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
+  if (F <= 64 && r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_generic_fwd(q);  // shapes with no instantiation
   return r;
 }
 
@@ -137,6 +139,7 @@ static int il_fwd_gather_impl(void* stream, const int64_t* ids, const int64_t* r
   int r = rs_il::il_unit_a_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_generic_fwd(q);
   return r;
 }
 
@@ -169,7 +172,14 @@ static int bwd_small(const rs_il::BwdReq& q) {
   int r = rs_il::il_unit_a_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
+  if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_generic_bwd(q);  // shapes with no instantiation
   return r;
+}
+
+// F > 64: the many-field instantiations, else the generic kernel
+static int bwd_large(const rs_il::BwdReq& q) {
+  const int r = rs_il::il_large_bwd(q);
+  return r == RS_ERR_UNSUPPORTED ? rs_il::il_generic_bwd(q) : r;
 }
 
 // the deferred weight gradient a backward launch carries (rs_il_bwd_saved_xt /
@@ -200,7 +210,7 @@ static int il_bwd_impl(void* stream, const float* x, const float* xsave, const f
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
   set_xt(q, xt);
-  if (F > 64) return xt ? RS_ERR_UNSUPPORTED : rs_il::il_large_bwd(q);
+  if (F > 64) return xt ? RS_ERR_UNSUPPORTED : bwd_large(q);
   return bwd_small(q);
 }
 
@@ -243,7 +253,6 @@ static int il_bwd_push_impl(void* stream, const float* x, const float* xsave, co
   if (B < 0 || F <= 0 || L <= 0 || H <= 0 || U % H != 0 || (L > 1 && (E != U || !xsave)))
     return RS_ERR_ARG;
   if (drop_rate < 0.f || drop_rate >= 1.f || dy_ld < (int64_t)F * U) return RS_ERR_ARG;
-  if (F > 64) return RS_ERR_UNSUPPORTED;  // the many-field kernels have no fused push
   rs_il::BwdReq q{rs_stream(stream), x, xsave, dy, W, bias, gamma, beta, dy_ld, B, F, E, U, H, L,
                   use_res, eps, drop_rate, seed, const_cast<float*>(dx_base), dx_base != nullptr,
                   dparams, dparams_accumulate, workspace, workspace_floats};
@@ -253,7 +262,8 @@ static int il_bwd_push_impl(void* stream, const float* x, const float* xsave, co
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
   set_xt(q, xt);
-  return bwd_small(q);
+  // F > 64: only the generic kernel fuses the push (the many-field instantiations do not)
+  return F > 64 ? rs_il::il_generic_bwd(q) : bwd_small(q);
 }
 
 RS_API int rs_il_bwd_push(void* stream, const float* x, const float* xsave, const float* dy,

@@ -192,6 +192,12 @@ class BucketedAllReduce:
         cur, cur_lo, cur_hi = [], None, None
         for off, n, p in reversed(spans):
             if id(p) in late_ids:
+                # a late parameter between two early ones ends the bucket: a range spanning it
+                # would all-reduce its gradient during backward (racing rs_l1l2_grad) and again
+                # in finish()
+                if cur:
+                    self.buckets.append((cur_lo, cur_hi - cur_lo, cur))
+                    cur, cur_lo, cur_hi = [], None, None
                 continue
             # adjacent in the arena up to its layer-alignment gap (< 16 floats of zeros)
             contiguous = cur_lo is None or 0 <= cur_lo - (off + n) < 16

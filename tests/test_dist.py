@@ -174,7 +174,7 @@ class _Fn(torch.autograd.Function):
         return gy @ W.t(), None
 
 
-def _bucket_worker(rank, world, port, out):
+def _bucket_worker(rank, world, port, out, late_mid=False, bucket_bytes=700):
     from torch import nn
     from recommendsystem_amd.dist import BucketedAllReduce
     from recommendsystem_amd.params import ParamArena
@@ -185,7 +185,9 @@ def _bucket_worker(rank, world, port, out):
     lin = [nn.Linear(16, 16) for _ in range(4)]
     Wk = nn.Parameter(torch.randn(16, 8) * 0.1)          # the in-place-writer's weight
     reg = nn.Parameter(torch.randn(8, 1) * 0.1)           # a 'late' (regularised) parameter
-    params = [p for l in lin for p in l.parameters()] + [Wk, reg]
+    # late_mid: the small late parameter (8 floats, under the arena's 16-float alignment gap)
+    # sits between two early ones
+    params = [p for l in lin for p in l.parameters()] + ([reg, Wk] if late_mid else [Wk, reg])
     arena = ParamArena(params)
     x = torch.randn(32, 16, generator=torch.Generator().manual_seed(10 + rank))
 
@@ -202,7 +204,7 @@ def _bucket_worker(rank, world, port, out):
     want = arena.grad.clone()
     dist.all_reduce(want)
     # bucketed: 700-B buckets (several per step), issued from the autograd hooks
-    b = BucketedAllReduce(arena, bucket_bytes=700, late=[reg])
+    b = BucketedAllReduce(arena, bucket_bytes=bucket_bytes, late=[reg])
     arena.grad.zero_()
     loss = loss_fn()
     b.arm(loss)
@@ -227,3 +229,18 @@ def test_bucketed_allreduce_during_backward_two_ranks():
     g1, w1, issued1, _ = out[1]
     assert nb > 2 and issued0 > 0 and issued0 == issued1
     assert np.array_equal(g0, w0) and np.array_equal(g1, w1) and np.array_equal(g0, g1)
+
+
+def test_bucketed_allreduce_late_param_between_early_ones():
+    """A small late (regularised) parameter between two early ones, 25 MB buckets: the bucket
+    closes at the late parameter (a range spanning it would reduce its gradient during backward
+    AND in finish(): world x the sum)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(world, _free_port(), out, True, 25 << 20), nprocs=world,
+             join=True)
+    g0, w0, _, nb = out[0]
+    g1, w1, _, _ = out[1]
+    assert nb == 2
+    assert np.array_equal(g0, w0) and np.array_equal(g1, w1)

@@ -244,7 +244,12 @@ IL_CASES = [  # (B, F, E, U, H, L, use_res)
     (11, 19, 8, 8, 2, 1, True),      # multi_head IL(1, 8, 2)
     (5, 26, 16, 8, 2, 1, True),
     (6, 13, 32, 32, 2, 2, True),
-    (4, 26, 16, 128, 1, 1, True),    # constructor defaults (config 1): forward only
+    (4, 26, 16, 128, 1, 1, True),    # constructor defaults (config 1): il_generic.hip
+    (9, 37, 16, 128, 1, 1, True),    # the defaults at the generic kernel's largest F (LDS)
+    (7, 26, 16, 24, 3, 1, True),     # dh = 8 over three heads: il_generic.hip
+    (6, 20, 32, 64, 4, 1, True),     # E 32, U 64, four heads of 16: il_generic.hip
+    (5, 30, 24, 24, 3, 2, False),    # tied iterations at a generic width, no residual
+    (3, 100, 12, 12, 3, 1, True),    # many fields at a generic width (F > 64, il_generic.hip)
     (5, 200, 8, 8, 2, 1, True),      # config 3 multi_head IL(1, 8, 2) over 200 fields (il_large)
     (3, 130, 8, 8, 2, 2, True),      # many fields, tied iterations
     (4, 97, 16, 16, 2, 2, False),
@@ -272,7 +277,7 @@ def test_interacting_forward(case):
     y = il(torch.from_numpy(x).float().to(DEV))
     W, b, g, be = _il_ref_params(il)
     ref = npo.interacting_layer(x.astype(np.float32).astype(np.float64), W, b, g, be, L, H, res)
-    assert_close(_np(y), ref, 2e-5, what=f"IL fwd {case}")
+    assert_close(_np(y), ref, 1e-5, what=f"IL fwd {case}")
 
 
 @pytest.mark.parametrize("F", [26, 20])          # exact-F instantiation and a padded one (FMAX 32)
@@ -318,7 +323,7 @@ def test_il_fwd_gather_matches_lookup_then_fwd(F, hash_mode, id_bits):
     assert torch.equal(y_a, y_b)
 
 
-@pytest.mark.parametrize("case", [c for c in IL_CASES if c[3] <= 32])
+@pytest.mark.parametrize("case", IL_CASES)
 def test_interacting_backward(case):
     from recommendsystem_amd.layers import InteractingLayer
     B, F, E, U, H, L, res = case
@@ -348,15 +353,18 @@ def test_interacting_backward(case):
 
 
 @pytest.mark.parametrize("with_base", [True, False])
-def test_interacting_backward_fused_push(with_base):
+@pytest.mark.parametrize("F,E,U,H,L", [(26, 16, 16, 2, 3), (26, 16, 128, 1, 1), (20, 24, 24, 3, 2),
+                                       (90, 12, 12, 3, 1)])
+def test_interacting_backward_fused_push(with_base, F, E, U, H, L):
     """rs_il_bwd_push == rs_il_bwd's dx (+ dx_base) scattered into the table rows (collisions,
-    skipped -1 rows), rows marked scan-mode; weight partials identical to rs_il_bwd's."""
+    skipped -1 rows), rows marked scan-mode; weight partials identical to rs_il_bwd's.  The
+    generic shapes (il_generic.hip) fuse the push too."""
     from recommendsystem_amd import _lib
     from recommendsystem_amd._lib import call, ptr, stream_handle
-    B, F, E, U, H, L = 64, 26, 16, 16, 2, 3
+    B = 64
     g = torch.Generator(device=DEV).manual_seed(12)
     x = torch.rand(B, F, E, device=DEV, generator=g) - 0.5
-    xs = torch.empty(L - 1, B, F, U, device=DEV)
+    xs = torch.empty(max(L - 1, 1), B, F, U, device=DEV)
     W = (torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.5
     bias = (torch.rand(4 * U, device=DEV, generator=g) - 0.5) * 0.1
     gam = torch.rand(U, device=DEV, generator=g) + 0.5
@@ -393,9 +401,10 @@ def test_interacting_backward_fused_push(with_base):
     assert torch.equal(ws1[:nb * npar], ws2[:nb * npar])
 
 
-def test_interacting_dropout_mask_matches_oracle():
+@pytest.mark.parametrize("E,U,H", [(16, 16, 2), (16, 128, 1), (24, 24, 3)])
+def test_interacting_dropout_mask_matches_oracle(E, U, H):
     from recommendsystem_amd.layers import InteractingLayer
-    B, F, E, U, H, L = 8, 26, 16, 16, 2, 2
+    B, F, L = 8, 26, (2 if E == U else 1)
     rng = np.random.default_rng(9)
     x = rng.uniform(-0.5, 0.5, size=(B, F, E)).astype(np.float32)
     il = InteractingLayer(L, U, H, use_dropout=True, dropout_rate=0.2, seed=11, device=DEV)
@@ -404,7 +413,7 @@ def test_interacting_dropout_mask_matches_oracle():
     y = il(torch.from_numpy(x).to(DEV))
     W, b, g, be = _il_ref_params(il)
     ref = npo.interacting_layer(x.astype(np.float64), W, b, g, be, L, H, True, drop_rate=0.2, seed=seed)
-    assert_close(_np(y), ref, 2e-5, what="IL dropout fwd")
+    assert_close(_np(y), ref, 1e-5, what="IL dropout fwd")
     # and its backward against autograd of the same masked graph
     xd = torch.from_numpy(x).to(DEV).requires_grad_(True)
     il._calls -= 1
@@ -414,6 +423,39 @@ def test_interacting_dropout_mask_matches_oracle():
     tr.interacting_layer(xr, Wt, bt, gt, bet, L, H, True, drop_rate=0.2, seed=seed).sum().backward()
     assert_grad_close(_np(xd.grad), xr.grad.numpy(), what="dropout dx")
     assert_grad_close(_np(il.kernel.grad), Wt.grad.numpy(), what="dropout dW")
+
+
+def test_interacting_ctor_defaults_train():
+    """InteractingLayer() with the reference's constructor defaults (layer_num 1, unit_num 128,
+    head_num 1: InteractingLayer.py:9-16) trains on the GPU (il_generic.hip): five Adam steps on
+    a regression target track the float64 autograd twin step for step, and the loss falls."""
+    from recommendsystem_amd.layers import InteractingLayer
+    B, F, E = 32, 26, 16
+    rng = np.random.default_rng(21)
+    x = rng.uniform(-0.5, 0.5, size=(B, F, E)).astype(np.float32)
+    tgt = rng.normal(size=(B, F, 128)).astype(np.float32)
+    il = InteractingLayer(device=DEV)
+    il.build((B, F, E), device=DEV)
+    ref = [torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il)]
+    opt = torch.optim.Adam(il.parameters(), lr=1e-2)
+    opt_r = torch.optim.Adam(ref, lr=1e-2)
+    xg, tg = torch.from_numpy(x).to(DEV), torch.from_numpy(tgt).to(DEV)
+    xr, tr_ = torch.from_numpy(x).double(), torch.from_numpy(tgt).double()
+    losses = []
+    for _ in range(5):
+        opt.zero_grad()
+        loss = (il(xg) - tg).square().mean()
+        loss.backward()
+        opt_r.zero_grad()
+        loss_r = (tr.interacting_layer(xr, *ref, 1, 1, True) - tr_).square().mean()
+        loss_r.backward()
+        assert abs(float(loss) - float(loss_r)) <= 1e-5 * float(loss_r)
+        for p, q in zip((il.kernel, il.bias, il.gamma, il.beta), ref):
+            assert_grad_close(_np(p.grad), q.grad.numpy(), what="ctor-default grads")
+        opt.step()
+        opt_r.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0]
 
 
 @pytest.mark.parametrize("F,L", [(200, 1), (150, 2)])
