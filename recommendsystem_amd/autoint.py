@@ -141,9 +141,12 @@ class AutoIntTrainer:
                  deterministic: bool = False, metrics=None):
         """metrics: a metrics.CtrMetrics updated with (p, labels) inside every step (the Keras
         'acc' / AUC() / tn.metric.COPC() of rank/ctr/base_model.py:183-190; one more launch per
-        step, captured with the rest).  None (the benchmark) skips it."""
+        step, captured with the rest), or one CtrMetrics per task for a multi-task head (task t
+        reads column t of p and labels).  None (the benchmark) skips it."""
         self.model = m = model
-        self.metrics = metrics
+        if metrics is not None and not isinstance(metrics, (list, tuple)):
+            metrics = [metrics]
+        self.metrics = list(metrics) if metrics is not None else None
         cfg = m.cfg
         self.B = B = int(batch_size)
         self.F, self.E, self.U = F, E, U = cfg.num_fields, cfg.embed_dim, cfg.unit_num
@@ -158,6 +161,8 @@ class AutoIntTrainer:
         self.D = D = cfg.mlp_hidden[-1]
         self.CW = CW = D + F * U
         self.T = self.logit_layers[-1].units
+        if self.metrics is not None and len(self.metrics) != self.T:
+            raise ValueError(f"metrics: one CtrMetrics per task ({self.T}), got {len(self.metrics)}")
         # static inputs
         self.ids = torch.zeros(B, F, device=dev, dtype=torch.int64)
         self.labels = torch.zeros(B, self.T, **f32)
@@ -200,9 +205,15 @@ class AutoIntTrainer:
         self.graph = None
         self.graph_opt = None
         self.pool_graphs = []
-        self.head = self._plan_head()
         if cfg.compute_dtype not in _lib.MATH_MODES:
             raise ValueError(f"compute_dtype must be one of {sorted(_lib.MATH_MODES)}")
+        # the InteractingLayer kernel variant (rs_il_set_variant) is pinned at construction: the
+        # plan below sizes the partial-row reduction from the variant's backward grid, and every
+        # step / capture runs under the same variant (a later process-wide change cannot land the
+        # step on a kernel with another grid)
+        self.il_variant = {v: k for k, v in _lib.IL_VARIANTS.items()}[int(lib.rs_il_get_variant())]
+        with _lib.il_variant(self.il_variant), _lib.math_mode(cfg.compute_dtype):
+            self.head = self._plan_head()
         if cfg.compute_dtype == "bf16" and (self.head is None or self.F > 32 or E != 16 or
                                             U != 16 or self.H != 2 or
                                             (self.head["N1"], self.head["N2"]) != (32, 16)):
@@ -410,13 +421,15 @@ class AutoIntTrainer:
     def _forward_backward(self):
         # math mode of the step; dropout seeds offset by the device step counter (fresh masks on
         # every graph replay, rs_set_seed_offset)
-        with _lib.math_mode(self.model.cfg.compute_dtype), _lib.seed_offset(self.step_count):
+        with _lib.math_mode(self.model.cfg.compute_dtype), _lib.seed_offset(self.step_count), \
+                _lib.il_variant(self.il_variant):
             self._forward_backward_modal()
 
     def _forward_backward_modal(self):
         self._forward_backward_core()
         if self.metrics is not None:
-            self.metrics.update(self.p, self.labels)
+            for t, mt in enumerate(self.metrics):  # column t of the [B, T] outputs / labels
+                mt.update(self.p[:, t:t + 1], self.labels[:, t:t + 1])
 
     def _forward_backward_core(self):
         if self.head is not None:
@@ -591,8 +604,8 @@ class AutoIntTrainer:
         out += [t.m, t.v] if hasattr(t, "m") else [t.g2sum]
         if self.head is not None:
             out.append(self.head["done"])
-        if self.metrics is not None:
-            out.append(self.metrics.state)  # warm-up steps leave the metric totals untouched
+        if self.metrics is not None:  # warm-up steps leave the metric totals untouched
+            out += [mt.state for mt in self.metrics]
         return out
 
     def _warmup(self, steps: int) -> None:

@@ -94,6 +94,22 @@ def _dense_state(trainer):
     return m, v, trainer.step_count
 
 
+def _moment_views(trainer, model):
+    """{parameter name: (m view, v view)}: each parameter's slice of the flat Adam moments (the
+    arenas put alignment gaps between layers, so the flat layout depends on an internal constant;
+    checkpoints store the moments per parameter instead)."""
+    m, v, _ = _dense_state(trainer)
+    arena = getattr(trainer, "arena", None) or getattr(model, "arena", None)
+    base = arena.data.data_ptr()
+    out = {}
+    for n, p in model.named_parameters():
+        off = (p.data_ptr() - base) // 4
+        if not (0 <= off and off + p.numel() <= m.numel()):
+            raise ValueError(f"parameter {n} is not in the trainer's arena")
+        out[n] = (m[off:off + p.numel()].view(p.shape), v[off:off + p.numel()].view(p.shape))
+    return out
+
+
 def _tables(model, trainer, tables):
     if tables is not None:
         return list(tables)
@@ -136,7 +152,9 @@ def save_checkpoint(path: str, model, trainer=None, tables=None) -> str:
         meta["params"] = json.dumps(names)
         st = _dense_state(trainer)
         if st is not None:
-            out["adam/m"], out["adam/v"], out["adam/step"] = st
+            out["adam/step"] = st[2]
+            for n, (mv, vv) in _moment_views(trainer, model).items():
+                out[f"adam/m/{n}"], out[f"adam/v/{n}"] = mv, vv
     tmeta = []
     for i, t in enumerate(tabs):
         if is_sharded(t) or rank == 0:
@@ -188,10 +206,22 @@ def load_checkpoint(path: str, model, trainer=None, tables=None) -> None:
                 params[n].copy_(f.get_tensor(f"dense/{n}"))
             st = _dense_state(trainer)
             if st is not None:
-                if "adam/m" not in f.keys():
+                keys = set(f.keys())
+                if "adam/step" not in keys:
                     raise ValueError("checkpoint holds no dense optimizer state")
-                for dst, k in zip(st, ("adam/m", "adam/v", "adam/step")):
-                    dst.copy_(f.get_tensor(k))
+                if "adam/m" in keys:  # an older flat-moment checkpoint: only the same layout
+                    fm = f.get_tensor("adam/m")
+                    if fm.numel() != st[0].numel():
+                        raise ValueError(f"checkpoint's flat Adam moments ({fm.numel()} floats) do "
+                                         f"not match the trainer's arena ({st[0].numel()}): it was "
+                                         f"written with another parameter layout")
+                    st[0].copy_(fm)
+                    st[1].copy_(f.get_tensor("adam/v"))
+                else:
+                    for n, (mv, vv) in _moment_views(trainer, model).items():
+                        mv.copy_(f.get_tensor(f"adam/m/{n}"))
+                        vv.copy_(f.get_tensor(f"adam/v/{n}"))
+                st[2].copy_(f.get_tensor("adam/step"))
                 # Trainer lr groups: every dense segment has its own Adam step counter, all
                 # advanced once per step (trainer._lr_segments), so they all resume at the step
                 for *_, cnt in getattr(trainer, "segments", ()):

@@ -7,6 +7,8 @@ staytime/model.py:81-82.
 ``CtrMetrics.update(p, y[, w])`` enqueues one accumulation kernel (no host read; safe inside a
 captured HIP graph); ``result()`` reads the totals back (call it between steps, like Keras'
 per-epoch / logging read-out); ``reset_states()`` zeroes them.  Kernels: csrc/metrics.hip.
+The totals are fp64 atomics: counts are exact, but WEIGHTED sums (non-integer w) depend on the
+order the blocks arrive in, so they can differ in the last bits from run to run.
 """
 from __future__ import annotations
 

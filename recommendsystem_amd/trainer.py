@@ -332,10 +332,19 @@ class Trainer:
                 t.copy_(v)
             torch.cuda.synchronize()
 
+    # sync-free DP: the sticky overflow word is read back every this many replays (one host
+    # read), so a run whose caps are too small stops within that many steps instead of training
+    # on truncated sparse gradients
+    dp_check_every = 256
+
     def step_pool(self, i: int):
         k = i % len(self.graphs)
         self.graphs[k].replay()
         if self.graph_opt is not None:
             self._dp_exchange()
             self.graph_opt.replay()
+            if self.dp_caps is not None:
+                self._dp_replays = getattr(self, "_dp_replays", 0) + 1
+                if self._dp_replays % self.dp_check_every == 0:
+                    self.check_dp_overflow()
         return self.graph_loss[k]

@@ -2,6 +2,7 @@
 Adam state and the sparse tables with their optimizer slots; owner-sharded checkpoints written
 by a gloo world-2 run load into a replicated table and into a world-3 sharded one; mismatched
 models are refused.  The named outputs / sub_models run kernels: tests/test_gpu_export.py."""
+import json
 import os
 import socket
 
@@ -25,9 +26,10 @@ def _model(seed, shard_group=None):
 
 def _perturb(j, trn, seed):
     g = torch.Generator().manual_seed(seed)
-    with torch.no_grad():
-        trn.m.copy_(torch.randn(trn.m.shape, generator=g))
-        trn.v.copy_(torch.rand(trn.v.shape, generator=g))
+    with torch.no_grad():  # per parameter: the arena's alignment gaps keep zero moments
+        for mv, vv in export._moment_views(trn, j).values():
+            mv.copy_(torch.randn(mv.shape, generator=g))
+            vv.copy_(torch.rand(vv.shape, generator=g))
         trn.step_count.fill_(7)
         j.table.g2sum.add_(torch.rand(j.table.g2sum.shape, generator=g))
 
@@ -108,7 +110,27 @@ def test_sharded_checkpoint_reshards(tmp_path):
     for r in range(2):
         assert torch.equal(rep.table.weight[r::2], parts[r]["table0/weight"])
         assert torch.equal(rep.table.g2sum[r::2], parts[r]["table0/g2sum"])
-    assert torch.equal(trep.m, parts[0]["adam/m"]) and int(trep.step_count) == 7
+    for n, (mv, vv) in export._moment_views(trep, rep).items():  # per-parameter Adam moments
+        assert torch.equal(mv, parts[0][f"adam/m/{n}"]) and torch.equal(vv, parts[0][f"adam/v/{n}"])
+    assert int(trep.step_count) == 7
+    # an older flat-moment checkpoint of another layout is refused with a clear error
+    from safetensors import safe_open
+    from safetensors.torch import save_file
+    with safe_open(os.path.join(path, "ckpt.rank0-of-2.safetensors"), framework="pt") as f:
+        meta = f.metadata()
+    old = {k: v for k, v in parts[0].items() if not k.startswith("adam/")}
+    old.update({"adam/m": torch.zeros(3), "adam/v": torch.zeros(3), "adam/step": parts[0]["adam/step"]})
+    legacy = tmp_path / "legacy"
+    os.makedirs(legacy)
+    save_file(old, str(legacy / "ckpt.safetensors"), metadata={**meta, "world": "1"})
+    t_old = {**meta}
+    tm = json.loads(t_old["tables"])
+    for t in tm:
+        t["sharded"] = False
+    save_file({**old, "table0/weight": rep.table.weight, "table0/g2sum": rep.table.g2sum},
+              str(legacy / "ckpt.safetensors"), metadata={**meta, "world": "1", "tables": json.dumps(tm)})
+    with pytest.raises(ValueError, match="another parameter layout"):
+        export.load_checkpoint(str(legacy), *_model(4))
     # into a world-3 sharded table
     out = mp.Manager().dict()
     mp.spawn(_load_worker, args=(3, _free_port(), path, out), nprocs=3, join=True)

@@ -95,3 +95,33 @@ def test_dp_trainer_graph_equals_eager(kind, sync_free):
         np.testing.assert_allclose(gt, et, rtol=1e-6, atol=1e-7, err_msg=f"rank {r} table")
     assert np.array_equal(out[0][3][0], out[1][3][0]), "graph DP: dense replicas diverged"
     assert np.array_equal(out[0][3][1], out[1][3][1]), "graph DP: table replicas diverged"
+
+
+def _overflow_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, trn, batches = _build("din", rank)
+    trn.capture_pool(batches, warmup=1, dp_caps=[8])  # far fewer rows than one step touches
+    trn.dp_check_every = 2
+    trn.step_pool(0)
+    raised = False
+    try:
+        trn.step_pool(1)  # the periodic read-back
+    except RuntimeError as e:
+        raised = "overflow" in str(e)
+    torch.cuda.synchronize()
+    out[rank] = raised
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_caps_overflow_is_reported():
+    """capture_pool(dp_caps) with caps below the rows a rank touches: step_pool reads the sticky
+    overflow word back every dp_check_every replays and raises (never trains on silently
+    truncated sparse gradients)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_overflow_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    assert out[0] and out[1]

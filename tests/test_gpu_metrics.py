@@ -76,3 +76,31 @@ def test_autoint_trainer_metrics_match_oracle():
     want = npo.ctr_metrics(np.concatenate(ps), np.concatenate(ys))
     for k in ("auc", "acc", "copc", "ctr"):
         assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k])), (k, got[k], want[k])
+
+
+def test_autoint_trainer_metrics_per_task():
+    """A two-task head (logits [2]) with one CtrMetrics per task: task t accumulates column t of
+    p and labels (a single CtrMetrics for T = 2 is refused at construction)."""
+    import pytest
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
+    from recommendsystem_amd.metrics import CtrMetrics
+    cfg = AutoIntConfig(vocab_per_field=1000, logits_hidden=(2,))
+    model = AutoInt(cfg, device=DEV, seed=1, max_batch=128)
+    with pytest.raises(ValueError):
+        AutoIntTrainer(model, 128, metrics=CtrMetrics(device=DEV))
+    ms = [CtrMetrics(device=DEV), CtrMetrics(device=DEV)]
+    tr = AutoIntTrainer(model, 128, metrics=ms)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    ps, ys = [], []
+    for _ in range(2):
+        ids = torch.randint(0, 1000, (128, 26), device=DEV, generator=g)
+        lab = (torch.rand(128, 2, device=DEV, generator=g) < 0.3).float()
+        tr.step(ids, lab)
+        ps.append(tr.p.detach().cpu().numpy().copy())
+        ys.append(lab.cpu().numpy())
+    P, Y = np.concatenate(ps), np.concatenate(ys)
+    for t in range(2):
+        got = ms[t].result()
+        want = npo.ctr_metrics(P[:, t:t + 1], Y[:, t:t + 1])
+        for k in ("auc", "acc", "copc", "ctr"):
+            assert abs(got[k] - want[k]) <= 1e-6 * max(1.0, abs(want[k])), (t, k, got[k], want[k])
