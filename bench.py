@@ -275,6 +275,7 @@ def workload_roofline(args, model, pool, B, dev):
                 f"{nvalid} ids)", "achieved": round(by / t / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(by / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
                 "launch_us": round(t * 1e6, 2), "bytes_per_launch": by}
+    out = staytime_gather_roofline(model, pool, B, dev, args.kernel_reps)
     K, N = 1712, 256
     X = torch.randn(B, K, device=dev, generator=g)
     Wt = torch.randn(K, N, device=dev, generator=g) * 0.02
@@ -283,10 +284,92 @@ def workload_roofline(args, model, pool, B, dev):
     t = time_kernel(lambda: call("rs_dense_fwd", s, ptr(X), B, K, K, ptr(Wt), ptr(bt), N, 1, ptr(Y), N),
                     args.kernel_reps)
     fl = 2 * B * K * N
-    return {"bound": "mfma", "kernel": f"gemm_kernel via rs_dense_fwd [{B}x{K}]x[{K}x{N}] relu (staytime "
-            "expert layer 1)", "achieved": round(fl / t / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(fl / t / 1e12 / FP32_PEAK_TFLOPS, 4), "traffic": None,
-            "launch_us": round(t * 1e6, 2), "flops_per_launch": fl}
+    out["gemm_roofline"] = {
+        "bound": "mfma", "kernel": f"gemm_kernel via rs_dense_fwd [{B}x{K}]x[{K}x{N}] relu (staytime "
+        "expert layer 1)", "achieved": round(fl / t / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s", "frac": round(fl / t / 1e12 / FP32_PEAK_TFLOPS, 4), "traffic": None,
+        "launch_us": round(t * 1e6, 2), "flops_per_launch": fl}
+    return out
+
+
+# config-5 gather side, algorithmic bytes (dim-32 fp32 rows = 128 B)
+LOOKUP_BYTES_PER_ID = 8 + 4 + 2 * 128      # id, hashed row out, row read, output row write
+SEQ_BYTES_PER_SLOT = 128 + 1 + 4           # output row (zero past the length), mask, row index
+SEQ_BYTES_PER_ID = 8 + 128                 # id, row read
+PUSH_BYTES_PER_ID32 = 4 + 128              # row index, dout row (per id)
+ROW_BYTES_PER_UNIQUE = 2 * 128 + 4 + 6 * 128 + 4   # grad row RMW + flag (push), AdaGrad: w, g2sum,
+#                                            grad read + write (zeroed), touched-list entry
+
+
+def staytime_gather_roofline(model, pool, B, dev, reps):
+    """Config 5's HBM-bound gather side (BASELINE.json configs[4] "HBM-bound gather roofline"),
+    timed live with HIP events on torch's current stream: the step's five lookups (91 single-hot
+    fields, 3 x 50-long sequences, 52 DSSM fields; rs_embedding_lookup_fwd /
+    rs_sequence_lookup_fwd), their five pushes into the gradient table (list mode: election +
+    claim kernels, rs_sparse_grad_accumulate_ws) and the sparse AdaGrad over the touched rows --
+    exactly the table-side launches of one training step, on pool batch 0.  Algorithmic bytes:
+    per id its id, row read, output write and dout read; per unique row the gradient row
+    read-modify-write, flag and the optimizer's row traffic."""
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    from recommendsystem_amd.embedding import COMBINERS
+    t = model.table
+    st_ids, seq_ids, seq_offs, rr_ids = pool[0][0], pool[0][1], pool[0][2], pool[0][3]
+    d = t.dim
+    g = torch.Generator(device=dev).manual_seed(8)
+    jobs = []  # (kind, layer, ids, offsets, F or T, out, rows, dout)
+    for lay, ids in ((model.fields, st_ids), (model.rr_fields, rr_ids)):
+        F = lay.num_fields
+        jobs.append(("fields", lay, ids, None, F, torch.empty(B, F, d, device=dev),
+                     torch.empty(B * F, device=dev, dtype=torch.int32),
+                     torch.randn(B, F, d, device=dev, generator=g)))
+    for lay, ids, offs in zip(model.seqs, seq_ids, seq_offs):
+        T = lay.seq_max_len
+        jobs.append(("seq", lay, ids, offs, T, torch.empty(B, T, d, device=dev),
+                     torch.empty(B * T, device=dev, dtype=torch.int32),
+                     torch.randn(B, T, d, device=dev, generator=g)))
+    mask = torch.empty(B, max(j[4] for j in jobs), device=dev, dtype=torch.uint8)
+    lens = torch.empty(B, device=dev, dtype=torch.int32)
+
+    def gather_side():
+        s = stream_handle()
+        for kind, lay, ids, offs, F, out, rows, _ in jobs:
+            if kind == "fields":
+                call("rs_embedding_lookup_fwd", s, ptr(ids), None, B, F, ptr(lay.row_base),
+                     ptr(lay.bucket), lay.hash_mode, lay.combiner, ptr(t.weight), t.rows, d,
+                     ptr(out), F * d, d, ptr(rows))
+            else:
+                call("rs_sequence_lookup_fwd", s, ptr(ids), ptr(offs), B, F, lay.row_base,
+                     lay.bucket, lay.hash_mode, ptr(t.weight), d, ptr(out), F * d, d, ptr(mask),
+                     F, ptr(lens), ptr(rows))
+        for kind, lay, ids, offs, F, out, rows, dout in reversed(jobs):
+            t.accumulate(rows, None, B, F, dout, F * d, d,
+                         lay.combiner if kind == "fields" else COMBINERS["sum"])
+        t.step(grad_scale=1.0)
+
+    saved = [x.clone() for x in (t.weight, t.g2sum)]
+    sec = time_kernel(gather_side, reps)
+    t.weight.copy_(saved[0])
+    t.g2sum.copy_(saved[1])
+    n_ids = n_slots_seq = n_ids_seq = 0
+    all_rows = []
+    for kind, lay, ids, offs, F, out, rows, _ in jobs:
+        valid = rows[rows >= 0]
+        all_rows.append(valid)
+        if kind == "fields":
+            n_ids += B * F
+        else:
+            n_slots_seq += B * F
+            n_ids_seq += int(valid.numel())
+    uniq = int(torch.unique(torch.cat(all_rows)).numel())
+    by = (LOOKUP_BYTES_PER_ID * n_ids + SEQ_BYTES_PER_SLOT * n_slots_seq +
+          SEQ_BYTES_PER_ID * n_ids_seq + PUSH_BYTES_PER_ID32 * (n_ids + n_ids_seq) +
+          ROW_BYTES_PER_UNIQUE * uniq)
+    return {"bound": "hbm", "kernel": "gather side of one step: 5 lookups (91 fields, 3 x 50 "
+            "sequences, 52 DSSM fields) + 5 pushes (election + claim) + sparse AdaGrad, "
+            f"{n_ids + n_ids_seq} ids, {uniq} unique rows of the 10M x 32 table",
+            "achieved": round(by / sec / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(by / sec / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "launch_us": round(sec * 1e6, 2), "bytes_per_launch": by}
 
 
 def workload_cpu_baseline(args, model, rng, B):
@@ -487,16 +570,23 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     il = model.interact
     E, U, H, L = cfg.embed_dim, cfg.unit_num, cfg.head_num, cfg.layer_num
 
+    xt = trainer.head["xt"] if trainer.head is not None else None
+    hd = trainer.head
+
     def il_bwd_once():
         # the exact launch the step makes: backward + fused sparse push into the gradient table
-        # (scan-mode marks); it adds into table.grad, which only matters after the timed region
-        # (the saved pair: it reads the forward's attention save left by the last step)
+        # (scan-mode marks) + the head's deferred dW1 = x0^T dz1 rows (rs_il_bwd_push_saved_xt);
+        # it adds into table.grad, which only matters after the timed region (the saved pair: it
+        # reads the forward's attention save left by the last step)
         t = model.table
-        call("rs_il_bwd_push_saved", stream_handle(), ptr(trainer.x0), ptr(trainer.xsave),
+        xa = (ptr(trainer.x0), F * E, ptr(xt["dz1"]), hd["N1"], hd["K0"], hd["N1"],
+              ptr(xt["slab"])) if xt else ()
+        call("rs_il_bwd_push_saved_xt" if xt else "rs_il_bwd_push_saved", stream_handle(),
+             ptr(trainer.x0), ptr(trainer.xsave),
              trainer.dcat.data_ptr() + 4 * trainer.D, trainer.CW, B, F, E, U, H, L,
              ptr(il.kernel), ptr(il.bias), ptr(il.gamma), ptr(il.beta), il.epsilon, 1, 0.0, 0,
              ptr(trainer.dx0), ptr(trainer.rows), ptr(t.grad), ptr(t.flag), None, 0,
-             ptr(trainer.il_ws), trainer.il_ws_n, ptr(trainer.asave), trainer.asave_n)
+             ptr(trainer.il_ws), trainer.il_ws_n, ptr(trainer.asave), trainer.asave_n, *xa)
 
     def il_fwd_once():
         call("rs_il_fwd_saved", stream_handle(), ptr(trainer.x0), B, F, E, U, H, L,
@@ -509,19 +599,25 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     with _lib.math_mode(compute_dtype):
         t_bwd = time_kernel(il_bwd_once, args.kernel_reps)
         t_fwd = time_kernel(il_fwd_once, args.kernel_reps)
-    bwd_flops = 2 * IL_FWD_FLOPS_PER_SAMPLE * B
+    # backward = 2 x the forward's matmul FLOPs, plus the deferred dW1 (2 K0 N1 per sample) the
+    # launch carries when the head defers it
+    bwd_flops = (2 * IL_FWD_FLOPS_PER_SAMPLE + (2 * hd["K0"] * hd["N1"] if xt else 0)) * B
     achieved = bwd_flops / t_bwd / 1e12
     # HBM traffic is not measurable inside this run (PMC needs its own rocprofv3 --pmc passes):
-    # the value is the committed PMC measurement of the same launch, labelled as such
+    # the value is the committed PMC measurement of the same launch (tools/il_traffic.py over
+    # this bench's own step), labelled as such
     traffic, traffic_src = None, None
-    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")  # from tools/profile_round.sh
+    kname = "rs_il::bwd4_kernel" if B > 1536 else "rs_il::wbwd_kernel"
+    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")
     if compute_dtype == "f32" and os.path.exists(tf_path):
         with open(tf_path) as f:
             tj = json.load(f)
-        if "bwd4" in tj.get("kernel", ""):
+        if tj.get("per_gpu_batch") == B and tj.get("kernel", "").split("<")[0] in kname and \
+                tj.get("launch") == ("rs_il_bwd_push_saved_xt" if xt else "rs_il_bwd_push_saved"):
             traffic = tj.get("hbm_bytes_per_launch")
-            traffic_src = ("committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes) "
-                           "in profiles/il_bwd_traffic.json, not measured in this run")
+            traffic_src = (f"committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes) "
+                           f"in profiles/il_bwd_traffic.json ({tj.get('source', '')}), not measured "
+                           f"in this run")
 
     samples = B * args.steps * world
     # BASELINE.md §3 step roofline: max(sum bytes / HBM BW, sum flops / peak), per GPU
@@ -552,9 +648,9 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
                    "global_batch": B * world, "per_gpu_batch": B, "fields": F, "emb_dim": E,
                    "layer_num": L,
                    "head_num": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": ("rs_il::bwd4_kernel" if B > 1536 else "rs_il::wbwd_kernel")
+        "roofline": {"bound": "mfma", "kernel": kname
                      + " (InteractingLayer backward over the forward's attention save + fused sparse "
-                       "push; the step's launch also carries the head's deferred dW1, not counted here)",
+                       "push" + (" + the head's deferred dW1, counted)" if xt else ")"),
                      "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
