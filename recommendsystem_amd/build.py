@@ -78,7 +78,10 @@ def build(verbose: bool = False, extra: list[str] | None = None) -> str:
     stamp = os.path.join(BUILD_DIR, "lib.flags")
     prev = open(stamp).read() if os.path.exists(stamp) else None
     if _newer(LIB_PATH, objs) or prev != _tag(extra):
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB_PATH]
+        # a host-sanitizer build (-Xarch_host -fsanitize=...) links the shared sanitizer runtime
+        san = [f for f in extra if f.startswith("-fsanitize=")]
+        link = [*san, "-shared-libasan"] if san else []
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *link, *objs, "-o", LIB_PATH]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

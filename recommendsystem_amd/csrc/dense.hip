@@ -464,6 +464,11 @@ static GemmPlan finish_plan(GemmPlan p, int64_t R) {
 
 static GemmPlan plan_gemm(int64_t M, int64_t N, int64_t R, bool allow_split) {
   const GemmTune& tu = gemm_tune();
+  // degenerate extents (size queries of empty or invalid shapes; the launches reject them
+  // before planning) plan as one tile: no tile count of 0 divides below
+  if (M < 1) M = 1;
+  if (N < 1) N = 1;
+  if (R < 0) R = 0;
   GemmPlan p;
   p.mf = 16;
   if (M * N * R >= tu.big_macs) {
@@ -581,6 +586,7 @@ RS_API int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const 
 }
 
 RS_API int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N) {
+  if (M < 0 || K <= 0 || N <= 0) return 0;  // (rs_dense_bwd_weight rejects these shapes)
   const GemmPlan p = plan_gemm(K, N, M, true);
   return (int64_t)p.splits * ((int64_t)K * N + N);
 }
@@ -832,6 +838,7 @@ static bool weight_group_plan(int G, const int64_t* desc, GroupPlan& gp) {
   int64_t shape[kMaxGroup][3];
   for (int p = 0; p < G; ++p) {
     const int64_t* d = desc + GD_BWD_WEIGHT * p;
+    if (d[0] <= 0 || d[1] <= 0 || d[2] <= 0) return false;  // (M, K, N)
     shape[p][0] = d[1]; shape[p][1] = d[2]; shape[p][2] = d[0];  // C[K, N] over M rows
   }
   return plan_group(G, shape, true, gp);
