@@ -446,9 +446,15 @@ def run_workload(args, world, rank, dev, pg):
         trainer = Trainer(model, 5e-4, [model.table], process_group=pg,
                           lr_groups=[(model.dssm, model.rr_cfg.lr_dense)])
         pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
-    graphed = world == 1 and not args.eager
+    sharded = getattr(model.table, "sharded", False)
+    graphed = not args.eager and not sharded
+    dp_caps = None
     if graphed:  # one HIP graph per pool batch (forward + autograd backward + optimizers)
-        trainer.capture_pool(pool, warmup=1)
+        if world > 1:
+            # the sync-free captured DP step: fixed-capacity all-gathers sized from the pool's
+            # own touched-row counts (max over ranks, 25 % headroom; overflow is detected)
+            dp_caps = trainer.measure_dp_caps(pool)
+        trainer.capture_pool(pool, warmup=1, dp_caps=dp_caps)
         step = trainer.step_pool
     else:
         def step(i):
@@ -475,6 +481,8 @@ def run_workload(args, world, rank, dev, pg):
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+    if dp_caps is not None:
+        trainer.check_dp_overflow()  # (outside the timed region)
     samples = B * args.steps * world
     roofline = workload_roofline(args, model, pool, B, dev)
     cpu = None
@@ -488,7 +496,9 @@ def run_workload(args, world, rank, dev, pg):
            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                       "parallelism": f"dp{world}",
                       "table": "owner-sharded" if getattr(model.table, "sharded", False) else "replicated",
-                      "execution": "one HIP graph per pool batch" if graphed else "eager autograd"},
+                      "execution": ("one HIP graph per pool batch" + (
+                          f" + sync-free fixed-capacity exchange (dp_caps {dp_caps})" if dp_caps
+                          else "")) if graphed else "eager autograd"},
            "roofline": roofline, "cpu_baseline": cpu, "final_loss": round(float(loss.detach()), 6)}
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -237,18 +237,28 @@ class AutoIntTrainer:
         if self.packed_dp:
             n = m.arena.n
             self.dp_n = n
-            self.dp_ld = ld = (n + 1 + 3) // 4 * 4
-            self.dp_send = torch.zeros(ld, **f32)
-            self.dp_recv = torch.zeros(self.world * ld, **f32)
             self.dp_rs = E + 1
-            self.dp_cap = B * F  # one rank touches at most B * F rows per step
-            self.dp_recs = torch.empty(self.dp_cap * self.dp_rs, **f32)
-            self.dp_recs_all = torch.empty(self.world * self.dp_cap * self.dp_rs, **f32)
             self.dp_nmax = 0
-            # exchange without a host read (dist.exchange_packed_fixed); RS_DP_SYNC=1 restores
-            # the count-sized exchange with one host synchronisation per step (A/B)
+            # exchange without a host read; RS_DP_SYNC=1 restores the count-sized exchange with
+            # one host synchronisation per step (A/B)
             import os
             self.dp_sync_free = not os.environ.get("RS_DP_SYNC")
+            if self.dp_sync_free:
+                # ONE all-gather per step (dist.packed_layout): [dense grad | count | records],
+                # cap = B x F records (one rank touches at most that many rows per step)
+                from .dist import packed_layout
+                self.dp_ld, self.dp_cap, self.dp_S = packed_layout(n, B * F, self.dp_rs)
+                self.dp_buf = torch.zeros(self.dp_S, **f32)
+                self.dp_send = self.dp_buf[:self.dp_ld]
+                self.dp_recs = self.dp_buf[self.dp_ld:]
+                self.dp_all = torch.zeros(self.world * self.dp_S, **f32)
+            else:
+                self.dp_ld = ld = (n + 1 + 3) // 4 * 4
+                self.dp_cap = B * F
+                self.dp_send = torch.zeros(ld, **f32)
+                self.dp_recv = torch.zeros(self.world * ld, **f32)
+                self.dp_recs = torch.empty(self.dp_cap * self.dp_rs, **f32)
+                self.dp_recs_all = torch.empty(self.world * self.dp_cap * self.dp_rs, **f32)
         elif self.world > 1:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
@@ -507,12 +517,11 @@ class AutoIntTrainer:
 
     def _exchange(self):
         """Data-parallel gradient exchange (recommendsystem_amd/dist.py)."""
-        from .dist import allreduce_flat, exchange_packed, exchange_packed_fixed, gather_sparse_lists
+        from .dist import allreduce_flat, exchange_packed, exchange_packed_merged, gather_sparse_lists
         m, t = self.model, self.model.table
         if self.packed_dp:
             if self.dp_sync_free:
-                exchange_packed_fixed(self.dp_send, self.dp_recv, self.dp_recs, self.dp_recs_all,
-                                      self.dp_cap, self.dp_rs, self.pg)
+                exchange_packed_merged(self.dp_buf, self.dp_all, self.pg)
                 return
             self.dp_nmax = exchange_packed(self.dp_send, self.dp_recv, self.dp_n, self.dp_recs,
                                            self.dp_recs_all, self.dp_rs, self.pg)
@@ -536,6 +545,13 @@ class AutoIntTrainer:
                  t.dim, ptr(t.grad), ptr(t.flag), None if scan else ptr(t.touched),
                  None if scan else ptr(t.n_touched), t.touched_cap)
 
+    def dp_gathered_counts(self) -> torch.Tensor:
+        """Every rank's record count of the last packed exchange, read from the gathered
+        buffers (tests / diagnostics: the sync-free step itself never reads them on the host)."""
+        if self.dp_sync_free:
+            return self.dp_all.view(torch.int32).view(self.world, self.dp_S)[:, self.dp_n]
+        return self.dp_recv.view(torch.int32).view(self.world, self.dp_ld)[:, self.dp_n]
+
     def _optimize(self):
         m, cfg = self.model, self.model.cfg
         ar = m.arena
@@ -557,11 +573,16 @@ class AutoIntTrainer:
         scale = 1.0 / self.world
         if self.packed_dp:
             s, t = stream_handle(), m.table
-            counts = self.dp_recv.data_ptr() + 4 * self.dp_n
+            if self.dp_sync_free:  # the merged layout: rank r's block at r * S
+                gat, row_ld = self.dp_all, self.dp_S
+                recs, stride = self.dp_all.data_ptr() + 4 * self.dp_ld, self.dp_S // self.dp_rs
+            else:
+                gat, row_ld = self.dp_recv, self.dp_ld
+                recs, stride = self.dp_recs_all.data_ptr(), 0
+            counts = gat.data_ptr() + 4 * self.dp_n
             for r in range(self.world):  # rank order: identical sums on every replica
-                call("rs_sparse_merge_packed_stride", s, ptr(self.dp_recs_all), counts,
-                     self.dp_ld, self.world, r, t.dim, ptr(t.grad), ptr(t.flag), t.rows,
-                     self.dp_cap, self.dp_cap if self.dp_sync_free else 0)
+                call("rs_sparse_merge_packed_stride", s, recs, counts, row_ld, self.world, r,
+                     t.dim, ptr(t.grad), ptr(t.flag), t.rows, self.dp_cap, stride)
             # dense: rank-ordered sum of the gathered buckets -> arena grad -> Adam, one launch
             tail = self._scan_tail(t)
             # small per-rank batches: walk the gathered records (the rows the merges marked, at
@@ -570,9 +591,10 @@ class AutoIntTrainer:
             rows_max = int(os.environ.get("RS_SPARSE_ROWS_MAXN", str(ROWS_MODE_MAXN)))
             rows = None
             if tail is not None and self.dp_sync_free and self.B * self.F <= rows_max:
-                rows = (self.dp_recs_all.data_ptr(), self.world * self.dp_cap, self.dp_rs,
-                        counts, self.dp_ld, self.dp_cap)
-            _lib.partials_reduce_adam(s, [(ptr(self.dp_recv), self.dp_ld, self.world, self.dp_n,
+                # segment r = rank r's block seen as records from its record start: its first
+                # count entries are rank r's records (the rest: padding / the next dense part)
+                rows = (recs, self.world * stride, self.dp_rs, counts, row_ld, stride)
+            _lib.partials_reduce_adam(s, [(ptr(gat), row_ld, self.world, self.dp_n,
                                            ptr(ar.grad), 1.0, 0)], ar.data, self.adam_m,
                                       self.adam_v, self.step_count, self.head["done"],
                                       cfg.lr_dense, 0.9, 0.999, 1e-8, scale, True,

@@ -104,6 +104,46 @@ def exchange_packed_fixed(send: torch.Tensor, recv: torch.Tensor, recs: torch.Te
     _all_gather_flat(recs_all[:world * k], recs[:k], group)
 
 
+def packed_layout(n_dense: int, cap: int, rec_floats: int):
+    """The merged send buffer of the sync-free AutoInt exchange: ONE all-gather per step.
+
+    [dense gradient (n_dense) | record count (int32 bits) | pad | records (cap x rec_floats)]
+    ld (the dense part) is rounded up to a multiple of lcm(4, rec_floats) and cap to a multiple
+    of 4, so the per-rank block S = ld + cap * rec_floats keeps 16-B row alignment for the dense
+    sum and every rank's records start on a record boundary: in the gathered buffer rank r's
+    records are at (r * S + ld) floats = record (r * S + ld) / rec_floats, i.e. a record stride
+    of S / rec_floats per rank (rs_sparse_merge_packed_stride).  Returns (ld, cap, S)."""
+    import math
+    q = 4 * rec_floats // math.gcd(4, rec_floats)
+    ld = -(-(n_dense + 1) // q) * q
+    cap = -(-cap // 4) * 4
+    return ld, cap, ld + cap * rec_floats
+
+
+def exchange_packed_merged(buf: torch.Tensor, buf_all: torch.Tensor, group=None) -> None:
+    """exchange_packed_fixed in ONE collective: every rank's whole packed_layout buffer (dense
+    gradient, count, capacity-sized records) all-gathered into buf_all [world * S] -- half the
+    collective launches of the two-gather form, no host read."""
+    _all_gather_flat(buf_all, buf, group)
+
+
+def merge_packed_merged_reference(buf_all, S, ld, n_dense, rec_floats, table_grad):
+    """Host restatement of the merges over the merged layout (CPU tests): rank r's count at
+    r * S + n_dense, its records from r * S + ld."""
+    world = buf_all.numel() // S
+    counts = buf_all.view(torch.int32).view(world, S)[:, n_dense].tolist()
+    touched = []
+    for r in range(world):
+        for u in range(counts[r]):
+            off = r * S + ld + u * rec_floats
+            rec = buf_all[off:off + rec_floats]
+            row = int(rec[:1].view(torch.int32)[0])
+            if row not in touched:
+                touched.append(row)
+            table_grad[row] += rec[1:].numpy()
+    return touched
+
+
 def merge_packed_reference(recv, ld, n_dense, recs_all, rec_floats, table_grad, stride=0):
     """Host restatement of rs_sparse_merge_packed (stride 0: rank r's records at r * nmax) /
     rs_sparse_merge_packed_stride (at r * stride) over every rank in order (CPU tests)."""
@@ -156,6 +196,14 @@ def exchange_counts(counts: torch.Tensor, group=None):
     recv = torch.empty_like(counts)
     all_to_all_v(recv, counts, [1] * world, [1] * world, group)
     return counts.tolist(), recv.tolist()
+
+
+def auto_bucket_bytes(arena_bytes: int) -> int:
+    """Default dense bucket for an arena of arena_bytes: about a quarter of it, between 1 MB and
+    25 MB -- several buckets for the configs-3/5 arenas (2.2 MB -> 1 MB, 13.9 MB -> 3.5 MB), so
+    the first ones go out while backward still runs, yet each all-reduce stays large enough for
+    the per-link bandwidth of xGMI (ring collectives pay a fixed latency per call)."""
+    return int(min(25 << 20, max(1 << 20, arena_bytes // 4)))
 
 
 class BucketedAllReduce:

@@ -51,7 +51,7 @@ class Trainer:
     is a contiguous range of the arena with its own step counter (same count every step)."""
 
     def __init__(self, model, lr_dense: float, tables=(), process_group=None, beta1=0.9,
-                 beta2=0.999, eps=1e-8, lr_groups=(), bucket_mb: float = 25.0):
+                 beta2=0.999, eps=1e-8, lr_groups=(), bucket_mb: float | None = None):
         self.model = model
         self.arena = ParamArena(model.parameters(), align=ARENA_ALIGN)
         dev = self.arena.data.device
@@ -74,11 +74,13 @@ class Trainer:
             if hasattr(model, "modules") else []
         # eager DP: the dense all-reduce in buckets issued during backward (dist.BucketedAllReduce;
         # regularised parameters in the final bucket, after rs_l1l2_grad); bucket_mb <= 0: one
-        # all-reduce after backward
+        # all-reduce after backward; None: sized from the arena (auto_bucket_bytes)
         self.bucketer = None
-        if self.world > 1 and bucket_mb and bucket_mb > 0:
-            from .dist import BucketedAllReduce
-            self.bucketer = BucketedAllReduce(self.arena, process_group, int(bucket_mb * (1 << 20)),
+        if self.world > 1 and (bucket_mb is None or bucket_mb > 0):
+            from .dist import BucketedAllReduce, auto_bucket_bytes
+            nbytes = (auto_bucket_bytes(4 * self.arena.n) if bucket_mb is None
+                      else int(bucket_mb * (1 << 20)))
+            self.bucketer = BucketedAllReduce(self.arena, process_group, nbytes,
                                               late=[p for p, _, _ in self.regs])
         if self.world == 1:
             # single-GPU: tables that ask for it run in scan mode (pushes mark flags with plain
@@ -269,6 +271,36 @@ class Trainer:
         for p, l1, l2 in self.regs:
             call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
         return loss
+
+    def measure_dp_caps(self, batches, headroom: float = 1.25, quantum: int = 256):
+        """dp_caps for capture_pool from the batches themselves: each batch's forward/backward
+        runs once (eagerly, no collectives) and every replicated table's claimed-row count is
+        read back; the per-table maximum over batches and ranks (one all-reduce MAX: every rank
+        must use the same capacities), times ``headroom``, rounded up to ``quantum``, capped at
+        the touched-list size.  The training state is restored afterwards.  A later step that
+        touches more rows is caught by the sticky overflow word (step_pool reads it every
+        dp_check_every replays), never trained on silently."""
+        rep = [t for t in self.tables if not is_sharded(t)]
+        saved = [t.clone() for t in self._state()]
+        peak = torch.zeros(max(len(rep), 1), dtype=torch.int64)
+        for b in batches:
+            for t in rep:
+                t.n_touched[:1].zero_()
+            self._forward_backward(*b)
+            for i, t in enumerate(rep):
+                peak[i] = max(int(peak[i]), int(t.n_touched[0].item()))
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+        if self.world > 1:
+            pk = peak.to(self.arena.data.device)
+            torch.distributed.all_reduce(pk, op=torch.distributed.ReduceOp.MAX, group=self.pg)
+            peak = pk.cpu()
+        torch.cuda.synchronize() if self.arena.data.is_cuda else None
+        caps = []
+        for i, t in enumerate(rep):
+            c = -(-int(int(peak[i]) * headroom) // quantum) * quantum
+            caps.append(int(min(max(c, quantum), t.touched_cap)))
+        return caps
 
     def check_dp_overflow(self) -> None:
         """Raise if a sync-free DP step (capture_pool(dp_caps=...)) saw a rank touch more rows

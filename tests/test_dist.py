@@ -158,6 +158,47 @@ def test_dp_packed_exchange_fixed_layout_two_ranks():
     assert np.allclose(t0, ref, atol=1e-6)
 
 
+def _packed_merged_worker(rank, world, port, out):
+    from recommendsystem_amd.dist import (exchange_packed_merged, merge_packed_merged_reference,
+                                          packed_layout)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    send, recs, _ = _packed_local(rank)
+    ld, cap, S = packed_layout(N_DENSE, CAP, REC)
+    assert ld % 4 == 0 and ld % REC == 0 and S % 4 == 0 and cap >= CAP
+    buf = torch.full((S,), float("nan"))
+    buf[:N_DENSE + 1] = send[:N_DENSE + 1]              # dense gradient + count
+    buf[ld:ld + CAP * REC] = recs[:CAP * REC]
+    buf_all = torch.zeros(world * S)
+    exchange_packed_merged(buf, buf_all)               # ONE collective
+    table = np.zeros((ROWS, DIM), np.float32)
+    touched = merge_packed_merged_reference(buf_all, S, ld, N_DENSE, REC, table)
+    dense = buf_all.view(world, S)[:, :N_DENSE].sum(0).numpy()
+    out[rank] = (table.copy(), sorted(touched), dense)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_packed_exchange_merged_layout_two_ranks():
+    """The AutoInt sync-free exchange as ONE all-gather of [dense | count | records] per rank
+    (dist.packed_layout): the same merged gradients as the two-gather form."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_packed_merged_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    (t0, tc0, d0), (t1, tc1, d1) = out[0], out[1]
+    assert np.array_equal(t0, t1) and tc0 == tc1 and np.array_equal(d0, d1)
+    ref = np.zeros((ROWS, DIM), np.float64)
+    for rank in range(world):
+        r, g, n = _local_lists(rank)
+        for k in range(n):
+            ref[r[k]] += g[k]
+    assert np.allclose(t0, ref, atol=1e-6)
+    dref = sum(_packed_local(r)[0][:N_DENSE] for r in range(world)).numpy()
+    assert np.allclose(d0, dref, atol=1e-6)
+
+
 class _Fn(torch.autograd.Function):
     """A kernel-style Function: writes its weight gradient IN PLACE into the arena and returns
     None for it (what the fused HIP kernels do), so only the node's saved W identifies it."""
@@ -243,4 +284,54 @@ def test_bucketed_allreduce_late_param_between_early_ones():
     g0, w0, _, nb = out[0]
     g1, w1, _, _ = out[1]
     assert nb == 2
+    assert np.array_equal(g0, w0) and np.array_equal(g1, w1)
+
+
+def _config5_bucket_worker(rank, world, port, out):
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import StaytimeRoughRank
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = StaytimeRoughRank(rows=1001, device="cpu", seed=0)  # config 5's dense towers
+    trn = Trainer(m, 5e-4, [m.table], process_group=dist.group.WORLD,
+                  lr_groups=[(m.dssm, m.rr_cfg.lr_dense)])   # default bucket size
+    params = list(m.parameters())
+    g = torch.Generator().manual_seed(100 + rank)
+    coef = [torch.randn(p.shape, generator=g) for p in params]
+
+    def loss_fn():  # every parameter in registration order: backward meets them in reverse
+        tot = torch.zeros(())
+        for p, c in zip(params, coef):
+            tot = tot + (p * c).sum()
+        return tot
+
+    trn.arena.grad.zero_()
+    loss_fn().backward()
+    want = trn.arena.grad.clone()
+    dist.all_reduce(want)
+    trn.arena.grad.zero_()
+    loss = loss_fn()
+    trn.bucketer.arm(loss)
+    loss.backward()
+    issued = trn.bucketer.issued_in_backward
+    trn.bucketer.finish()
+    out[rank] = (trn.arena.grad.numpy().copy(), want.numpy().copy(), issued,
+                 len(trn.bucketer.buckets), 4 * trn.arena.n)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config5_arena_buckets_issue_during_backward():
+    """The config-5 (staytime + rough_rank) dense arena with the Trainer's default bucket size
+    (dist.auto_bucket_bytes: ~1/4 of the arena): several buckets, more than one of them issued
+    from the autograd hooks while backward still runs, and the result equals one flat
+    all-reduce."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_config5_bucket_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    g0, w0, issued, nb, nbytes = out[0]
+    g1, w1, _, _, _ = out[1]
+    assert nbytes > 10 << 20 and nb >= 4 and issued > 1, (nbytes, nb, issued)
     assert np.array_equal(g0, w0) and np.array_equal(g1, w1)

@@ -120,7 +120,7 @@ def _worker_full(rank, world, port, out):
     h = model.table.weight.double().sum(1).cpu().numpy()  # per-row checksum of the table
     # the last exchange's largest record count, read from the gathered buckets (the sync-free
     # exchange never reads it on the host itself)
-    nmax = int(trn.dp_recv.view(torch.int32).view(world, trn.dp_ld)[:, trn.dp_n].max())
+    nmax = int(trn.dp_gathered_counts().max())
     out[rank] = (params, h, float(trn.loss), nmax)
     dist.barrier()
     dist.destroy_process_group()

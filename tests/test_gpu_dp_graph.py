@@ -68,7 +68,13 @@ def _worker(rank, world, port, kind, out, sync_free=False):
     torch.cuda.synchronize()
     eager = _snapshot(m)
     m, trn, batches = _build(kind, rank)
-    trn.capture_pool(batches, warmup=1, dp_caps=_caps(kind) if sync_free else None)
+    caps = None
+    if sync_free == "measured":  # what bench.py does: capacities from the pool's own counts
+        caps = trn.measure_dp_caps(batches)
+        assert len(caps) == 1 and 0 < caps[0] <= _caps(kind)[0] * 2
+    elif sync_free:
+        caps = _caps(kind)
+    trn.capture_pool(batches, warmup=1, dp_caps=caps)
     assert trn.graph_opt is not None and len(trn.graphs) == 2
     graph_losses = [float(trn.step_pool(s)) for s in range(STEPS)]
     torch.cuda.synchronize()
@@ -79,7 +85,7 @@ def _worker(rank, world, port, kind, out, sync_free=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sync_free", [False, True])
+@pytest.mark.parametrize("sync_free", [False, True, "measured"])
 @pytest.mark.parametrize("kind", ["din", "staytime"])
 def test_dp_trainer_graph_equals_eager(kind, sync_free):
     """sync_free: capture_pool(dp_caps=...) -- fixed-size all-gathers, no host read per step
