@@ -681,6 +681,7 @@ struct RedArgs {
   int64_t st_list_stride;      // int32 words between entries (packed DP records: dim + 1)
   const int32_t* st_counts;    // per-segment valid counts (packed DP: one segment per rank), or null
   int64_t st_counts_stride, st_seg_len;
+  int32_t st_chunk;            // rows mode: positions per block chunk of the de-duplicating walk (0: off)
 };
 
 // Rows mode of the fused sparse Adam: the marked rows are exactly the rows the step looked up
@@ -718,6 +719,74 @@ __device__ __forceinline__ void rows_opt_block(const RedArgs& a, int vb, int nbl
   }
 }
 
+// Rows mode with a per-block de-duplication (round 5).  A Zipf batch looks the hottest row of
+// each field up in ~18 % of its samples, so in rows_opt_block those rows' positions (~750 each at
+// B = 4096) all race for one flag word and their atomic exchanges serialise at the memory side
+// (rows mode lost to the flag sweep above B = 1024).  Here a block takes a chunk of P <= 1024
+// consecutive positions (one per thread) and:
+//   1. inserts their rows into an LDS hash (2P slots, linear probing, atomicCAS): one entry per
+//      distinct row of the chunk -> a distinct-row list;
+//   2. one thread per distinct row releases the row's flag with ONE global atomic exchange; the
+//      rows it took from -2 (marked by this step's push and not yet taken by another chunk) go
+//      to an owned list;
+//   3. dim/4-lane groups apply the sparse Adam to the owned rows (each marked row exactly once,
+//      the same per-row arithmetic as the sweep).
+// A hot row now costs one exchange per chunk that holds it instead of one per position.
+__device__ __forceinline__ void rows_opt_block_dedup(const RedArgs& a, int vb, int nblk, int P) {
+  __shared__ int32_t keys[2048];
+  __shared__ int32_t dlist[1024];
+  __shared__ int32_t olist[1024];
+  __shared__ int32_t ncnt[2];
+  const int nv = a.st_dim >> 2;
+  const int lpr = nv < 64 ? nv : 64;
+  const int sub = (int)threadIdx.x % lpr;
+  const int S = 2 * P;  // hash slots (a power of two)
+  const int t = (int)threadIdx.x;
+  for (int64_t c0 = (int64_t)vb * P; c0 < a.st_nlist; c0 += (int64_t)nblk * P) {
+    for (int k = t; k < S; k += 1024) keys[k] = -1;
+    if (t < 2) ncnt[t] = 0;
+    __syncthreads();
+    if (t < P) {
+      const int64_t i = c0 + t;
+      bool in = i < a.st_nlist;
+      if (in && a.st_counts) {
+        const int64_t seg = i / a.st_seg_len;
+        in = (i - seg * a.st_seg_len) < (int64_t)a.st_counts[seg * a.st_counts_stride];
+      }
+      const int32_t r = in ? a.st_list[i * a.st_list_stride] : -1;
+      if (r >= 0 && r < a.st_rows) {
+        uint32_t h = ((uint32_t)r * 0x9E3779B1u) >> 16;
+        for (;;) {
+          h &= (uint32_t)(S - 1);
+          const int32_t prev = atomicCAS(&keys[h], -1, r);
+          if (prev == -1) { dlist[atomicAdd(&ncnt[0], 1)] = r; break; }
+          if (prev == r) break;
+          ++h;
+        }
+      }
+    }
+    __syncthreads();
+    const int nd = ncnt[0];
+    for (int k = t; k < nd; k += 1024) {
+      const int32_t r = dlist[k];
+      if (atomicExch(a.st_flag + r, -1) == -2) olist[atomicAdd(&ncnt[1], 1)] = r;
+    }
+    __syncthreads();
+    const int no = ncnt[1];
+    for (int k = t / lpr; k < no; k += 1024 / lpr) {
+      const int32_t r = olist[k];
+      for (int e4 = sub; e4 < nv; e4 += lpr) {
+        ScanRow<true> x;
+        const int64_t o = (int64_t)r * a.st_dim + 4 * e4;
+        x.load(a.st_table, a.st_m, a.st_v, a.st_grad, o);
+        x.update_store(a.st_table, a.st_m, a.st_v, a.st_grad, o, a.st_lr, a.st_b1, a.st_b2,
+                       a.st_eps, a.st_gscale);
+      }
+    }
+    __syncthreads();  // the LDS lists are rebuilt for the next chunk
+  }
+}
+
 // Block shape per segment (host-chosen): G row groups x (1024 / G) columns, G the smallest power
 // of two with <= 16 rows per thread (IL partials: 1024 rows -> 64 groups x 16 columns over 70
 // blocks; head partials: 256 rows -> 16 x 64 over 224 blocks: the whole launch is one round).  Spreading deep segments over many CUs matters:
@@ -729,7 +798,10 @@ __global__ void __launch_bounds__(1024) partials_reduce_adam_kernel(RedArgs a) {
   const int vb = a.scan_first ? (is_scan ? (int)blockIdx.x : (int)blockIdx.x - a.nblk_scan)
                               : (is_scan ? (int)blockIdx.x - a.nblk_red : (int)blockIdx.x);
   if (is_scan && a.st_list) {  // rows mode
-    rows_opt_block(a, vb, a.nblk_scan);
+    if (a.st_chunk > 0)
+      rows_opt_block_dedup(a, vb, a.nblk_scan, a.st_chunk);
+    else
+      rows_opt_block(a, vb, a.nblk_scan);
     return;
   }
   if (is_scan) {  // the fused sparse sweep (independent of the dense part)
@@ -843,6 +915,7 @@ static int reduce_adam_impl(void* stream, int nseg, const float* const* parts,
     a.st_list = tail->st_list; a.st_nlist = tail->st_nlist; a.st_list_stride = tail->st_list_stride;
     a.st_counts = tail->st_counts; a.st_counts_stride = tail->st_counts_stride;
     a.st_seg_len = tail->st_seg_len;
+    a.st_chunk = tail->st_chunk;
   }
   const int64_t total = nblk + (tail ? tail_blocks : 0);
   if (total == 0) return RS_OK;
@@ -900,7 +973,20 @@ RS_API int rs_partials_reduce_adam_rows_ex(
   t.st_eps = seps; t.st_gscale = sgrad_scale; t.st_list = rows; t.st_nlist = nlist;
   t.st_list_stride = list_stride; t.st_counts = counts; t.st_counts_stride = counts_stride;
   t.st_seg_len = counts ? seg_len : 1;
-  const int64_t per_block = 1024 / (dim / 4 < 64 ? dim / 4 : 64);
+  // the de-duplicating walk (rows_opt_block_dedup): chunks of P positions, P in {256, 512,
+  // 1024} so that the walk still spreads over >= 128 blocks; RS_ROWS_DEDUP=0 keeps the
+  // one-exchange-per-position walk (A/B)
+  static const bool dedup = [] {
+    const char* e = getenv("RS_ROWS_DEDUP");
+    return e && e[0] == '1';
+  }();
+  int64_t per_block = 1024 / (dim / 4 < 64 ? dim / 4 : 64);
+  if (dedup) {
+    int P = 1024;
+    while (P > 256 && (nlist + P - 1) / P < 128) P >>= 1;
+    t.st_chunk = P;
+    per_block = P;
+  }
   int64_t blocks = (nlist + per_block - 1) / per_block;
   if (blocks < 1) blocks = 1;
   if (blocks > 1024) blocks = 1024;
