@@ -68,6 +68,16 @@ RS_API int64_t rs_il_bwd_workspace_floats(int64_t B, int E, int U) {
   return grid * (int64_t)rs_il_param_count(E, U);
 }
 
+// RS_IL_FORCE_GENERIC=1: every shape the generic kernels take runs them (A/B timing against the
+// compiled-in instantiations; read once)
+static bool force_generic() {
+  static const bool on = [] {
+    const char* e = getenv("RS_IL_FORCE_GENERIC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 static int il_fwd_impl(void* stream, const float* x, int64_t B, int F, int E, int U, int H,
                        int L, const float* W, const float* bias, const float* gamma,
                        const float* beta, float eps, int use_res, float drop_rate, uint64_t seed,
@@ -80,6 +90,10 @@ static int il_fwd_impl(void* stream, const float* x, int64_t B, int F, int E, in
                   eps, drop_rate, seed, y, xsave, y_ld};
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   q.asave = asave;
+  if (force_generic()) {
+    const int g = rs_il::il_generic_fwd(q);
+    if (g != RS_ERR_UNSUPPORTED) return g;
+  }
   int r = F > 64 ? rs_il::il_large_fwd(q) : rs_il::il_unit_a_fwd(q);
   if (F <= 64 && r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_fwd(q);
   if (F <= 64 && r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_fwd(q);
@@ -169,6 +183,10 @@ RS_API int rs_il_fwd_gather_saved(void* stream, const int64_t* ids, const int64_
 }
 
 static int bwd_small(const rs_il::BwdReq& q) {
+  if (force_generic() && !q.xt_x) {
+    const int g = rs_il::il_generic_bwd(q);
+    if (g != RS_ERR_UNSUPPORTED) return g;
+  }
   int r = rs_il::il_unit_a_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_b_bwd(q);
   if (r == RS_ERR_UNSUPPORTED) r = rs_il::il_unit_c_bwd(q);
