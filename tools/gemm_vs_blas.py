@@ -27,8 +27,8 @@ def main():
     lib = _lib.load()
     dev = torch.device("cuda")
     s = stream_handle()
-    for M, K, N in ((2048, 1712, 256), (2048, 256, 128), (4096, 1616, 224), (2048, 1712, 32),
-                    (2048, 224, 768)):
+    for M, K, N in ((2048, 1712, 960), (2048, 1840, 400), (4096, 1616, 273), (2048, 224, 1152),
+                    (2048, 528, 400), (2048, 1712, 256), (4096, 1600, 32)):
         X = torch.randn(M, K, device=dev)
         W = torch.randn(K, N, device=dev) * 0.02
         b = torch.zeros(N, device=dev)
@@ -43,9 +43,14 @@ def main():
         ours_w = t_us(lambda: call("rs_dense_bwd_weight", s, ptr(X), K, ptr(dY), N, ptr(dY), N, 0, M,
                                    K, N, ptr(dW), ptr(db), 0, ptr(ws), wsn))
         blas_w = t_us(lambda: torch.mm(X.t(), dY, out=dW))
+        dX = torch.empty(M, K, device=dev)
+        ours_d = t_us(lambda: call("rs_dense_bwd_data", s, ptr(dY), N, ptr(dY), N, 0, ptr(W), M, K, N,
+                                   ptr(dX), K, 0))
+        blas_d = t_us(lambda: torch.mm(dY, W.t(), out=dX))
         fl = 2 * M * K * N
         print(json.dumps({"M": M, "K": K, "N": N, "fwd_us": round(ours_f, 1), "blas_fwd_us": round(blas_f, 1),
                           "wgrad_us": round(ours_w, 1), "blas_wgrad_us": round(blas_w, 1),
+                          "dgrad_us": round(ours_d, 1), "blas_dgrad_us": round(blas_d, 1),
                           "fwd_tf": round(fl / ours_f / 1e6, 1), "blas_fwd_tf": round(fl / blas_f / 1e6, 1)}))
 
 
