@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -180,15 +181,17 @@ def _packed_merged_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_dp_packed_exchange_merged_layout_two_ranks():
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_packed_exchange_merged_layout_two_ranks(world):
     """The AutoInt sync-free exchange as ONE all-gather of [dense | count | records] per rank
-    (dist.packed_layout): the same merged gradients as the two-gather form."""
-    world = 2
+    (dist.packed_layout): the same merged gradients as the two-gather form (2 and 4 ranks)."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_packed_merged_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    (t0, tc0, d0), (t1, tc1, d1) = out[0], out[1]
-    assert np.array_equal(t0, t1) and tc0 == tc1 and np.array_equal(d0, d1)
+    (t0, tc0, d0) = out[0]
+    for r in range(1, world):
+        t1, tc1, d1 = out[r]
+        assert np.array_equal(t0, t1) and tc0 == tc1 and np.array_equal(d0, d1)
     ref = np.zeros((ROWS, DIM), np.float64)
     for rank in range(world):
         r, g, n = _local_lists(rank)
