@@ -166,22 +166,10 @@ __device__ __forceinline__ void load_slab(Slab<BX, Z>& sl, const float* p, int64
 // a transposing scalar store into [x][r] rows hit the same few banks from every lane), and a
 // lane reads its four k-steps as four ds_read_b32 -- pad 4 (MF 16: the four lane groups' rows
 // 4 apart land 16 banks apart) or 8 (MF 32: the two half-waves' rows land 32 banks apart).
-// RS_GEMM_TRS (build-time, variant libraries): operands contiguous along x are TRANSPOSED at
-// LDS-store time into the k-contiguous [x][GBK + 4] image of the ALONG_R operands (4 scalar
-// ds_write_b32 per float4 loaded, once per slab), so every fragment read is one ds_read_b128 for
-// four MFMA k-steps instead of four ds_read_b32 (the weight gradient has both operands in this
-// form, the forward its B).  The k offset inside a row is XOR-swizzled by 4 * ((x >> 2) & 7):
-// float4 groups stay contiguous and 16-B aligned, and the transposing stores of the 16 lanes that
-// share a k row spread over 32 banks instead of 16.
-#ifndef RS_GEMM_TRS
-#define RS_GEMM_TRS 0
-#endif
-__device__ __forceinline__ int trs_swz(int x) { return ((x >> 2) & 7) << 2; }
-
 template <int BX, int MF, bool ALONG_R>
 struct OpLay {
   static constexpr int LDX = BX + (MF == 32 ? 8 : 4);
-  static constexpr int SIZE = (ALONG_R || RS_GEMM_TRS) ? BX * LDP : GBK * LDX;
+  static constexpr int SIZE = ALONG_R ? BX * LDP : GBK * LDX;
 };
 
 template <int BX, int MF, bool ALONG_R, bool Z>
@@ -198,12 +186,6 @@ __device__ __forceinline__ void store_slab(float* s, const Slab<BX, Z>& sl, int 
     }
     if (ALONG_R) {
       *reinterpret_cast<float4*>(s + (idx / RQ) * LDP + 4 * (idx % RQ)) = v;
-    } else if (RS_GEMM_TRS) {
-      const int ri = idx / (BX / 4), x = 4 * (idx % (BX / 4));
-      s[x * LDP + (ri ^ trs_swz(x))] = v.x;
-      s[(x + 1) * LDP + (ri ^ trs_swz(x + 1))] = v.y;
-      s[(x + 2) * LDP + (ri ^ trs_swz(x + 2))] = v.z;
-      s[(x + 3) * LDP + (ri ^ trs_swz(x + 3))] = v.w;
     } else {
       const int ri = idx / (BX / 4), xq = idx % (BX / 4);
       *reinterpret_cast<float4*>(s + ri * OpLay<BX, MF, false>::LDX + 4 * xq) = v;
@@ -215,7 +197,6 @@ __device__ __forceinline__ void store_slab(float* s, const Slab<BX, Z>& sl, int 
 template <int BX, int MF, bool ALONG_R>
 __device__ __forceinline__ float4 frag4(const float* s, int x, int kb) {
   if (ALONG_R) return *reinterpret_cast<const float4*>(s + x * LDP + kb);
-  if (RS_GEMM_TRS) return *reinterpret_cast<const float4*>(s + x * LDP + (kb ^ trs_swz(x)));
   constexpr int LDX = OpLay<BX, MF, false>::LDX;
   return make_float4(s[kb * LDX + x], s[(kb + 1) * LDX + x], s[(kb + 2) * LDX + x],
                      s[(kb + 3) * LDX + x]);
@@ -276,9 +257,7 @@ __device__ __forceinline__ void gemm_block(const GemmArgs& g, const int64_t bx, 
     if (do_db && t < BN) {
 #pragma unroll
       for (int k = 0; k < GBK; ++k)
-        csum += B_ALONG_R ? Bs[cb][t * LDP + k]
-                : RS_GEMM_TRS ? Bs[cb][t * LDP + (k ^ trs_swz(t))]
-                              : Bs[cb][k * OpLay<BN, MF, false>::LDX + t];
+        csum += B_ALONG_R ? Bs[cb][t * LDP + k] : Bs[cb][k * OpLay<BN, MF, false>::LDX + t];
     }
     if constexpr (MF == 16) {
 #pragma unroll

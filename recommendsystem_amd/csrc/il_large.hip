@@ -204,281 +204,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
   }
 }
 
-
-// ---- matrix-core attention for dh = 4 (config 3: U = 8, H = 2) -------------------------------
-// v_mfma_f32_16x16x4_f32 with k = dh: one instruction is a 16 x 16 score tile of one head.  Lane l
-// = (q = l >> 4, j = l & 15) supplies A[j][q] and B[q][j] and holds D[4q + r][j] (r < 4) -- so a
-// lane owns 4 rows of one column of each tile.  Waves take (16-row tile, head) jobs.
-//   forward, job (query tile, head): pass 1 S tiles -> row max (per lane, then a 16-lane DPP
-//     max); pass 2 S tiles again -> p = exp2(s log2e / sqrt(dh) - max), row sums, the counter-based
-//     keep bits (ballots: 16 bits of a row per tile, two tiles per 32-key word), O += p_kept v_j
-//     on the VALU (the lane's key row v_j is one ds_read_b128); 16-lane DPP sums of O and the row
-//     sums at the end.  Same O / stats / bits save as attn_rows.
-//   backward, Q-pass job (query tile, head): S and dP = dO V^T tiles (two MFMAs per tile), P from
-//     the saved stats, dS = P (dP keep / (1 - rate) - D), dq += dS k_j (VALU, the lane's key row);
-//     16-lane sums at the end.  K-pass job (key tile, head): the transposed tiles S^T = K Q^T and
-//     dP^T = V dO^T (rows = keys), dk += dS q_i and dv += P keep / (1 - rate) dO_i for the lane's
-//     query column; 16-lane sums at the end.
-// Replaces one thread per query row with broadcast K / V row reads (attn_rows / passes A and B):
-// the score dot products leave the VALU and each lane reads one key row per 4 scores.
-namespace mf {
-__device__ __forceinline__ float g16_max(float v) {
-  v = fmaxf(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
-  v = fmaxf(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
-  v = fmaxf(v, dpp_mov<0x141>(v));  // row_half_mirror
-  v = fmaxf(v, dpp_mov<0x140>(v));  // row_mirror
-  return v;
-}
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ float pick4(const float (&v)[4], int k) {
-  return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
-}
-}  // namespace mf
-
 template <class C>
-__device__ __forceinline__ void attn_mfma_fwd(const float* Qs, const float* Ks, const float* Vs,
-                                              float* Os, int F, float sc2, bool drop,
-                                              float drop_rate, float inv_keep, uint32_t kb,
-                                              float* sv, float4* st4 = nullptr,
-                                              uint32_t* mask = nullptr) {
-  static_assert(C::DH == 4, "matrix-core attention: dh == 4");
-  const int lane = lane_id(), q = lane >> 4, j = lane & 15;
-  const int KT = (F + 15) >> 4, W32 = (F + 31) >> 5;
-  for (int job = wave_id(); job < KT * C::H; job += NT / 64) {
-    const int qt = job / C::H, h = job - qt * C::H;
-    const int ar = 16 * qt + j;
-    const float aq = ar < F ? Qs[ar * C::U + h * 4 + q] : 0.f;
-    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll 2
-    for (int kt = 0; kt < KT; ++kt) {
-      const int kr = 16 * kt + j;
-      const bool ok = kr < F;
-      const f32x4 s = mfma_16x16x4(aq, ok ? Ks[kr * C::U + h * 4 + q] : 0.f, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx[r] = ok ? fmaxf(mx[r], s[r]) : mx[r];
-    }
-    float msc[4], l[4] = {0.f, 0.f, 0.f, 0.f}, o[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      msc[r] = mf::g16_max(mx[r]) * sc2;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[r][d] = 0.f;
-    }
-    uint32_t wb[4] = {0u, 0u, 0u, 0u};
-    uint32_t* bits = sv ? reinterpret_cast<uint32_t*>(sv + F * C::U + 2 * C::H * F) : nullptr;
-#pragma unroll 2
-    for (int kt = 0; kt < KT; ++kt) {
-      const int kr = 16 * kt + j;
-      const bool ok = kr < F;
-      const f32x4 s = mfma_16x16x4(aq, ok ? Ks[kr * C::U + h * 4 + q] : 0.f, f32x4{0.f, 0.f, 0.f, 0.f});
-      const float4 v = ok ? mf::ld4(Vs + kr * C::U + h * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * qt + 4 * q + r;
-        const float e = ok ? __builtin_amdgcn_exp2f(fmaf(s[r], sc2, -msc[r])) : 0.f;
-        l[r] += e;
-        float ek = e;
-        if (drop) {
-          const bool keep = ok && dropout_keep_k(kb, h, i, kr, drop_rate);
-          ek = keep ? e : 0.f;
-          const uint64_t bal = __ballot(keep);
-          wb[r] |= (uint32_t)((bal >> (16 * q)) & 0xFFFFu) << (16 * (kt & 1));
-        }
-        o[r][0] = fmaf(ek, v.x, o[r][0]);
-        o[r][1] = fmaf(ek, v.y, o[r][1]);
-        o[r][2] = fmaf(ek, v.z, o[r][2]);
-        o[r][3] = fmaf(ek, v.w, o[r][3]);
-      }
-      if (drop && ((kt & 1) || kt == KT - 1)) {
-        if ((bits || mask) && j < 4) {
-          const int i = 16 * qt + 4 * q + j;
-          const uint32_t wj = j == 0 ? wb[0] : j == 1 ? wb[1] : j == 2 ? wb[2] : wb[3];
-          if (i < F && bits) bits[(i * W32 + (kt >> 1)) * C::H + h] = wj;
-          if (i < F && mask) mask[(i * W32 + (kt >> 1)) * C::H + h] = wj;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wb[r] = 0u;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      l[r] = group_sum<16>(l[r]);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[r][d] = group_sum<16>(o[r][d]);
-    }
-    if (j < 4) {  // lane j of each row group stores row 4q + j
-      const int i = 16 * qt + 4 * q + j;
-      if (i < F) {
-        const float lj = mf::pick4(l, j), mj = mf::pick4(msc, j);
-        const float il = 1.0f / lj;
-        const float inv = (drop ? inv_keep : 1.f) * il;
-        float oj[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const float od[4] = {o[0][d], o[1][d], o[2][d], o[3][d]};
-          oj[d] = mf::pick4(od, j) * inv;
-        }
-        const float4 ov = make_float4(oj[0], oj[1], oj[2], oj[3]);
-        *reinterpret_cast<float4*>(Os + i * C::U + h * 4) = ov;
-        if (st4) { st4[i * C::H + h].x = mj; st4[i * C::H + h].y = il; }
-        if (sv) {
-          *reinterpret_cast<float4*>(sv + i * C::U + h * 4) = ov;
-          sv[F * C::U + 2 * (i * C::H + h)] = mj;
-          sv[F * C::U + 2 * (i * C::H + h) + 1] = il;
-        }
-      }
-    }
-  }
-}
-
-
-// backward attention on the matrix cores (after the LN backward: Gs = dO, st4[i H + h] = {scaled
-// max, 1 / sum, D, -}, mask = keep bits [i][word][h]): Q-pass jobs write dQ (ReLU-masked,
-// x 1/sqrt(dh)) into Os, K-pass jobs dK / dV into DKs / DVs.  Reads Qs / Ks / Vs / Gs only.
-template <class C>
-__device__ __forceinline__ void attn_mfma_bwd(const float* Qs, const float* Ks, const float* Vs,
-                                              const float* Gs, float* Os, float* DKs, float* DVs,
-                                              const float4* st4, const uint32_t* mask, int F,
-                                              const LBwd& a) {
-  static_assert(C::DH == 4, "matrix-core attention: dh == 4");
-  const int lane = lane_id(), q = lane >> 4, j = lane & 15;
-  const int KT = (F + 15) >> 4, W32 = (F + 31) >> 5;
-  const int njobs = 2 * KT * C::H;
-  for (int job = wave_id(); job < njobs; job += NT / 64) {
-    const bool kpass = job >= KT * C::H;
-    const int jj = kpass ? job - KT * C::H : job;
-    const int tt = jj / C::H, h = jj - tt * C::H;
-    const int ar = 16 * tt + j;             // this lane's A row (query or key)
-    const bool aok = ar < F;
-    if (!kpass) {
-      // ---- Q-pass: rows = queries 16 tt + 4q + r, columns = keys 16 kt + j ----
-      const float aq = aok ? Qs[ar * C::U + h * 4 + q] : 0.f;
-      const float ag = aok ? Gs[ar * C::U + h * 4 + q] : 0.f;
-      float m[4], il[4], D[4], dq[4][4];
-      int ir[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ir[r] = 16 * tt + 4 * q + r;
-        const float4 st = st4[(ir[r] < F ? ir[r] : 0) * C::H + h];
-        m[r] = st.x; il[r] = st.y; D[r] = st.z;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) dq[r][d] = 0.f;
-      }
-#pragma unroll 2
-      for (int kt = 0; kt < KT; ++kt) {
-        const int kr = 16 * kt + j;
-        const bool ok = kr < F;
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 sc = mfma_16x16x4(aq, ok ? Ks[kr * C::U + h * 4 + q] : 0.f, z);
-        const f32x4 dp = mfma_16x16x4(ag, ok ? Vs[kr * C::U + h * 4 + q] : 0.f, z);
-        const float4 k4 = ok ? mf::ld4(Ks + kr * C::U + h * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], a.sc2, -m[r])) * il[r] : 0.f;
-          float dpr = dp[r];
-          if (a.drop) {
-            const int irr = ir[r] < F ? ir[r] : 0;
-            const uint32_t wd = mask[(irr * W32 + (kt >> 1)) * C::H + h];
-            dpr = ((wd >> (16 * (kt & 1) + j)) & 1u) ? dpr * a.inv_keep : 0.f;
-          }
-          const float ds = p * (dpr - D[r]);
-          dq[r][0] = fmaf(ds, k4.x, dq[r][0]);
-          dq[r][1] = fmaf(ds, k4.y, dq[r][1]);
-          dq[r][2] = fmaf(ds, k4.z, dq[r][2]);
-          dq[r][3] = fmaf(ds, k4.w, dq[r][3]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) dq[r][d] = group_sum<16>(dq[r][d]);
-      if (j < 4) {
-        const int i = 16 * tt + 4 * q + j;
-        if (i < F) {
-          const float4 qv = mf::ld4(Qs + i * C::U + h * 4);
-          const float qa[4] = {qv.x, qv.y, qv.z, qv.w};
-          float o[4];
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const float vd[4] = {dq[0][d], dq[1][d], dq[2][d], dq[3][d]};
-            o[d] = qa[d] > 0.f ? mf::pick4(vd, j) * a.inv_sdh : 0.f;
-          }
-          *reinterpret_cast<float4*>(Os + i * C::U + h * 4) = make_float4(o[0], o[1], o[2], o[3]);
-        }
-      }
-    } else {
-      // ---- K-pass: rows = keys 16 tt + 4q + r, columns = queries 16 qt + j ----
-      const float ak = aok ? Ks[ar * C::U + h * 4 + q] : 0.f;
-      const float av = aok ? Vs[ar * C::U + h * 4 + q] : 0.f;
-      float dk[4][4], dv[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) { dk[r][d] = 0.f; dv[r][d] = 0.f; }
-      const int kw = (16 * tt + 4 * q) >> 5;        // the keys' 32-bit mask word (4 | 32)
-      const int kb0 = (16 * tt + 4 * q) & 31;       // bit of key row r = kb0 + r
-#pragma unroll 2
-      for (int qt = 0; qt < KT; ++qt) {
-        const int qi = 16 * qt + j;
-        const bool ok = qi < F;
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 sc = mfma_16x16x4(ak, ok ? Qs[qi * C::U + h * 4 + q] : 0.f, z);
-        const f32x4 dp = mfma_16x16x4(av, ok ? Gs[qi * C::U + h * 4 + q] : 0.f, z);
-        const int qs = ok ? qi : 0;
-        const float4 st = st4[qs * C::H + h];
-        const float4 q4 = mf::ld4(Qs + qs * C::U + h * 4);
-        const float4 g4 = mf::ld4(Gs + qs * C::U + h * 4);
-        const uint32_t wd = a.drop ? mask[(qs * W32 + kw) * C::H + h] >> kb0 : ~0u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], a.sc2, -st.x)) * st.y : 0.f;
-          float pd = p, dpr = dp[r];
-          if (a.drop) {
-            const bool keep = (wd >> r) & 1u;
-            pd = keep ? p * a.inv_keep : 0.f;
-            dpr = keep ? dpr * a.inv_keep : 0.f;
-          }
-          const float ds = p * (dpr - st.z);
-          dk[r][0] = fmaf(ds, q4.x, dk[r][0]);
-          dk[r][1] = fmaf(ds, q4.y, dk[r][1]);
-          dk[r][2] = fmaf(ds, q4.z, dk[r][2]);
-          dk[r][3] = fmaf(ds, q4.w, dk[r][3]);
-          dv[r][0] = fmaf(pd, g4.x, dv[r][0]);
-          dv[r][1] = fmaf(pd, g4.y, dv[r][1]);
-          dv[r][2] = fmaf(pd, g4.z, dv[r][2]);
-          dv[r][3] = fmaf(pd, g4.w, dv[r][3]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          dk[r][d] = group_sum<16>(dk[r][d]);
-          dv[r][d] = group_sum<16>(dv[r][d]);
-        }
-      if (j < 4) {
-        const int kr = 16 * tt + 4 * q + j;
-        if (kr < F) {
-          const float4 kv = mf::ld4(Ks + kr * C::U + h * 4);
-          const float4 vv = mf::ld4(Vs + kr * C::U + h * 4);
-          const float ka[4] = {kv.x, kv.y, kv.z, kv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
-          float ok4[4], ov4[4];
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const float kd[4] = {dk[0][d], dk[1][d], dk[2][d], dk[3][d]};
-            const float vd[4] = {dv[0][d], dv[1][d], dv[2][d], dv[3][d]};
-            ok4[d] = ka[d] > 0.f ? mf::pick4(kd, j) * a.inv_sdh : 0.f;
-            ov4[d] = va[d] > 0.f ? mf::pick4(vd, j) : 0.f;
-          }
-          *reinterpret_cast<float4*>(DKs + kr * C::U + h * 4) = make_float4(ok4[0], ok4[1], ok4[2], ok4[3]);
-          *reinterpret_cast<float4*>(DVs + kr * C::U + h * 4) = make_float4(ov4[0], ov4[1], ov4[2], ov4[3]);
-        }
-      }
-    }
-  }
-}
-
-template <class C, bool MF = false>
 __global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int F = a.F;
@@ -508,10 +234,7 @@ __global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
       project<C>(xs, Qs, F, wcol, bc);
       __syncthreads();
       float* sv = a.asave ? a.asave + ((int64_t)it * a.B + b) * save_stride(F, C::U, C::H) : nullptr;
-      if constexpr (MF)
-        attn_mfma_fwd<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, a.drop_rate, a.inv_keep, kb, sv);
-      else
-        attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, nullptr, nullptr, sv);
+      attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, nullptr, nullptr, sv);
       __syncthreads();
       const bool last = it == a.L - 1;
       for (int i = t; i < F; i += NT) {
@@ -544,7 +267,7 @@ __global__ void __launch_bounds__(NT) fwd_kernel(LFwd a) {
   }
 }
 
-template <class C, bool MF = false>
+template <class C>
 __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int F = a.F;
@@ -619,11 +342,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
         __syncthreads();
         project<C>(xs, Qs, F, wcol, bc);
         __syncthreads();
-        if constexpr (MF)
-          attn_mfma_fwd<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, a.drop_rate, a.inv_keep, kb, nullptr,
-                           st4, mask);
-        else
-          attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, st4, mask, nullptr);
+        attn_rows<C>(Qs, Ks, Vs, Os, F, a.sc2, a.drop, kb, a.drop_rate, a.inv_keep, st4, mask, nullptr);
         __syncthreads();
       }
       // ---- epilogue backward: LN, ReLU, residual; D = dO . O per (row, head) ----
@@ -673,9 +392,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
       // rows {r, r + NH}, threads [NT/2, NT) pass B (dK, dV) over key rows {r, r + NH}, NH =
       // ceil(F/2).  Two rows per thread halve the broadcast K/V (pass A) and Q/dO/stats (pass B)
       // LDS reads per score -- the passes are LDS-read bound -- and the two halves overlap.
-      if constexpr (MF) {
-        attn_mfma_bwd<C>(Qs, Ks, Vs, Gs, Os, DKs, DVs, st4, mask, F, a);
-      } else {
+      {
         const int NH = (F + 1) / 2;
         const int half = t / (NT / 2), r = t % (NT / 2);
         const int r1 = r + NH;
@@ -846,17 +563,6 @@ inline size_t bwd_lds(int F, int E, int U, int H) {
   return main > red ? main : red;
 }
 
-// dh == 4 shapes run the matrix-core attention (attn_mfma_*); RS_ILL_MFMA=0 keeps the
-// thread-per-row VALU passes (A/B runs; read once)
-template <class C>
-inline bool use_mfma() {
-  static const bool on = [] {
-    const char* e = getenv("RS_ILL_MFMA");
-    return e && e[0] == '1';
-  }();
-  return C::DH == 4 && on;
-}
-
 template <int E, int U, int H>
 int run_fwd(const FwdReq& q) {
   using C = LC<E, U, H>;
@@ -867,10 +573,7 @@ int run_fwd(const FwdReq& q) {
   if (q.B == 0) return RS_OK;
   const size_t lds = fwd_lds(q.F, E, U);
   int64_t grid = q.B < 4096 ? q.B : 4096;
-  if (use_mfma<C>())
-    fwd_kernel<C, C::DH == 4><<<(int)grid, NT, lds, q.stream>>>(a);
-  else
-    fwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
+  fwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
   return rs_status_after_launch();
 }
 
@@ -886,10 +589,7 @@ int run_bwd(const BwdReq& q) {
          1.4426950408889634f / sqrtf((float)C::DH), 1.0f / sqrtf((float)C::DH), q.seed, (uint64_t)(uintptr_t)rs_seed_offset_now(), q.dx,
          q.dx_accumulate, q.workspace, q.asave};
   const size_t lds = bwd_lds(q.F, E, U, H);
-  if (use_mfma<C>())
-    bwd_kernel<C, C::DH == 4><<<(int)grid, NT, lds, q.stream>>>(a);
-  else
-    bwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
+  bwd_kernel<C><<<(int)grid, NT, lds, q.stream>>>(a);
   int st = rs_status_after_launch();
   if (st || !q.dparams) return st;
   launch_column_reduce(q.stream, q.workspace, (int)grid, C::NPARAM, C::NPARAM, C::NPARAM,

@@ -309,10 +309,6 @@ class MultiHeadRanker(nn.Module):
         F, E = cfg.num_fields, cfg.embed_dim
         self.table = SparseTable(F * cfg.vocab_per_field, E, SparseAdam(cfg.lr_sparse), device=dev,
                                  seed=seed, max_touched=max_touched)
-        # RS_MULTIHEAD_SCAN=1: single-GPU scan mode (plain-store marks in the multi-hot push, the
-        # sparse Adam sweeps the 53 M flags) instead of list mode's CAS claims (A/B)
-        import os
-        self.table.prefer_scan = os.environ.get("RS_MULTIHEAD_SCAN", "0") == "1"
         self.embedding = EmbeddingFeatures(self.table, [cfg.vocab_per_field] * F, combiner="mean")
         self.interact = InteractingLayer(1, E, 2, use_dropout=True, dropout_rate=cfg.dropout_rate,
                                          use_res=True, seed=seed + 1, device=dev)
