@@ -447,12 +447,15 @@ def run_workload(args, world, rank, dev, pg):
                           lr_groups=[(model.dssm, model.rr_cfg.lr_dense)])
         pool = [W.staytime_batch(rng, B, model, dev) for _ in range(args.pool)]
     sharded = getattr(model.table, "sharded", False)
-    graphed = not args.eager and not sharded
+    # owner-sharded tables are captured with fixed routing, their all-to-alls inside the graph:
+    # RCCL only (gloo collectives are host calls)
+    graphed = not args.eager and (not sharded or torch.distributed.get_backend(pg) == "nccl")
     dp_caps = None
     if graphed:  # one HIP graph per pool batch (forward + autograd backward + optimizers)
         if world > 1:
             # the sync-free captured DP step: fixed-capacity all-gathers sized from the pool's
-            # own touched-row counts (max over ranks, 25 % headroom; overflow is detected)
+            # own touched-row counts (max over ranks, 25 % headroom; overflow is detected);
+            # owner-sharded tables get their fixed routing capacity (owner_cap) the same way
             dp_caps = trainer.measure_dp_caps(pool)
         trainer.capture_pool(pool, warmup=1, dp_caps=dp_caps)
         step = trainer.step_pool
@@ -495,7 +498,9 @@ def run_workload(args, world, rank, dev, pg):
            "data": "synthetic (SURVEY §8d config generators; random-init weights)",
            "config": {"workload": desc, "global_batch": B * world, "per_gpu_batch": B,
                       "parallelism": f"dp{world}",
-                      "table": "owner-sharded" if getattr(model.table, "sharded", False) else "replicated",
+                      "table": ("owner-sharded" + (f" (fixed routing, owner_cap {model.table.owner_cap})"
+                                                   if getattr(model.table, "owner_cap", None) else "")
+                                if sharded else "replicated"),
                       "execution": ("one HIP graph per pool batch" + (
                           f" + sync-free fixed-capacity exchange (dp_caps {dp_caps})" if dp_caps
                           else "")) if graphed else "eager autograd"},

@@ -106,11 +106,19 @@ int rs_sparse_grad_accumulate_sorted(void* stream, const int32_t* rows, const in
  * rs_gather_rows: dst[i] = src[idx[i]] (idx < 0: zero row); rs_scatter_rows: dst[idx[i]] =
  * src[i] (idx < 0 skipped); rows of dim floats (dim % 4 == 0), leading dimensions in floats.
  * rs_segment_expand: dE[k] = scale(s) * dout[b*dout_ld + f*dout_fstride] for every id k of
- * segment s = b*F + f (offsets [B*F+1]; the combiner's per-id gradient of a VarLen lookup). */
+ * segment s = b*F + f (offsets [B*F+1]; the combiner's per-id gradient of a VarLen lookup).
+ * rs_owner_route_fixed: the sync-free route -- the same stable owner order, but owner w's k-th
+ * row goes to slot w*cap + k of send_local [world*cap] (pads -1) for k < cap, slot[i] = the slot
+ * of position i (-1: invalid row or past its owner's cap, dropped); stats[0] (device int32,
+ * sticky) = max(stats[0], the largest per-owner count), so stats[0] > cap means rows were
+ * dropped.  Equal splits of cap per rank make the all-to-alls graph-capturable. */
 int64_t rs_owner_route_workspace_bytes(int64_t n, int world);
 int rs_owner_route(void* stream, const int32_t* rows, int64_t n, int world, int64_t table_rows,
                    int32_t* send_local, int32_t* send_pos, int32_t* counts, void* workspace,
                    int64_t workspace_bytes);
+int rs_owner_route_fixed(void* stream, const int32_t* rows, int64_t n, int world,
+                         int64_t table_rows, int cap, int32_t* send_local, int32_t* slot,
+                         int32_t* stats, void* workspace, int64_t workspace_bytes);
 int rs_gather_rows(void* stream, const float* src, int64_t src_ld, const int32_t* idx, int64_t n,
                    int dim, float* dst, int64_t dst_ld);
 int rs_scatter_rows(void* stream, const float* src, int64_t src_ld, const int32_t* idx, int64_t n,
@@ -373,6 +381,14 @@ int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* dY, int
                  const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K, int N,
                  float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db, int w_accumulate,
                  float* workspace, int64_t workspace_floats);
+/* Large plain GEMMs (M K N >= 2^28 multiply-adds by default; RS_GEMM_BLAS=0 off,
+ * RS_GEMM_BLAS_MACS=n threshold) run on hipBLASLt inside the four entries above: forward with
+ * its bias / ReLU epilogue (sigmoid stays on the engine), weight gradient and rs_dense_bwd with
+ * dZ = dY act'(Y) materialised in the workspace (the workspace query covers it) and db from a
+ * fixed-order column reduction, rs_dense_bwd_data only for act 0.  A shape the library declines
+ * runs on the engine.  rs_dense_uses_library(M, K, N): 1 when a Dense layer of that shape takes
+ * the library route (results then equal the engine's to fp32 rounding, not bitwise). */
+int rs_dense_uses_library(int64_t M, int K, int N);
 /* Grouped Dense: G <= 8 independent layers of one kind in ONE launch (plus one grouped split-K
  * reduce for weight gradients) -- the per-expert / per-task layers that staytime/VideoDnn.py:130-191
  * and rough_rank/layer.py:174-233 build in Python loops.  desc: G records of int64 (pointers cast):

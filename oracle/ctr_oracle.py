@@ -288,6 +288,26 @@ def owner_route(rows, world: int, table_rows: int):
     return (rows[order] // world).astype(np.int32), pos[order].astype(np.int32), counts.astype(np.int32)
 
 
+def owner_route_fixed(rows, world: int, table_rows: int, cap: int):
+    """The fixed-capacity route (rs_owner_route_fixed; the sync-free form of owner_route, no
+    reference counterpart -- tensornet's PS client sends variable-size requests): owner w's k-th
+    valid row (owner_route's stable order) goes to slot w * cap + k if k < cap.
+    -> (send_local [world * cap] int32 (row // world, -1 pads), slot [n] int32 (-1: invalid row or
+    past its owner's cap), peak = the largest per-owner count)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    send_local, send_pos, counts = owner_route(rows, world, table_rows)
+    out = np.full(world * cap, -1, dtype=np.int32)
+    slot = np.full(rows.size, -1, dtype=np.int32)
+    i = 0
+    for w in range(world):
+        for k in range(int(counts[w])):
+            if k < cap:
+                out[w * cap + k] = send_local[i]
+                slot[send_pos[i]] = w * cap + k
+            i += 1
+    return out, slot, int(counts.max()) if counts.size else 0
+
+
 def sharded_lookup_reference(rows_per_rank, world: int, table_rows: int, table):
     """Every rank's per-id rows gathered through the owners (what the route + all-to-all + gather
     + scatter sequence computes): table[rows] with zero rows where rows < 0."""

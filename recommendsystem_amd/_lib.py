@@ -50,6 +50,7 @@ SIGNATURES: dict[str, tuple] = {
                                                 _i64]),
     "rs_owner_route_workspace_bytes": (_i64, [_i64, _i32]),
     "rs_owner_route": (_i32, [_vp, _vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _i64]),
+    "rs_owner_route_fixed": (_i32, [_vp, _vp, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _i64]),
     "rs_gather_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
     "rs_scatter_rows": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64]),
     "rs_segment_expand": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _i32, _i32, _vp]),
@@ -80,6 +81,7 @@ SIGNATURES: dict[str, tuple] = {
     "rs_dense_bwd_data": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp, _i64,
                                  _i32]),
     "rs_dense_bwd_weight_workspace_floats": (_i64, [_i64, _i32, _i32]),
+    "rs_dense_uses_library": (_i32, [_i64, _i32, _i32]),
     "rs_dense_bwd_weight": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _i32,
                                    _vp, _vp, _i32, _vp, _i64]),
     "rs_dense_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp,

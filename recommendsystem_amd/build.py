@@ -81,7 +81,8 @@ def build(verbose: bool = False, extra: list[str] | None = None) -> str:
         # a host-sanitizer build (-Xarch_host -fsanitize=...) links the shared sanitizer runtime
         san = [f for f in extra if f.startswith("-fsanitize=")]
         link = [*san, "-shared-libasan"] if san else []
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *link, *objs, "-o", LIB_PATH]
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *link, *objs,
+               "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB_PATH]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

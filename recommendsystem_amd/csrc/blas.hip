@@ -1,0 +1,131 @@
+// hipBLASLt for the large plain fp32 GEMMs of the Dense layers (blas.hpp).  One handle and one
+// workspace per process, created on the first eligible call (an eager step: graph capture
+// replays the plans a warm-up step made); one plan per (shape, layout, epilogue): matmul
+// descriptor, four matrix layouts and the heuristic's first algorithm, cached.  The bias pointer
+// is set on the cached descriptor per call (host-side attribute; a captured launch keeps the one
+// it was recorded with).
+#include "blas.hpp"
+
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace {
+
+constexpr size_t kWsBytes = (size_t)64 << 20;
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  bool ok = false;
+};
+
+using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int>;
+
+struct Ctx {
+  std::mutex mu;
+  bool tried = false, ok = false;
+  hipblasLtHandle_t h = nullptr;
+  void* ws = nullptr;
+  std::map<Key, Plan> plans;
+};
+
+Ctx& ctx() {
+  static Ctx c;
+  return c;
+}
+
+bool init_locked(Ctx& c) {
+  if (c.tried) return c.ok;
+  c.tried = true;
+  if (hipblasLtCreate(&c.h) != HIPBLAS_STATUS_SUCCESS) return false;
+  if (hipMalloc(&c.ws, kWsBytes) != hipSuccess) {
+    c.ws = nullptr;
+    return false;
+  }
+  c.ok = true;
+  return true;
+}
+
+Plan make_plan(Ctx& c, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+               int64_t ldd, int epi, bool beta) {
+  Plan p;
+  if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS)
+    return p;
+  const hipblasOperation_t oa = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, ob = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &oa, sizeof(oa));
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &ob, sizeof(ob));
+  const hipblasLtEpilogue_t e = (hipblasLtEpilogue_t)epi;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
+  if (epi != HIPBLASLT_EPILOGUE_DEFAULT) {
+    const hipDataType bt = HIP_R_32F;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  // stored shapes: A is m x k (k x m transposed), B k x n (n x k transposed)
+  hipblasLtMatrixLayoutCreate(&p.a, HIP_R_32F, ta ? k : m, ta ? m : k, lda);
+  hipblasLtMatrixLayoutCreate(&p.b, HIP_R_32F, tb ? n : k, tb ? k : n, ldb);
+  hipblasLtMatrixLayoutCreate(&p.d, HIP_R_32F, m, n, ldd);
+  hipblasLtMatmulPreference_t pref = nullptr;
+  hipblasLtMatmulPreferenceCreate(&pref);
+  const uint64_t wsb = kWsBytes;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
+                                        sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int got = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.d, p.d, pref,
+                                                             1, res, &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  (void)beta;
+  if (st == HIPBLAS_STATUS_SUCCESS && got > 0 && res[0].workspaceSize <= kWsBytes) {
+    p.algo = res[0].algo;
+    p.ok = true;
+  }
+  return p;
+}
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  if (!e || !*e) return dflt;
+  return (int64_t)strtoll(e, nullptr, 10);
+}
+
+}  // namespace
+
+bool rs_blas_wanted(int64_t m, int64_t n, int64_t k) {
+  // measured (tools/gemm_vs_blas.py, profiles/r05/blas/gemm.log): the library leads
+  // on the towers' weight / data gradients from ~0.4 G multiply-adds (1.3-4x on the trunks); at
+  // 0.2 G (4096 x 1600 x 32) the engine's split-K weight gradient is faster
+  static const int64_t thr = env_i64("RS_GEMM_BLAS_MACS", (int64_t)1 << 28);
+  static const bool on = env_i64("RS_GEMM_BLAS", 1) != 0;
+  return on && m > 0 && n > 0 && k > 0 && m * n * k >= thr;
+}
+
+int rs_blas_gemm_cm(hipStream_t s, bool ta, bool tb, int64_t m, int64_t n, int64_t k,
+                    const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* D,
+                    int64_t ldd, const float* bias, bool relu) {
+  Ctx& c = ctx();
+  const int epi = bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
+                       : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
+  Plan* p = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!init_locked(c)) return 1;
+    const Key key{ta, tb, m, n, k, lda, ldb, ldd, epi, beta != 0.f};
+    auto it = c.plans.find(key);
+    if (it == c.plans.end())
+      it = c.plans.emplace(key, make_plan(c, ta, tb, m, n, k, lda, ldb, ldd, epi, beta != 0.f)).first;
+    p = &it->second;
+    if (!p->ok) return 1;
+    if (bias)
+      hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+    const float alpha = 1.f;
+    const hipblasStatus_t st = hipblasLtMatmul(c.h, p->desc, &alpha, A, p->a, B, p->b, &beta, D, p->d,
+                                               D, p->d, &p->algo, c.ws, kWsBytes, s);
+    return st == HIPBLAS_STATUS_SUCCESS ? 0 : 1;
+  }
+}

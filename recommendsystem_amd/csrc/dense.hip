@@ -15,6 +15,7 @@
 //                dX = dZ W^T       (optionally accumulated)
 //                dW = X^T dZ, db = colsum(dZ): split over M chunks -> per-chunk partials ->
 //                fixed-order reduce (deterministic, no float atomics)
+#include "blas.hpp"
 #include "common.hpp"
 
 #include <cstdint>
@@ -555,11 +556,97 @@ static void launch_gemm(hipStream_t s, const GemmPlan& p, const GemmArgs& g, boo
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ---------------------------------------------------------------------------------------------
+// The library route (blas.hpp) for the large plain GEMMs.  Row-major C[M, N] = A B is the
+// column-major C^T = B^T A^T, so every call below swaps its operands:
+//   forward   Y^T [N x M] = W^T-view (W row-major [K, N] = col-major N x K) . X^T-view, + bias, relu
+//   data      dX^T [K x M] = op_T(W col-major N x K) . dZ^T-view (col-major N x M)
+//   weight    dW^T [N x K] = dZ^T-view (N x M) . op_T(X^T-view col-major K x M)
+// dZ = dY act'(Y) is materialised once in the workspace (act != none) by dz_partial_kernel,
+// which also forms db's column partials per row split (fixed order; column_reduce sums them).
+// ---------------------------------------------------------------------------------------------
+constexpr int kDzMaxSplits = 256;
+
+__global__ void __launch_bounds__(1024) dz_partial_kernel(const float* __restrict__ dY, int64_t lddy,
+                                                          const float* __restrict__ Y, int64_t ldy,
+                                                          int act, int64_t M, int N, int64_t rchunk,
+                                                          float* __restrict__ dz,
+                                                          float* __restrict__ part) {
+  __shared__ float red[16][64];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lc;
+  const int64_t r0 = (int64_t)blockIdx.y * rchunk;
+  const int64_t r1 = r0 + rchunk < M ? r0 + rchunk : M;
+  float s = 0.f;
+  if (c < N) {
+    for (int64_t r = r0 + g; r < r1; r += 16) {
+      const float v = act_bwd(dY[r * lddy + c], act ? Y[r * ldy + c] : 0.f, act);
+      if (dz) dz[r * N + c] = v;
+      s += v;
+    }
+  }
+  red[g][lc] = s;
+  __syncthreads();
+  if (g == 0 && c < N) {
+    float t = red[0][lc];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][lc];
+    part[(int64_t)blockIdx.y * N + c] = t;
+  }
+}
+
+static int64_t dz_splits(int64_t M, int N) {
+  int64_t s = cdiv(256, cdiv(N, 64));
+  const int64_t max_s = cdiv(M, 64);
+  if (s > max_s) s = max_s;
+  if (s > kDzMaxSplits) s = kDzMaxSplits;
+  return s < 1 ? 1 : s;
+}
+
+static int64_t blas_bwd_workspace_floats(int64_t M, int N) {
+  return M * N + (int64_t)kDzMaxSplits * N;
+}
+
+// 0: done; nonzero: nothing but workspace was written (the caller runs its own kernels)
+static int blas_dense_bwd(hipStream_t s, const float* X, int64_t ldx, const float* dY, int64_t lddy,
+                          const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K,
+                          int N, float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db,
+                          int w_accumulate, float* ws, int64_t wsf) {
+  if (!ws || wsf < blas_bwd_workspace_floats(M, N)) return 1;
+  const int64_t S = dz_splits(M, N), rc = cdiv(M, S);
+  float* dz = act != RS_ACT_NONE ? ws : nullptr;
+  float* part = ws + M * N;
+  const float* Z = dz ? dz : dY;
+  const int64_t ldz = dz ? N : lddy;
+  dz_partial_kernel<<<dim3((unsigned)cdiv(N, 64), (unsigned)cdiv(M, rc)), 1024, 0, s>>>(
+      dY, lddy, Y, ldy, act, M, N, rc, dz, part);
+  if (rs_blas_gemm_cm(s, false, true, N, K, M, Z, ldz, X, ldx, w_accumulate ? 1.f : 0.f, dW, N,
+                      nullptr, false))
+    return 1;
+  launch_column_reduce(s, part, (int)cdiv(M, rc), N, N, N, db, nullptr, w_accumulate);
+  if (dX && rs_blas_gemm_cm(s, true, false, K, M, N, W, N, Z, ldz, dx_accumulate ? 1.f : 0.f, dX,
+                            lddx, nullptr, false)) {
+    // the data gradient on the engine (dZ recomputed from dY, Y on load)
+    GemmArgs g{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, 0, act, EPI_STORE, 0, nullptr, dX, lddx,
+               dx_accumulate, nullptr};
+    GemmPlan p = plan_gemm(M, K, N, false);
+    g.rchunk = p.rchunk;
+    const bool vec = aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 &&
+                     ldy % 4 == 0 && N % 4 == 0;
+    launch_gemm<LAY_ROW, LAY_COL, true, false>(s, p, g, vec);
+  }
+  return 0;
+}
+
 RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t ldx,
                         const float* W, const float* bias, int N, int act, float* Y,
                         int64_t ldy) {
   if (!X || !W || !bias || !Y || M < 0 || K <= 0 || N <= 0 || ldx < K || ldy < N) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
+  if (act != RS_ACT_SIGMOID && rs_blas_wanted(M, N, K) &&
+      rs_blas_gemm_cm(rs_stream(stream), false, false, N, M, K, W, N, X, ldx, 0.f, Y, ldy, bias,
+                      act == RS_ACT_RELU) == 0)
+    return rs_status_after_launch();
   GemmArgs g{X, ldx, nullptr, 0, W, N, nullptr, 0, M, N, K, 0, 0, EPI_FWD, act, bias, Y, ldy, 0, nullptr};
   GemmPlan p = plan_gemm(M, N, K, false);
   g.rchunk = p.rchunk;
@@ -574,6 +661,11 @@ RS_API int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const 
                              float* dX, int64_t lddx, int accumulate) {
   if (!dY || !Y || !W || !dX || M < 0 || K <= 0 || N <= 0 || lddx < K) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
+  // (the library route needs dZ = dY: no workspace here to materialise it)
+  if (act == RS_ACT_NONE && rs_blas_wanted(M, K, N) &&
+      rs_blas_gemm_cm(rs_stream(stream), true, false, K, M, N, W, N, dY, lddy,
+                      accumulate ? 1.f : 0.f, dX, lddx, nullptr, false) == 0)
+    return rs_status_after_launch();
   // C[M, K] = dZ[M, N] . W^T : B(r = n, c = k) = W[k * N + n] (column layout, ldb = N)
   GemmArgs g{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, 0, act, EPI_STORE, 0, nullptr, dX, lddx,
              accumulate, nullptr};
@@ -585,10 +677,17 @@ RS_API int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const 
   return rs_status_after_launch();
 }
 
+RS_API int rs_dense_uses_library(int64_t M, int K, int N) {
+  return rs_blas_wanted(K, N, M) ? 1 : 0;
+}
+
 RS_API int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N) {
   if (M < 0 || K <= 0 || N <= 0) return 0;  // (rs_dense_bwd_weight rejects these shapes)
   const GemmPlan p = plan_gemm(K, N, M, true);
-  return (int64_t)p.splits * ((int64_t)K * N + N);
+  const int64_t own = (int64_t)p.splits * ((int64_t)K * N + N);
+  if (!rs_blas_wanted(K, N, M)) return own;
+  const int64_t lib = blas_bwd_workspace_floats(M, N);  // (or the engine's, if the library declines)
+  return lib > own ? lib : own;
 }
 
 RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const float* dY,
@@ -604,6 +703,10 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
     }
     return rs_status_after_launch();
   }
+  if (rs_blas_wanted(K, N, M) &&
+      blas_dense_bwd(s, X, ldx, dY, lddy, Y, ldy, act, nullptr, M, K, N, nullptr, 0, 0, dW, db,
+                     accumulate, workspace, workspace_floats) == 0)
+    return rs_status_after_launch();
   // C[K, N] = sum_m X[m][k] dZ[m][n]: A(k, m) = X[m * ldx + k] (column layout), B = dZ rows
   const GemmPlan p = plan_gemm(K, N, M, true);
   const bool split = p.splits > 1;
@@ -668,6 +771,10 @@ RS_API int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* 
                         int w_accumulate, float* workspace, int64_t workspace_floats) {
   if (!X || !dY || !Y || !W || !dX || !dW || !db || M < 0 || K <= 0 || N <= 0 || lddx < K)
     return RS_ERR_ARG;
+  if (M > 0 && rs_blas_wanted(K, N, M) &&
+      blas_dense_bwd(rs_stream(stream), X, ldx, dY, lddy, Y, ldy, act, W, M, K, N, dX, lddx,
+                     dx_accumulate, dW, db, w_accumulate, workspace, workspace_floats) == 0)
+    return rs_status_after_launch();
   const GemmPlan pd = plan_gemm(M, K, N, false);
   const GemmPlan pw = plan_gemm(K, N, M, true);
   const bool vec_d = aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 && ldy % 4 == 0 &&

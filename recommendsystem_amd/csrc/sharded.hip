@@ -18,6 +18,10 @@
 //   gather    rs_gather_rows(dE, send_pos) -> gradients in owner order
 //   push      (owner) rs_sparse_grad_accumulate over recv_local into the shard's gradient rows.
 // All launches are async on the caller's stream; the only host sync is the count exchange.
+// Sync-free form (rs_owner_route_fixed): every (requester, owner) pair gets a fixed block of cap
+// slots, so the all-to-alls have equal splits known before the step (no count exchange, no host
+// read, capturable in a HIP graph); pads carry row -1 (zero rows on gather, skipped by the push)
+// and a per-owner count past cap is recorded in a sticky stats word.
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
@@ -122,10 +126,63 @@ __global__ void __launch_bounds__(256) segment_expand_kernel(
   }
 }
 
+// fixed-capacity routing (rs_owner_route_fixed): start[w] = first sorted position of owner w
+// (binary search over the sorted keys, w = 0 .. world), the largest per-owner count folded into
+// the sticky stats word (device-side overflow detection / capacity measurement, no host read)
+__global__ void owner_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n, int world,
+                                    int32_t* __restrict__ start, int32_t* __restrict__ stats) {
+  __shared__ int32_t s[1025];
+  for (int w = threadIdx.x; w <= world; w += blockDim.x) {
+    int64_t lo = 0, hi = n;  // first i with keys[i] >= w
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < (uint32_t)w) lo = mid + 1; else hi = mid;
+    }
+    s[w] = (int32_t)lo;
+    start[w] = (int32_t)lo;
+  }
+  __syncthreads();
+  int32_t mx = 0;
+  for (int w = threadIdx.x; w < world; w += blockDim.x) mx = max(mx, s[w + 1] - s[w]);
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0 && mx > 0) atomicMax(&stats[0], mx);
+}
+
+// id i (owner order) -> slot w * cap + (i - start[w]) of the fixed [world][cap] send layout;
+// ids past an owner's cap and invalid rows get slot -1 (dropped; the stats word says so)
+__global__ void owner_emit_fixed_kernel(const int32_t* __restrict__ rows,
+                                        const uint32_t* __restrict__ keys,
+                                        const int32_t* __restrict__ pos_sorted,
+                                        const int32_t* __restrict__ start, int64_t n, int world,
+                                        int cap, int32_t* __restrict__ send_local,
+                                        int32_t* __restrict__ slot) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = keys[i];
+    const int32_t p = pos_sorted[i];
+    int32_t sl = -1;
+    if (w < (uint32_t)world) {
+      const int64_t k = i - start[w];
+      if (k < cap) {
+        sl = (int32_t)(w * (int64_t)cap + k);
+        send_local[sl] = rows[p] / world;
+      }
+    }
+    slot[p] = sl;
+  }
+}
+
+__global__ void fill_i32_kernel(int32_t* __restrict__ p, int64_t n, int32_t v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
 struct RouteWs {
   uint32_t *keys_in, *keys_out;
   int32_t *pos_in, *pos_out;
   void* temp;
+  int32_t* start;  // [world + 1] (rs_owner_route_fixed)
   size_t temp_bytes, total;
 };
 
@@ -147,6 +204,7 @@ RouteWs carve_route(char* base, int64_t n, int world) {
   w.pos_in = (int32_t*)take(a);
   w.pos_out = (int32_t*)take(a);
   w.temp = take(t);
+  w.start = (int32_t*)take((size_t)(world + 1) * 4);
   w.total = off;
   return w;
 }
@@ -189,6 +247,31 @@ RS_API int rs_owner_route(void* stream, const int32_t* rows, int64_t n, int worl
     return RS_ERR_LAUNCH;
   owner_emit_kernel<<<nb, 256, 0, s>>>(rows, w.keys_out, w.pos_out, n, world, send_local, send_pos,
                                        counts);
+  return rs_status_after_launch();
+}
+
+RS_API int rs_owner_route_fixed(void* stream, const int32_t* rows, int64_t n, int world,
+                                int64_t table_rows, int cap, int32_t* send_local, int32_t* slot,
+                                int32_t* stats, void* workspace, int64_t workspace_bytes) {
+  if (world < 1 || world > 1024 || n < 0 || n > INT32_MAX || table_rows <= 0 || cap < 1 ||
+      (int64_t)world * cap > INT32_MAX || !send_local || !stats)
+    return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  const int64_t ns = (int64_t)world * cap;
+  fill_i32_kernel<<<grid_for(ns, 256), 256, 0, s>>>(send_local, ns, -1);
+  if (n == 0) return rs_status_after_launch();
+  if (!rows || !slot || !workspace) return RS_ERR_ARG;
+  const RouteWs w = carve_route((char*)workspace, n, world);
+  if ((int64_t)w.total > workspace_bytes) return RS_ERR_ARG;
+  const unsigned nb = grid_for(n, 256);
+  owner_keys_kernel<<<nb, 256, 0, s>>>(rows, n, world, table_rows, w.keys_in, w.pos_in);
+  size_t tb = w.temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, w.keys_out, w.pos_in, w.pos_out,
+                                         (int)n, 0, owner_bits(world), s) != hipSuccess)
+    return RS_ERR_LAUNCH;
+  owner_bounds_kernel<<<1, 1024, 0, s>>>(w.keys_out, n, world, w.start, stats);
+  owner_emit_fixed_kernel<<<nb, 256, 0, s>>>(rows, w.keys_out, w.pos_out, w.start, n, world, cap,
+                                             send_local, slot);
   return rs_status_after_launch();
 }
 

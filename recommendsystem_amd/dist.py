@@ -8,8 +8,9 @@
            autograd post-hooks while the rest of backward runs; its graph-captured DP step: one
            all-reduce of the whole arena after the captured forward / backward.
   sharded: owner-sharded tables (embedding.ShardedSparseTable, row owner = row % world) move
-           lookups and gradients with two variable-split all-to-alls each way instead
-           (all_to_all_v; counts first).
+           lookups and gradients with two all-to-alls each way instead: variable splits
+           (all_to_all_v; counts first, read on the host) or, with owner_cap, equal fixed-size
+           blocks (all_to_all_fixed; no host read, graph-capturable under RCCL).
   sparse : each rank pre-reduces its touched rows locally (rs_sparse_grad_accumulate), compacts
            them into (rows, grads) lists, the lists are all-gathered (counts first, then lists
            padded to the max count with row -1), and every rank merges the lists IN RANK ORDER
@@ -187,6 +188,18 @@ def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, gr
         out.copy_(o)
     else:
         dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=group)
+
+
+def all_to_all_fixed(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """Equal-split all-to-all along dim 0 (world blocks of inp.shape[0] / world rows): the
+    fixed-capacity routing of owner-sharded tables.  Nothing host-side depends on the data, so
+    under RCCL it can be captured in a HIP graph; gloo stages device tensors through the host."""
+    if inp.is_cuda and dist.get_backend(group) != "nccl":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, group=group)
 
 
 def exchange_counts(counts: torch.Tensor, group=None):

@@ -213,15 +213,23 @@ class ShardedSparseTable:
     route them to their owners (rs_owner_route + all_to_all_v), the owners gather
     (rs_gather_rows) and send the rows back (rs_scatter_rows into id order); backward sends the
     per-id gradients the same way and the owner pushes them into its shard, so the sparse
-    optimizer step (``step``) is local and no table-sized exchange runs.  The routing needs the
-    per-owner counts on the host (one small all-to-all per lookup and per backward), so a step
-    over a sharded table runs eagerly (no graph capture).  Everything else (``weight``, ``grad``,
-    ``optimizer``, ``step``, ``check_overflow``, ...) is the local shard's."""
+    optimizer step (``step``) is local and no table-sized exchange runs.
+
+    Two routings.  ``owner_cap=None``: variable splits, the per-owner counts exchanged and read
+    on the host once per lookup (exact sizes, one host synchronisation per lookup).
+    ``owner_cap=c``: sync-free -- each (requester, owner) pair has a fixed block of c id slots
+    (rs_owner_route_fixed), so every all-to-all has equal splits known in advance, nothing is read
+    back and the whole step can be captured in one HIP graph (Trainer.capture_pool under RCCL);
+    a lookup that sends more than c ids to one owner drops the excess and records it in the sticky
+    ``route_stats`` word, which ``check_overflow`` reports (Trainer.measure_dp_caps sizes c from
+    the batches).  Everything else (``weight``, ``grad``, ``optimizer``, ``step``, ...) is the
+    local shard's."""
 
     sharded = True
 
     def __init__(self, rows: int, dim: int, optimizer=None, device=None, init_scale: float = 0.05,
-                 seed: int = 0, max_touched: int | None = None, process_group=None):
+                 seed: int = 0, max_touched: int | None = None, process_group=None,
+                 owner_cap: int | None = None):
         import torch.distributed as dist
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
@@ -235,6 +243,10 @@ class ShardedSparseTable:
         self.local = SparseTable(shard.shape[0], dim, optimizer, device=device, initial=shard,
                                  max_touched=max_touched)
         self._route_ws = None
+        self.owner_cap = None if owner_cap is None else int(owner_cap)
+        # [0]: the largest ids one lookup sent to one owner (sticky; device, fixed routing)
+        self.route_stats = torch.zeros(1, device=self.local.weight.device, dtype=torch.int32)
+        self.peak_owner_ids = 0  # the same on the host (variable routing: from the counts it reads)
 
     def __getattr__(self, name):  # the shard's state and methods
         if name == "local":
@@ -265,9 +277,23 @@ class ShardedSparseTable:
             self._route_ws = torch.empty(need, device=self.local.weight.device, dtype=torch.uint8)
         return self._route_ws
 
+    def check_overflow(self) -> None:
+        """The shard's touched-list check, and (fixed routing) whether a lookup sent more ids to
+        one owner than owner_cap (those ids were dropped).  Reads the device."""
+        self.local.check_overflow()
+        if self.owner_cap is not None:
+            n = int(self.route_stats[0].item())
+            if n > self.owner_cap:
+                self.route_stats.zero_()
+                raise RuntimeError(f"sharded table routing overflow: a lookup sent {n} ids to one "
+                                   f"owner, owner_cap is {self.owner_cap} (raise owner_cap)")
+
     def route(self, rows: torch.Tensor):
-        """Global rows int32 [n] (-1 = no row) -> the routing plan shared by gather and push:
-        (send_pos [nv], send_splits, recv_splits, recv_local [nr])."""
+        """Global rows int32 [n] (-1 = no row) -> the routing plan shared by gather and push.
+        Variable routing: ("v", send_pos [nv], send_splits, recv_splits, recv_local [nr]);
+        fixed routing: ("f", slot [n], recv_local [world * owner_cap])."""
+        if self.owner_cap is not None:
+            return self._route_fixed(rows)
         from .dist import all_to_all_v, exchange_counts
         n, dev = rows.numel(), rows.device
         send_local = torch.empty(n, device=dev, dtype=torch.int32)
@@ -277,17 +303,42 @@ class ShardedSparseTable:
         call("rs_owner_route", stream_handle(), ptr(rows), n, self.world, self.rows, ptr(send_local),
              ptr(send_pos), ptr(counts), ptr(ws), ws.numel())
         sc, rc = exchange_counts(counts, self.pg)
+        self.peak_owner_ids = max(self.peak_owner_ids, max(sc, default=0))
         nv, nr = sum(sc), sum(rc)
         recv_local = torch.empty(nr, device=dev, dtype=torch.int32)
         all_to_all_v(recv_local, send_local[:nv], rc, sc, self.pg)
-        return send_pos[:nv], sc, rc, recv_local
+        return "v", send_pos[:nv], sc, rc, recv_local
+
+    def _route_fixed(self, rows: torch.Tensor):
+        from .dist import all_to_all_fixed
+        n, dev, c = rows.numel(), rows.device, self.owner_cap
+        send_local = torch.empty(self.world * c, device=dev, dtype=torch.int32)
+        slot = torch.empty(n, device=dev, dtype=torch.int32)
+        ws = self._workspace(n)
+        call("rs_owner_route_fixed", stream_handle(), ptr(rows), n, self.world, self.rows, c,
+             ptr(send_local), ptr(slot), ptr(self.route_stats), ptr(ws), ws.numel())
+        recv_local = torch.empty_like(send_local)
+        all_to_all_fixed(recv_local, send_local, self.pg)
+        return "f", slot, recv_local
 
     def gather(self, rows: torch.Tensor):
         """-> (E [n, dim] with E[k] = table[rows[k]] (zero where rows[k] < 0), plan)."""
-        from .dist import all_to_all_v
+        from .dist import all_to_all_fixed, all_to_all_v
         plan = self.route(rows)
-        send_pos, sc, rc, recv_local = plan
         dev, d = rows.device, self.dim
+        if plan[0] == "f":  # fixed blocks: pads (-1) gather zero rows, slot -1 reads a zero row
+            _, slot, recv_local = plan
+            served = torch.empty(recv_local.numel(), d, device=dev)
+            call("rs_gather_rows", stream_handle(), ptr(self.local.weight), d, ptr(recv_local),
+                 recv_local.numel(), d, ptr(served), d)
+            back = torch.empty_like(served)
+            all_to_all_fixed(back, served, self.pg)
+            E = torch.empty(rows.numel(), d, device=dev)
+            if rows.numel():
+                call("rs_gather_rows", stream_handle(), ptr(back), d, ptr(slot), rows.numel(), d,
+                     ptr(E), d)
+            return E, plan
+        _, send_pos, sc, rc, recv_local = plan
         served = torch.empty(recv_local.numel(), d, device=dev)
         if served.numel():
             call("rs_gather_rows", stream_handle(), ptr(self.local.weight), d, ptr(recv_local),
@@ -302,9 +353,20 @@ class ShardedSparseTable:
 
     def push(self, dE: torch.Tensor, plan) -> None:
         """Per-id gradients dE [n, dim] (the rows of gather's E) -> the owners' gradient rows."""
-        from .dist import all_to_all_v
-        send_pos, sc, rc, recv_local = plan
+        from .dist import all_to_all_fixed, all_to_all_v
         d = self.dim
+        if plan[0] == "f":  # pad slots travel unwritten: their row at the owner is -1 (skipped)
+            _, slot, recv_local = plan
+            g = torch.empty(recv_local.numel(), d, device=dE.device)
+            if slot.numel():
+                call("rs_scatter_rows", stream_handle(), ptr(dE), d, ptr(slot), slot.numel(), d,
+                     ptr(g), d)
+            recv = torch.empty_like(g)
+            all_to_all_fixed(recv, g, self.pg)
+            self.local.accumulate(recv_local, None, recv_local.numel(), 1, recv, d, d,
+                                  COMBINERS["sum"])
+            return
+        _, send_pos, sc, rc, recv_local = plan
         g = torch.empty(send_pos.numel(), d, device=dE.device)
         if g.numel():
             call("rs_gather_rows", stream_handle(), ptr(dE), d, ptr(send_pos), send_pos.numel(), d,

@@ -171,12 +171,26 @@ class Trainer:
     # one all-gather per table of nmax rows / gradient rows -- or, with dp_caps, fixed-size
     # all-gathers and no host read) -> graph B (rank-ordered merges that read the counts on the
     # device, rs_sparse_merge_rows_dev[_stride]; dense Adam; sparse optimizers).
+    #
+    # Owner-sharded tables route their lookups and pushes with all-to-alls INSIDE forward and
+    # backward; with fixed routing (owner_cap, equal splits, no host read) those collectives are
+    # captured into the forward/backward graph itself, which needs a backend whose collectives
+    # are graph-capturable: RCCL ('nccl').  Their optimizer step is local (graph B).
     def _dp_setup(self, dp_caps=None):
         dev = self.arena.data.device
         self._rep = [t for t in self.tables if not is_sharded(t)]
-        if len(self._rep) != len(self.tables):
-            raise NotImplementedError("graph capture under DP needs replicated tables (owner-sharded "
-                                      "tables exchange host-sized all-to-alls inside backward)")
+        sharded = [t for t in self.tables if is_sharded(t)]
+        if sharded:
+            from .dist import uses_flat_all_gather
+            if any(t.owner_cap is None for t in sharded):
+                raise NotImplementedError(
+                    "graph capture under DP with owner-sharded tables needs their fixed routing "
+                    "(ShardedSparseTable(owner_cap=...) or Trainer.measure_dp_caps): variable "
+                    "splits read the per-owner counts on the host inside the step")
+            if not uses_flat_all_gather(self.pg):
+                raise NotImplementedError(
+                    "graph capture under DP with owner-sharded tables needs RCCL ('nccl'): the "
+                    "tables' all-to-alls are captured into the forward/backward graph")
         T = len(self._rep)
         self.dp_counts = torch.zeros(max(T, 1), device=dev, dtype=torch.int32)
         self.dp_counts_all = torch.zeros(self.world * max(T, 1), device=dev, dtype=torch.int32)
@@ -274,15 +288,21 @@ class Trainer:
 
     def measure_dp_caps(self, batches, headroom: float = 1.25, quantum: int = 256):
         """dp_caps for capture_pool from the batches themselves: each batch's forward/backward
-        runs once (eagerly, no collectives) and every replicated table's claimed-row count is
-        read back; the per-table maximum over batches and ranks (one all-reduce MAX: every rank
-        must use the same capacities), times ``headroom``, rounded up to ``quantum``, capped at
-        the touched-list size.  The training state is restored afterwards.  A later step that
-        touches more rows is caught by the sticky overflow word (step_pool reads it every
-        dp_check_every replays), never trained on silently."""
+        runs once (eagerly; owner-sharded tables route with variable splits) and every
+        replicated table's claimed-row count is read back; the per-table maximum over batches
+        and ranks (one all-reduce MAX: every rank must use the same capacities), times
+        ``headroom``, rounded up to ``quantum``, capped at the touched-list size.  Owner-sharded
+        tables get their ``owner_cap`` set the same way from the largest number of ids one
+        lookup sent to one owner (rounded up to quantum / 8).  The training state is restored
+        afterwards.  A later step that touches more rows (or routes more ids) is caught by the
+        sticky overflow words (step_pool reads them every dp_check_every replays), never trained
+        on silently.  Returns the replicated tables' caps."""
         rep = [t for t in self.tables if not is_sharded(t)]
+        sharded = [t for t in self.tables if is_sharded(t)]
+        for t in sharded:
+            t.owner_cap, t.peak_owner_ids = None, 0
         saved = [t.clone() for t in self._state()]
-        peak = torch.zeros(max(len(rep), 1), dtype=torch.int64)
+        peak = torch.zeros(max(len(rep) + len(sharded), 1), dtype=torch.int64)
         for b in batches:
             for t in rep:
                 t.n_touched[:1].zero_()
@@ -291,6 +311,8 @@ class Trainer:
                 peak[i] = max(int(peak[i]), int(t.n_touched[0].item()))
             for t, v in zip(self._state(), saved):
                 t.copy_(v)
+        for i, t in enumerate(sharded):
+            peak[len(rep) + i] = int(t.peak_owner_ids)
         if self.world > 1:
             pk = peak.to(self.arena.data.device)
             torch.distributed.all_reduce(pk, op=torch.distributed.ReduceOp.MAX, group=self.pg)
@@ -300,6 +322,11 @@ class Trainer:
         for i, t in enumerate(rep):
             c = -(-int(int(peak[i]) * headroom) // quantum) * quantum
             caps.append(int(min(max(c, quantum), t.touched_cap)))
+        q8 = max(1, quantum // 8)
+        for i, t in enumerate(sharded):
+            c = -(-int(int(peak[len(rep) + i]) * headroom) // q8) * q8
+            t.owner_cap = int(max(c, q8))
+            t.route_stats.zero_()
         return caps
 
     def check_dp_overflow(self) -> None:
@@ -310,6 +337,9 @@ class Trainer:
             self.dp_overflow.zero_()
             raise RuntimeError(f"sparse DP exchange overflow: a rank touched {n} rows, dp_caps "
                                f"{self.dp_caps} (raise dp_caps)")
+        for t in self.tables:  # owner-sharded tables: ids past owner_cap in a fixed route
+            if is_sharded(t) and t.owner_cap is not None:
+                t.check_overflow()
 
     def capture_pool(self, batches, warmup: int = 1, dp_caps=None) -> None:
         """Record one whole training step per device-resident batch (forward, autograd backward,
@@ -320,7 +350,9 @@ class Trainer:
         Data parallel (world > 1): per batch a forward/backward graph (ending with the sparse
         lists packed), the collectives eager, then ONE merge + optimizer graph (_dp_* above);
         with dp_caps (per replicated table: rows one rank can touch per step) the collectives
-        have fixed sizes and the host reads nothing back (sync-free; check_dp_overflow)."""
+        have fixed sizes and the host reads nothing back (sync-free; check_dp_overflow).
+        Owner-sharded tables with fixed routing put their all-to-alls inside the forward/
+        backward graph (RCCL only; _dp_setup)."""
         if self.world > 1:
             self._dp_setup(dp_caps)
         saved = [t.clone() for t in self._state()]

@@ -4,6 +4,8 @@ the op path with the layer path, and a torch.compile(backend="aot_eager") trace 
 routes its layers through the ops."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -12,6 +14,7 @@ from _tol import assert_close, assert_grad_close, to_np
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(autouse=True)
@@ -253,9 +256,13 @@ def test_gated_group_matches_gated():
                                        (2048, 64, 3, 0)])
 def test_dense_bwd_one_launch_equals_two(M, K, N, act):
     """rs_dense_bwd (data + weight gradient blocks in one launch) == rs_dense_bwd_data followed by
-    rs_dense_bwd_weight, bitwise (same block plans, same summation order), with accumulation."""
+    rs_dense_bwd_weight, bitwise (same block plans, same summation order), with accumulation.  A
+    shape on the library route (rs_dense_uses_library; the data gradient of rs_dense_bwd then
+    reads the materialised dZ, rs_dense_bwd_data's recomputes it on the engine) agrees to fp32
+    rounding instead."""
     from recommendsystem_amd import _lib
     from recommendsystem_amd._lib import call, ptr, stream_handle
+    lib_route = bool(_lib.load().rs_dense_uses_library(M, K, N))
     g = torch.Generator(device="cuda").manual_seed(M + K + N)
     s = stream_handle()
     X = torch.rand(M, K, device="cuda", generator=g) - 0.5
@@ -279,4 +286,74 @@ def test_dense_bwd_one_launch_equals_two(M, K, N, act):
         torch.cuda.synchronize()
         res.append((dX, dW, db))
     for a, b in zip(*res):
-        assert torch.equal(a, b)
+        if lib_route:
+            assert_close(to_np(a), to_np(b), 1e-7 * max(K, N) * 8, 1e-5, what="one vs two (library)")
+        else:
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,K,N,act", [(2048, 1712, 960, 1), (4096, 1616, 273, 0), (2048, 1840, 400, 2),
+                                       (2048, 1712, 256, 1)])
+def test_dense_library_route_matches_engine(M, K, N, act):
+    """The library route (hipBLASLt, rs_dense_uses_library) against the engine forced by
+    RS_GEMM_BLAS=0 in a child process and against float64: forward (bias + activation),
+    rs_dense_bwd (dX accumulated, dW / db accumulated), repeated launches bitwise equal."""
+    import subprocess, sys
+    from recommendsystem_amd import _lib
+    lib = _lib.load()
+    if not lib.rs_dense_uses_library(M, K, N):
+        pytest.skip("below the library threshold")
+    code = f"""
+import sys, torch, numpy as np
+sys.path.insert(0, {repr(ROOT)})
+from recommendsystem_amd import _lib
+from recommendsystem_amd._lib import call, ptr, stream_handle
+M, K, N, act = {M}, {K}, {N}, {act}
+g = torch.Generator(device="cuda").manual_seed(M + K + N)
+X = torch.rand(M, K, device="cuda", generator=g) - 0.5
+W = (torch.rand(K, N, device="cuda", generator=g) - 0.5) * 0.1
+b = torch.rand(N, device="cuda", generator=g) - 0.5
+dY = torch.rand(M, N, device="cuda", generator=g) - 0.5
+s = stream_handle()
+outs = []
+for rep in range(2):
+    Y = torch.empty(M, N, device="cuda")
+    call("rs_dense_fwd", s, ptr(X), M, K, K, ptr(W), ptr(b), N, act, ptr(Y), N)
+    wsn = int(_lib.load().rs_dense_bwd_weight_workspace_floats(M, K, N))
+    ws = torch.full((max(wsn, 1),), float("nan"), device="cuda")
+    dX = torch.full((M, K), 0.5, device="cuda")
+    dW = torch.full((K, N), 0.25, device="cuda")
+    db = torch.full((N,), 0.125, device="cuda")
+    call("rs_dense_bwd", s, ptr(X), K, ptr(dY), N, ptr(Y), N, act, ptr(W), M, K, N, ptr(dX), K, 1,
+         ptr(dW), ptr(db), 1, ptr(ws), wsn)
+    torch.cuda.synchronize()
+    outs.append([t.cpu() for t in (Y, dX, dW, db)])
+assert all(torch.equal(a, b) for a, b in zip(*outs))
+np.savez(sys.argv[1], *[t.numpy() for t in outs[0]])
+"""
+    import tempfile
+    res = {}
+    for mode in ("lib", "engine"):
+        env = dict(os.environ)
+        if mode == "engine":
+            env["RS_GEMM_BLAS"] = "0"
+        with tempfile.NamedTemporaryFile(suffix=".npz") as f:
+            r = subprocess.run([sys.executable, "-c", code, f.name], env=env, capture_output=True,
+                               text=True, timeout=120)
+            assert r.returncode == 0, r.stderr[-3000:]
+            z = np.load(f.name)
+            res[mode] = [z[f"arr_{i}"] for i in range(4)]
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    X = (torch.rand(M, K, device="cuda", generator=g) - 0.5).double()
+    W = ((torch.rand(K, N, device="cuda", generator=g) - 0.5) * 0.1).double()
+    b = (torch.rand(N, device="cuda", generator=g) - 0.5).double()
+    dY = (torch.rand(M, N, device="cuda", generator=g) - 0.5).double()
+    z = X @ W + b
+    Y = torch.relu(z) if act == 1 else torch.sigmoid(z) if act == 2 else z
+    Yf = torch.from_numpy(res["lib"][0]).cuda().double()
+    dZ = dY * (Yf > 0) if act == 1 else dY * Yf * (1 - Yf) if act == 2 else dY
+    ref = [Y, dZ @ W.T + 0.5, X.T @ dZ + 0.25, dZ.sum(0) + 0.125]
+    tols = [1e-7 * K * 0.25 * 8, 1e-7 * N * 0.05 * 8, 1e-7 * M * 0.25 * 8, 1e-7 * M * 8]
+    for i, what in enumerate(("y", "dX", "dW", "db")):
+        for mode in ("lib", "engine"):
+            assert_close(res[mode][i], ref[i].cpu().numpy(), tols[i], 1e-5, what=f"{what} ({mode})")

@@ -56,6 +56,31 @@ def test_owner_route_matches_oracle(world, n):
     assert np.array_equal(sl[:nv], esl) and np.array_equal(sp[:nv], esp)
 
 
+@pytest.mark.parametrize("world,cap", [(1, 7), (2, 300), (3, 1), (8, 40_000), (8, 130)])
+@pytest.mark.parametrize("n", [0, 1, 1000, 300_000])
+def test_owner_route_fixed_matches_oracle(world, cap, n):
+    """rs_owner_route_fixed bit-exact vs oracle/ctr_oracle.py::owner_route_fixed: the fixed
+    [world][cap] send blocks (pads -1), every position's slot (-1 past its owner's cap or for an
+    invalid row) and the sticky peak count (starts at 5: only raised, never lowered)."""
+    from recommendsystem_amd._lib import load, ptr, stream_handle
+    rng = np.random.default_rng(world * 11 + n + cap)
+    R = 1_000_003
+    rows = rng.integers(-1, R + 50, size=n).astype(np.int32)
+    rd = torch.from_numpy(rows).to(DEV)
+    ws = torch.empty(int(load().rs_owner_route_workspace_bytes(n, world)), device=DEV,
+                     dtype=torch.uint8)
+    sl = torch.full((world * cap,), -7, device=DEV, dtype=torch.int32)
+    slot = torch.full((max(n, 1),), -7, device=DEV, dtype=torch.int32)
+    stats = torch.full((1,), 5, device=DEV, dtype=torch.int32)
+    _call("rs_owner_route_fixed", stream_handle(), ptr(rd), n, world, R, cap, ptr(sl), ptr(slot),
+          ptr(stats), ptr(ws), ws.numel())
+    torch.cuda.synchronize()
+    esl, eslot, peak = npo.owner_route_fixed(rows, world, R, cap)
+    assert np.array_equal(sl.cpu().numpy(), esl)
+    assert np.array_equal(slot.cpu().numpy()[:n], eslot)
+    assert int(stats[0]) == max(5, peak)
+
+
 def test_gather_scatter_expand_rows():
     from recommendsystem_amd._lib import ptr, stream_handle
     g = torch.Generator().manual_seed(3)
@@ -160,11 +185,12 @@ def _lookup_batch(rank):
     return ids, offs, single, sids, soffs
 
 
-def _lookup_worker(rank, world, port, out):
+def _lookup_worker(rank, world, port, out, owner_cap=None):
     _init(rank, world, port)
     from recommendsystem_amd.embedding import (EmbeddingFeatures, SequenceEmbedding,
                                                ShardedSparseTable, SparseAdaGrad)
-    t = ShardedSparseTable(ROWS, DIM, SparseAdaGrad(), device=DEV, seed=4, process_group=dist.group.WORLD)
+    t = ShardedSparseTable(ROWS, DIM, SparseAdaGrad(), device=DEV, seed=4, process_group=dist.group.WORLD,
+                           owner_cap=owner_cap)
     ids, offs, single, sids, soffs = (torch.from_numpy(x).to(DEV) for x in _lookup_batch(rank))
     var = EmbeddingFeatures(t, [9000, 9000, 2011], combiner="mean", hash_mode="splitmix")
     one = EmbeddingFeatures(t, [ROWS] * 3, row_base=[0] * 3, combiner="sqrtn", hash_mode="splitmix")
@@ -175,6 +201,7 @@ def _lookup_worker(rank, world, port, out):
     dv, do, ds = (torch.randn(x.shape, generator=gen).to(DEV) for x in (ev, eo, es))
     torch.autograd.backward([ev, eo, es], [dv, do, ds])
     torch.cuda.synchronize()
+    t.check_overflow()
     out[rank] = dict(ev=ev.detach().cpu().numpy(), eo=eo.detach().cpu().numpy(),
                      es=es.detach().cpu().numpy(), mask=mask.cpu().numpy(), dv=dv.cpu().numpy(),
                      do=do.cpu().numpy(), ds=ds.cpu().numpy(), grad=t.grad.cpu().numpy(),
@@ -183,10 +210,13 @@ def _lookup_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_sharded_lookups_world2_match_oracle():
+@pytest.mark.parametrize("owner_cap", [None, 512])
+def test_sharded_lookups_world2_match_oracle(owner_cap):
+    """owner_cap: the sync-free fixed routing (equal-split all-to-alls; the largest lookup here
+    sends < 512 ids to one owner, check_overflow confirms)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_lookup_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    mp.spawn(_lookup_worker, args=(WORLD, _free_port(), out, owner_cap), nprocs=WORLD, join=True)
     from recommendsystem_amd.embedding import SparseAdaGrad, SparseTable
     W = SparseTable.initial_weight(ROWS, DIM, SparseAdaGrad(), 0.05, 4).numpy().astype(np.float64)
     gsum = np.zeros((ROWS, DIM))
@@ -228,8 +258,9 @@ def _train_worker(rank, world, port, out):
     from recommendsystem_amd.workloads import StaytimeRoughRank, staytime_batch
     pg = dist.group.WORLD
     res = {}
-    for kind in ("replicated", "sharded"):
-        j = StaytimeRoughRank(rows=ROWS, device=DEV, seed=3, shard_group=pg if kind == "sharded" else None)
+    for kind in ("replicated", "sharded", "sharded_fixed"):
+        j = StaytimeRoughRank(rows=ROWS, device=DEV, seed=3,
+                              shard_group=pg if kind.startswith("sharded") else None)
         trn = Trainer(j, 5e-4, [j.table], process_group=pg)
         grads = []
         # pack the arena gradient (layer-alignment gaps, trainer.ARENA_ALIGN) in parameter order
@@ -239,6 +270,9 @@ def _train_worker(rank, world, port, out):
             (torch.cat([g[o:o + n] for o, n in spans]) * scale).cpu().numpy())
         rng = np.random.default_rng(90 + rank)
         batches = [staytime_batch(rng, B5, j, DEV) for _ in range(2)]
+        if kind == "sharded_fixed":  # fixed routing sized from the batches (max over ranks)
+            trn.measure_dp_caps(batches)
+            assert j.table.owner_cap is not None
         losses = [float(trn.step(*batches[s % 2])) for s in range(STEPS)]
         torch.cuda.synchronize()
         j.table.check_overflow()
@@ -257,17 +291,23 @@ def test_config5_sharded_dp_matches_replicated_dp():
     gradients are compared at every step; the dense parameters with the Adam ill-conditioning
     rule of tests/_tol.py::adam_close: an entry whose gradient is ~0, or whose two gradients
     differ by more than 0.1 % relative at any step, may differ by Adam's scale-free update; such
-    entries must be rare (<= 0.1 %), everything else must match."""
-    from _tol import adam_close, assert_grad_close
+    entries must be rare (<= 0.1 %), everything else must match.  Both routings of the sharded
+    table (variable splits; fixed owner_cap blocks sized by Trainer.measure_dp_caps) are checked."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_train_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
     rep0, rep1 = out[0]["replicated"], out[1]["replicated"]
     assert np.array_equal(rep0[2], rep1[2])  # replicated tables stay bitwise identical
+    for kind in ("sharded", "sharded_fixed"):
+        _check_sharded_vs_replicated(out, kind, rep0)
+
+
+def _check_sharded_vs_replicated(out, kind, rep0):
+    from _tol import adam_close, assert_grad_close
     table = np.empty_like(rep0[2])
     g2 = np.empty_like(rep0[3])
     for r in range(WORLD):
-        losses, params, w, g, dg = out[r]["sharded"]
+        losses, params, w, g, dg = out[r][kind]
         rl, rp, _, _, rdg = out[r]["replicated"]
         np.testing.assert_allclose(losses, rl, rtol=2e-5)
         assert dg.shape == rdg.shape == (STEPS, params.size)
@@ -285,3 +325,61 @@ def test_config5_sharded_dp_matches_replicated_dp():
     from recommendsystem_amd.embedding import SparseAdaGrad, SparseTable
     init = SparseTable.initial_weight(ROWS, 32, SparseAdaGrad(), 0.05, 3).numpy()
     assert (np.abs(table - init).max(1) > 0).sum() > 1000  # the shards really trained
+
+
+_CAPTURED_CHILD = r"""
+import os, sys, traceback
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch, torch.distributed as dist
+DEV = torch.device("cuda", 0)
+os.environ["MASTER_ADDR"] = "127.0.0.1"
+os.environ["MASTER_PORT"] = sys.argv[2]
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=DEV)
+rc = 0
+try:
+    from recommendsystem_amd.trainer import Trainer
+    from recommendsystem_amd.workloads import StaytimeRoughRank, staytime_batch
+    pg = dist.group.WORLD
+    res = []
+    for graphed in (False, True):
+        j = StaytimeRoughRank(rows=20_011, device=DEV, seed=3, shard_group=pg)
+        j.table.deterministic = True
+        trn = Trainer(j, 5e-4, [j.table], process_group=pg)
+        rng = np.random.default_rng(91)
+        batches = [staytime_batch(rng, 64, j, DEV) for _ in range(2)]
+        caps = trn.measure_dp_caps(batches)
+        assert caps == [] and 0 < j.table.owner_cap <= 64 * (91 + 150 + 52), j.table.owner_cap
+        if graphed:
+            trn.capture_pool(batches, warmup=1)
+            losses = [float(trn.step_pool(s)) for s in range(3)]
+        else:
+            losses = [float(trn.step(*batches[s % 2])) for s in range(3)]
+        torch.cuda.synchronize()
+        j.table.check_overflow()
+        params = torch.cat([p.detach().reshape(-1).cpu() for p in j.parameters()])
+        res.append((losses, params, j.table.weight.cpu().clone()))
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+    print("CAPTURED-SHARDED-OK", res[1][0], flush=True)
+except Exception:
+    traceback.print_exc()
+    rc = 1
+sys.stdout.flush()
+sys.stderr.flush()
+os._exit(rc)  # (no process-group teardown: the test judges the step, not RCCL's shutdown)
+"""
+
+
+def test_sharded_table_captured_step_rccl_world1():
+    """Owner-sharded config 5 on RCCL ('nccl'; a world-1 group on this one-GPU box -- the 8-GPU
+    node runs the same calls): Trainer.measure_dp_caps gives the table its fixed routing
+    capacity, capture_pool records whole steps whose equal-split all-to-alls are captured into
+    the HIP graph, and the replays equal eager steps over the same batches bitwise (deterministic
+    pushes), with no routing overflow.  Runs in a child process under a time limit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _CAPTURED_CHILD, root, str(_free_port())],
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and "CAPTURED-SHARDED-OK" in r.stdout, (r.stdout[-2000:] +
+                                                                     r.stderr[-4000:])

@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -33,6 +34,12 @@ def _host_call(name, *a):
         send_local[:sl.size] = torch.from_numpy(sl)
         send_pos[:sp.size] = torch.from_numpy(sp)
         counts.copy_(torch.from_numpy(c))
+    elif name == "rs_owner_route_fixed":
+        _, rows, n, world, table_rows, cap, send_local, slot, stats, _ws, _wn = a
+        sl, st, peak = npo.owner_route_fixed(rows.numpy(), world, table_rows, cap)
+        send_local.copy_(torch.from_numpy(sl))
+        slot.copy_(torch.from_numpy(st))
+        stats[0] = max(int(stats[0]), peak)
     elif name == "rs_gather_rows":
         _, src, src_ld, idx, n, dim, dst, dst_ld = a
         s = src.reshape(-1, src_ld)[:, :dim]
@@ -123,15 +130,18 @@ def _batch(rank):
     return [torch.from_numpy(x) for x in (ids, offs, single, sids, soffs)]
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, owner_cap=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     _patch()
+    from recommendsystem_amd import dist as rdist
     from recommendsystem_amd.embedding import (EmbeddingFeatures, SequenceEmbedding,
                                                ShardedSparseTable, SparseAdaGrad)
     t = ShardedSparseTable(ROWS, DIM, SparseAdaGrad(), device="cpu", seed=4,
-                           process_group=dist.group.WORLD)
+                           process_group=dist.group.WORLD, owner_cap=owner_cap)
+    if owner_cap is not None:  # fixed routing: no count exchange may run
+        rdist.exchange_counts = None
     ids, offs, single, sids, soffs = _batch(rank)
     var = EmbeddingFeatures(t, [50, 40, 13], combiner="mean", hash_mode="splitmix")
     one = EmbeddingFeatures(t, [ROWS] * 3, row_base=[0] * 3, combiner="sum", hash_mode="splitmix")
@@ -142,17 +152,37 @@ def _worker(rank, world, port, out):
     gen = torch.Generator().manual_seed(rank)
     dv, do, ds = (torch.randn(x.shape, generator=gen) for x in (ev, eo, es))
     torch.autograd.backward([ev, eo, es], [dv, do, ds])
+    overflow = None
+    if owner_cap is not None:
+        try:
+            t.check_overflow()
+        except RuntimeError as e:
+            overflow = str(e)
     out[rank] = dict(ev=ev.detach().numpy(), eo=eo.detach().numpy(), es=es.detach().numpy(),
                      mask=mask.numpy(), dv=dv.numpy(), do=do.numpy(), ds=ds.numpy(),
-                     grad=t.grad.numpy().copy(), local_rows=t.weight.shape[0])
+                     grad=t.grad.numpy().copy(), local_rows=t.weight.shape[0], overflow=overflow)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharded_table_protocol_world2():
+def test_owner_route_fixed_oracle():
+    rows = np.array([7, -1, 4, 9, 2, 11, 3, 100, 0, 5], dtype=np.int64)
+    sl, slot, peak = npo.owner_route_fixed(rows, 3, 12, 2)
+    # owner 0: 9, 3, 0 (0 past cap 2); owner 1: 7, 4; owner 2: 2, 11, 5 (5 past cap)
+    assert peak == 3
+    assert sl.tolist() == [3, 1, 2, 1, 0, 3]
+    assert slot.tolist() == [2, -1, 3, 0, 4, 5, 1, -1, -1, -1]
+    sl, slot, peak = npo.owner_route_fixed(np.array([], dtype=np.int64), 2, 10, 3)
+    assert sl.tolist() == [-1] * 6 and slot.size == 0 and peak == 0
+
+
+@pytest.mark.parametrize("owner_cap", [None, 64])
+def test_sharded_table_protocol_world2(owner_cap):
+    """owner_cap: the sync-free fixed routing (equal-split all-to-alls, no count exchange); 64
+    ids per (requester, owner) per lookup holds every lookup here, so the results are the same."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(WORLD, _free_port(), out), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(WORLD, _free_port(), out, owner_cap), nprocs=WORLD, join=True)
     from recommendsystem_amd.embedding import SparseAdaGrad, SparseTable
     W = SparseTable.initial_weight(ROWS, DIM, SparseAdaGrad(), 0.05, 4).numpy().astype(np.float64)
     assert out[0]["local_rows"] == 52 and out[1]["local_rows"] == 51
@@ -181,6 +211,17 @@ def test_sharded_table_protocol_world2():
         np.add.at(gsum, srows.reshape(-1)[ok], o["ds"].reshape(-1, DIM)[ok])
     for r in range(WORLD):  # owner r holds rows r, r + 2, ...
         np.testing.assert_allclose(out[r]["grad"], gsum[r::WORLD], rtol=1e-5, atol=1e-6)
+        assert out[r]["overflow"] is None
+
+
+def test_sharded_fixed_routing_overflow_is_reported():
+    """A lookup that sends more ids to one owner than owner_cap drops the excess and the sticky
+    route word makes check_overflow raise (never trained on silently)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(WORLD, _free_port(), out, 4), nprocs=WORLD, join=True)
+    for r in range(WORLD):
+        assert out[r]["overflow"] is not None and "owner_cap is 4" in out[r]["overflow"]
 
 
 def test_initial_shard_equals_slice_of_full_table():
