@@ -20,10 +20,15 @@
 //     block's partial row (column_reduce over blocks, deterministic), dX = dZ W^T thread = (row, e)
 //     -> the previous iteration's dY, dx, or the fused sparse push at iteration 0.
 //
-// LDS bounds the shape: the backward needs F (E + 8U) + 2 QT F + small floats (<= 160 KB), e.g.
-// the constructor defaults (E 16, U 128) up to F = 37 fields; larger shapes return
-// RS_ERR_UNSUPPORTED.  fp32 only (a bf16 math-mode request is RS_ERR_UNSUPPORTED).
+// The per-sample working set is F (E + 8U) + 2 QT F + small floats (backward).  When it fits the
+// 160 KB LDS (e.g. the constructor defaults (E 16, U 128) up to F = 37 fields) it lives there;
+// larger shapes (up to F = 256 at any E, U) run the SAME kernels with the working set in a
+// per-workgroup global scratch slab (GS = true: L1 / L2-resident, one slab per workgroup of a
+// 256-workgroup grid, grown on demand outside graph capture).  fp32 only (a bf16 math-mode
+// request is RS_ERR_UNSUPPORTED).
 #include "il_kernels.hpp"
+
+#include <mutex>
 
 namespace rs_il {
 namespace gen {
@@ -88,6 +93,7 @@ struct GArgs {
   float* push_table;
   int32_t* push_flag;
   Layout lay;
+  float* gscratch;  // GS kernels: lay.total floats per workgroup
 };
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -178,8 +184,10 @@ __device__ __forceinline__ uint32_t layer_key(const GArgs& a, int it, int64_t b)
                 : 0u;
 }
 
+template <bool GS>
 __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+  extern __shared__ __attribute__((aligned(16))) float lds_[];
+  float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
   const Layout& l = a.lay;
   const int F = a.F, U = a.U, E = a.E, XS = E;
   float* xs = sm + l.xs;
@@ -245,8 +253,10 @@ __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
   }
 }
 
+template <bool GS>
 __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+  extern __shared__ __attribute__((aligned(16))) float lds_[];
+  float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
   const Layout& l = a.lay;
   const int F = a.F, U = a.U, E = a.E, DH = a.DH, NC = 4 * U, XS = E;
   const int NPARAM = E * NC + NC + 2 * U;
@@ -453,14 +463,42 @@ GArgs make_args(int64_t B, int F, int E, int U, int H, int L, int use_res, float
   return a;
 }
 
+// GS (global-scratch) mode: workgroups of the grid, and the scratch slab shared by every GS launch
+// of the process (one stream at a time, like the launches themselves).  Grown only outside graph
+// capture (a captured step replays the size its eager warm-up established).
+constexpr int64_t kGsGrid = 256;
+
+float* gs_scratch(size_t floats, hipStream_t s) {
+  static std::mutex mu;
+  static float* buf = nullptr;
+  static size_t cap = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (floats <= cap) return buf;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  if (buf) {
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // (in-flight GS launches)
+    hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+  }
+  if (hipMalloc(&buf, floats * sizeof(float)) != hipSuccess) {
+    buf = nullptr;
+    return nullptr;
+  }
+  cap = floats;
+  return buf;
+}
+
 }  // namespace gen
 
 int il_generic_fwd(const FwdReq& q) {
   using namespace gen;
   if (q.bf16 || q.F > FMAXG || q.U % q.H != 0 || q.E <= 0 || (q.L > 1 && q.E != q.U))
     return RS_ERR_UNSUPPORTED;
-  const int qt = pick_qt(q.F, q.E, q.U, q.H, false);
-  if (qt == 0) return RS_ERR_UNSUPPORTED;
+  int qt = pick_qt(q.F, q.E, q.U, q.H, false);
+  const bool gs = qt == 0;
+  if (gs) qt = q.F < 64 ? q.F : 64;
   if (q.B == 0) return RS_OK;
   GArgs a = make_args(q.B, q.F, q.E, q.U, q.H, q.L, q.use_res, q.eps, q.drop_rate, q.seed);
   a.x = q.x; a.W = q.W; a.bias = q.bias; a.gamma = q.gamma; a.beta = q.beta;
@@ -469,8 +507,15 @@ int il_generic_fwd(const FwdReq& q) {
   a.g_table = q.gather_table; a.g_table_rows = q.gather_table_rows; a.g_rows = q.gather_rows;
   a.g_hash = q.gather_hash;
   a.lay = make_layout(q.F, q.E, q.U, q.H, qt, false);
+  if (gs) {
+    const int64_t grid = q.B < kGsGrid ? q.B : kGsGrid;
+    a.gscratch = gs_scratch((size_t)grid * a.lay.total, q.stream);
+    if (!a.gscratch) return RS_ERR_UNSUPPORTED;
+    fwd_kernel<true><<<(int)grid, NT, 0, q.stream>>>(a);
+    return rs_status_after_launch();
+  }
   const int64_t grid = q.B < 4096 ? q.B : 4096;
-  fwd_kernel<<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  fwd_kernel<false><<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
   return rs_status_after_launch();
 }
 
@@ -478,10 +523,12 @@ int il_generic_bwd(const BwdReq& q) {
   using namespace gen;
   if (q.bf16 || q.xt_x || q.F > FMAXG || q.U % q.H != 0 || q.E <= 0 || (q.L > 1 && q.E != q.U))
     return RS_ERR_UNSUPPORTED;
-  const int qt = pick_qt(q.F, q.E, q.U, q.H, true);
-  if (qt == 0) return RS_ERR_UNSUPPORTED;
+  int qt = pick_qt(q.F, q.E, q.U, q.H, true);
+  const bool gs = qt == 0;
+  if (gs) qt = q.F < 64 ? q.F : 64;
   const int nparam = q.E * 4 * q.U + 4 * q.U + 2 * q.U;
-  int64_t grid = q.B < kMaxBwdGrid ? q.B : kMaxBwdGrid;
+  const int64_t gmax = gs ? kGsGrid : kMaxBwdGrid;
+  int64_t grid = q.B < gmax ? q.B : gmax;
   const int64_t max_grid = q.workspace_floats / nparam;
   if (grid > max_grid) grid = max_grid;
   if (q.grid_out) { *q.grid_out = (int)(grid > 0 ? grid : 0); return RS_OK; }
@@ -493,7 +540,13 @@ int il_generic_bwd(const BwdReq& q) {
   a.dx = q.dx; a.dx_accumulate = q.dx_accumulate; a.part = q.workspace;
   a.push_rows = q.push_rows; a.push_table = q.push_table; a.push_flag = q.push_flag;
   a.lay = make_layout(q.F, q.E, q.U, q.H, qt, true);
-  bwd_kernel<<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  if (gs) {
+    a.gscratch = gs_scratch((size_t)grid * a.lay.total, q.stream);
+    if (!a.gscratch) return RS_ERR_UNSUPPORTED;
+    bwd_kernel<true><<<(int)grid, NT, 0, q.stream>>>(a);
+  } else {
+    bwd_kernel<false><<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  }
   int st = rs_status_after_launch();
   if (st || !q.dparams) return st;
   reduce_params(q.stream, q.workspace, (int)grid, nparam, q.dparams, q.dparams_accumulate);

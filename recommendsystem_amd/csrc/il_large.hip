@@ -580,8 +580,13 @@ int run_fwd(const FwdReq& q) {
 template <int E, int U, int H>
 int run_bwd(const BwdReq& q) {
   using C = LC<E, U, H>;
-  if (q.B == 0) return RS_OK;
   int64_t grid = q.B < kMaxBwdGrid ? q.B : kMaxBwdGrid;
+  if (q.grid_out) {  // dry run (rs_il_bwd_partial_blocks)
+    const int64_t by_ws = q.workspace_floats / C::NPARAM;
+    *q.grid_out = (int)(grid < by_ws ? grid : by_ws);
+    return RS_OK;
+  }
+  if (q.B == 0) return RS_OK;
   if (q.workspace_floats < grid * C::NPARAM) return RS_ERR_ARG;
   LBwd a{q.x, q.xsave, q.dy, q.W, q.bias, q.gamma, q.beta, q.dy_ld, q.B, q.F, q.L, q.use_res,
          q.drop_rate > 0.f, q.eps, q.drop_rate,

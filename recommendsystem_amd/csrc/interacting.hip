@@ -360,13 +360,7 @@ RS_API int rs_il_bwd_push_saved_xt(void* stream, const float* x, const float* xs
 
 static int il_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t workspace_floats,
                              bool saved) {
-  if (F > 64) {  // il_large.hip's grid rule
-    int64_t grid = B < rs_il::kMaxBwdGrid ? B : rs_il::kMaxBwdGrid;
-    const int64_t by_ws = workspace_floats / rs_il_param_count(E, U);
-    if (grid > by_ws) grid = by_ws;
-    return (int)(grid < 0 ? 0 : grid);
-  }
-  // the F <= 64 kernels pick a variant per shape: ask the dispatch (dry run, nothing launched).
+  // the kernels pick a variant per shape: ask the dispatch (dry run, nothing launched).
   // Pointers only need the alignment the real call has (the fused trainer's dy is 16-B aligned);
   // saved: the entry points that read the forward's attention save (another kernel pair for the
   // shapes that have one)
@@ -378,8 +372,8 @@ static int il_partial_blocks(int64_t B, int F, int E, int U, int H, int64_t work
   q.grid_out = &grid;
   q.bf16 = rs_math_mode_now() == RS_MATH_BF16;
   if (saved && rs_il_attn_save_floats(B < 1 ? 1 : B, F, U, H, 1) > 0) q.asave = kDummy;
-  if (bwd_small(q) != RS_OK) return 0;
-  return grid;
+  if ((F > 64 ? bwd_large(q) : bwd_small(q)) != RS_OK) return 0;
+  return grid < 0 ? 0 : grid;
 }
 
 RS_API int rs_il_bwd_partial_blocks(int64_t B, int F, int E, int U, int H,

@@ -246,6 +246,10 @@ IL_CASES = [  # (B, F, E, U, H, L, use_res)
     (6, 13, 32, 32, 2, 2, True),
     (4, 26, 16, 128, 1, 1, True),    # constructor defaults (config 1): il_generic.hip
     (9, 37, 16, 128, 1, 1, True),    # the defaults at the generic kernel's largest F (LDS)
+    (3, 64, 16, 128, 1, 1, True),    # the defaults past the LDS: global-scratch generic kernels
+    (2, 256, 16, 128, 1, 1, True),   # ... at F = 256
+    (2, 100, 128, 128, 1, 2, True),  # E = U = 128 tied iterations over 100 fields (global scratch)
+    (2, 256, 16, 16, 2, 1, True),    # AutoInt width at F = 256 (il_large's LDS exceeded)
     (7, 26, 16, 24, 3, 1, True),     # dh = 8 over three heads: il_generic.hip
     (6, 20, 32, 64, 4, 1, True),     # E 32, U 64, four heads of 16: il_generic.hip
     (5, 30, 24, 24, 3, 2, False),    # tied iterations at a generic width, no residual
