@@ -21,6 +21,7 @@ from torch import nn
 
 from . import _lib
 from ._lib import call, ptr, stream_handle
+from .dist import capture_error_mode
 from .embedding import EmbeddingFeatures, SparseAdam, SparseTable
 from .layers import ACTIVATIONS, InteractingLayer, MultiLayerDense
 from .params import ParamArena
@@ -652,7 +653,7 @@ class AutoIntTrainer:
         (N = 1), or the forward/backward half only (N > 1: the collectives stay eager and the
         optimizer half is recorded once by _record_opt)."""
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=capture_error_mode()):
             if self.world == 1:
                 self._step_eager()
             else:
@@ -662,7 +663,7 @@ class AutoIntTrainer:
     def _record_opt(self):
         if getattr(self, "graph_opt", None) is None:
             self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt):
+            with torch.cuda.graph(self.graph_opt, capture_error_mode=capture_error_mode()):
                 self._optimize()
 
     def capture(self, warmup: int = 2) -> None:

@@ -26,6 +26,17 @@ import torch
 import torch.distributed as dist
 
 
+def capture_error_mode() -> str:
+    """HIP-graph capture mode for the trainers: "thread_local" whenever an RCCL process group
+    exists.  Its watchdog thread polls the events of earlier (eager) collectives with
+    hipEventQuery, which a global-mode capture forbids process-wide (hipErrorStreamCaptureUnsupported
+    -> the watchdog aborts the process); thread-local mode restricts only the capturing thread.
+    Otherwise torch's default ("global")."""
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        return "thread_local"
+    return "global"
+
+
 def allreduce_flat(grad: torch.Tensor, group=None) -> None:
     """Sum the flat dense gradient over ranks in place (the optimizer scales by 1/world)."""
     dist.all_reduce(grad, group=group)

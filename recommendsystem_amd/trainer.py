@@ -367,9 +367,11 @@ class Trainer:
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         self.graphs, self.graph_loss = [], []
+        from .dist import capture_error_mode
+        mode = capture_error_mode()
         for b in batches:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                 if self.world > 1:
                     loss = self._forward_backward(*b)
                     self._dp_pack()
@@ -380,7 +382,7 @@ class Trainer:
         self.graph_opt = None
         if self.world > 1:
             self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt):  # allocates nothing
+            with torch.cuda.graph(self.graph_opt, capture_error_mode=mode):  # allocates nothing
                 self._dp_merge_optimize()
         # prime: replay each graph once and roll the state back (a graph's first launch after
         # capture is slower; AutoIntTrainer._prime_graphs)
