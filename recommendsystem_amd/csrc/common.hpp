@@ -275,6 +275,17 @@ __device__ __forceinline__ bool dropout_keep_k(uint32_t kb, uint32_t h, uint32_t
   return (float)(r >> 8) * (1.0f / 16777216.0f) >= rate;
 }
 
+// the same decision against an integer threshold (dropout_thr24(rate) = ceil(rate * 2^24)):
+// (r >> 8) * 2^-24 >= rate  <=>  (r >> 8) >= ceil(rate * 2^24), both sides exact -- bit-identical
+// masks, two VALU operations fewer per element (no convert / multiply)
+__host__ __device__ __forceinline__ uint32_t dropout_thr24(float rate) {
+  return (uint32_t)ceilf(rate * 16777216.0f);
+}
+__device__ __forceinline__ bool dropout_keep_t(uint32_t kb, uint32_t h, uint32_t i, uint32_t j,
+                                               uint32_t thr24) {
+  return (fmix32(kb ^ ((h << 24) | (i << 12) | j)) >> 8) >= thr24;
+}
+
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t b, uint32_t h, uint32_t i,
                                              uint32_t j, float rate) {
   return dropout_keep_k(dropout_sample_key(seed, b), h, i, j, rate);

@@ -140,6 +140,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
                                           float drop_rate, float inv_keep, float4* st4,
                                           uint32_t* mask, float* sv) {
   const int W32 = (F + 31) / 32;
+  const uint32_t thr24 = dropout_thr24(drop_rate);
   for (int i = threadIdx.x; i < F; i += NT) {
     float q[C::U];
     ld<C::U>(q, Qs + i * C::U);
@@ -173,7 +174,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
         for (int h = 0; h < C::H; ++h) {
           const float e = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), sc2, -msc[h]));
           l[h] += e;
-          const bool keep = !drop || dropout_keep_k(kb, h, i, j, drop_rate);
+          const bool keep = !drop || dropout_keep_t(kb, h, i, j, thr24);
           bits[h] |= (uint32_t)keep << jj;
           const float ek = keep ? e : 0.f;
           haxpy<C>(o, ek, v, h);
@@ -382,10 +383,22 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
           da[u] = z[u] > 0.f ? dz : 0.f;
           dr[u] = (a.use_res && r[u] > 0.f) ? da[u] : 0.f;
         }
-        st<C::U>(Gs + i * C::U, da);
         st<C::U>(Rs + i * C::U, dr);
+        // passes A / B read the softmax 1/sum and the dropout scale pre-folded (they are per
+        // (row, head) constants of dS_ij = P_ij (keep inv_keep dO_i . v_j - D_i) with
+        // P_ij = e_ij / sum_i):  dS_ij = e_ij (keep (g'_i . v_j) - D'_i) with
+        // g'_i = dO_i inv_keep / sum_i and D'_i = D_i / sum_i, and dV_j += keep e_ij g'_i -- two
+        // to three multiplies fewer per score and head in the VALU-bound passes
+        const float ks = a.drop ? a.inv_keep : 1.f;
 #pragma unroll
-        for (int h = 0; h < C::H; ++h) st4[i * C::H + h].z = hdot<C>(da, o, h);
+        for (int h = 0; h < C::H; ++h) {
+          const float inv = st4[i * C::H + h].y;
+          st4[i * C::H + h].z = hdot<C>(da, o, h) * inv;
+          const float gs = inv * ks;
+#pragma unroll
+          for (int d = 0; d < C::DH; ++d) da[h * C::DH + d] *= gs;
+        }
+        st<C::U>(Gs + i * C::U, da);
       }
       __syncthreads();
       // ---- passes A and B side by side: threads [0, NT/2) run pass A (dQ -> Os) over query
@@ -425,12 +438,12 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
               ld<C::U>(v, Vs + j * C::U);
 #pragma unroll
               for (int h = 0; h < C::H; ++h) {
-                const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q0, k, h), a.sc2, -s0[h].x)) * s0[h].y;
-                const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q1, k, h), a.sc2, -s1[h].x)) * s1[h].y;
+                const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q0, k, h), a.sc2, -s0[h].x));
+                const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q1, k, h), a.sc2, -s1[h].x));
                 float dP0 = hdot<C>(g0, v, h), dP1 = hdot<C>(g1, v, h);
                 if (a.drop) {
-                  dP0 = ((m0[h] >> jj) & 1u) ? dP0 * a.inv_keep : 0.f;
-                  dP1 = ((m1[h] >> jj) & 1u) ? dP1 * a.inv_keep : 0.f;
+                  dP0 = ((m0[h] >> jj) & 1u) ? dP0 : 0.f;
+                  dP1 = ((m1[h] >> jj) & 1u) ? dP1 : 0.f;
                 }
                 haxpy<C>(dq0, pe0 * (dP0 - s0[h].z), k, h);
                 haxpy<C>(dq1, pe1 * (dP1 - s1[h].z), k, h);
@@ -462,18 +475,18 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
 #pragma unroll
             for (int h = 0; h < C::H; ++h) {
               const float4 sh = st4[i * C::H + h];
-              const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k0, h), a.sc2, -sh.x)) * sh.y;
-              const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k1, h), a.sc2, -sh.x)) * sh.y;
+              const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k0, h), a.sc2, -sh.x));
+              const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k1, h), a.sc2, -sh.x));
               float dP0 = hdot<C>(g, v0, h), pd0 = pe0;
               float dP1 = hdot<C>(g, v1, h), pd1 = pe1;
               if (a.drop) {
                 const uint32_t* mr = mask + i * W32 * C::H + h;  // [i][w][h]: both heads' words adjacent
                 const bool keep0 = ((mr[jw0 * C::H] >> jb0) & 1u) != 0u;
                 const bool keep1 = ((mr[jw1 * C::H] >> jb1) & 1u) != 0u;
-                dP0 = keep0 ? dP0 * a.inv_keep : 0.f;
-                pd0 = keep0 ? pe0 * a.inv_keep : 0.f;
-                dP1 = keep1 ? dP1 * a.inv_keep : 0.f;
-                pd1 = keep1 ? pe1 * a.inv_keep : 0.f;
+                dP0 = keep0 ? dP0 : 0.f;
+                pd0 = keep0 ? pe0 : 0.f;
+                dP1 = keep1 ? dP1 : 0.f;
+                pd1 = keep1 ? pe1 : 0.f;
               }
               haxpy<C>(dk0, pe0 * (dP0 - sh.z), q, h);
               haxpy<C>(dv0, pd0, g, h);
