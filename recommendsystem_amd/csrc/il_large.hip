@@ -101,6 +101,22 @@ __device__ __forceinline__ float hdot(const float (&a)[C::U], const float (&b)[C
                                     f32x2v{b[h * C::DH + d], b[h * C::DH + d + 1]}, acc);
   return acc.x + acc.y;
 }
+// init + dot product of head h's DH-slice (the score's -max folded into the accumulator)
+template <class C>
+__device__ __forceinline__ float hdot_from(const float (&a)[C::U], const float (&b)[C::U], int h,
+                                           float init) {
+  f32x2v acc = {init, 0.f};
+#pragma unroll
+  for (int d = 0; d < C::DH; d += 2)
+    acc = __builtin_elementwise_fma(f32x2v{a[h * C::DH + d], a[h * C::DH + d + 1]},
+                                    f32x2v{b[h * C::DH + d], b[h * C::DH + d + 1]}, acc);
+  return acc.x + acc.y;
+}
+// v if bit `bit` of the keep word m is set, else +0 (v_bfe_i32 -> all-ones / zero mask, one AND)
+__device__ __forceinline__ float keep_bit(float v, uint32_t m, uint32_t bit) {
+  const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)m, bit, 1u);
+  return __uint_as_float(__float_as_uint(v) & msk);
+}
 // o[h-slice] += p * x[h-slice], packed
 template <class C>
 __device__ __forceinline__ void haxpy(float (&o)[C::U], float p, const float (&x)[C::U], int h) {
@@ -144,6 +160,8 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
   for (int i = threadIdx.x; i < F; i += NT) {
     float q[C::U];
     ld<C::U>(q, Qs + i * C::U);
+#pragma unroll
+    for (int u = 0; u < C::U; ++u) q[u] *= sc2;  // scores straight into the exp2 domain
     float mx[C::H];
 #pragma unroll
     for (int h = 0; h < C::H; ++h) mx[h] = -INFINITY;
@@ -155,8 +173,13 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
       for (int h = 0; h < C::H; ++h) mx[h] = fmaxf(mx[h], hdot<C>(q, k, h));
     }
     float msc[C::H], l[C::H], o[C::U];
+    uint32_t kbh[C::H];  // the dropout counter's (head, row) part: per key one xor (j < 4096)
 #pragma unroll
-    for (int h = 0; h < C::H; ++h) { msc[h] = mx[h] * sc2; l[h] = 0.f; }
+    for (int h = 0; h < C::H; ++h) {
+      msc[h] = mx[h];
+      l[h] = 0.f;
+      kbh[h] = kb ^ (((uint32_t)h << 24) | ((uint32_t)i << 12));
+    }
 #pragma unroll
     for (int u = 0; u < C::U; ++u) o[u] = 0.f;
     for (int w = 0; w < W32; ++w) {
@@ -172,9 +195,9 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
         ld<C::U>(v, Vs + j * C::U);
 #pragma unroll
         for (int h = 0; h < C::H; ++h) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k, h), sc2, -msc[h]));
+          const float e = __builtin_amdgcn_exp2f(hdot_from<C>(q, k, h, -msc[h]));
           l[h] += e;
-          const bool keep = !drop || dropout_keep_t(kb, h, i, j, thr24);
+          const bool keep = !drop || (fmix32(kbh[h] ^ (uint32_t)j) >> 8) >= thr24;
           bits[h] |= (uint32_t)keep << jj;
           const float ek = keep ? e : 0.f;
           haxpy<C>(o, ek, v, h);
@@ -418,7 +441,10 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
           ld<C::U>(q1, Qs + rr1 * C::U);
           ld<C::U>(g1, Gs + rr1 * C::U);
 #pragma unroll
-          for (int u = 0; u < C::U; ++u) { dq0[u] = 0.f; dq1[u] = 0.f; }
+          for (int u = 0; u < C::U; ++u) {
+            dq0[u] = 0.f; dq1[u] = 0.f;
+            q0[u] *= a.sc2; q1[u] *= a.sc2;  // scores in the exp2 domain (signs, the dq ReLU masks, kept)
+          }
           float4 s0[C::H], s1[C::H];
 #pragma unroll
           for (int h = 0; h < C::H; ++h) { s0[h] = st4[r * C::H + h]; s1[h] = st4[rr1 * C::H + h]; }
@@ -438,12 +464,12 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
               ld<C::U>(v, Vs + j * C::U);
 #pragma unroll
               for (int h = 0; h < C::H; ++h) {
-                const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q0, k, h), a.sc2, -s0[h].x));
-                const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q1, k, h), a.sc2, -s1[h].x));
+                const float pe0 = __builtin_amdgcn_exp2f(hdot_from<C>(q0, k, h, -s0[h].x));
+                const float pe1 = __builtin_amdgcn_exp2f(hdot_from<C>(q1, k, h, -s1[h].x));
                 float dP0 = hdot<C>(g0, v, h), dP1 = hdot<C>(g1, v, h);
                 if (a.drop) {
-                  dP0 = ((m0[h] >> jj) & 1u) ? dP0 : 0.f;
-                  dP1 = ((m1[h] >> jj) & 1u) ? dP1 : 0.f;
+                  dP0 = keep_bit(dP0, m0[h], (uint32_t)jj);
+                  dP1 = keep_bit(dP1, m1[h], (uint32_t)jj);
                 }
                 haxpy<C>(dq0, pe0 * (dP0 - s0[h].z), k, h);
                 haxpy<C>(dq1, pe1 * (dP1 - s1[h].z), k, h);
@@ -465,7 +491,10 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
           ld<C::U>(k1, Ks + rr1 * C::U);
           ld<C::U>(v1, Vs + rr1 * C::U);
 #pragma unroll
-          for (int u = 0; u < C::U; ++u) { dk0[u] = 0.f; dv0[u] = 0.f; dk1[u] = 0.f; dv1[u] = 0.f; }
+          for (int u = 0; u < C::U; ++u) {
+            dk0[u] = 0.f; dv0[u] = 0.f; dk1[u] = 0.f; dv1[u] = 0.f;
+            k0[u] *= a.sc2; k1[u] *= a.sc2;  // (signs, the dk ReLU masks, kept)
+          }
           const int jw0 = r >> 5, jb0 = r & 31, jw1 = rr1 >> 5, jb1 = rr1 & 31;
 #pragma unroll 1
           for (int i = 0; i < F; ++i) {
@@ -475,18 +504,17 @@ __global__ void __launch_bounds__(NT) bwd_kernel(LBwd a) {
 #pragma unroll
             for (int h = 0; h < C::H; ++h) {
               const float4 sh = st4[i * C::H + h];
-              const float pe0 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k0, h), a.sc2, -sh.x));
-              const float pe1 = __builtin_amdgcn_exp2f(fmaf(hdot<C>(q, k1, h), a.sc2, -sh.x));
+              const float pe0 = __builtin_amdgcn_exp2f(hdot_from<C>(q, k0, h, -sh.x));
+              const float pe1 = __builtin_amdgcn_exp2f(hdot_from<C>(q, k1, h, -sh.x));
               float dP0 = hdot<C>(g, v0, h), pd0 = pe0;
               float dP1 = hdot<C>(g, v1, h), pd1 = pe1;
               if (a.drop) {
                 const uint32_t* mr = mask + i * W32 * C::H + h;  // [i][w][h]: both heads' words adjacent
-                const bool keep0 = ((mr[jw0 * C::H] >> jb0) & 1u) != 0u;
-                const bool keep1 = ((mr[jw1 * C::H] >> jb1) & 1u) != 0u;
-                dP0 = keep0 ? dP0 : 0.f;
-                pd0 = keep0 ? pe0 : 0.f;
-                dP1 = keep1 ? dP1 : 0.f;
-                pd1 = keep1 ? pe1 : 0.f;
+                const uint32_t w0 = mr[jw0 * C::H], w1 = mr[jw1 * C::H];
+                dP0 = keep_bit(dP0, w0, (uint32_t)jb0);
+                pd0 = keep_bit(pe0, w0, (uint32_t)jb0);
+                dP1 = keep_bit(dP1, w1, (uint32_t)jb1);
+                pd1 = keep_bit(pe1, w1, (uint32_t)jb1);
               }
               haxpy<C>(dk0, pe0 * (dP0 - sh.z), q, h);
               haxpy<C>(dv0, pd0, g, h);
