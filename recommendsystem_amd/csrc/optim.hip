@@ -1022,7 +1022,12 @@ RS_API int rs_partials_reduce_adam_scan(
     const int64_t nc = 1024 >> lg;
     nblk_red += (ncols[k] + nc - 1) / nc;
   }
-  int64_t cap_blocks = 512 - nblk_red;
+  static const int64_t cap_total = [] {  // tuning runs: RS_TAIL_BLOCKS (resident-round target)
+    const char* e = getenv("RS_TAIL_BLOCKS");
+    const long long v = e ? atoll(e) : 0;
+    return (int64_t)(v > 0 ? v : 512);
+  }();
+  int64_t cap_blocks = cap_total - nblk_red;
   if (cap_blocks < 256) cap_blocks = 256;
   if (tail_blocks > cap_blocks) tail_blocks = cap_blocks;
   return reduce_adam_impl(stream, nseg, parts, lds, nrows, ncols, outs, scales, adam_offs, params,
