@@ -143,16 +143,19 @@ def fmix32(h):
 
 def dropout_keep(seed: int, b, h, i, j, rate: float) -> np.ndarray:
     """Counter-based dropout mask shared bit-for-bit with csrc/common.hpp::dropout_keep:
-    kb = fmix32(lo32(seed) ^ fmix32(hi32(seed) + b)); r = fmix32(kb ^ (h<<24 | i<<12 | j));
-    keep iff (r >> 8) / 2^24 >= rate."""
+    kb = fmix32(lo32(seed) ^ fmix32(hi32(seed) + b)); one draw per key pair
+    r = fmix32(kb ^ (h<<24 | i<<12 | (j & ~1))); keep iff half / 2^16 >= rate with
+    half = r & 0xFFFF for even j, r >> 16 for odd j."""
     seed = int(seed) & MASK64
     lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
     with np.errstate(over="ignore"):
         kb = fmix32(lo ^ fmix32(hi + np.asarray(b, dtype=np.uint32)))
+    jj = np.asarray(j, np.uint32)
     ctr = ((np.asarray(h, np.uint32) << np.uint32(24)) | (np.asarray(i, np.uint32) << np.uint32(12))
-           | np.asarray(j, np.uint32))
+           | (jj & np.uint32(0xFFFFFFFE)))
     r = fmix32(kb ^ ctr)
-    u = (r >> np.uint32(8)).astype(np.float64) * (1.0 / 16777216.0)
+    half = np.where((jj & np.uint32(1)) != 0, r >> np.uint32(16), r & np.uint32(0xFFFF))
+    u = half.astype(np.float64) * (1.0 / 65536.0)
     return u >= np.float32(rate)
 
 

@@ -245,9 +245,13 @@ static inline void rs_fill_u32(hipStream_t s, void* p, uint32_t value, int64_t n
 // TF's stateful RNG cannot be reproduced, so the framework pins its own.  For the 64-bit layer
 // seed s (splitmix64(seed + iteration)) and sample b, a per-sample key
 //   kb = fmix32(lo32(s) ^ fmix32(hi32(s) + b))
-// then per element r = fmix32(kb ^ (h << 24 | i << 12 | j))  (h < 256, i, j < 4096);
-// keep iff (r >> 8) / 2^24 >= rate.  fmix32 is the murmur3 finaliser: two 32-bit multiplies per
-// element (a 64-bit SplitMix per element costs ~3x more on the VALU), and kb is hoisted per sample.
+// then per PAIR of keys (j, j ^ 1) one draw r = fmix32(kb ^ (h << 24 | i << 12 | (j & ~1)))
+// (h < 256, i, j < 4096) whose 16-bit halves decide the two keys: keep iff
+// half_j / 2^16 >= rate with half_j = j even ? r & 0xFFFF : r >> 16 (round 5; until then one
+// 24-bit draw per element -- the per-score hash was a third of the many-field forward).
+// fmix32 is the murmur3 finaliser: two 32-bit multiplies per draw (a 64-bit SplitMix costs ~3x
+// more on the VALU), and kb is hoisted per sample.  A 2^-16 probability granularity: rate 0.2
+// keeps 0.799988 of the scores instead of 0.8.
 // ---------------------------------------------------------------------------------------------
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -269,21 +273,24 @@ __device__ __forceinline__ uint32_t dropout_sample_key(uint64_t seed, uint32_t b
   return fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) + b));
 }
 
+__device__ __forceinline__ uint32_t dropout_half(uint32_t r, uint32_t j) {
+  return (j & 1u) ? (r >> 16) : (r & 0xFFFFu);
+}
 __device__ __forceinline__ bool dropout_keep_k(uint32_t kb, uint32_t h, uint32_t i, uint32_t j,
                                                float rate) {
-  const uint32_t r = fmix32(kb ^ ((h << 24) | (i << 12) | j));
-  return (float)(r >> 8) * (1.0f / 16777216.0f) >= rate;
+  const uint32_t r = fmix32(kb ^ ((h << 24) | (i << 12) | (j & ~1u)));
+  return (float)dropout_half(r, j) * (1.0f / 65536.0f) >= rate;
 }
 
-// the same decision against an integer threshold (dropout_thr24(rate) = ceil(rate * 2^24)):
-// (r >> 8) * 2^-24 >= rate  <=>  (r >> 8) >= ceil(rate * 2^24), both sides exact -- bit-identical
-// masks, two VALU operations fewer per element (no convert / multiply)
-__host__ __device__ __forceinline__ uint32_t dropout_thr24(float rate) {
-  return (uint32_t)ceilf(rate * 16777216.0f);
+// the same decision against an integer threshold (dropout_thr16(rate) = ceil(rate * 2^16)):
+// half * 2^-16 >= rate  <=>  half >= ceil(rate * 2^16), both sides exact -- bit-identical masks
+// without the convert / multiply; a kernel sweeping keys in order draws once per key pair
+// (dropout_draw) and tests both halves
+__host__ __device__ __forceinline__ uint32_t dropout_thr16(float rate) {
+  return (uint32_t)ceilf(rate * 65536.0f);
 }
-__device__ __forceinline__ bool dropout_keep_t(uint32_t kb, uint32_t h, uint32_t i, uint32_t j,
-                                               uint32_t thr24) {
-  return (fmix32(kb ^ ((h << 24) | (i << 12) | j)) >> 8) >= thr24;
+__device__ __forceinline__ uint32_t dropout_draw(uint32_t kb, uint32_t h, uint32_t i, uint32_t j) {
+  return fmix32(kb ^ ((h << 24) | (i << 12) | (j & ~1u)));
 }
 
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t b, uint32_t h, uint32_t i,

@@ -156,7 +156,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
                                           float drop_rate, float inv_keep, float4* st4,
                                           uint32_t* mask, float* sv) {
   const int W32 = (F + 31) / 32;
-  const uint32_t thr24 = dropout_thr24(drop_rate);
+  const uint32_t thr16 = dropout_thr16(drop_rate);
   for (int i = threadIdx.x; i < F; i += NT) {
     float q[C::U];
     ld<C::U>(q, Qs + i * C::U);
@@ -173,7 +173,7 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
       for (int h = 0; h < C::H; ++h) mx[h] = fmaxf(mx[h], hdot<C>(q, k, h));
     }
     float msc[C::H], l[C::H], o[C::U];
-    uint32_t kbh[C::H];  // the dropout counter's (head, row) part: per key one xor (j < 4096)
+    uint32_t kbh[C::H];  // the dropout counter's (head, row) part: per key pair one xor (j < 4096)
 #pragma unroll
     for (int h = 0; h < C::H; ++h) {
       msc[h] = mx[h];
@@ -184,20 +184,25 @@ __device__ __forceinline__ void attn_rows(const float* Qs, const float* Ks, cons
     for (int u = 0; u < C::U; ++u) o[u] = 0.f;
     for (int w = 0; w < W32; ++w) {
       const int jn = F - 32 * w < 32 ? F - 32 * w : 32;
-      uint32_t bits[C::H];
+      uint32_t bits[C::H], draw[C::H];
 #pragma unroll
-      for (int h = 0; h < C::H; ++h) bits[h] = 0u;
+      for (int h = 0; h < C::H; ++h) { bits[h] = 0u; draw[h] = 0u; }
 #pragma unroll 2
       for (int jj = 0; jj < jn; ++jj) {
         const int j = 32 * w + jj;
         float k[C::U], v[C::U];
         ld<C::U>(k, Ks + j * C::U);
         ld<C::U>(v, Vs + j * C::U);
+        // one draw per key pair (words start at even keys: jj even <=> j even)
+        if (drop && (jj & 1) == 0) {
+#pragma unroll
+          for (int h = 0; h < C::H; ++h) draw[h] = fmix32(kbh[h] ^ (uint32_t)j);
+        }
 #pragma unroll
         for (int h = 0; h < C::H; ++h) {
           const float e = __builtin_amdgcn_exp2f(hdot_from<C>(q, k, h, -msc[h]));
           l[h] += e;
-          const bool keep = !drop || (fmix32(kbh[h] ^ (uint32_t)j) >> 8) >= thr24;
+          const bool keep = !drop || dropout_half(draw[h], (uint32_t)j) >= thr16;
           bits[h] |= (uint32_t)keep << jj;
           const float ek = keep ? e : 0.f;
           haxpy<C>(o, ek, v, h);

@@ -30,17 +30,15 @@ def test_dropout_mask_rate():
 
 
 def test_dropout_integer_threshold_is_exact():
-    """csrc/common.hpp::dropout_keep_t compares the 24-bit draw against ceil(rate * 2^24) (float32
-    arithmetic, as the device computes it) instead of (r >> 8) * 2^-24 >= rate: the two decisions
-    agree for every draw, including the draws at and next to each threshold."""
-    rng = np.random.default_rng(3)
+    """csrc/common.hpp::dropout_thr16: the many-field forward compares the 16-bit half draw
+    against ceil(rate * 2^16) (float32 arithmetic, as the device computes it) instead of
+    half * 2^-16 >= rate: the two decisions agree for every draw, including the draws at and next
+    to each threshold."""
     for rate in (0.1, 0.2, 0.25, 1.0 / 3.0, 0.5, 0.7, 0.999, 1e-7, 0.0):
         r32 = np.float32(rate)
-        thr = np.uint32(np.ceil(np.float32(r32 * np.float32(16777216.0))))
-        draws = np.concatenate([rng.integers(0, 1 << 24, size=200_000),
-                                np.clip(np.arange(int(thr) - 3, int(thr) + 4), 0, (1 << 24) - 1)])
-        draws = draws.astype(np.uint32)
-        ref = draws.astype(np.float32) * np.float32(1.0 / 16777216.0) >= r32
+        thr = np.uint32(np.ceil(np.float32(r32 * np.float32(65536.0))))
+        draws = np.arange(0, 1 << 16, dtype=np.uint32)  # every half-draw value
+        ref = draws.astype(np.float32) * np.float32(1.0 / 65536.0) >= r32
         assert np.array_equal(draws >= thr, ref), rate
 
 
