@@ -8,7 +8,8 @@
 //                (all experts + all gates of a layer are one [K, sum N] Dense), so the mixture
 //                kernel is the only extra pass.
 //   cross        CrossNet (rough_rank/layer.py:236-270) == DeepCrossLayer (staytime/layer.py:44-80):
-//                x_{l+1} = x0 * (x_l . w_l) + b_l + x_l, all layers per row in registers.
+//                x_{l+1} = x0 * (x_l . w_l) + b_l + x_l, evaluated in closed form (one batched
+//                reduction per row).
 //   fm           FMLayer (staytime/layer.py:83-116, rank/finish/videodnn.py:23-52) and the SENet
 //                reweight + FM cross term of staytime/VideoDnn.py:81-115: y_f = x_f * a_f,
 //                cross = (sum_f y_f)^2 - sum_f y_f^2, fm = 0.5 * sum_e cross.
@@ -178,148 +179,296 @@ __global__ void __launch_bounds__(256) gate_mix_bwd_kernel(GM a, const float* __
 // =============================================================================================
 constexpr int CR_MAXL = 4;
 
-// Thread owns columns c = threadIdx.x + 256 v (v < NV); the layer count L is a template parameter
-// so the per-layer register arrays hold exactly L rows.
+// Closed form of the recurrence x_{l+1} = x0 (x_l . w_l) + b_l + x_l: by induction every layer
+// is x_l = A_l x0 + B_l with a per-row scalar A_l and a row-independent vector
+// B_l = sum_{k<l} b_k, so with q_l = x0 . w_l and the per-model constants c_l = B_l . w_l
+//     s_l = x_l . w_l = A_l q_l + c_l,   A_0 = 1,   A_{l+1} = A_l + s_l,   y = A_L x0 + B_L.
+// One batched block reduction per row (the L dots q_l) replaces L dependent ones.
+// Backward (g_l = dL/dx_{l+1}, g_{L-1} = dY):  ds_l = g_l . x0 = p + sum_{k>l} ds_k q_k with
+// p = dY . x0, so the whole chain is again ONE batched reduction {q_l, p} plus scalar algebra:
+//     dX0  = A_L dY + sum_l (A_l ds_l) w_l
+//     dW_l = sum_rows (A_l ds_l) x0 + B_l sum_rows ds_l
+//     db_l = sum_rows dY + sum_{k>l} w_k sum_rows ds_k.
+// The row pass writes dX0 and the per-row scalars (A_l ds_l, ds_l); a column pass forms the three
+// row sums in fixed order (per-split partials) and a finalize pass assembles dW and db.
+
+// Block-wide sums of K floats per thread (256 threads = 4 waves); `red` = 2 * 4 * K floats of LDS,
+// double-buffered by `phase` like block_sum256.
+template <int K>
+__device__ __forceinline__ void block_sumk(float (&v)[K], float* red, int phase) {
+  float* r = red + (phase & 1) * 4 * K;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = group_sum<64>(v[k]);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[wave_id() * K + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = (r[k] + r[K + k]) + (r[2 * K + k] + r[3 * K + k]);
+}
+
+// w_l in registers, c_l = B_l . w_l (block-reduced once), B_L returned in `bl`.
+// Thread owns columns c = threadIdx.x + 256 v (v < NV).
+template <int NV, int L>
+__device__ __forceinline__ void cross_setup(const float* __restrict__ W,
+                                            const float* __restrict__ bias, int D,
+                                            float (&w)[L][NV], float (&cl)[L], float (&bl)[NV],
+                                            float* red) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) bl[v] = 0.f;
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    float part = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + 256 * v;
+      w[l][v] = c < D ? W[(int64_t)l * D + c] : 0.f;
+      part = fmaf(bl[v], w[l][v], part);
+      bl[v] += c < D ? bias[(int64_t)l * D + c] : 0.f;
+    }
+    cl[l] = part;
+  }
+  block_sumk<L>(cl, red, 0);  // red: its own 4 L floats, not the row loop's buffer
+}
+
+// s_l recursion: A[l] = A_l for l <= L
+template <int L>
+__device__ __forceinline__ void cross_scales(const float (&q)[L], const float (&cl)[L],
+                                             float (&A)[L + 1]) {
+  A[0] = 1.f;
+#pragma unroll
+  for (int l = 0; l < L; ++l) A[l + 1] = A[l] + fmaf(A[l], q[l], cl[l]);
+}
+
 template <int NV, int L>
 __global__ void __launch_bounds__(256) cross_fwd_kernel(const float* __restrict__ X0, int64_t ldx,
                                                         int64_t M, int D,
                                                         const float* __restrict__ W,
                                                         const float* __restrict__ bias,
                                                         float* __restrict__ Y, int64_t ldy) {
-  __shared__ float red[8];
-  float w[L][NV], b[L][NV];
-#pragma unroll
-  for (int l = 0; l < L; ++l)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = threadIdx.x + 256 * v;
-      w[l][v] = c < D ? W[(int64_t)l * D + c] : 0.f;
-      b[l][v] = c < D ? bias[(int64_t)l * D + c] : 0.f;
-    }
+  __shared__ float red0[4 * L], red[2 * 4 * L];
+  float w[L][NV], cl[L], bl[NV];
+  cross_setup<NV, L>(W, bias, D, w, cl, bl, red0);
   int phase = 0;
   for (int64_t m = blockIdx.x; m < M; m += gridDim.x) {
-    float x0[NV], xl[NV];
+    float x0[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = threadIdx.x + 256 * v;
       x0[v] = c < D ? X0[m * ldx + c] : 0.f;
-      xl[v] = x0[v];
     }
+    float q[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      float part = 0.f;
+      q[l] = 0.f;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) part = fmaf(xl[v], w[l][v], part);
-      const float s = block_sum256(part, red, phase++);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) xl[v] = fmaf(x0[v], s, b[l][v] + xl[v]);
+      for (int v = 0; v < NV; ++v) q[l] = fmaf(x0[v], w[l][v], q[l]);
     }
+    block_sumk<L>(q, red, phase++);
+    float A[L + 1];
+    cross_scales<L>(q, cl, A);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = threadIdx.x + 256 * v;
-      if (c < D) Y[m * ldy + c] = xl[v];
+      if (c < D) Y[m * ldy + c] = fmaf(A[L], x0[v], bl[v]);
     }
   }
 }
 
-// Backward: recompute x_1..x_{L-1} and s_l = x_l . w_l per row, then for l = L-1 .. 0 with
-// g = dL/dx_{l+1}:  dx0 += g s_l;  ds = g . x0;  dw_l += x_l ds;  db_l += g;  g += w_l ds.
-// dX0 = dx0 + g.  w and b live in LDS (read once per row), dw/db accumulate in registers across
-// the block's rows and leave as one partial row per block.
+// Row pass of the backward: dX0 and coef[m] = [A_l ds_l (l < L) | ds_l (l < L)].
 template <int NV, int L>
-__global__ void __launch_bounds__(256) cross_bwd_kernel(
+__global__ void __launch_bounds__(256) cross_bwd_rows_kernel(
     const float* __restrict__ X0, int64_t ldx, int64_t M, int D, const float* __restrict__ W,
     const float* __restrict__ bias, const float* __restrict__ dY, int64_t lddy,
-    float* __restrict__ dX0, int64_t lddx, int dx_accumulate, float* __restrict__ part) {
-  extern __shared__ float wb[];  // [L][D] w | [L][D] b
-  __shared__ float red[8];
-  for (int i = threadIdx.x; i < L * D; i += blockDim.x) { wb[i] = W[i]; wb[L * D + i] = bias[i]; }
-  __syncthreads();
-  const float* ws = wb;
-  const float* bs = wb + L * D;
-  float dw[L][NV], db[L][NV];
-#pragma unroll
-  for (int l = 0; l < L; ++l)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) { dw[l][v] = 0.f; db[l][v] = 0.f; }
+    float* __restrict__ dX0, int64_t lddx, int dx_accumulate, float* __restrict__ coef) {
+  __shared__ float red0[4 * L], red[2 * 4 * (L + 1)];
+  float w[L][NV], cl[L], bl[NV];
+  cross_setup<NV, L>(W, bias, D, w, cl, bl, red0);
   int phase = 0;
   for (int64_t m = blockIdx.x; m < M; m += gridDim.x) {
-    float x0[NV], xs[L][NV], s[L];
+    float x0[NV], g[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = threadIdx.x + 256 * v;
       x0[v] = c < D ? X0[m * ldx + c] : 0.f;
+      g[v] = c < D ? dY[m * lddy + c] : 0.f;
     }
-    float xl[NV];
+    float r[L + 1];  // q_0 .. q_{L-1}, p
 #pragma unroll
-    for (int v = 0; v < NV; ++v) xl[v] = x0[v];
-#pragma unroll
-    for (int l = 0; l < L; ++l) {
-      float pp = 0.f;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = threadIdx.x + 256 * v;
-        xs[l][v] = xl[v];
-        if (c < D) pp = fmaf(xl[v], ws[l * D + c], pp);
-      }
-      s[l] = block_sum256(pp, red, phase++);
-      if (l + 1 < L) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          const int c = threadIdx.x + 256 * v;
-          xl[v] = fmaf(x0[v], s[l], (c < D ? bs[l * D + c] : 0.f) + xl[v]);
-        }
-      }
-    }
-    float g[NV], dx0[NV];
+    for (int l = 0; l <= L; ++l) r[l] = 0.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int c = threadIdx.x + 256 * v;
-      g[v] = c < D ? dY[m * lddy + c] : 0.f;
-      dx0[v] = 0.f;
+#pragma unroll
+      for (int l = 0; l < L; ++l) r[l] = fmaf(x0[v], w[l][v], r[l]);
+      r[L] = fmaf(g[v], x0[v], r[L]);
     }
+    block_sumk<L + 1>(r, red, phase++);
+    float q[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) q[l] = r[l];
+    float A[L + 1];
+    cross_scales<L>(q, cl, A);
+    float ds[L], al[L];
 #pragma unroll
     for (int l = L - 1; l >= 0; --l) {
-      float pp = 0.f;
+      float d = r[L];
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        dx0[v] = fmaf(g[v], s[l], dx0[v]);
-        pp = fmaf(g[v], x0[v], pp);
-        db[l][v] += g[v];
-      }
-      const float ds = block_sum256(pp, red, phase++);
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = threadIdx.x + 256 * v;
-        dw[l][v] = fmaf(xs[l][v], ds, dw[l][v]);
-        if (c < D) g[v] = fmaf(ws[l * D + c], ds, g[v]);
-      }
+      for (int k = l + 1; k < L; ++k) d = fmaf(ds[k], q[k], d);
+      ds[l] = d;
+      al[l] = A[l] * d;
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = threadIdx.x + 256 * v;
       if (c < D) {
-        const float val = dx0[v] + g[v];
+        float val = A[L] * g[v];
+#pragma unroll
+        for (int l = 0; l < L; ++l) val = fmaf(al[l], w[l][v], val);
         float* dst = dX0 + m * lddx + c;
         *dst = dx_accumulate ? *dst + val : val;
       }
     }
-  }
-  // per-block partial row [dW (L*D) | db (L*D)]
-  float* pr = part + (int64_t)blockIdx.x * 2 * L * D;
+    if (threadIdx.x < 2 * L) {
+      float o = 0.f;
 #pragma unroll
-  for (int l = 0; l < L; ++l)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = threadIdx.x + 256 * v;
-      if (c < D) {
-        pr[(int64_t)l * D + c] = dw[l][v];
-        pr[(int64_t)(L + l) * D + c] = db[l][v];
+      for (int l = 0; l < L; ++l) {
+        if (threadIdx.x == l) o = al[l];
+        if (threadIdx.x == L + l) o = ds[l];
       }
+      coef[m * 2 * L + threadIdx.x] = o;
     }
+  }
 }
 
-static int cross_bwd_grid(int64_t M) { return (int)(M < 128 ? (M < 1 ? 1 : M) : 128); }
+// Column pass: split s of gridDim.y sums rows [m0, m1) of  x0 * (A_l ds_l)  (l < L) and dY into
+// part[s][(L+1) D], and (column tile 0) the row sums of ds_l into part[s][(L+1) D + l].
+template <int L>
+__global__ void __launch_bounds__(256) cross_bwd_cols_kernel(
+    const float* __restrict__ X0, int64_t ldx, int64_t M, int D, const float* __restrict__ dY,
+    int64_t lddy, const float* __restrict__ coef, int64_t rows_per_split,
+    float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t m1 = m0 + rows_per_split < M ? m0 + rows_per_split : M;
+  const bool col = c < D;
+  float acc[L + 1], t[L];
+#pragma unroll
+  for (int l = 0; l <= L; ++l) acc[l] = 0.f;
+#pragma unroll
+  for (int l = 0; l < L; ++l) t[l] = 0.f;
+  int64_t m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    float x[4], g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x[u] = col ? X0[(m + u) * ldx + c] : 0.f;
+      g[u] = col ? dY[(m + u) * lddy + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* cf = coef + (m + u) * 2 * L;
+#pragma unroll
+      for (int l = 0; l < L; ++l) { acc[l] = fmaf(x[u], cf[l], acc[l]); t[l] += cf[L + l]; }
+      acc[L] += g[u];
+    }
+  }
+  for (; m < m1; ++m) {
+    const float x = col ? X0[m * ldx + c] : 0.f;
+    const float g = col ? dY[m * lddy + c] : 0.f;
+    const float* cf = coef + m * 2 * L;
+#pragma unroll
+    for (int l = 0; l < L; ++l) { acc[l] = fmaf(x, cf[l], acc[l]); t[l] += cf[L + l]; }
+    acc[L] += g;
+  }
+  float* pr = part + (int64_t)blockIdx.y * ((L + 1) * (int64_t)D + L);
+  if (col) {
+#pragma unroll
+    for (int l = 0; l <= L; ++l) pr[(int64_t)l * D + c] = acc[l];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < L) {
+    float o = 0.f;
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+      if (threadIdx.x == l) o = t[l];
+    pr[(int64_t)(L + 1) * D + threadIdx.x] = o;
+  }
+}
+
+// Finalize: dW_l = R_l + B_l T_l, db_l = S + sum_{k>l} w_k T_k (R, S, T summed over the splits)
+// -> dparams [dW (L D) | db (L D)], written or accumulated.  Block = 64 columns x 16 split groups
+// (thread group g sums splits g, g+16, ... in order, the groups are combined in g order, as
+// column_reduce_kernel): a fixed summation order.
+template <int L>
+__global__ void __launch_bounds__(64 * 16) cross_bwd_final_kernel(
+    const float* __restrict__ part, int nsplit, int D, const float* __restrict__ W,
+    const float* __restrict__ bias, float* __restrict__ dparams, int accumulate) {
+  constexpr int G = 16;
+  __shared__ float red[G][L + 1][64];
+  __shared__ float redt[G][L];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const int64_t stride = (L + 1) * (int64_t)D + L;
+  float R[L + 1], T[L];
+#pragma unroll
+  for (int l = 0; l <= L; ++l) R[l] = 0.f;
+#pragma unroll
+  for (int l = 0; l < L; ++l) T[l] = 0.f;
+#pragma unroll 4
+  for (int s = g; s < nsplit; s += G) {
+    const float* pr = part + s * stride;
+    if (c < D) {
+#pragma unroll
+      for (int l = 0; l <= L; ++l) R[l] += pr[(int64_t)l * D + c];
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) T[l] += pr[(int64_t)(L + 1) * D + l];
+  }
+#pragma unroll
+  for (int l = 0; l <= L; ++l) red[g][l][lc] = R[l];
+  if (lc < L) {
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+      if (lc == l) redt[g][l] = T[l];
+  }
+  __syncthreads();
+  if (g != 0 || c >= D) return;
+#pragma unroll
+  for (int k = 1; k < G; ++k) {
+#pragma unroll
+    for (int l = 0; l <= L; ++l) R[l] += red[k][l][lc];
+  }
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    float t = redt[0][l];
+#pragma unroll
+    for (int k = 1; k < G; ++k) t += redt[k][l];
+    T[l] = t;
+  }
+  float B = 0.f;
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    const float dw = fmaf(B, T[l], R[l]);
+    float db = R[L];
+#pragma unroll
+    for (int k = l + 1; k < L; ++k) db = fmaf(W[(int64_t)k * D + c], T[k], db);
+    float* pw = dparams + (int64_t)l * D + c;
+    float* pb = dparams + (int64_t)(L + l) * D + c;
+    *pw = accumulate ? *pw + dw : dw;
+    *pb = accumulate ? *pb + db : db;
+    B += bias[(int64_t)l * D + c];
+  }
+}
+
+static int64_t cross_rows_per_split(int64_t M) {
+  const int64_t rps = 32;  // B = 2048, D = 1712: 64 splits x 7 column tiles = 448 blocks
+  const int64_t nsplit = (M + rps - 1) / rps;
+  return nsplit <= 128 ? rps : (M + 127) / 128;
+}
+static int cross_nsplit(int64_t M) {
+  const int64_t rps = cross_rows_per_split(M);
+  return (int)((M + rps - 1) / rps);
+}
 
 // =============================================================================================
 // fm (+ optional per-field scale = SENet reweight)
@@ -790,7 +939,7 @@ RS_API int rs_gate_mix_bwd(void* stream, const float* E, int64_t lde, int e_act,
 // ------------------------------- cross ---------------------------------------------------------
 RS_API int64_t rs_cross_bwd_workspace_floats(int64_t M, int D, int L) {
   if (M <= 0 || D <= 0 || L <= 0) return 0;
-  return (int64_t)cross_bwd_grid(M) * 2 * L * D;
+  return M * 2 * L + (int64_t)cross_nsplit(M) * ((int64_t)(L + 1) * D + L);
 }
 
 static int cross_nv(int D) {
@@ -818,13 +967,25 @@ static int cross_nv(int D) {
     default: CALL(8, 4); break;         \
   }
 
+static int cross_row_grid(int64_t M, bool fwd) {
+  static const int cap[2] = {[] {  // tuning runs: RS_CROSS_GRID_BWD / RS_CROSS_GRID_FWD
+    const char* e = getenv("RS_CROSS_GRID_BWD");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }(), [] {
+    const char* e = getenv("RS_CROSS_GRID_FWD");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }()};
+  const int c = cap[fwd ? 1 : 0];
+  return (int)(M > c ? c : M);
+}
+
 RS_API int rs_cross_fwd(void* stream, const float* X0, int64_t ldx, int64_t M, int D, int L,
                         const float* W, const float* b, float* Y, int64_t ldy) {
   if (!X0 || !W || !b || !Y || M < 0 || D <= 0 || L <= 0) return RS_ERR_ARG;
   if (L > CR_MAXL || D > 256 * 8) return RS_ERR_UNSUPPORTED;
   if (M == 0) return RS_OK;
   const int nv = cross_nv(D);
-  const int grid = (int)(M > 2048 ? 2048 : M);
+  const int grid = cross_row_grid(M, true);
   hipStream_t s = rs_stream(stream);
 #define RS_CF(NV, LL) cross_fwd_kernel<NV, LL><<<grid, 256, 0, s>>>(X0, ldx, M, D, W, b, Y, ldy)
   RS_CROSS_SWITCH(nv, L, RS_CF)
@@ -839,20 +1000,33 @@ RS_API int rs_cross_bwd(void* stream, const float* X0, int64_t ldx, int64_t M, i
   if (!X0 || !W || !b || !dY || !dX0 || M < 0 || D <= 0 || L <= 0) return RS_ERR_ARG;
   if (L > CR_MAXL || D > 256 * 8) return RS_ERR_UNSUPPORTED;
   if (M == 0) return RS_OK;
-  const int grid = cross_bwd_grid(M);
-  if (!workspace || workspace_floats < (int64_t)grid * 2 * L * D) return RS_ERR_ARG;
+  if (!workspace || workspace_floats < rs_cross_bwd_workspace_floats(M, D, L)) return RS_ERR_ARG;
   const int nv = cross_nv(D);
-  const size_t lds = (size_t)2 * L * D * 4;
+  const int grid = cross_row_grid(M, false);
+  float* coef = workspace;
+  float* part = workspace + M * 2 * L;
   hipStream_t s = rs_stream(stream);
 #define RS_CB(NV, LL)                                                                           \
-  cross_bwd_kernel<NV, LL><<<grid, 256, lds, s>>>(X0, ldx, M, D, W, b, dY, lddy, dX0, lddx,     \
-                                                  dx_accumulate, workspace)
+  cross_bwd_rows_kernel<NV, LL><<<grid, 256, 0, s>>>(X0, ldx, M, D, W, b, dY, lddy, dX0, lddx,  \
+                                                     dx_accumulate, coef)
   RS_CROSS_SWITCH(nv, L, RS_CB)
 #undef RS_CB
   int st = rs_status_after_launch();
   if (st || !dparams) return st;
-  const int64_t n = 2 * (int64_t)L * D;
-  launch_column_reduce(s, workspace, grid, n, n, n, dparams, dparams, dparams_accumulate);
+  const int64_t rps = cross_rows_per_split(M);
+  const int nsplit = cross_nsplit(M);
+  const dim3 cgrid((D + 255) / 256, nsplit);
+  const int fgrid = (D + 63) / 64;
+  switch (L) {
+#define RS_CC(LL)                                                                                \
+  case LL:                                                                                       \
+    cross_bwd_cols_kernel<LL><<<cgrid, 256, 0, s>>>(X0, ldx, M, D, dY, lddy, coef, rps, part);   \
+    cross_bwd_final_kernel<LL><<<fgrid, 64 * 16, 0, s>>>(part, nsplit, D, W, b, dparams,             \
+                                                     dparams_accumulate);                        \
+    break;
+    RS_CC(1) RS_CC(2) RS_CC(3) RS_CC(4)
+#undef RS_CC
+  }
   return rs_status_after_launch();
 }
 

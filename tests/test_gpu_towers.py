@@ -98,12 +98,13 @@ def test_expert_gate_mixtures(kind):
     _check(outs, ref, [(x, xc, "dx"), (mix.kernel, Wc, "dW"), (mix.bias, bc, "db")], R, 2e-5)
 
 
-@pytest.mark.parametrize("kind,D,L", [("crossnet", 832, 2), ("deepcross", 1712, 3), ("crossnet", 40, 1),
-                                      ("deepcross", 300, 4)])
-def test_cross_layers(kind, D, L):
+@pytest.mark.parametrize("kind,D,L,M", [("crossnet", 832, 2, 97), ("deepcross", 1712, 3, 97),
+                                        ("crossnet", 40, 1, 97), ("deepcross", 300, 4, 97),
+                                        ("deepcross", 1712, 3, 2085), ("crossnet", 257, 2, 1)])
+def test_cross_layers(kind, D, L, M):
+    """M = 2085: rows > the row grid (1024) and 66 column splits with a ragged last one."""
     from recommendsystem_amd.towers import CrossNet, DeepCrossLayer
     rng = np.random.default_rng(3)
-    M = 97
     x = torch.from_numpy(_x(rng, M, D, scale=0.2)).to(DEV).requires_grad_(True)
     layer = CrossNet(layer_num=L) if kind == "crossnet" else DeepCrossLayer(num_layer=L)
     layer.build((M, D), device=x.device)
@@ -116,6 +117,34 @@ def test_cross_layers(kind, D, L):
         ref = tr.deep_cross_layer(xc, [Wc[l].reshape(D, 1) for l in range(L)], [bc[l] for l in range(L)])
     R = rng.normal(size=(M, D))
     _check(out, ref, [(x, xc, "dx"), (layer.W, Wc, "dW"), (layer.b, bc, "db")], R, 2e-5)
+
+
+def test_cross_bwd_accumulates():
+    """rs_cross_bwd with dx_accumulate = dparams_accumulate = 1 adds onto what is there."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(11)
+    M, D, L = 300, 520, 3
+    x = torch.from_numpy(_x(rng, M, D, scale=0.3)).to(DEV)
+    W = torch.from_numpy(_x(rng, L, D, scale=0.05)).to(DEV)
+    b = torch.from_numpy(_x(rng, L, D, scale=0.05)).to(DEV)
+    dy = torch.from_numpy(_x(rng, M, D)).to(DEV)
+    n = int(_lib.load().rs_cross_bwd_workspace_floats(M, D, L))
+    ws = torch.empty(n, device=DEV)
+
+    def run(dx, dp, acc):
+        call("rs_cross_bwd", stream_handle(), ptr(x), D, M, D, L, ptr(W), ptr(b), ptr(dy), D, ptr(dx), D,
+             acc, ptr(dp), acc, ptr(ws), n)
+
+    dx1, dp1 = torch.empty(M, D, device=DEV), torch.empty(2 * L * D, device=DEV)
+    run(dx1, dp1, 0)
+    dx0 = torch.from_numpy(_x(rng, M, D)).to(DEV)
+    dp0 = torch.from_numpy(_x(rng, 2 * L * D)).to(DEV)
+    dx2, dp2 = dx0.clone(), dp0.clone()
+    run(dx2, dp2, 1)
+    torch.cuda.synchronize()
+    assert_close(to_np(dx2), to_np(dx0 + dx1), 1e-6, 1e-6, "dx accumulate")
+    assert_close(to_np(dp2), to_np(dp0 + dp1), 1e-6, 1e-6, "dparams accumulate")
 
 
 def test_fm_layer_and_senet_fm():
