@@ -1992,15 +1992,17 @@ __host__ __forceinline__ size_t bwd4_lds_bytes(int F) {
 #ifndef RS_IL4_PK  // 0: the same even / odd accumulator pairs as scalar v_fma_f32 (tuning builds)
 #define RS_IL4_PK 1
 #endif
+// init: the even chain's starting value (a bias folded into the dot for free)
 template <int N>
-__device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b)[N]) {
+__device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b)[N],
+                                            float init = 0.f) {
   if constexpr (!RS_IL4_PK) {
-    float e = 0.f, o = 0.f;
+    float e = init, o = 0.f;
 #pragma unroll
     for (int d = 0; d < N; d += 2) { e = fmaf(a[d], b[d], e); o = fmaf(a[d + 1], b[d + 1], o); }
     return e + o;
   }
-  f32x2v acc = {0.f, 0.f};
+  f32x2v acc = {init, 0.f};
 #pragma unroll
   for (int d = 0; d < N; d += 2)
     acc = __builtin_elementwise_fma(f32x2v{a[d], a[d + 1]}, f32x2v{b[d], b[d + 1]}, acc);
@@ -2012,13 +2014,13 @@ __device__ __forceinline__ float dot_reg_pk(const float (&a)[N], const float (&b
 template <int N>
 __device__ __forceinline__ void dot2_reg_pk(const float (&a)[N], const float (&b)[N],
                                             const float (&c)[N], const float (&d)[N], float& ab,
-                                            float& cd) {
+                                            float& cd, float ab0 = 0.f, float cd0 = 0.f) {
   if constexpr (!RS_IL4_PK) {
-    ab = dot_reg_pk(a, b);
-    cd = dot_reg_pk(c, d);
+    ab = dot_reg_pk(a, b, ab0);
+    cd = dot_reg_pk(c, d, cd0);
     return;
   }
-  f32x2v x = {0.f, 0.f}, y = {0.f, 0.f};
+  f32x2v x = {ab0, 0.f}, y = {cd0, 0.f};
 #pragma unroll
   for (int k = 0; k < N; k += 2) {
     x = __builtin_elementwise_fma(f32x2v{a[k], a[k + 1]}, f32x2v{b[k], b[k + 1]}, x);
@@ -2286,9 +2288,14 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
           gr[d] = (a.use_res && gr[d] > 0.f) ? dt[d] : 0.f;
         }
         if (act) {
-          store_row(SB + f * U + h * DH, dt);
+          // dO and D stored pre-multiplied by the row's softmax 1/sum, so both key sweeps use
+          // the unnormalised e_ij = exp2(s_ij - max_i) for P_ij (one multiply per score fewer)
+          const float isum = SB[F * U + 2 * (h * F + f) + 1];
           store_row(PR + f * C::PRS + 3 * U + h * DH, gr);
-          DL[h * F + f] = dd;
+#pragma unroll
+          for (int d = 0; d < DH; ++d) dt[d] *= isum;
+          store_row(SB + f * U + h * DH, dt);
+          DL[h * F + f] = dd * isum;
         }
       }
       wave_lds_sync();
@@ -2299,9 +2306,11 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         const int h = act ? lane / F : 0, i = act ? lane - h * F : 0;
         float qv[DH], dO[DH], dq[DH];
         load_row(qv, PR + i * C::PRS + h * DH);
-        load_row(dO, SB + i * U + h * DH);
+        load_row(dO, SB + i * U + h * DH);  // x 1/sum_i (P3)
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] *= a.sc2;  // scores straight in the exp2 domain
         const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (h * F + i));
-        const float D = DL[h * F + i];
+        const float D = DL[h * F + i];  // x 1/sum_i
         const float* kb = PR + U + h * DH;
         const float* vb = PR + 2 * U + h * DH;
         // lanes past H * F store their P values into DY (dead until this pass's dq stores,
@@ -2320,12 +2329,17 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
           load_row(v, vb + j * C::PRS);
         };
         auto key = [&](int j, const float (&k)[DH], const float (&v)[DH]) {
+          // sv = s_ij - max_i (-max as the dot's initial value); without dropout dp = dP_ij - D_i
+          // the same way, both already x 1/sum_i
           float sv, dp;
-          dot2_reg_pk(qv, k, dO, v, sv, dp);
-          const float p = __builtin_amdgcn_exp2f(fmaf(sv, a.sc2, nm)) * stt.y;
+          dot2_reg_pk(qv, k, dO, v, sv, dp, nm, DROP ? 0.f : -D);
+          const float p = __builtin_amdgcn_exp2f(sv);  // e_ij; P_ij = e_ij / sum_i
           pm_row[j] = p;
-          if (DROP) dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
-          axpy_reg_pk(dq, p * (dp - D), k);  // (x 1/sqrt(dh) once, after the loop)
+          if (DROP) {
+            dp = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate) ? dp * a.drop_scale : 0.f;
+            dp -= D;
+          }
+          axpy_reg_pk(dq, p * dp, k);  // (x 1/sqrt(dh) once, after the loop)
         };
         ld(k0, v0, 0);
 RS_UNROLL(RS_IL4_UNROLL_Q)
@@ -2363,15 +2377,16 @@ RS_UNROLL(RS_IL4_UNROLL_Q)
           D = dl[i];
         };
         auto query = [&](int i, const float (&dOi)[DH], const float (&qi)[DH], float P, float D) {
+          // P = e_ij, dO_i and D_i x 1/sum_i (P3): the products are P_ij dO_i and P_ij (dP - D)
           float pd = P;
-          float dp = dot_reg_pk(dOi, vj);
+          float dp = dot_reg_pk(dOi, vj, DROP ? 0.f : -D);
           if (DROP) {
             const bool keep = dropout_keep(lseed, (uint32_t)b, h, i, j, a.drop_rate);
             pd = keep ? P * a.drop_scale : 0.f;
-            dp = keep ? dp * a.drop_scale : 0.f;
+            dp = (keep ? dp * a.drop_scale : 0.f) - D;
           }
           axpy_reg_pk(dv, pd, dOi);
-          axpy_reg_pk(dk, P * (dp - D), qi);  // (x 1/sqrt(dh) once, after the loop)
+          axpy_reg_pk(dk, P * dp, qi);  // (x 1/sqrt(dh) once, after the loop)
         };
         ld(o0, q0, p0, d0, 0);
 RS_UNROLL(RS_IL4_UNROLL_K)

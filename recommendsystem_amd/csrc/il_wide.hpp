@@ -449,10 +449,12 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         // D_{h,f} = dO_f . O_f over head h = the 4 lanes of this column quad
         const float dd = quad_sum(fmaf(o2.x, dt0, o2.y * dt1));
         if (act) {
-          *reinterpret_cast<float2*>(SB + f * U + u0) = make_float2(dt0, dt1);
+          // dO and D stored x the row's softmax 1/sum (as bwd4): the sweeps use e_ij for P_ij
+          const float isum = SB[F * U + 2 * ((u0 >> 3) * F + f) + 1];
           *reinterpret_cast<float2*>(PR + f * C::PRS + 3 * U + u0) =
               make_float2((a.use_res && r2.x > 0.f) ? dt0 : 0.f, (a.use_res && r2.y > 0.f) ? dt1 : 0.f);
-          if ((t_ & 3) == 0) DL[(u0 >> 3) * F + f] = dd;
+          *reinterpret_cast<float2*>(SB + f * U + u0) = make_float2(dt0 * isum, dt1 * isum);
+          if ((t_ & 3) == 0) DL[(u0 >> 3) * F + f] = dd * isum;
         }
       }
       lds_barrier();
@@ -467,9 +469,11 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         const int i = act ? lane - h * F : 0;
         float qv[DH], dO[DH], dq[DH];
         ld8(qv, PR + i * C::PRS + h * DH);
-        ld8(dO, SB + i * U + h * DH);
+        ld8(dO, SB + i * U + h * DH);  // x 1/sum_i (P3)
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] *= a.sc2;  // scores straight in the exp2 domain
         const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (h * F + i));
-        const float D = DL[h * F + i];
+        const float D = DL[h * F + i];  // x 1/sum_i
         const float* kb = PR + U + h * DH;
         const float* vb = PR + 2 * U + h * DH;
         // row = lane = h F + i; the idle lanes (>= H F) share the dummy row H F (never read)
@@ -488,16 +492,18 @@ __global__ void __launch_bounds__(kWideThreads, 4) wbwd_kernel(
         };
         auto key = [&](int m, const float (&kv)[DH], const float (&vv)[DH]) {
           const int j = w + 4 * m;
+          // sv_ = s_ij - max_i and (without dropout) dp = dP_ij - D_i by the dots' initial
+          // values; p = e_ij = P_ij sum_i, with dO and D already x 1/sum_i
           float sv_, dp;
-          dot2_reg_pk(qv, kv, dO, vv, sv_, dp);
-          const float p = __builtin_amdgcn_exp2f(fmaf(sv_, a.sc2, -stt.x)) * stt.y;
+          dot2_reg_pk(qv, kv, dO, vv, sv_, dp, -stt.x, DROP ? 0.f : -D);
+          const float p = __builtin_amdgcn_exp2f(sv_);
           float pdrop = p;
           if (DROP) {
             const bool keep = dropout_keep_k(kb_drop, h, i, j, a.drop_rate);
             pdrop = keep ? p * a.drop_scale : 0.f;
-            dp = keep ? dp * a.drop_scale : 0.f;
+            dp = (keep ? dp * a.drop_scale : 0.f) - D;
           }
-          const float ds = p * (dp - D);
+          const float ds = p * dp;
           pm_row[j] = pdrop;
           pd_row[j] = ds;
           axpy_reg_pk(dq, ds, kv);
