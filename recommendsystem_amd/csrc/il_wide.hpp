@@ -192,6 +192,8 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
       if constexpr (!(SKIP & 2)) {
         float qv[DH];
         ld8(qv, PR + ai * C::PRS + ah * DH);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] *= a.sc2;  // scores straight in the exp2 domain
         const float* kb = PR + U + ah * DH;
         const float* vb = PR + 2 * U + ah * DH;
         float s[MQ];
@@ -202,8 +204,8 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
           const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
           float kv[DH];
           ld8(kv, kb + (ok ? j : 0) * C::PRS);
-          s[m] = dot_reg_pk(qv, kv);  // raw q . k; scaled into the exp2 domain below
-          mx = ok ? fmaxf(mx, s[m] * a.sc2) : mx;
+          s[m] = dot_reg_pk(qv, kv);
+          mx = ok ? fmaxf(mx, s[m]) : mx;
         }
         mx = quad_max(mx);
         float sum = 0.f;
@@ -211,7 +213,7 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
         for (int m = 0; m < MQ; ++m) {
           const int j = qq + 4 * m;
           const bool ok = (C::EXACT && 4 * m + 3 < C::FMAX) || j < F;
-          s[m] = ok ? __builtin_amdgcn_exp2f(fmaf(s[m], a.sc2, -mx)) : 0.f;
+          s[m] = ok ? __builtin_amdgcn_exp2f(s[m] - mx) : 0.f;
           sum += s[m];
         }
         sum = quad_sum(sum);
