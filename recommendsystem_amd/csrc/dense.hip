@@ -1034,16 +1034,31 @@ __global__ void __launch_bounds__(1024) bce_clip_kernel(const float* __restrict_
   const float inv_m = 1.0f / (float)M;
   const float gs = gscale ? gscale[0] * inv_m : inv_m;
   float acc = 0.f;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const float sv = s[i];
-    const float p = fminf(fmaxf(sv, lo), hi);
-    const float yv = y[i];
-    const float li = -yv * logf(p + log_eps) - (1.0f - yv) * logf(1.0f - p + log_eps);
-    acc += li;
-    if (p_out) p_out[i] = p;
-    if (ds) {
-      const float dp = (-yv / (p + log_eps) + (1.0f - yv) / (1.0f - p + log_eps)) * gs;
-      ds[i] = (sv >= lo && sv <= hi) ? dp : 0.f;
+  // U elements per thread have their loads issued before any is used (one block walks all M T
+  // elements: a load -> use chain per element made this launch latency-bound, 23 us at 4096 x 7);
+  // each thread still adds its elements i = tid, tid + 1024, ... in order
+  constexpr int U = 8;
+  const int64_t step = (int64_t)blockDim.x;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += U * step) {
+    float sv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * step;
+      sv[u] = i < n ? s[i] : 0.f;
+      yv[u] = i < n ? y[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * step;
+      if (i >= n) break;
+      const float p = fminf(fmaxf(sv[u], lo), hi);
+      const float li = -yv[u] * logf(p + log_eps) - (1.0f - yv[u]) * logf(1.0f - p + log_eps);
+      acc += li;
+      if (p_out) p_out[i] = p;
+      if (ds) {
+        const float dp = (-yv[u] / (p + log_eps) + (1.0f - yv[u]) / (1.0f - p + log_eps)) * gs;
+        ds[i] = (sv[u] >= lo && sv[u] <= hi) ? dp : 0.f;
+      }
     }
   }
   red[threadIdx.x] = acc;
