@@ -385,8 +385,14 @@ static int fwd_grid(int64_t B) {
   return (int)(g > 4096 ? 4096 : g);
 }
 static int bwd_grid(int64_t B) {
-  // about two samples per wave: enough waves to cover the latency, few partial rows to reduce
-  int64_t g = (B + 2 * WPB - 1) / (2 * WPB);
+  // one sample per wave: the per-sample chain is latency-bound, so waves beat fewer partial rows
+  // (two samples per wave: config 4 0.1222 ms, config 5 1.890 ms; one: 0.1115 / 1.861 ms,
+  // profiles/r05/din_spw/); tuning runs: RS_DIN_BWD_SPW
+  static const int spw = [] {
+    const char* e = getenv("RS_DIN_BWD_SPW");
+    return e && atoi(e) > 0 ? atoi(e) : 1;
+  }();
+  int64_t g = (B + spw * WPB - 1) / (spw * WPB);
   if (g > 1024) g = 1024;
   return (int)(g < 1 ? 1 : g);
 }
