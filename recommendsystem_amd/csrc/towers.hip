@@ -721,8 +721,19 @@ __global__ void __launch_bounds__(256) ffm_bwd_kernel(FFM a, const float* __rest
 }
 
 static int ffm_grid(int64_t M) {
-  int64_t g = (M + 15) / 16;
-  return (int)(g > 256 ? 256 : (g < 1 ? 1 : g));
+  // 8 rows per block, <= 512 blocks: config 5 (B = 2048) runs 256 blocks, not 128 (16 rows /
+  // 256 blocks: 1.855 ms, 8 / 512: 1.846 ms, profiles/r05/ffm_ab/); tuning runs: RS_FFM_RPB,
+  // RS_FFM_MAXGRID
+  static const int rpb = [] {
+    const char* e = getenv("RS_FFM_RPB");
+    return e && atoi(e) > 0 ? atoi(e) : 8;
+  }();
+  static const int cap = [] {
+    const char* e = getenv("RS_FFM_MAXGRID");
+    return e && atoi(e) > 0 ? atoi(e) : 512;
+  }();
+  int64_t g = (M + rpb - 1) / rpb;
+  return (int)(g > cap ? cap : (g < 1 ? 1 : g));
 }
 
 // =============================================================================================
@@ -1484,10 +1495,11 @@ RS_API int rs_bce_rows(void* stream, const float* P, const float* Y, int64_t M, 
                        float* dP) {
   if (!P || !Y || M < 0 || T <= 0) return RS_ERR_ARG;
   if (M == 0) return RS_OK;
-  int64_t grid = (M + 255) / 256;
+  // one row per thread, 64-thread blocks: B = 2048 rows spread over 32 CUs instead of 8
+  int64_t grid = (M + 63) / 64;
   if (grid > 4096) grid = 4096;
-  bce_rows_kernel<<<(int)grid, 256, 0, rs_stream(stream)>>>(P, Y, M, T, lo, hi, log_eps, W, gscale,
-                                                          loss_rows, dP);
+  bce_rows_kernel<<<(int)grid, 64, 0, rs_stream(stream)>>>(P, Y, M, T, lo, hi, log_eps, W, gscale,
+                                                         loss_rows, dP);
   return rs_status_after_launch();
 }
 
