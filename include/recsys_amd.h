@@ -534,6 +534,15 @@ int rs_act_bwd(void* stream, const float* Y, const float* dY, int64_t n, int act
 int rs_bce_clip_loss(void* stream, const float* s, const float* y, int64_t M, int T,
                      float clip_lo, float clip_hi, float log_eps, const float* gscale,
                      float* p_out, float* loss, float* ds);
+/* The same over several workgroups: per-block sums in `workspace` (rs_bce_clip_workspace_floats;
+ * its first 288 (RS_DONE_WORDS) words are completion counters that must be zero before the first call
+ * and are left zero by every call), added in block order by the last block (deterministic for a
+ * given M, T).  Calls sharing one workspace must not run concurrently. */
+int64_t rs_bce_clip_workspace_floats(int64_t M, int T);
+int rs_bce_clip_loss_ws(void* stream, const float* s, const float* y, int64_t M, int T,
+                        float clip_lo, float clip_hi, float log_eps, const float* gscale,
+                        float* p_out, float* loss, float* ds, float* workspace,
+                        int64_t workspace_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H11  dense Adam over a flat parameter arena (tn.optimizer.Optimizer(tn.core.Adam(...)):
@@ -553,6 +562,10 @@ int rs_dense_adam_done(void* stream, float* params, float* grads, float* m, floa
 /* Keras kernel regularisers as a gradient term (L1L2 at rank/multi_head/multidnn.py:62-63,
  * L2 at :85,103 and rough_rank/layer.py:77): grads += l1 * sign(w) + 2 * l2 * w. */
 int rs_l1l2_grad(void* stream, const float* params, float* grads, int64_t n, float l1, float l2);
+/* The same for n <= 16 tensors in one launch: tensor k = (params[k], grads[k], counts[k] elements,
+ * l1[k], l2[k]); the pointer / count arrays are host memory read at the call. */
+int rs_l1l2_grad_grouped(void* stream, int n, const float* const* params, float* const* grads,
+                         const int64_t* counts, const float* l1, const float* l2);
 
 /* ---------------------------------------------------------------------------------------
  * H4 + H10 fused: the AutoInt head training pass (autoint:38-52 + rank/ctr/base_model.py:7-12).

@@ -91,6 +91,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_dense_bwd_weight_grouped_workspace_floats": (_i64, [_i32, _vp]),
     "rs_dense_bwd_weight_grouped": (_i32, [_vp, _i32, _vp, _vp, _i64]),
     "rs_bce_clip_loss": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _vp, _vp, _vp]),
+    "rs_bce_clip_workspace_floats": (_i64, [_i64, _i32]),
+    "rs_bce_clip_loss_ws": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _vp, _vp, _vp,
+                                   _vp, _i64]),
     "rs_dense_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
                              _i32]),
     "rs_dense_adam_done": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32,
@@ -139,6 +142,7 @@ SIGNATURES: dict[str, tuple] = {
                                    _i64, _vp, _i64, _vp, _i32, _vp, _i64]),
     "rs_row_select": (_i32, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp, _vp]),
     "rs_l1l2_grad": (_i32, [_vp, _vp, _vp, _i64, _f32, _f32]),
+    "rs_l1l2_grad_grouped": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     "rs_act_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "rs_act_bwd": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "rs_bce_rows": (_i32, [_vp, _vp, _vp, _i64, _i32, _f32, _f32, _f32, _vp, _f32, _vp, _vp]),

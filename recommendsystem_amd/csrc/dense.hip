@@ -1070,6 +1070,75 @@ __global__ void __launch_bounds__(1024) bce_clip_kernel(const float* __restrict_
   if (threadIdx.x == 0 && loss) loss[0] = red[0] * inv_m;
 }
 
+// Multi-block form: each block sums its elements (same per-element arithmetic), the block sums
+// go to ws partials, and the last block (rs_last_block over the counters at the head of ws) adds
+// them in block order -> a fixed summation order for a given (M, T).  One workgroup was issue-
+// bound on its own CU at config 3 (4096 x 7 elements, two logs and two divides each: 17.5 us).
+constexpr int kBceThreads = 256;
+constexpr int kBceMaxBlocks = 64;
+static int bce_blocks(int64_t n) {
+  const int64_t b = (n + 4 * kBceThreads - 1) / (4 * kBceThreads);
+  return (int)(b < 1 ? 1 : (b > kBceMaxBlocks ? kBceMaxBlocks : b));
+}
+
+__global__ void __launch_bounds__(kBceThreads) bce_clip_multi_kernel(
+    const float* __restrict__ s, const float* __restrict__ y, int64_t M, int T, float lo, float hi,
+    float log_eps, const float* __restrict__ gscale, float* __restrict__ p_out,
+    float* __restrict__ loss, float* __restrict__ ds, int32_t* __restrict__ ctr,
+    float* __restrict__ partials) {
+  __shared__ float red[kBceThreads / 64];
+  const int64_t n = M * T;
+  const float inv_m = 1.0f / (float)M;
+  const float gs = gscale ? gscale[0] * inv_m : inv_m;
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float sv = s[i];
+    const float p = fminf(fmaxf(sv, lo), hi);
+    const float yv = y[i];
+    acc += -yv * logf(p + log_eps) - (1.0f - yv) * logf(1.0f - p + log_eps);
+    if (p_out) p_out[i] = p;
+    if (ds) {
+      const float dp = (-yv / (p + log_eps) + (1.0f - yv) / (1.0f - p + log_eps)) * gs;
+      ds[i] = (sv >= lo && sv <= hi) ? dp : 0.f;
+    }
+  }
+  acc = group_sum<64>(acc);
+  if (lane_id() == 0) red[wave_id()] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBceThreads / 64; ++w) b += red[w];
+    partials[blockIdx.x] = b;
+    __threadfence();  // release this block's partial before it counts as done
+  }
+  if (rs_last_block(ctr)) {
+    __threadfence();  // acquire: every block's partial is visible
+    float t = 0.f;
+    for (int k = 0; k < (int)gridDim.x; ++k) t += partials[k];
+    if (loss) loss[0] = t * inv_m;
+  }
+}
+
+RS_API int64_t rs_bce_clip_workspace_floats(int64_t M, int T) {
+  if (M <= 0 || T <= 0) return 0;
+  return RS_DONE_WORDS + bce_blocks(M * (int64_t)T);
+}
+
+RS_API int rs_bce_clip_loss_ws(void* stream, const float* s, const float* y, int64_t M, int T,
+                               float clip_lo, float clip_hi, float log_eps, const float* gscale,
+                               float* p_out, float* loss, float* ds, float* workspace,
+                               int64_t workspace_floats) {
+  if (!s || !y || M <= 0 || T <= 0) return RS_ERR_ARG;
+  if (!workspace || workspace_floats < rs_bce_clip_workspace_floats(M, T)) return RS_ERR_ARG;
+  int32_t* ctr = reinterpret_cast<int32_t*>(workspace);
+  bce_clip_multi_kernel<<<bce_blocks(M * (int64_t)T), kBceThreads, 0, rs_stream(stream)>>>(
+      s, y, M, T, clip_lo, clip_hi, log_eps, gscale, p_out, loss, ds, ctr,
+      workspace + RS_DONE_WORDS);
+  return rs_status_after_launch();
+}
+
 RS_API int rs_bce_clip_loss(void* stream, const float* s, const float* y, int64_t M, int T,
                             float clip_lo, float clip_hi, float log_eps, const float* gscale,
                             float* p_out, float* loss, float* ds) {

@@ -35,13 +35,25 @@ def _act_code(activation) -> int:
 # InteractingLayer
 # ============================================================================================
 class _InteractingFn(torch.autograd.Function):
+    """lead: None -> y [B, F, U]; a [B, Dl] tensor -> the concat [lead | y.reshape(B, F U)]
+    [B, Dl + F U] with y written in place by the kernel (y_ld) and its backward reading its dy
+    slice in place (dy_ld): no concat copy forward, no contiguous copy of the split gradient."""
+
     @staticmethod
-    def forward(ctx, x, W, bias, gamma, beta, layer, seed, drop_rate):
+    def forward(ctx, x, W, bias, gamma, beta, layer, seed, drop_rate, lead=None):
         _lib.require_device(x, W)
         x = x.contiguous()
         B, F, E = x.shape
         U, H, L = layer.unit_num, layer.head_num, layer.layer_num
-        y = torch.empty(B, F, U, device=x.device, dtype=torch.float32)
+        if lead is not None:
+            Dl = lead.shape[1]
+            out = torch.empty(B, Dl + F * U, device=x.device, dtype=torch.float32)
+            out[:, :Dl].copy_(lead)
+            y, y_ld = out[:, Dl:], Dl + F * U
+        else:
+            Dl = 0
+            y = out = torch.empty(B, F, U, device=x.device, dtype=torch.float32)
+            y_ld = F * U
         xsave = torch.empty(max(L - 1, 0), B, F, U, device=x.device, dtype=torch.float32)
         # many-field shapes (F > 64): the forward also saves the attention output, softmax stats
         # and dropout bits so the backward does not recompute them (rs_il_fwd_saved)
@@ -49,18 +61,27 @@ class _InteractingFn(torch.autograd.Function):
         asave = torch.empty(n_save, device=x.device, dtype=torch.float32)
         call("rs_il_fwd_saved", stream_handle(), ptr(x), B, F, E, U, H, L, ptr(W), ptr(bias),
              ptr(gamma), ptr(beta), layer.epsilon, int(layer.use_res), drop_rate, seed, ptr(y),
-             F * U, ptr(xsave) if L > 1 else None, ptr(asave) if n_save else None, n_save)
+             y_ld, ptr(xsave) if L > 1 else None, ptr(asave) if n_save else None, n_save)
         ctx.save_for_backward(x, xsave, W, bias, gamma, beta, asave)
-        ctx.layer, ctx.seed, ctx.drop_rate = layer, seed, drop_rate
-        return y
+        ctx.layer, ctx.seed, ctx.drop_rate, ctx.Dl = layer, seed, drop_rate, Dl
+        ctx.has_lead = lead is not None
+        return out
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dout):
         x, xsave, W, bias, gamma, beta, asave = ctx.saved_tensors
         layer = ctx.layer
-        dy = dy.contiguous()
         B, F, E = x.shape
         U, H, L = layer.unit_num, layer.head_num, layer.layer_num
+        Dl = ctx.Dl
+        if ctx.has_lead:
+            if dout.stride(1) != 1 or dout.stride(0) % 4 or dout.dtype != torch.float32:
+                dout = dout.contiguous().float()
+            d_lead = dout[:, :Dl]
+            dy, dy_ld = dout[:, Dl:], dout.stride(0)
+        else:
+            d_lead = None
+            dy, dy_ld = dout.contiguous(), F * U
         dx = torch.empty_like(x)
         ws_n = int(_lib.load().rs_il_bwd_workspace_floats(B, E, U))
         ws = torch.empty(ws_n, device=x.device, dtype=torch.float32)
@@ -70,17 +91,17 @@ class _InteractingFn(torch.autograd.Function):
         dparams = block if in_place else torch.empty(
             sum(p.numel() for p in params), device=x.device, dtype=torch.float32)
         call("rs_il_bwd_saved", stream_handle(), ptr(x), ptr(xsave) if L > 1 else None, ptr(dy),
-             F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), layer.epsilon,
+             dy_ld, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(gamma), ptr(beta), layer.epsilon,
              int(layer.use_res), ctx.drop_rate, ctx.seed, ptr(dx), 0, ptr(dparams),
              1 if in_place else 0, ptr(ws), ws_n, ptr(asave) if asave.numel() else None,
              asave.numel())
         if in_place:
-            return dx, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, d_lead
         outs, off = [], 0
         for p in params:
             outs.append(dparams[off:off + p.numel()].view(p.shape))
             off += p.numel()
-        return (dx, *outs, None, None, None)
+        return (dx, *outs, None, None, None, d_lead)
 
 
 class InteractingLayer(nn.Module):
@@ -157,6 +178,24 @@ class InteractingLayer(nn.Module):
                                          self.epsilon, drop, seed)
         return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
                                     self, seed, drop)
+
+    def forward_concat(self, lead, inputs):
+        """tf.concat([lead, Flatten()(self(inputs))], axis=1) (rank/multi_head/multidnn.py:71)
+        with the layer's output written straight into the concat and its gradient read from
+        there in place."""
+        if not self.built:
+            self.build(tuple(inputs.shape), device=inputs.device)
+        from . import ops
+        if ops.custom_ops_enabled() or lead.dim() != 2 or lead.shape[1] % 4:
+            return torch.cat([lead, self(inputs).reshape(inputs.shape[0], -1)], dim=1)
+        if inputs.dim() != 3:
+            raise ValueError('The rank of input of InteractingLayer must be 3, but now is %d'
+                             % inputs.dim())
+        drop = self.dropout_rate if (self.use_dropout and self.training) else 0.0
+        seed = (self.seed * 1000003 + self._calls) & 0xFFFFFFFFFFFFFFFF
+        self._calls += 1
+        return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
+                                    self, seed, drop, lead.float())
 
 
 # ============================================================================================

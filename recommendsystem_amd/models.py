@@ -340,11 +340,12 @@ class MultiHeadRanker(nn.Module):
     def forward(self, ids, offsets):
         x0 = self.embedding(ids, offsets)                       # [B, F, 8]
         B = x0.shape[0]
-        auto = self.interact(x0).reshape(B, -1)                 # :54-56
         deep = x0.reshape(B, -1)                                # :60
         for layer in self.deep:
             deep = layer(deep)                                  # :61-63
-        result = torch.cat([deep, auto], dim=1)                 # :71
+        # :54-56 interacting layers, :71 concat [deep, autoint]: the layer writes its output
+        # into the concat directly
+        result = self.interact.forward_concat(deep, x0)
         gated_out = self.mix.forward_flat(result)               # :77-120, the 7 outputs side by side
         return self.towers(gated_out)                           # :122-204 -> [B, 7]
 

@@ -748,6 +748,24 @@ class KDLoss(nn.Module):
         return _MSERowsFn.apply(student_predictions, teacher_predictions)
 
 
+_BCE_WS: dict = {}
+
+
+def _bce_workspace(device):
+    """One persistent, zero-initialised workspace per device for rs_bce_clip_loss_ws (its size is
+    bounded: 288 counter words + at most 64 block sums, so it is never reallocated under a
+    captured graph that holds its address).  None while capturing before the first eager call
+    (the single-workgroup rs_bce_clip_loss then runs)."""
+    ws = _BCE_WS.get(device)
+    if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        n = int(_lib.load().rs_bce_clip_workspace_floats(1 << 40, 1))
+        ws = torch.zeros(n, device=device, dtype=torch.float32)
+        _BCE_WS[device] = ws
+    return ws
+
+
 class _BCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p, y, lo, hi, log_eps):
@@ -755,8 +773,13 @@ class _BCEFn(torch.autograd.Function):
         M, T = p.shape
         loss = torch.empty(1, device=p.device)
         ds = torch.empty_like(p)
-        call("rs_bce_clip_loss", stream_handle(), ptr(p), ptr(y), M, T, lo, hi, log_eps, None, None,
-             ptr(loss), ptr(ds))
+        ws = _bce_workspace(p.device)
+        if ws is not None:
+            call("rs_bce_clip_loss_ws", stream_handle(), ptr(p), ptr(y), M, T, lo, hi, log_eps, None,
+                 None, ptr(loss), ptr(ds), ptr(ws), ws.numel())
+        else:
+            call("rs_bce_clip_loss", stream_handle(), ptr(p), ptr(y), M, T, lo, hi, log_eps, None,
+                 None, ptr(loss), ptr(ds))
         ctx.save_for_backward(ds)
         return loss[0]
 

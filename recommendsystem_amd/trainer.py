@@ -16,6 +16,8 @@ correction (pinned); sparse tables use the optimizer they were cr
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -132,9 +134,17 @@ class Trainer:
             return self._step(*batch)
 
     def _regularise(self):
+        """All Keras kernel regularisers in one launch (rs_l1l2_grad_grouped, <= 16 per launch)."""
         s = stream_handle()
-        for p, l1, l2 in self.regs:
-            call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
+        for k0 in range(0, len(self.regs), 16):
+            chunk = self.regs[k0:k0 + 16]
+            n = len(chunk)
+            wa, wp = _lib.c_array(ctypes.c_void_p, [ptr(p) for p, _, _ in chunk])
+            ga, gp = _lib.c_array(ctypes.c_void_p, [ptr(p.grad) for p, _, _ in chunk])
+            ca, cp = _lib.c_array(ctypes.c_int64, [p.numel() for p, _, _ in chunk])
+            la, lp = _lib.c_array(ctypes.c_float, [float(l1) for _, l1, _ in chunk])
+            ra, rp = _lib.c_array(ctypes.c_float, [float(l2) for _, _, l2 in chunk])
+            call("rs_l1l2_grad_grouped", s, n, wp, gp, cp, lp, rp)
 
     def _step(self, *batch):
         loss = self.model.loss(*batch)
@@ -281,9 +291,7 @@ class Trainer:
         with _lib.seed_offset(self.step_count):
             loss = self.model.loss(*batch)
             loss.backward(self._seed)
-        s = stream_handle()
-        for p, l1, l2 in self.regs:
-            call("rs_l1l2_grad", s, ptr(p), ptr(p.grad), p.numel(), float(l1), float(l2))
+        self._regularise()
         return loss
 
     def measure_dp_caps(self, batches, headroom: float = 1.25, quantum: int = 256):

@@ -673,6 +673,62 @@ def test_bce_clip_loss():
     assert_close(_np(ds), st.grad.numpy(), 1e-7, 1e-4, what="dloss/ds")
 
 
+@pytest.mark.parametrize("M,T", [(3000, 2), (4096, 7), (1, 1), (70000, 1)])
+def test_bce_clip_loss_multiblock(M, T):
+    """rs_bce_clip_loss_ws: same p / ds as the one-workgroup form, loss vs the fp64 oracle, and a
+    repeated call (counters left zero by the last block) gives the bitwise-same loss."""
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(15)
+    s = rng.uniform(-0.2, 1.2, size=(M, T)).astype(np.float32)
+    y = (rng.uniform(size=(M, T)) < 0.3).astype(np.float32)
+    sd, yd = torch.from_numpy(s).to(DEV), torch.from_numpy(y).to(DEV)
+    n = int(_lib.load().rs_bce_clip_workspace_floats(M, T))
+    ws = torch.zeros(n, device=DEV)
+    outs = []
+    for _ in range(3):
+        p, loss, ds = torch.empty_like(sd), torch.empty(1, device=DEV), torch.empty_like(sd)
+        call("rs_bce_clip_loss_ws", stream_handle(), ptr(sd), ptr(yd), M, T, 1e-6, 1.0, 1e-6, None,
+             ptr(p), ptr(loss), ptr(ds), ptr(ws), n)
+        outs.append((p, loss, ds))
+    p1, loss1, ds1 = torch.empty_like(sd), torch.empty(1, device=DEV), torch.empty_like(sd)
+    call("rs_bce_clip_loss", stream_handle(), ptr(sd), ptr(yd), M, T, 1e-6, 1.0, 1e-6, None, ptr(p1),
+         ptr(loss1), ptr(ds1))
+    torch.cuda.synchronize()
+    assert int((ws[:288] != 0).sum()) == 0  # counters left zero
+    for p, loss, ds in outs:
+        assert torch.equal(loss, outs[0][1])
+        assert_close(_np(p), _np(p1), 0.0, what="clip")
+        assert_close(_np(ds), _np(ds1), 1e-9, 1e-6, what="ds")
+    st = torch.from_numpy(s).double()
+    lr_ = tr.cross_entropy(torch.from_numpy(y).double(), torch.clamp(st, 1e-6, 1.0))
+    assert_close(_np(outs[0][1]), [float(lr_)], 1e-5, 1e-6, what="loss")
+
+
+def test_l1l2_grad_grouped_matches_single():
+    """rs_l1l2_grad_grouped over three tensors (one with exact zeros: tf.sign(0) = 0) == three
+    rs_l1l2_grad launches, bitwise."""
+    import ctypes
+    from recommendsystem_amd import _lib
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    rng = np.random.default_rng(16)
+    sizes, l1s, l2s = [1000, 7, 33333], [1e-5, 0.0, 3e-3], [1e-5, 0.01, 0.0]
+    ws = [torch.from_numpy(rng.normal(size=n).astype(np.float32)).to(DEV) for n in sizes]
+    ws[0][::5] = 0.0
+    gs = [torch.from_numpy(rng.normal(size=n).astype(np.float32)).to(DEV) for n in sizes]
+    ref = [g.clone() for g in gs]
+    for w, g, n, a, b in zip(ws, ref, sizes, l1s, l2s):
+        call("rs_l1l2_grad", stream_handle(), ptr(w), ptr(g), n, a, b)
+    wa, wp = _lib.c_array(ctypes.c_void_p, [ptr(w) for w in ws])
+    ga, gp = _lib.c_array(ctypes.c_void_p, [ptr(g) for g in gs])
+    ca, cp = _lib.c_array(ctypes.c_int64, sizes)
+    la, lp = _lib.c_array(ctypes.c_float, l1s)
+    ra, rp = _lib.c_array(ctypes.c_float, l2s)
+    call("rs_l1l2_grad_grouped", stream_handle(), 3, wp, gp, cp, lp, rp)
+    for g, r in zip(gs, ref):
+        assert torch.equal(g, r)
+
+
 def test_dense_adam_matches_oracle():
     from recommendsystem_amd._lib import call, ptr, stream_handle
     rng = np.random.default_rng(14)
