@@ -62,33 +62,70 @@ struct GM {
   const int32_t* sel;
 };
 
+// Per row: the activations of the row's experts are staged once in LDS (each lane stages and
+// reads only its own columns d = dl + c DP, so no barrier) when `stage` (RPB n_exp D floats of
+// dynamic LDS), and each task's gate softmax is formed once in registers (one exp per gate):
+// every task re-reads every selected expert, and the per-(task, expert, column) exp and global
+// load made this kernel latency-bound.  p_k = exp(g_k - max) / sum exactly as before.
 template <int DP>
 __global__ void __launch_bounds__(256) gate_mix_fwd_kernel(GM a, float* __restrict__ Y, int64_t ldy,
-                                                           float* __restrict__ P, int64_t ldp) {
+                                                           float* __restrict__ P, int64_t ldp,
+                                                           int stage) {
   constexpr int RPB = 256 / DP;
+  extern __shared__ float act_all[];  // [RPB][n_exp][D] when stage
   __shared__ int32_t sel[GM_MAXSEL * 8];
   for (int i = threadIdx.x; i < a.n_task * a.n_sel; i += blockDim.x) sel[i] = a.sel[i];
   __syncthreads();
   const int rl = threadIdx.x / DP, dl = threadIdx.x % DP;
+  const int nch = (a.D + DP - 1) / DP;
+  float* ar = act_all + (int64_t)rl * a.n_exp * a.D;
   for (int64_t m = (int64_t)blockIdx.x * RPB + rl; m < a.M; m += (int64_t)gridDim.x * RPB) {
     const float* g = a.G + m * a.ldg;
     const float* e = a.E + m * a.lde;
+    if (stage) {
+      for (int x = 0; x < a.n_exp; ++x)
+#pragma unroll
+        for (int c = 0; c < GM_MAXCH; ++c) {
+          const int d = dl + c * DP;
+          if (c < nch && d < a.D) ar[x * a.D + d] = act_f(e[(int64_t)x * a.D + d], a.e_act);
+        }
+    }
     for (int t = 0; t < a.n_task; ++t) {
+      float pk[GM_MAXSEL];
       float mx = -INFINITY;
-      for (int k = 0; k < a.n_sel; ++k) mx = fmaxf(mx, g[t * a.n_sel + k]);
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) {
+        pk[k] = k < a.n_sel ? g[t * a.n_sel + k] : -INFINITY;
+        mx = fmaxf(mx, pk[k]);
+      }
       float sum = 0.f;
-      for (int k = 0; k < a.n_sel; ++k) sum += expf(g[t * a.n_sel + k] - mx);
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) {
+        pk[k] = k < a.n_sel ? expf(pk[k] - mx) : 0.f;
+        sum += pk[k];
+      }
       const float inv = 1.0f / sum;
-      for (int d = dl; d < a.D; d += DP) {
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) pk[k] *= inv;
+#pragma unroll
+      for (int c = 0; c < GM_MAXCH; ++c) {
+        const int d = dl + c * DP;
+        if (c >= nch || d >= a.D) continue;
         float acc = 0.f;
-        for (int k = 0; k < a.n_sel; ++k) {
-          const float p = expf(g[t * a.n_sel + k] - mx) * inv;
-          acc = fmaf(p, act_f(e[(int64_t)sel[t * a.n_sel + k] * a.D + d], a.e_act), acc);
+#pragma unroll
+        for (int k = 0; k < GM_MAXSEL; ++k) {
+          if (k < a.n_sel) {
+            const int x = sel[t * a.n_sel + k];
+            const float v = stage ? ar[x * a.D + d] : act_f(e[(int64_t)x * a.D + d], a.e_act);
+            acc = fmaf(pk[k], v, acc);
+          }
         }
         Y[m * ldy + (int64_t)t * a.D + d] = acc;
       }
       if (P) {
-        for (int k = dl; k < a.n_sel; k += DP) P[m * ldp + t * a.n_sel + k] = expf(g[t * a.n_sel + k] - mx) * inv;
+#pragma unroll
+        for (int k = 0; k < GM_MAXSEL; ++k)
+          if (k < a.n_sel && (k % DP) == dl) P[m * ldp + t * a.n_sel + k] = pk[k];
       }
     }
   }
@@ -98,14 +135,15 @@ template <int DP>
 __global__ void __launch_bounds__(256) gate_mix_bwd_kernel(GM a, const float* __restrict__ dY,
                                                            int64_t lddy, float* __restrict__ dE,
                                                            int64_t ldde, float* __restrict__ dG,
-                                                           int64_t lddg) {
+                                                           int64_t lddg, int stage) {
   constexpr int RPB = 256 / DP;
-  extern __shared__ float acc_all[];  // [RPB][n_exp][D]
+  extern __shared__ float acc_all[];  // [RPB][n_exp][D] (+ [RPB][n_exp][D] activations: stage)
   __shared__ int32_t sel[GM_MAXSEL * 8];
   for (int i = threadIdx.x; i < a.n_task * a.n_sel; i += blockDim.x) sel[i] = a.sel[i];
   __syncthreads();
   const int rl = threadIdx.x / DP, dl = threadIdx.x % DP;
   float* acc = acc_all + (int64_t)rl * a.n_exp * a.D;
+  float* ar = acc_all + (int64_t)(RPB + rl) * a.n_exp * a.D;
   const int nch = (a.D + DP - 1) / DP;
   // every thread walks the same number of rows (so the group reductions stay converged)
   const int64_t nrow_iter = (a.M + (int64_t)gridDim.x * RPB - 1) / ((int64_t)gridDim.x * RPB);
@@ -116,9 +154,13 @@ __global__ void __launch_bounds__(256) gate_mix_bwd_kernel(GM a, const float* __
     const float* g = a.G + mm * a.ldg;
     const float* e = a.E + mm * a.lde;
     for (int x = 0; x < a.n_exp; ++x)
-      for (int c = 0; c < nch; ++c) {
+#pragma unroll
+      for (int c = 0; c < GM_MAXCH; ++c) {
         const int d = dl + c * DP;
-        if (d < a.D) acc[x * a.D + d] = 0.f;
+        if (c < nch && d < a.D) {
+          acc[x * a.D + d] = 0.f;
+          if (stage) ar[x * a.D + d] = act_f(e[(int64_t)x * a.D + d], a.e_act);
+        }
       }
     for (int t = 0; t < a.n_task; ++t) {
       float dy[GM_MAXCH];
@@ -127,24 +169,33 @@ __global__ void __launch_bounds__(256) gate_mix_bwd_kernel(GM a, const float* __
         const int d = dl + c * DP;
         dy[c] = (c < nch && d < a.D && live) ? dY[mm * lddy + (int64_t)t * a.D + d] : 0.f;
       }
-      float mx = -INFINITY;
-      for (int k = 0; k < a.n_sel; ++k) mx = fmaxf(mx, g[t * a.n_sel + k]);
-      float sum = 0.f;
-      for (int k = 0; k < a.n_sel; ++k) sum += expf(g[t * a.n_sel + k] - mx);
-      const float inv = 1.0f / sum;
       float p[GM_MAXSEL], s[GM_MAXSEL];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) {
+        p[k] = k < a.n_sel ? g[t * a.n_sel + k] : -INFINITY;
+        mx = fmaxf(mx, p[k]);
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < GM_MAXSEL; ++k) {
+        p[k] = k < a.n_sel ? expf(p[k] - mx) : 0.f;
+        sum += p[k];
+      }
+      const float inv = 1.0f / sum;
       float ps = 0.f;
 #pragma unroll
       for (int k = 0; k < GM_MAXSEL; ++k) {
-        p[k] = 0.f; s[k] = 0.f;
+        p[k] *= inv;
+        s[k] = 0.f;
         if (k < a.n_sel) {
-          p[k] = expf(g[t * a.n_sel + k] - mx) * inv;
           const int64_t col = (int64_t)sel[t * a.n_sel + k] * a.D;
           float part = 0.f;
 #pragma unroll
           for (int c = 0; c < GM_MAXCH; ++c) {
             const int d = dl + c * DP;
-            if (c < nch && d < a.D) part = fmaf(dy[c], act_f(e[col + d], a.e_act), part);
+            if (c < nch && d < a.D)
+              part = fmaf(dy[c], stage ? ar[col + d] : act_f(e[col + d], a.e_act), part);
           }
           s[k] = group_sum<DP>(part);
           ps = fmaf(p[k], s[k], ps);
@@ -914,12 +965,15 @@ RS_API int rs_gate_mix_fwd(void* stream, const float* E, int64_t lde, int e_act,
   if (M == 0) return RS_OK;
   const int dp = gm_dp(D);
   const int grid = rows_grid(M, 256 / dp);
+  const size_t act_lds = (size_t)(256 / dp) * n_exp * D * 4;
+  const int stage = act_lds <= 32 * 1024;
+  const size_t lds = stage ? act_lds : 0;
   hipStream_t s = rs_stream(stream);
   switch (dp) {
-    case 8: gate_mix_fwd_kernel<8><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
-    case 16: gate_mix_fwd_kernel<16><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
-    case 32: gate_mix_fwd_kernel<32><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
-    default: gate_mix_fwd_kernel<64><<<grid, 256, 0, s>>>(a, Y, ldy, P, ldp); break;
+    case 8: gate_mix_fwd_kernel<8><<<grid, 256, lds, s>>>(a, Y, ldy, P, ldp, stage); break;
+    case 16: gate_mix_fwd_kernel<16><<<grid, 256, lds, s>>>(a, Y, ldy, P, ldp, stage); break;
+    case 32: gate_mix_fwd_kernel<32><<<grid, 256, lds, s>>>(a, Y, ldy, P, ldp, stage); break;
+    default: gate_mix_fwd_kernel<64><<<grid, 256, lds, s>>>(a, Y, ldy, P, ldp, stage); break;
   }
   return rs_status_after_launch();
 }
@@ -934,15 +988,18 @@ RS_API int rs_gate_mix_bwd(void* stream, const float* E, int64_t lde, int e_act,
   if (M == 0) return RS_OK;
   const int dp = gm_dp(D);
   const int rpb = 256 / dp;
-  const size_t lds = (size_t)rpb * n_exp * D * 4;
-  if (lds > 64 * 1024) return RS_ERR_UNSUPPORTED;
+  const size_t acc_lds = (size_t)rpb * n_exp * D * 4;
+  if (acc_lds > 64 * 1024) return RS_ERR_UNSUPPORTED;
+  // the staged activations double the LDS: kept while the total stays <= 64 KB
+  const int stage = 2 * acc_lds <= 64 * 1024;
+  const size_t lds = stage ? 2 * acc_lds : acc_lds;
   const int grid = rows_grid(M, rpb);
   hipStream_t s = rs_stream(stream);
   switch (dp) {
-    case 8: gate_mix_bwd_kernel<8><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
-    case 16: gate_mix_bwd_kernel<16><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
-    case 32: gate_mix_bwd_kernel<32><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
-    default: gate_mix_bwd_kernel<64><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg); break;
+    case 8: gate_mix_bwd_kernel<8><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg, stage); break;
+    case 16: gate_mix_bwd_kernel<16><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg, stage); break;
+    case 32: gate_mix_bwd_kernel<32><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg, stage); break;
+    default: gate_mix_bwd_kernel<64><<<grid, 256, lds, s>>>(a, dY, lddy, dE, ldde, dG, lddg, stage); break;
   }
   return rs_status_after_launch();
 }

@@ -750,6 +750,27 @@ class KDLoss(nn.Module):
 
 _BCE_WS: dict = {}
 
+# Backward seeds known to hold exactly 1.0 for good (the Trainer's private loss.backward seed):
+# the loss Functions return their pre-computed gradient as is for such a seed instead of
+# launching a multiply by it.  The tensors are kept referenced, so their addresses never go to
+# another tensor.
+_UNIT_SEEDS: list = []
+_UNIT_SEED_PTRS: set = set()
+
+
+def register_unit_seed(t: torch.Tensor) -> None:
+    """t: a 0-d float32 tensor holding 1.0 that nothing writes again."""
+    if t.dim() != 0 or t.dtype != torch.float32:
+        raise ValueError("a unit seed is a 0-d float32 tensor")
+    _UNIT_SEEDS.append(t)
+    _UNIT_SEED_PTRS.add(t.data_ptr())
+
+
+def _times_seed(g: torch.Tensor, dl: torch.Tensor) -> torch.Tensor:
+    if dl.dim() == 0 and dl.dtype == torch.float32 and dl.data_ptr() in _UNIT_SEED_PTRS:
+        return g
+    return g * dl
+
 
 def _bce_workspace(device):
     """One persistent, zero-initialised workspace per device for rs_bce_clip_loss_ws (its size is
@@ -786,7 +807,7 @@ class _BCEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dl):
         (ds,) = ctx.saved_tensors
-        return ds * dl, None, None, None, None
+        return _times_seed(ds, dl), None, None, None, None
 
 
 def keras_bce(y_true, y_pred, eps=1e-7):
@@ -848,7 +869,7 @@ class _FusedLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dl):
         (G,) = ctx.saved_tensors
-        G = G * dl
+        G = _times_seed(G, dl)
         grads, off = [], 0
         for n, shp in zip(ctx.sizes, ctx.shapes):
             grads.append(G[off:off + n].view(shp))

@@ -66,6 +66,8 @@ class Trainer:
         # the step counter) and the backward's seed (no ones_like fill launch per step)
         self._adam_done = [torch.zeros(288, device=dev, dtype=torch.int32) for _ in self.segments]
         self._seed = torch.ones((), device=dev)
+        from .towers import register_unit_seed
+        register_unit_seed(self._seed)  # the loss backward skips its multiply by this seed
         self.tables = list(tables)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
