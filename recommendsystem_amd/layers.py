@@ -34,13 +34,26 @@ def _act_code(activation) -> int:
 # ============================================================================================
 # InteractingLayer
 # ============================================================================================
+class GradSink:
+    """Hands one consumer's input gradient to another consumer of the same input so the second
+    one's backward ADDS its share in its own launch (rs_dense_bwd with dx accumulate) instead of
+    autograd summing two [B, K] gradients with an extra elementwise launch.  The producer's
+    backward must run first: it does whenever the producer sits downstream of the consumer in
+    the forward (the interacting layer's concat takes the deep tower's output)."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
 class _InteractingFn(torch.autograd.Function):
     """lead: None -> y [B, F, U]; a [B, Dl] tensor -> the concat [lead | y.reshape(B, F U)]
     [B, Dl + F U] with y written in place by the kernel (y_ld) and its backward reading its dy
     slice in place (dy_ld): no concat copy forward, no contiguous copy of the split gradient."""
 
     @staticmethod
-    def forward(ctx, x, W, bias, gamma, beta, layer, seed, drop_rate, lead=None):
+    def forward(ctx, x, W, bias, gamma, beta, layer, seed, drop_rate, lead=None, sink=None):
         _lib.require_device(x, W)
         x = x.contiguous()
         B, F, E = x.shape
@@ -65,6 +78,7 @@ class _InteractingFn(torch.autograd.Function):
         ctx.save_for_backward(x, xsave, W, bias, gamma, beta, asave)
         ctx.layer, ctx.seed, ctx.drop_rate, ctx.Dl = layer, seed, drop_rate, Dl
         ctx.has_lead = lead is not None
+        ctx.sink = sink
         return out
 
     @staticmethod
@@ -95,13 +109,15 @@ class _InteractingFn(torch.autograd.Function):
              int(layer.use_res), ctx.drop_rate, ctx.seed, ptr(dx), 0, ptr(dparams),
              1 if in_place else 0, ptr(ws), ws_n, ptr(asave) if asave.numel() else None,
              asave.numel())
+        if ctx.sink is not None:  # the deep tower's first Dense adds its dx onto this one
+            ctx.sink.buf, dx = dx.view(B, F * E), None
         if in_place:
-            return dx, None, None, None, None, None, None, None, d_lead
+            return dx, None, None, None, None, None, None, None, d_lead, None
         outs, off = [], 0
         for p in params:
             outs.append(dparams[off:off + p.numel()].view(p.shape))
             off += p.numel()
-        return (dx, *outs, None, None, None, d_lead)
+        return (dx, *outs, None, None, None, d_lead, None)
 
 
 class InteractingLayer(nn.Module):
@@ -179,10 +195,12 @@ class InteractingLayer(nn.Module):
         return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
                                     self, seed, drop)
 
-    def forward_concat(self, lead, inputs):
+    def forward_concat(self, lead, inputs, grad_sink=None):
         """tf.concat([lead, Flatten()(self(inputs))], axis=1) (rank/multi_head/multidnn.py:71)
         with the layer's output written straight into the concat and its gradient read from
-        there in place."""
+        there in place.  grad_sink: a GradSink shared with the Dense that consumes
+        inputs.reshape(B, -1) upstream of `lead` (Dense.forward(x, grad_sink=...)); the layer's
+        input gradient then reaches `inputs` through that Dense's backward."""
         if not self.built:
             self.build(tuple(inputs.shape), device=inputs.device)
         from . import ops
@@ -195,7 +213,7 @@ class InteractingLayer(nn.Module):
         seed = (self.seed * 1000003 + self._calls) & 0xFFFFFFFFFFFFFFFF
         self._calls += 1
         return _InteractingFn.apply(inputs.float(), self.kernel, self.bias, self.gamma, self.beta,
-                                    self, seed, drop, lead.float())
+                                    self, seed, drop, lead.float(), grad_sink)
 
 
 # ============================================================================================
@@ -251,7 +269,7 @@ def gather_multi(src, plans):
 
 class _DenseFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, b, act):
+    def forward(ctx, x, W, b, act, sink=None):
         _lib.require_device(x, W)
         x = _row_major(x)
         M, K = x.shape
@@ -261,6 +279,7 @@ class _DenseFn(torch.autograd.Function):
              ptr(y), N)
         ctx.save_for_backward(x, y, W, b)
         ctx.act = act
+        ctx.sink = sink
         return y
 
     @staticmethod
@@ -276,16 +295,21 @@ class _DenseFn(torch.autograd.Function):
         dW = W.grad if in_place else torch.empty_like(W)
         db = b.grad if in_place else torch.empty_like(b)
         dx = None
+        sink = ctx.sink
         if ctx.needs_input_grad[0]:  # data and weight gradients in one launch
-            dx = torch.empty(M, K, device=x.device, dtype=torch.float32)
+            acc = sink is not None and sink.buf is not None and sink.buf.shape == (M, K)
+            dx = sink.buf if acc else torch.empty(M, K, device=x.device, dtype=torch.float32)
+            if sink is not None:
+                sink.buf = None
             call("rs_dense_bwd", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N, ctx.act,
-                 ptr(W), M, K, N, ptr(dx), K, 0, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
+                 ptr(W), M, K, N, ptr(dx), K, 1 if acc else 0, ptr(dW), ptr(db),
+                 1 if in_place else 0, ptr(ws), ws_n)
         else:
             call("rs_dense_bwd_weight", s, ptr(x), x.stride(0), ptr(dy), dy.stride(0), ptr(y), N,
                  ctx.act, M, K, N, ptr(dW), ptr(db), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
-            return dx, None, None, None
-        return dx, dW, db, None
+            return dx, None, None, None, None
+        return dx, dW, db, None, None
 
 
 class Dense(nn.Module):
@@ -310,7 +334,9 @@ class Dense(nn.Module):
         self.input_dim = K
         self.built = True
 
-    def forward(self, x):
+    def forward(self, x, grad_sink=None):
+        """grad_sink: a GradSink whose producer's input gradient this layer's dx is added onto
+        (see GradSink; only for a 2-D input)."""
         if not self.built:
             self.build(tuple(x.shape), device=x.device)
         lead = x.shape[:-1]  # Keras Dense = tensordot over the last axis
@@ -318,7 +344,8 @@ class Dense(nn.Module):
         if ops.custom_ops_enabled():
             y = torch.ops.ctr.dense(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act)
             return y.reshape(*lead, self.units)
-        y = _DenseFn.apply(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act)
+        y = _DenseFn.apply(x.reshape(-1, x.shape[-1]).float(), self.kernel, self.bias, self.act,
+                           grad_sink)
         return y.reshape(*lead, self.units)
 
 

@@ -27,7 +27,7 @@ from torch import nn
 from ._lib import call, ptr, stream_handle
 from .din import StaytimeDIN
 from .embedding import EmbeddingFeatures, SequenceEmbedding, SparseAdaGrad, SparseAdam, SparseTable
-from .layers import (Dense, InteractingLayer, _act_code, _DenseFn, _row_major, gather_multi,
+from .layers import (Dense, GradSink, InteractingLayer, _act_code, _DenseFn, _row_major, gather_multi,
                      grouped_dense)
 from .params import FlatBlock, glorot_uniform_, grads_contiguous
 from . import _lib
@@ -340,12 +340,15 @@ class MultiHeadRanker(nn.Module):
     def forward(self, ids, offsets):
         x0 = self.embedding(ids, offsets)                       # [B, F, 8]
         B = x0.shape[0]
-        deep = x0.reshape(B, -1)                                # :60
-        for layer in self.deep:
-            deep = layer(deep)                                  # :61-63
+        # :60-63 the deep tower; its first Dense also adds the interacting layers' dx0 in its
+        # backward (GradSink: no separate sum of the two [B, F E] gradients)
+        sink = GradSink()
+        deep = self.deep[0](x0.reshape(B, -1), grad_sink=sink)
+        for layer in self.deep[1:]:
+            deep = layer(deep)
         # :54-56 interacting layers, :71 concat [deep, autoint]: the layer writes its output
         # into the concat directly
-        result = self.interact.forward_concat(deep, x0)
+        result = self.interact.forward_concat(deep, x0, grad_sink=sink)
         gated_out = self.mix.forward_flat(result)               # :77-120, the 7 outputs side by side
         return self.towers(gated_out)                           # :122-204 -> [B, 7]
 
