@@ -62,14 +62,17 @@ def main(path, steps, pair=0, out=None):
                                "us_per_step": round(e["us"] / steps, 2), "origin": e["origin"],
                                "share": round(e["us"] / busy, 4)} for k, e in per.items()),
                              key=lambda x: -x["us_per_step"])}
-    print(f"wall {res['wall_us_per_step']} us/step, GPU busy {res['gpu_busy_us_per_step']} us/step; "
-          f"by origin {res['share_by_origin']}")
-    for k in res["kernels"][:40]:
-        print(f"  {k['us_per_step']:9.2f} us {k['calls_per_step']:6.1f}x {k['share']*100:5.1f}%  "
-              f"[{k['origin'][:5]}] {k['name']}")
-    if out:
+    if out:  # written before the listing: a reader that closes the pipe early loses only lines
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
+    try:
+        print(f"wall {res['wall_us_per_step']} us/step, GPU busy {res['gpu_busy_us_per_step']} "
+              f"us/step; by origin {res['share_by_origin']}")
+        for k in res["kernels"][:40]:
+            print(f"  {k['us_per_step']:9.2f} us {k['calls_per_step']:6.1f}x {k['share']*100:5.1f}%  "
+                  f"[{k['origin'][:5]}] {k['name']}")
+    except BrokenPipeError:
+        pass
 
 
 if __name__ == "__main__":
