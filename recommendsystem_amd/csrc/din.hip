@@ -116,13 +116,32 @@ struct SampleW {
   }
 };
 
-// Layer-1 pre-activations of rows t0 + 4g + r (column j) minus nothing: z1[r] = acc[r] + c.
-__device__ __forceinline__ f32x4 layer1(const float* __restrict__ krow0, int64_t k_rs, int t0,
-                                        int T, const float bw[4]) {
+// The key rows t0 .. t0 + 15 as this lane's A fragment (row t0 + (l & 15), columns 4 (l >> 4)..).
+// The sweeps load step t0 + 16's keys / values while step t0 computes (one step ahead), so a
+// wave's per-step HBM round trip overlaps its MFMA / DPP work instead of serialising with it.
+__device__ __forceinline__ float4 load_keys(const float* __restrict__ krow0, int64_t k_rs, int t0,
+                                            int T) {
   const int l = lane_id();
   const int row = t0 + (l & 15);
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (row < T) a = *reinterpret_cast<const float4*>(krow0 + (int64_t)row * k_rs + 4 * (l >> 4));
+  return a;
+}
+// values (or any [T, >= 16] row set) of rows t0 + 4g + r, column j, r < 4
+struct Vals { float v[4]; };
+__device__ __forceinline__ Vals load_vals(const float* __restrict__ vrow0, int64_t v_rs, int t0,
+                                          int T) {
+  const int l = lane_id(), g = l >> 4, j = l & 15;
+  Vals out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = t0 + 4 * g + r;
+    out.v[r] = t < T ? vrow0[(int64_t)t * v_rs + j] : 0.f;
+  }
+  return out;
+}
+// Layer-1 pre-activations of rows t0 + 4g + r (column j) minus nothing: z1[r] = acc[r] + c.
+__device__ __forceinline__ f32x4 layer1_frag(float4 a, const float bw[4]) {
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   acc = mfma4(a.x, bw[0], acc);
   acc = mfma4(a.y, bw[1], acc);
@@ -154,8 +173,17 @@ __global__ void __launch_bounds__(64 * WPB) din_fwd_kernel(Geo geo, const float*
     const float* vrow0 = geo.v + b * geo.v_ss;
     const int len = geo.lengths ? min(geo.lengths[b], T) : T;
     float o = 0.f, mx = -INFINITY;
+    float4 an = load_keys(krow0, geo.k_rs, 0, T);
+    Vals vn{};
+    if (VAR == 0) vn = load_vals(vrow0, geo.v_rs, 0, T);
     for (int t0 = 0; t0 < T; t0 += 16) {
-      const f32x4 acc = layer1(krow0, geo.k_rs, t0, T, sw.bw);
+      const float4 a = an;
+      const Vals vc = vn;
+      if (t0 + 16 < T) {
+        an = load_keys(krow0, geo.k_rs, t0 + 16, T);
+        if (VAR == 0) vn = load_vals(vrow0, geo.v_rs, t0 + 16, T);
+      }
+      const f32x4 acc = layer1_frag(a, sw.bw);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float z1 = acc[r] + sw.c;
@@ -166,7 +194,7 @@ __global__ void __launch_bounds__(64 * WPB) din_fwd_kernel(Geo geo, const float*
           const bool on = pos_on(geo, b, t, len);
           if (VAR == 0) {
             const float s = on ? fmaxf(z2, 0.f) : 0.f;
-            o = fmaf(s, vrow0[(int64_t)t * geo.v_rs + j], o);
+            o = fmaf(s, vc.v[r], o);
           } else {
             const float sc = on ? z2 : PAD;
             mx = fmaxf(mx, sc);
@@ -180,14 +208,17 @@ __global__ void __launch_bounds__(64 * WPB) din_fwd_kernel(Geo geo, const float*
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       wave_lds_sync();
       float lsum = 0.f;
+      Vals fn = load_vals(vrow0, geo.v_rs, 0, T);
       for (int t0 = 0; t0 < T; t0 += 16) {
+        const Vals fc = fn;
+        if (t0 + 16 < T) fn = load_vals(vrow0, geo.v_rs, t0 + 16, T);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = t0 + 4 * g + r;
           if (t < T) {
             const float e = __expf(sbuf[t] - mx);
             lsum += e;
-            o = fmaf(e, vrow0[(int64_t)t * geo.v_rs + j], o);
+            o = fmaf(e, fc.v[r], o);
           }
         }
       }
@@ -245,11 +276,14 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
     const float* prow = VAR == 1 ? probs + b * T : nullptr;
     float sdp = 0.f;
     if (VAR == 1) {  // pass 1: dp_t = dout . f_t, sum_t p_t dp_t
+      Vals fn = load_vals(vrow0, geo.v_rs, 0, T);
       for (int t0 = 0; t0 < T; t0 += 16) {
+        const Vals fc = fn;
+        if (t0 + 16 < T) fn = load_vals(vrow0, geo.v_rs, t0 + 16, T);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int t = t0 + 4 * g + r;
-          const float fv = t < T ? vrow0[(int64_t)t * geo.v_rs + j] : 0.f;
+          const float fv = fc.v[r];
           const float dp = group_sum<16>(doj * fv);
           if (t < T) {
             sdp = fmaf(prow[t], dp, sdp);
@@ -263,8 +297,16 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
     }
     f32x4 G = {0.f, 0.f, 0.f, 0.f};
     float gs = 0.f;
+    float4 an = load_keys(krow0, geo.k_rs, 0, T);
+    Vals vn = load_vals(vrow0, geo.v_rs, 0, T);
     for (int t0 = 0; t0 < T; t0 += 16) {
-      const f32x4 acc = layer1(krow0, geo.k_rs, t0, T, sw.bw);
+      const float4 a = an;
+      const Vals vc = vn;
+      if (t0 + 16 < T) {
+        an = load_keys(krow0, geo.k_rs, t0 + 16, T);
+        vn = load_vals(vrow0, geo.v_rs, t0 + 16, T);
+      }
+      const f32x4 acc = layer1_frag(a, sw.bw);
       float dz1[4], kv[4], dvv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -276,7 +318,7 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
         float dz2, vval;
         if (VAR == 0) {
           const float z2 = group_sum<16>(h * fr.w2) + fr.b2;
-          vval = in ? vrow0[(int64_t)t * geo.v_rs + j] : 0.f;
+          vval = vc.v[r];
           const float ds = group_sum<16>(doj * vval);
           const float s = on ? fmaxf(z2, 0.f) : 0.f;
           dz2 = (on && z2 > 0.f) ? ds : 0.f;
@@ -286,7 +328,7 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
         } else {
           const float p = in ? prow[t] : 0.f;
           dz2 = on ? p * (sbuf[in ? t : 0] - sdp) : 0.f;
-          vval = in ? vrow0[(int64_t)t * geo.v_rs + j] : 0.f;
+          vval = vc.v[r];
           dvv[r] = p * doj;                                   // d facts through the pooling
           kv[r] = vval;
           dz1[r] = dz2 * fr.w2 * h * (1.0f - h);
