@@ -482,7 +482,7 @@ def test_interacting_many_fields_dropout(F, L):
     y = il(xd)
     W, b, g, be = _il_ref_params(il)
     ref = npo.interacting_layer(x.astype(np.float64), W, b, g, be, L, H, True, drop_rate=0.2, seed=seed)
-    assert_close(_np(y), ref, 2e-5, what="IL many-field dropout fwd")
+    assert_close(_np(y), ref, 1e-5, what="IL many-field dropout fwd")
     dy = rng.normal(size=(B, F, U)).astype(np.float32)
     y.backward(torch.from_numpy(dy).to(DEV))
     Wt, bt, gt, bet = (torch.from_numpy(a).requires_grad_(True) for a in _il_ref_params(il))
