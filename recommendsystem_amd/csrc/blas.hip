@@ -1,9 +1,11 @@
 // hipBLASLt for the large plain fp32 GEMMs of the Dense layers (blas.hpp).  One handle and one
 // workspace per process, created on the first eligible call (an eager step: graph capture
 // replays the plans a warm-up step made); one plan per (shape, layout, epilogue): matmul
-// descriptor, four matrix layouts and the heuristic's first algorithm, cached.  The bias pointer
-// is set on the cached descriptor per call (host-side attribute; a captured launch keeps the one
-// it was recorded with).
+// descriptor, four matrix layouts and an algorithm, cached.  The algorithm is the fastest of the
+// heuristic's top candidates, each timed on scratch operands of the plan's shape on a private
+// stream when the plan is made outside a graph capture (the heuristic's first pick otherwise, or
+// with RS_GEMM_BLAS_TUNE=0).  The bias pointer is set on the cached descriptor per call
+// (host-side attribute; a captured launch keeps the one it was recorded with).
 #include "blas.hpp"
 
 #include <hipblaslt/hipblaslt.h>
@@ -52,8 +54,56 @@ bool init_locked(Ctx& c) {
   return true;
 }
 
+// Times each usable candidate (1 warm-up + 5 timed runs) on zero-filled scratch operands of the
+// plan's shape; returns the index of the fastest (`dflt` if anything fails).
+int time_candidates(Ctx& c, Plan& p, const hipblasLtMatmulHeuristicResult_t* res, int got, int dflt,
+                    bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                    int64_t ldd, int epi, bool beta) {
+  const size_t na = (size_t)lda * (size_t)(ta ? m : k), nb = (size_t)ldb * (size_t)(tb ? k : n);
+  const size_t nd = (size_t)ldd * (size_t)n, nbias = (size_t)(m > n ? m : n);
+  float *A = nullptr, *B = nullptr, *D = nullptr, *bias = nullptr;
+  hipStream_t ts = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int pick = dflt;
+  const bool ok = hipMalloc(&A, na * 4) == hipSuccess && hipMalloc(&B, nb * 4) == hipSuccess &&
+                  hipMalloc(&D, nd * 4) == hipSuccess && hipMalloc(&bias, nbias * 4) == hipSuccess &&
+                  hipStreamCreateWithFlags(&ts, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+                  hipMemsetAsync(A, 0, na * 4, ts) == hipSuccess &&
+                  hipMemsetAsync(B, 0, nb * 4, ts) == hipSuccess &&
+                  hipMemsetAsync(D, 0, nd * 4, ts) == hipSuccess &&
+                  hipMemsetAsync(bias, 0, nbias * 4, ts) == hipSuccess;
+  if (ok) {
+    if (epi != HIPBLASLT_EPILOGUE_DEFAULT)
+      hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias,
+                                      sizeof(bias));
+    const float alpha = 1.f, bt = beta ? 1.f : 0.f;
+    float best_ms = 1e30f;
+    for (int i = 0; i < got; ++i) {
+      if (res[i].workspaceSize > kWsBytes) continue;
+      bool good = true;
+      for (int r = 0; r < 6 && good; ++r) {
+        if (r == 1) good = hipEventRecord(e0, ts) == hipSuccess;
+        good = good && hipblasLtMatmul(c.h, p.desc, &alpha, A, p.a, B, p.b, &bt, D, p.d, D, p.d,
+                                       &res[i].algo, c.ws, kWsBytes, ts) == HIPBLAS_STATUS_SUCCESS;
+      }
+      float ms = 0.f;
+      good = good && hipEventRecord(e1, ts) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+             hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+      if (good && ms < best_ms) { best_ms = ms; pick = i; }
+    }
+    hipStreamSynchronize(ts);
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (ts) hipStreamDestroy(ts);
+  hipFree(A); hipFree(B); hipFree(D); hipFree(bias);
+  (void)hipGetLastError();
+  return pick;
+}
+
 Plan make_plan(Ctx& c, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
-               int64_t ldd, int epi, bool beta) {
+               int64_t ldd, int epi, bool beta, bool tune) {
   Plan p;
   if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS)
     return p;
@@ -75,16 +125,22 @@ Plan make_plan(Ctx& c, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_
   const uint64_t wsb = kWsBytes;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                         sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t res[1];
+  constexpr int kCand = 8;
+  hipblasLtMatmulHeuristicResult_t res[kCand];
   int got = 0;
+  const int want = tune ? kCand : 1;
   const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.d, p.d, pref,
-                                                             1, res, &got);
+                                                             want, res, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
-  (void)beta;
-  if (st == HIPBLAS_STATUS_SUCCESS && got > 0 && res[0].workspaceSize <= kWsBytes) {
-    p.algo = res[0].algo;
-    p.ok = true;
-  }
+  if (st != HIPBLAS_STATUS_SUCCESS || got <= 0) return p;
+  int best = -1;
+  for (int i = 0; i < got && best < 0; ++i)
+    if (res[i].workspaceSize <= kWsBytes) best = i;
+  if (best < 0) return p;
+  if (tune && got > 1) best = time_candidates(c, p, res, got, best, ta, tb, m, n, k, lda, ldb, ldd,
+                                              epi, beta);
+  p.algo = res[best].algo;
+  p.ok = true;
   return p;
 }
 
@@ -117,8 +173,14 @@ int rs_blas_gemm_cm(hipStream_t s, bool ta, bool tb, int64_t m, int64_t n, int64
     if (!init_locked(c)) return 1;
     const Key key{ta, tb, m, n, k, lda, ldb, ldd, epi, beta != 0.f};
     auto it = c.plans.find(key);
-    if (it == c.plans.end())
-      it = c.plans.emplace(key, make_plan(c, ta, tb, m, n, k, lda, ldb, ldd, epi, beta != 0.f)).first;
+    if (it == c.plans.end()) {
+      static const bool tune_on = env_i64("RS_GEMM_BLAS_TUNE", 1) != 0;
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      const bool capturing = hipStreamIsCapturing(s, &cs) != hipSuccess ||
+                             cs != hipStreamCaptureStatusNone;
+      it = c.plans.emplace(key, make_plan(c, ta, tb, m, n, k, lda, ldb, ldd, epi, beta != 0.f,
+                                          tune_on && !capturing)).first;
+    }
     p = &it->second;
     if (!p->ok) return 1;
     if (bias)
