@@ -381,7 +381,7 @@ int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* dY, int
                  const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K, int N,
                  float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db, int w_accumulate,
                  float* workspace, int64_t workspace_floats);
-/* Large plain GEMMs (M K N >= 2^28 multiply-adds by default; RS_GEMM_BLAS=0 off,
+/* Large plain GEMMs (M K N >= 2^26 multiply-adds by default; RS_GEMM_BLAS=0 off,
  * RS_GEMM_BLAS_MACS=n threshold) run on hipBLASLt inside the four entries above: forward with
  * its bias / ReLU epilogue (sigmoid stays on the engine), weight gradient and rs_dense_bwd with
  * dZ = dY act'(Y) materialised in the workspace (the workspace query covers it) and db from a

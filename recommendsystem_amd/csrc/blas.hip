@@ -154,9 +154,10 @@ int64_t env_i64(const char* name, int64_t dflt) {
 
 bool rs_blas_wanted(int64_t m, int64_t n, int64_t k) {
   // measured (tools/gemm_vs_blas.py, profiles/r05/blas/gemm.log): the library leads
-  // on the towers' weight / data gradients from ~0.4 G multiply-adds (1.3-4x on the trunks); at
-  // 0.2 G (4096 x 1600 x 32) the engine's split-K weight gradient is faster
-  static const int64_t thr = env_i64("RS_GEMM_BLAS_MACS", (int64_t)1 << 28);
+  // on the towers' weight / data gradients from ~0.4 G multiply-adds (1.3-4x on the trunks); with
+  // the timed algorithm choice it also wins from 67 M (config 3 1.586 -> 1.570 ms, config 5
+  // 1.791 -> 1.784 ms against the 268 M threshold, profiles/r05/thr/)
+  static const int64_t thr = env_i64("RS_GEMM_BLAS_MACS", (int64_t)1 << 26);
   static const bool on = env_i64("RS_GEMM_BLAS", 1) != 0;
   return on && m > 0 && n > 0 && k > 0 && m * n * k >= thr;
 }
