@@ -355,6 +355,17 @@ int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t q_ld, 
                        float* dq, int64_t dq_ld, float* dkeys, float* dvalues, int64_t dkv_rs,
                        int dkv_width, float* dparams, int dparams_accumulate, float* workspace,
                        int64_t workspace_floats);
+/* rs_din_bwd_strided that also adds the query's other gradient: dq = dq_base + dL/dq (dq_base
+ * [B, >= H] at row stride dq_base_ld, nullable; may not alias dq).  Used when the query is also
+ * concatenated after the pooled output (the config-4 head's [pooled, q]). */
+int rs_din_bwd_ex(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,
+                  int64_t k_ss, int64_t k_rs, const float* values, int64_t v_ss, int64_t v_rs,
+                  int64_t B, int T, int H, const int32_t* lengths, const uint8_t* mask,
+                  int64_t mask_ld, const float* W1, const float* b1, const float* W2,
+                  const float* b2, const float* probs, const float* dout, int64_t dout_ld,
+                  float* dq, int64_t dq_ld, const float* dq_base, int64_t dq_base_ld,
+                  float* dkeys, float* dvalues, int64_t dkv_rs, int dkv_width, float* dparams,
+                  int dparams_accumulate, float* workspace, int64_t workspace_floats);
 
 /* ---------------------------------------------------------------------------------------
  * H4/H5/H8/H9  Keras Dense(units, activation) towers (autoint:36-52 MultiLayerDense,

@@ -108,6 +108,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_din_bwd_strided": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32,
                                   _i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                   _i64, _vp, _vp, _i64, _i32, _vp, _i32, _vp, _i64]),
+    "rs_din_bwd_ex": (_i32, [_vp, _i32, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i64, _i32,
+                             _i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                             _i64, _vp, _i64, _vp, _vp, _i64, _i32, _vp, _i32, _vp, _i64]),
     "rs_gate_mix_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
                                _vp, _i64, _vp, _i64]),
     "rs_gate_mix_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp,

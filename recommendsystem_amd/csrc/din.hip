@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ probs,
     const float* __restrict__ dout, int64_t dout_ld, float* __restrict__ dq, int64_t dq_ld,
     float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ part, int64_t dkv_rs,
-    int dkv_pad) {
+    int dkv_pad, const float* __restrict__ dq_base, int64_t dqb_ld) {
   constexpr int NP = nparam(VAR);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int l = lane_id(), g = l >> 4, j = l & 15, w = wave_id();
@@ -385,8 +385,13 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
       accQG[r] = fmaf(sw.qv[r], G[r], accQG[r]);
     }
     if (g == 0) accb1 += gs;
-    if (j == 0) *reinterpret_cast<float4*>(dq + b * dq_ld + 4 * g) =
-        make_float4(dqv[0], dqv[1], dqv[2], dqv[3]);
+    if (j == 0) {
+      if (dq_base) {  // dq = the query's other gradient + this one (no separate sum launch)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dqv[r] += dq_base[b * dqb_ld + 4 * g + r];
+      }
+      *reinterpret_cast<float4*>(dq + b * dq_ld + 4 * g) = make_float4(dqv[0], dqv[1], dqv[2], dqv[3]);
+    }
   }
   // ---- weight-gradient partials: wave -> block (LDS, wave order) -> part[blockIdx] ----
   accw2 += __shfl_xor(accw2, 16, 64);
@@ -485,19 +490,20 @@ RS_API int rs_din_fwd(void* stream, int variant, const float* q, int64_t q_ld, c
   return rs_status_after_launch();
 }
 
-RS_API int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t q_ld,
-                              const float* keys, int64_t k_ss, int64_t k_rs, const float* values,
-                              int64_t v_ss, int64_t v_rs, int64_t B, int T, int H,
-                              const int32_t* lengths, const uint8_t* mask, int64_t mask_ld,
-                              const float* W1, const float* b1, const float* W2, const float* b2,
-                              const float* probs, const float* dout, int64_t dout_ld, float* dq,
-                              int64_t dq_ld, float* dkeys, float* dvalues, int64_t dkv_rs,
-                              int dkv_width, float* dparams, int dparams_accumulate,
-                              float* workspace, int64_t workspace_floats) {
+RS_API int rs_din_bwd_ex(void* stream, int variant, const float* q, int64_t q_ld,
+                         const float* keys, int64_t k_ss, int64_t k_rs, const float* values,
+                         int64_t v_ss, int64_t v_rs, int64_t B, int T, int H,
+                         const int32_t* lengths, const uint8_t* mask, int64_t mask_ld,
+                         const float* W1, const float* b1, const float* W2, const float* b2,
+                         const float* probs, const float* dout, int64_t dout_ld, float* dq,
+                         int64_t dq_ld, const float* dq_base, int64_t dq_base_ld, float* dkeys,
+                         float* dvalues, int64_t dkv_rs, int dkv_width, float* dparams,
+                         int dparams_accumulate, float* workspace, int64_t workspace_floats) {
   int st = din_check(variant, q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T, H);
   if (st) return st;
   if (dkv_rs < H || dkv_width < H || dkv_width > dkv_rs || dkv_width > 2 * H) return RS_ERR_ARG;
   if (!W1 || !b1 || !W2 || !b2 || !dout || !dq || dq_ld % 4 || dq_ld < H) return RS_ERR_ARG;
+  if (dq_base && dq_base_ld < H) return RS_ERR_ARG;
   if (variant == 1 && !probs) return RS_ERR_ARG;
   if (B == 0) return RS_OK;
   const int grid = bwd_grid(B);
@@ -513,15 +519,30 @@ RS_API int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t
   if (variant == 0)
     din_bwd_kernel<0><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld, dq,
                                                   dq_ld, dkeys, dvalues, workspace, dkv_rs,
-                                                  dkv_width);
+                                                  dkv_width, dq_base, dq_base_ld);
   else
     din_bwd_kernel<1><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld, dq,
                                                   dq_ld, dkeys, dvalues, workspace, dkv_rs,
-                                                  dkv_width);
+                                                  dkv_width, dq_base, dq_base_ld);
   st = rs_status_after_launch();
   if (st || !dparams) return st;
   launch_column_reduce(s, workspace, grid, np, np, np, dparams, dparams, dparams_accumulate);
   return rs_status_after_launch();
+}
+
+RS_API int rs_din_bwd_strided(void* stream, int variant, const float* q, int64_t q_ld,
+                              const float* keys, int64_t k_ss, int64_t k_rs, const float* values,
+                              int64_t v_ss, int64_t v_rs, int64_t B, int T, int H,
+                              const int32_t* lengths, const uint8_t* mask, int64_t mask_ld,
+                              const float* W1, const float* b1, const float* W2, const float* b2,
+                              const float* probs, const float* dout, int64_t dout_ld, float* dq,
+                              int64_t dq_ld, float* dkeys, float* dvalues, int64_t dkv_rs,
+                              int dkv_width, float* dparams, int dparams_accumulate,
+                              float* workspace, int64_t workspace_floats) {
+  return rs_din_bwd_ex(stream, variant, q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T, H,
+                       lengths, mask, mask_ld, W1, b1, W2, b2, probs, dout, dout_ld, dq, dq_ld,
+                       nullptr, 0, dkeys, dvalues, dkv_rs, dkv_width, dparams, dparams_accumulate,
+                       workspace, workspace_floats);
 }
 
 RS_API int rs_din_bwd(void* stream, int variant, const float* q, int64_t q_ld, const float* keys,

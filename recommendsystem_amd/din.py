@@ -37,8 +37,13 @@ def _rows_view(t: torch.Tensor) -> torch.Tensor:
 
 
 class _DINFn(torch.autograd.Function):
+    """cat_q: return [pooled, q] [B, 2H] (the pooled rows written by the kernel into the left
+    half); the backward reads d pooled in place and adds the right half's gradient onto the
+    query's (rs_din_bwd_ex dq_base) -- no concat gradient slice copy, no separate sum launch."""
+
     @staticmethod
-    def forward(ctx, q, keys, values, lengths, mask, W1, b1, W2, b2, variant, wide=False):
+    def forward(ctx, q, keys, values, lengths, mask, W1, b1, W2, b2, variant, wide=False,
+                cat_q=False):
         _lib.require_device(q, keys, values, W1)
         q = _rows_view(q)
         keys = _rows_view(keys)
@@ -50,16 +55,22 @@ class _DINFn(torch.autograd.Function):
         same = values is None or values.data_ptr() == keys.data_ptr() and values.shape == keys.shape
         values = keys if same else _rows_view(values)
         B, T, H = keys.shape
-        out = torch.empty(B, H, device=q.device, dtype=torch.float32)
+        if cat_q:
+            buf = torch.empty(B, 2 * H, device=q.device, dtype=torch.float32)
+            buf[:, H:].copy_(q)
+            out, out_ld = buf[:, :H], 2 * H
+        else:
+            buf = out = torch.empty(B, H, device=q.device, dtype=torch.float32)
+            out_ld = H
         probs = torch.empty(B, T, device=q.device, dtype=torch.float32) if variant == 1 else None
         m8 = mask.view(torch.uint8) if mask is not None else None
         call("rs_din_fwd", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys), keys.stride(0),
              keys.stride(1), ptr(values), values.stride(0), values.stride(1), B, T, H, ptr(lengths),
              ptr(m8), m8.stride(0) if m8 is not None else 0, ptr(W1), ptr(b1), ptr(W2), ptr(b2),
-             ptr(out), H, ptr(probs))
+             ptr(out), out_ld, ptr(probs))
         ctx.save_for_backward(q, keys, values, lengths, m8, W1, b1, W2, b2, probs)
-        ctx.variant, ctx.same = variant, same
-        return out
+        ctx.variant, ctx.same, ctx.cat_q = variant, same, cat_q
+        return buf
 
     @staticmethod
     def backward(ctx, dout):
@@ -67,6 +78,7 @@ class _DINFn(torch.autograd.Function):
         variant = ctx.variant
         dout = _rows_view(dout)
         B, T, H = keys.shape
+        base = dout[:, H:] if ctx.cat_q else None
         dev = q.device
         dq = torch.empty(B, H, device=dev, dtype=torch.float32)
         Wd = ctx.wide_w or H
@@ -80,11 +92,12 @@ class _DINFn(torch.autograd.Function):
         dparams = block if in_place else torch.empty(sum(p.numel() for p in params), device=dev)
         if ctx.wide_w and not (ctx.same or variant == 1):
             raise NotImplementedError("wide facts need keys == values")
-        call("rs_din_bwd_strided", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys),
+        call("rs_din_bwd_ex", stream_handle(), variant, ptr(q), q.stride(0), ptr(keys),
              keys.stride(0), keys.stride(1), ptr(values), values.stride(0), values.stride(1), B, T,
              H, ptr(lengths), ptr(m8), m8.stride(0) if m8 is not None else 0, ptr(W1), ptr(b1),
-             ptr(W2), ptr(b2), ptr(probs), ptr(dout), dout.stride(0), ptr(dq), H, ptr(dk), ptr(dv),
-             Wd, Wd, ptr(dparams), 1 if in_place else 0, ptr(ws), ws_n)
+             ptr(W2), ptr(b2), ptr(probs), ptr(dout), dout.stride(0), ptr(dq), H,
+             ptr(base) if base is not None else None, dout.stride(0), ptr(dk), ptr(dv), Wd, Wd,
+             ptr(dparams), 1 if in_place else 0, ptr(ws), ws_n)
         if in_place:
             wgrads = (None, None, None, None)
         else:
@@ -94,8 +107,8 @@ class _DINFn(torch.autograd.Function):
                 off += p.numel()
             wgrads = tuple(outs)
         if ctx.same or variant == 1:
-            return (dq, dk, None, None, None, *wgrads, None, None)
-        return (dq, dk, dv, None, None, *wgrads, None, None)
+            return (dq, dk, None, None, None, *wgrads, None, None, None)
+        return (dq, dk, dv, None, None, *wgrads, None, None, None)
 
 
 class _DINBase(nn.Module):
@@ -138,6 +151,21 @@ class _DINBase(nn.Module):
         return _DINFn.apply(q, keys, values, lengths, mask, self.W1, self.b1, self.W2, self.b2,
                             self.VARIANT)
 
+    def pool_concat(self, q, keys, values=None, lengths=None, mask=None):
+        """torch.cat([pool(q, keys, values, lengths, mask), q], dim=1) with the pooled rows
+        written into the concat by the kernel and the query's two gradients summed inside the
+        backward launch."""
+        from . import ops
+        if ops.custom_ops_enabled() or q.dim() != 2 or keys.dim() != 3:
+            return torch.cat([self._pool(q, keys, values, lengths, mask), q], dim=1)
+        if not self.built:
+            self.build(tuple(keys.shape), device=keys.device)
+        if keys.shape[0] != q.shape[0] or keys.shape[2] != q.shape[1]:
+            raise ValueError(f"expected query [B, H] and keys [B, T, H], got {tuple(q.shape)} and "
+                             f"{tuple(keys.shape)}")
+        return _DINFn.apply(q, keys, values, lengths, mask, self.W1, self.b1, self.W2, self.b2,
+                            self.VARIANT, False, True)
+
 
 class DIN(_DINBase):
     """din.py:6-47.  ``seq_length`` [B] int: positions t >= seq_length[b] get score 0
@@ -151,6 +179,16 @@ class DIN(_DINBase):
         if values.shape != keys.shape:
             raise ValueError("keys and values must have the same shape [B, T, H]")
         return self._pool(queries, keys, values, lengths, None)
+
+    def forward_concat(self, queries, keys, values, seq_length=None):
+        """torch.cat([self(queries, keys, values, seq_length), queries], dim=1) (the config-4
+        head input, din.py's pooled output next to its query) via pool_concat."""
+        lengths = None
+        if seq_length is not None:
+            lengths = seq_length.reshape(-1).to(device=keys.device, dtype=torch.int32).contiguous()
+        if values.shape != keys.shape:
+            raise ValueError("keys and values must have the same shape [B, T, H]")
+        return self.pool_concat(queries, keys, values, lengths, None)
 
 
 class StaytimeDIN(_DINBase):

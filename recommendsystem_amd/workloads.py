@@ -78,8 +78,9 @@ class DINPool(nn.Module):
     def forward(self, qids, hids, hoffs):
         q = self.query(qids.reshape(-1, 1)).reshape(qids.shape[0], -1)          # [B, 16]
         keys, _, lengths = self.hist(hids, hoffs, return_lengths=True)          # [B, T, 16]
-        pooled = self.din(q, keys, keys, lengths)                                # din.py:18-47
-        return self.out(torch.cat([pooled, q], dim=1))
+        # din.py:18-47 pooling, then the head's concat [pooled, q]: the DIN kernel writes into the
+        # concat and sums the query's two gradients in its backward (forward_concat)
+        return self.out(self.din.forward_concat(q, keys, keys, lengths))
 
     def loss(self, qids, hids, hoffs, labels):
         return cross_entropy_sum(labels, self.forward(qids, hids, hoffs))

@@ -182,3 +182,31 @@ def test_sequence_lookup_and_push(hash_mode):
     untouched = np.setdiff1d(np.arange(table.rows), rows)
     assert np.array_equal(table.weight.cpu().numpy()[untouched], w[untouched])
     assert int(table.n_touched[0].item()) == 0 and bool((table.flag == -1).all())
+
+
+@pytest.mark.parametrize("B,T", [(37, 23), (1024, 100)])
+def test_din_forward_concat_matches_cat(B, T):
+    """DIN.forward_concat == torch.cat([DIN(q, k, k, lens), q], 1): the same output, and the same
+    gradients for q (its two shares summed inside rs_din_bwd_ex), keys and the weights."""
+    from recommendsystem_amd import DIN
+    rng = np.random.default_rng(7 + B)
+    q, k, _ = _inputs(rng, B, T)
+    lens = rng.integers(1, T + 1, size=B).astype(np.int32)
+    layer = DIN(seed=3)
+    layer.build((B, T, 16), device=DEV)
+    R = torch.from_numpy(rng.normal(size=(B, 32)).astype(np.float32)).to(DEV)
+    outs, grads = [], []
+    for fused in (False, True):
+        qd = torch.from_numpy(q).to(DEV).requires_grad_(True)
+        kd = torch.from_numpy(k).to(DEV).requires_grad_(True)
+        ld = torch.from_numpy(lens).to(DEV)
+        for p in (layer.W1, layer.b1, layer.W2, layer.b2):
+            p.grad = None
+        y = layer.forward_concat(qd, kd, kd, ld) if fused else torch.cat([layer(qd, kd, kd, ld), qd], 1)
+        (y * R).sum().backward()
+        outs.append(to_np(y))
+        grads.append([to_np(qd.grad), to_np(kd.grad)] + [to_np(p.grad) for p in (layer.W1, layer.b1, layer.W2, layer.b2)])
+    assert np.array_equal(outs[0], outs[1])
+    for a, b in zip(grads[0], grads[1]):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+
