@@ -427,8 +427,329 @@ __global__ void __launch_bounds__(64 * WPB) din_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split form: TWO waves per sample (a block = 2 samples), wave half h taking the 16-position steps
+// t0 = 16 (2 c + h): each wave's dependent chain of steps is half as long (the one-wave form is
+// latency-bound at one wave per SIMD for config 4).  The halves meet through LDS: the softmax max
+// and sum (VAR 1), the pooled partial sums, and in the backward sum_t p_t dp_t (VAR 1) and the
+// per-sample G / gsum partials, which half 0 combines (in half order) for dq and the weight
+// accumulators.  Every wave of a block runs the same number of sample iterations and barriers.
+// ---------------------------------------------------------------------------------------------
+template <int VAR>
+__global__ void __launch_bounds__(64 * WPB) din_fwd_split_kernel(
+    Geo geo, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ out,
+    int64_t out_ld, float* __restrict__ probs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int l = lane_id(), g = l >> 4, j = l & 15, w = wave_id(), pr = w >> 1, hf = w & 1;
+  const int T = geo.T;
+  float* sbuf = smem + pr * T;              // VAR 1: the pair's scores
+  float* xo = smem + 2 * T + pr * 24;       // [16] half 1's pooled partial, [16..17] max, [18..19] sum
+  Frags<VAR> fr;
+  fr.load(W1, b1, W2, b2);
+  const int64_t per_it = (int64_t)gridDim.x * 2;
+  const int64_t n_it = (geo.B + per_it - 1) / per_it;
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int64_t b = it * per_it + (int64_t)blockIdx.x * 2 + pr;
+    const bool live = b < geo.B;
+    const int64_t bb = live ? b : 0;
+    SampleW<VAR> sw;
+    sw.build(fr, geo.q + bb * geo.q_ld);
+    const float* krow0 = geo.k + bb * geo.k_ss;
+    const float* vrow0 = geo.v + bb * geo.v_ss;
+    const int len = geo.lengths ? min(geo.lengths[bb], T) : T;
+    float o = 0.f, mx = -INFINITY;
+    if (live) {
+      float4 an = load_keys(krow0, geo.k_rs, 16 * hf, T);
+      Vals vn{};
+      if (VAR == 0) vn = load_vals(vrow0, geo.v_rs, 16 * hf, T);
+      for (int t0 = 16 * hf; t0 < T; t0 += 32) {
+        const float4 a = an;
+        const Vals vc = vn;
+        if (t0 + 32 < T) {
+          an = load_keys(krow0, geo.k_rs, t0 + 32, T);
+          if (VAR == 0) vn = load_vals(vrow0, geo.v_rs, t0 + 32, T);
+        }
+        const f32x4 acc = layer1_frag(a, sw.bw);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z1 = acc[r] + sw.c;
+          const float h = VAR == 0 ? fmaxf(z1, 0.f) : sigm(z1);
+          const float z2 = group_sum<16>(h * fr.w2) + fr.b2;
+          const int t = t0 + 4 * g + r;
+          if (t < T) {
+            const bool on = pos_on(geo, bb, t, len);
+            if (VAR == 0) {
+              o = fmaf(on ? fmaxf(z2, 0.f) : 0.f, vc.v[r], o);
+            } else {
+              const float sc = on ? z2 : PAD;
+              mx = fmaxf(mx, sc);
+              if (j == 0) sbuf[t] = sc;
+            }
+          }
+        }
+      }
+    }
+    float inv = 1.f;
+    if (VAR == 1) {
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (l == 0) xo[16 + hf] = mx;
+      __syncthreads();  // both halves' scores and maxima
+      mx = fmaxf(xo[16], xo[17]);
+      float lsum = 0.f;
+      if (live) {
+        Vals fn = load_vals(vrow0, geo.v_rs, 16 * hf, T);
+        for (int t0 = 16 * hf; t0 < T; t0 += 32) {
+          const Vals fc = fn;
+          if (t0 + 32 < T) fn = load_vals(vrow0, geo.v_rs, t0 + 32, T);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + 4 * g + r;
+            if (t < T) {
+              const float e = __expf(sbuf[t] - mx);
+              lsum += e;
+              o = fmaf(e, fc.v[r], o);
+            }
+          }
+        }
+      }
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+      if (l == 0) xo[18 + hf] = lsum;
+    }
+    o += __shfl_xor(o, 16, 64);
+    o += __shfl_xor(o, 32, 64);
+    if (hf == 1 && g == 0) xo[j] = o;
+    __syncthreads();  // half 1's partials (and both sums)
+    if (VAR == 1) inv = 1.0f / (xo[18] + xo[19]);
+    if (live && hf == 0 && g == 0) out[b * out_ld + j] = (o + xo[j]) * inv;
+    if (VAR == 1 && live && probs) {
+      for (int t = l + 64 * hf; t < T; t += 128) probs[b * T + t] = __expf(sbuf[t] - mx) * inv;
+    }
+    __syncthreads();  // sbuf / exchange reuse
+  }
+}
+
+template <int VAR>
+__global__ void __launch_bounds__(64 * WPB) din_bwd_split_kernel(
+    Geo geo, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ probs,
+    const float* __restrict__ dout, int64_t dout_ld, float* __restrict__ dq, int64_t dq_ld,
+    float* __restrict__ dk, float* __restrict__ dv, float* __restrict__ part, int64_t dkv_rs,
+    int dkv_pad, const float* __restrict__ dq_base, int64_t dqb_ld) {
+  constexpr int NP = nparam(VAR);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int l = lane_id(), g = l >> 4, j = l & 15, w = wave_id(), pr = w >> 1, hf = w & 1;
+  const int T = geo.T;
+  float* tt = smem + w * (16 * TT_LD);                      // [16][TT_LD] transpose tile
+  float* sbuf = smem + WPB * 16 * TT_LD + pr * T;           // VAR 1: the pair's dp_t
+  float* xg = smem + WPB * 16 * TT_LD + 2 * T + pr * (64 * 5 + 4);  // [64][5] half 1, [320..] sdp
+  float* red = smem;                                        // [WPB][NP], aliases the above at the end
+  const bool alias_kv = geo.k == geo.v;
+  const bool alias_d = dk != nullptr && dk == dv;
+  Frags<VAR> fr;
+  fr.load(W1, b1, W2, b2);
+  float accA[4] = {0.f, 0.f, 0.f, 0.f}, accG[4] = {0.f, 0.f, 0.f, 0.f};
+  float accQG[4] = {0.f, 0.f, 0.f, 0.f};
+  float accb1 = 0.f, accw2 = 0.f, accb2 = 0.f;
+  const int64_t per_it = (int64_t)gridDim.x * 2;
+  const int64_t n_it = (geo.B + per_it - 1) / per_it;
+  for (int64_t it = 0; it < n_it; ++it) {
+    const int64_t b = it * per_it + (int64_t)blockIdx.x * 2 + pr;
+    const bool live = b < geo.B;
+    const int64_t bb = live ? b : 0;
+    SampleW<VAR> sw;
+    const float* qrow = geo.q + bb * geo.q_ld;
+    sw.build(fr, qrow);
+    const float qi = qrow[j];
+    float tb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tb[r] = fmaf(qi, fr.tqk[r], fr.tk[r]);  // W1'[j][4g + r]
+    const float* krow0 = geo.k + bb * geo.k_ss;
+    const float* vrow0 = geo.v + bb * geo.v_ss;
+    const int len = geo.lengths ? min(geo.lengths[bb], T) : T;
+    const float doj = dout[bb * dout_ld + j];
+    const float* prow = VAR == 1 ? probs + bb * T : nullptr;
+    float sdp = 0.f;
+    if (VAR == 1) {  // pass 1: dp_t = dout . f_t over this half's steps, sum_t p_t dp_t
+      if (live) {
+        Vals fn = load_vals(vrow0, geo.v_rs, 16 * hf, T);
+        for (int t0 = 16 * hf; t0 < T; t0 += 32) {
+          const Vals fc = fn;
+          if (t0 + 32 < T) fn = load_vals(vrow0, geo.v_rs, t0 + 32, T);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = t0 + 4 * g + r;
+            const float dp = group_sum<16>(doj * fc.v[r]);
+            if (t < T) {
+              sdp = fmaf(prow[t], dp, sdp);
+              if (j == 0) sbuf[t] = dp;
+            }
+          }
+        }
+      }
+      sdp += __shfl_xor(sdp, 16, 64);
+      sdp += __shfl_xor(sdp, 32, 64);
+      if (l == 0) xg[320 + hf] = sdp;
+      __syncthreads();
+      sdp = xg[320] + xg[321];
+    }
+    f32x4 G = {0.f, 0.f, 0.f, 0.f};
+    float gs = 0.f;
+    if (live) {
+      float4 an = load_keys(krow0, geo.k_rs, 16 * hf, T);
+      Vals vn = load_vals(vrow0, geo.v_rs, 16 * hf, T);
+      for (int t0 = 16 * hf; t0 < T; t0 += 32) {
+        const float4 a = an;
+        const Vals vc = vn;
+        if (t0 + 32 < T) {
+          an = load_keys(krow0, geo.k_rs, t0 + 32, T);
+          vn = load_vals(vrow0, geo.v_rs, t0 + 32, T);
+        }
+        const f32x4 acc = layer1_frag(a, sw.bw);
+        float dz1[4], kv[4], dvv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = t0 + 4 * g + r;
+          const bool in = t < T;
+          const float z1 = acc[r] + sw.c;
+          const float h = VAR == 0 ? fmaxf(z1, 0.f) : sigm(z1);
+          const bool on = in && pos_on(geo, bb, t, len);
+          float dz2, vval;
+          if (VAR == 0) {
+            const float z2 = group_sum<16>(h * fr.w2) + fr.b2;
+            vval = vc.v[r];
+            const float ds = group_sum<16>(doj * vval);
+            const float s = on ? fmaxf(z2, 0.f) : 0.f;
+            dz2 = (on && z2 > 0.f) ? ds : 0.f;
+            dvv[r] = s * doj;
+            kv[r] = alias_kv ? vval : (in ? krow0[(int64_t)t * geo.k_rs + j] : 0.f);
+            dz1[r] = h > 0.f ? dz2 * fr.w2 : 0.f;
+          } else {
+            const float p = in ? prow[t] : 0.f;
+            dz2 = on ? p * (sbuf[in ? t : 0] - sdp) : 0.f;
+            vval = vc.v[r];
+            dvv[r] = p * doj;
+            kv[r] = vval;
+            dz1[r] = dz2 * fr.w2 * h * (1.0f - h);
+          }
+          accw2 = fmaf(h, dz2, accw2);
+          if (j == 0) accb2 += dz2;
+          gs += dz1[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) G = mfma4(kv[r], dz1[r], G);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tt[(4 * g + r) * TT_LD + j] = dz1[r];
+        wave_lds_sync();
+        const float4 az = *reinterpret_cast<const float4*>(tt + (l & 15) * TT_LD + 4 * g);
+        wave_lds_sync();
+        f32x4 DK = {0.f, 0.f, 0.f, 0.f};
+        DK = mfma4(az.x, tb[0], DK);
+        DK = mfma4(az.y, tb[1], DK);
+        DK = mfma4(az.z, tb[2], DK);
+        DK = mfma4(az.w, tb[3], DK);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = t0 + 4 * g + r;
+          if (t < T) {
+            const int64_t off = (b * T + t) * dkv_rs + j;
+            const bool zpad = j + HD < dkv_pad;
+            if (VAR == 1 || alias_d) {
+              float* base = dk ? dk : dv;
+              if (base) {
+                base[off] = DK[r] + dvv[r];
+                if (zpad) base[off + HD] = 0.f;
+              }
+            } else {
+              if (dk) { dk[off] = DK[r]; if (zpad) dk[off + HD] = 0.f; }
+              if (dv) { dv[off] = dvv[r]; if (zpad) dv[off + HD] = 0.f; }
+            }
+          }
+        }
+      }
+    }
+    gs += __shfl_xor(gs, 16, 64);
+    gs += __shfl_xor(gs, 32, 64);  // this half's gsum_j, in every lane of column j
+    if (hf == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xg[l * 5 + r] = G[r];
+      xg[l * 5 + 4] = gs;
+    }
+    __syncthreads();  // half 1's G / gsum
+    if (hf == 0 && live) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) G[r] += xg[l * 5 + r];
+      gs += xg[l * 5 + 4];
+      float dqv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dqv[r] = group_sum<16>(fmaf(fr.rq[r], gs, fr.rqk[r] * G[r]));
+        accA[r] = fmaf(sw.qv[r], gs, accA[r]);
+        accG[r] += G[r];
+        accQG[r] = fmaf(sw.qv[r], G[r], accQG[r]);
+      }
+      if (g == 0) accb1 += gs;
+      if (j == 0) {
+        if (dq_base) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dqv[r] += dq_base[b * dqb_ld + 4 * g + r];
+        }
+        *reinterpret_cast<float4*>(dq + b * dq_ld + 4 * g) = make_float4(dqv[0], dqv[1], dqv[2], dqv[3]);
+      }
+    }
+    __syncthreads();  // exchange / sbuf reuse
+  }
+  // ---- weight-gradient partials: wave -> block (LDS, wave order) -> part[blockIdx] ----
+  accw2 += __shfl_xor(accw2, 16, 64);
+  accw2 += __shfl_xor(accw2, 32, 64);
+  accb2 += __shfl_xor(accb2, 16, 64);
+  accb2 += __shfl_xor(accb2, 32, 64);
+  __syncthreads();
+  float* mine = red + w * NP;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * g + r;
+    mine[(0 * HD + i) * D1 + j] = accA[r];
+    mine[(1 * HD + i) * D1 + j] = accG[r];
+    if (VAR == 0) {
+      mine[(2 * HD + i) * D1 + j] = accQG[r];
+    } else {
+      mine[(2 * HD + i) * D1 + j] = accA[r] - accG[r];
+      mine[(3 * HD + i) * D1 + j] = accQG[r];
+    }
+  }
+  constexpr int OB = nblk(VAR) * HD * D1;
+  if (g == 0) {
+    mine[OB + j] = accb1;
+    mine[OB + D1 + j] = accw2;
+  }
+  if (l == 0) mine[OB + 2 * D1] = accb2;
+  __syncthreads();
+  for (int c = threadIdx.x; c < NP; c += blockDim.x) {
+    float s = red[c];
+#pragma unroll
+    for (int ww = 1; ww < WPB; ++ww) s += red[ww * NP + c];
+    part[(int64_t)blockIdx.x * NP + c] = s;
+  }
+}
+
+// Two waves per sample while one wave per sample would leave fewer than two waves per SIMD
+// (B < 2048 on 1024 SIMDs): config 4 (B = 1024, T = 100) 0.0998 -> 0.0975 ms; at config 5
+// (B = 2048, T = 50) the split measured 1.780 -> 1.797 ms (twice the partial rows, and the chip
+// already holds two waves per SIMD), profiles/r05/split_ab/.  Tuning runs: RS_DIN_SPLIT=0 / 1.
+static bool din_split(int64_t B) {
+  static const int mode = [] {
+    const char* e = getenv("RS_DIN_SPLIT");
+    return e && *e ? atoi(e) : -1;
+  }();
+  return mode >= 0 ? mode != 0 : B < 2048;
+}
+
 static int fwd_grid(int64_t B) {
-  int64_t g = (B + WPB - 1) / WPB;
+  const int spb = din_split(B) ? WPB / 2 : WPB;  // samples per block
+  int64_t g = (B + spb - 1) / spb;
   return (int)(g > 4096 ? 4096 : g);
 }
 static int bwd_grid(int64_t B) {
@@ -439,7 +760,8 @@ static int bwd_grid(int64_t B) {
     const char* e = getenv("RS_DIN_BWD_SPW");
     return e && atoi(e) > 0 ? atoi(e) : 1;
   }();
-  int64_t g = (B + spw * WPB - 1) / (spw * WPB);
+  const int64_t spb = din_split(B) ? WPB / 2 : (int64_t)spw * WPB;  // samples per block
+  int64_t g = (B + spb - 1) / spb;
   if (g > 1024) g = 1024;
   return (int)(g < 1 ? 1 : g);
 }
@@ -482,6 +804,16 @@ RS_API int rs_din_fwd(void* stream, int variant, const float* q, int64_t q_ld, c
   if (B == 0) return RS_OK;
   Geo geo{q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T, lengths, mask, mask_ld};
   hipStream_t s = rs_stream(stream);
+  if (din_split(B)) {
+    const size_t lds = ((size_t)2 * T + 48) * 4;
+    if (variant == 0)
+      din_fwd_split_kernel<0><<<fwd_grid(B), 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, out, out_ld,
+                                                                 probs);
+    else
+      din_fwd_split_kernel<1><<<fwd_grid(B), 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, out, out_ld,
+                                                                 probs);
+    return rs_status_after_launch();
+  }
   const size_t lds = variant == 1 ? (size_t)WPB * T * 4 : 0;
   if (variant == 0)
     din_fwd_kernel<0><<<fwd_grid(B), 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, out, out_ld, probs);
@@ -511,12 +843,22 @@ RS_API int rs_din_bwd_ex(void* stream, int variant, const float* q, int64_t q_ld
   if (dparams && (!workspace || workspace_floats < (int64_t)grid * np)) return RS_ERR_ARG;
   Geo geo{q, q_ld, keys, k_ss, k_rs, values, v_ss, v_rs, B, T, lengths, mask, mask_ld};
   hipStream_t s = rs_stream(stream);
-  size_t lds = ((size_t)WPB * 16 * TT_LD + (variant == 1 ? (size_t)WPB * T : 0)) * 4;
+  const bool split = din_split(B);
+  size_t lds = split ? ((size_t)WPB * 16 * TT_LD + 2 * (size_t)T + 2 * (64 * 5 + 4)) * 4
+                     : ((size_t)WPB * 16 * TT_LD + (variant == 1 ? (size_t)WPB * T : 0)) * 4;
   const size_t red = (size_t)WPB * np * 4;
   if (lds < red) lds = red;
   // without dparams the partials still need somewhere to go: the caller must pass a workspace
   if (!workspace || workspace_floats < (int64_t)grid * np) return RS_ERR_ARG;
-  if (variant == 0)
+  if (split && variant == 0)
+    din_bwd_split_kernel<0><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld,
+                                                        dq, dq_ld, dkeys, dvalues, workspace,
+                                                        dkv_rs, dkv_width, dq_base, dq_base_ld);
+  else if (split)
+    din_bwd_split_kernel<1><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld,
+                                                        dq, dq_ld, dkeys, dvalues, workspace,
+                                                        dkv_rs, dkv_width, dq_base, dq_base_ld);
+  else if (variant == 0)
     din_bwd_kernel<0><<<grid, 64 * WPB, lds, s>>>(geo, W1, b1, W2, b2, probs, dout, dout_ld, dq,
                                                   dq_ld, dkeys, dvalues, workspace, dkv_rs,
                                                   dkv_width, dq_base, dq_base_ld);
