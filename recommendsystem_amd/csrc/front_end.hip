@@ -479,23 +479,24 @@ struct SumSrc {
   int64_t ld[kMaxSumSrc];
 };
 
+// 2-D grid: a thread owns one output column c (its nsrc map entries in registers) and walks rows
+// b = blockIdx.y, + gridDim.y, ... (the flat form paid a 64-bit division and nsrc map loads per
+// element: 33.5 us for config 5's 2048 x 2912 d_emb).
 __global__ void __launch_bounds__(kBlk) gather_sum_cols_kernel(SumSrc src, int nsrc,
                                                                const int32_t* __restrict__ map,
                                                                int64_t B, int ncols,
                                                                float* __restrict__ out,
                                                                int64_t out_ld) {
-  const int64_t n = B * ncols;
-  for (int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlk) {
-    const int64_t b = i / ncols;
-    const int c = (int)(i - b * ncols);
+  const int c = blockIdx.x * kBlk + threadIdx.x;
+  if (c >= ncols) return;
+  int32_t sc[kMaxSumSrc];
+#pragma unroll
+  for (int k = 0; k < kMaxSumSrc; ++k) sc[k] = k < nsrc ? map[(int64_t)k * ncols + c] : -1;
+  for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < kMaxSumSrc; ++k) {
-      if (k < nsrc) {
-        const int32_t sc = map[(int64_t)k * ncols + c];
-        if (sc >= 0) v += src.p[k][b * src.ld[k] + sc];
-      }
-    }
+    for (int k = 0; k < kMaxSumSrc; ++k)
+      if (sc[k] >= 0) v += src.p[k][b * src.ld[k] + sc[k]];
     out[b * out_ld + c] = v;
   }
 }
@@ -514,7 +515,11 @@ RS_API int rs_gather_sum_columns(void* stream, int nsrc, const float* const* src
     s.ld[k] = src_lds[k];
   }
   if (B * ncols == 0) return RS_OK;
-  gather_sum_cols_kernel<<<grid_for(B * ncols), kBlk, 0, rs_stream(stream)>>>(s, nsrc, map, B,
-                                                                              ncols, out, out_ld);
+  const unsigned gx = (unsigned)((ncols + kBlk - 1) / kBlk);
+  int64_t gy = (2048 + gx - 1) / gx;  // ~2048 blocks in all
+  if (gy > B) gy = B;
+  if (gy > 65535) gy = 65535;
+  gather_sum_cols_kernel<<<dim3(gx, (unsigned)gy), kBlk, 0, rs_stream(stream)>>>(s, nsrc, map, B,
+                                                                                 ncols, out, out_ld);
   return rs_status_after_launch();
 }

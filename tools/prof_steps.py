@@ -16,7 +16,8 @@ import sys
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)                 # drop the argument list
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)                    # drop the argument list
     n = re.sub(r"<.*", "", n) if n.count("<") > 2 else n
     return n[:90]
 
