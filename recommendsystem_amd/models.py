@@ -661,8 +661,9 @@ class StaytimeMTL(nn.Module):
                           cfg.num_experts, 0)                                       # :153-164
         Hh = cfg.hidden_units[-1]
         mmoe = split_cols(mm, [Hh] * cfg.num_tasks)
-        cross = self.dcn(concated)                                                  # :167
-        ext = torch.cat([mmoe[0], cross], dim=1)                                    # :168
+        # :167-168 cross = DeepCrossLayer(concated); ext = concat([mmoe[0], cross]): the cross
+        # kernel writes into ext directly
+        ext = self.dcn.forward_concat(mmoe[0], concated)
         dl = grouped_dense(self.deep_logit, [mmoe[1], mmoe[2]])
         short, long_ = grouped_dense(self.task_out, [torch.cat([fm_logit, dl[0]], dim=1),  # :182-185
                                                      torch.cat([fm_logit, dl[1]], dim=1)])  # :188-191

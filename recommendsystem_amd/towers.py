@@ -275,22 +275,31 @@ class PLE(nn.Module):
 # CrossNet / DeepCrossLayer
 # ============================================================================================
 class _CrossFn(torch.autograd.Function):
+    """lead [M, Dl] (optional): return the concat [lead, y] [M, Dl + D] with y written in place by
+    the kernel (ldy) and its gradient read from the concat's slice (lddy) -- no concat copy."""
+
     @staticmethod
-    def forward(ctx, x, W, b, L):
+    def forward(ctx, x, W, b, L, lead=None):
         _lib.require_device(x, W)
         x = _rows(x)
         M, D = x.shape
-        y = torch.empty(M, D, device=x.device, dtype=torch.float32)
-        call("rs_cross_fwd", stream_handle(), ptr(x), x.stride(0), M, D, L, ptr(W), ptr(b), ptr(y), D)
+        Dl = 0 if lead is None else lead.shape[1]
+        out = torch.empty(M, Dl + D, device=x.device, dtype=torch.float32)
+        if lead is not None:
+            out[:, :Dl].copy_(lead)
+        call("rs_cross_fwd", stream_handle(), ptr(x), x.stride(0), M, D, L, ptr(W), ptr(b),
+             out.data_ptr() + 4 * Dl, Dl + D)
         ctx.save_for_backward(x, W, b)
-        ctx.L = L
-        return y
+        ctx.L, ctx.Dl = L, Dl
+        return out
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dout):
         x, W, b = ctx.saved_tensors
-        L = ctx.L
-        dy = _row_major(dy)
+        L, Dl = ctx.L, ctx.Dl
+        dout = _row_major(dout)
+        d_lead = dout[:, :Dl] if Dl else None
+        dy = dout[:, Dl:] if Dl else dout
         M, D = x.shape
         dx = torch.empty(M, D, device=x.device, dtype=torch.float32)
         ws_n = int(_lib.load().rs_cross_bwd_workspace_floats(M, D, L))
@@ -300,9 +309,9 @@ class _CrossFn(torch.autograd.Function):
         call("rs_cross_bwd", stream_handle(), ptr(x), x.stride(0), M, D, L, ptr(W), ptr(b), ptr(dy),
              dy.stride(0), ptr(dx), D, 0, ptr(dpar), 1 if block is not None else 0, ptr(ws), ws_n)
         if block is not None:
-            return dx, None, None, None
+            return dx, None, None, None, d_lead
         dW, db = _split_grads((W, b), dpar)
-        return dx, dW, db, None
+        return dx, dW, db, None, d_lead
 
 
 class _CrossBase(nn.Module):
@@ -332,6 +341,15 @@ class _CrossBase(nn.Module):
         if not self.built:
             self.build(tuple(inputs.shape), device=inputs.device)
         return _CrossFn.apply(inputs, self.W, self.b, self.layer_num)
+
+    def forward_concat(self, lead, inputs):
+        """torch.cat([lead, self(inputs)], dim=1) with the cross output written into the concat
+        (staytime/VideoDnn.py:168 ext = concat([mmoe[0], cross]))."""
+        if inputs.dim() != 2 or lead.dim() != 2:
+            raise ValueError("cross layers take 2-D inputs [batch, dim]")
+        if not self.built:
+            self.build(tuple(inputs.shape), device=inputs.device)
+        return _CrossFn.apply(inputs, self.W, self.b, self.layer_num, lead.float())
 
 
 class CrossNet(_CrossBase):

@@ -119,6 +119,29 @@ def test_cross_layers(kind, D, L, M):
     _check(out, ref, [(x, xc, "dx"), (layer.W, Wc, "dW"), (layer.b, bc, "db")], R, 2e-5)
 
 
+def test_cross_forward_concat_matches_cat():
+    """DeepCrossLayer.forward_concat(lead, x) == torch.cat([lead, layer(x)], 1): output and the
+    gradients of lead, x, W and b (the layer writes into / reads from the concat in place)."""
+    from recommendsystem_amd.towers import DeepCrossLayer
+    rng = np.random.default_rng(21)
+    M, D, Dl, L = 300, 1712, 128, 3
+    layer = DeepCrossLayer(num_layer=L)
+    layer.build((M, D), device=DEV)
+    _randomise([layer.W, layer.b], rng, 0.05)
+    R = torch.from_numpy(rng.normal(size=(M, Dl + D)).astype(np.float32)).to(DEV)
+    res = []
+    for fused in (False, True):
+        x = torch.from_numpy(_x(np.random.default_rng(5), M, D, scale=0.2)).to(DEV).requires_grad_(True)
+        lead = torch.from_numpy(_x(np.random.default_rng(6), M, Dl)).to(DEV).requires_grad_(True)
+        layer.W.grad = None
+        layer.b.grad = None
+        y = layer.forward_concat(lead, x) if fused else torch.cat([lead, layer(x)], 1)
+        (y * R).sum().backward()
+        res.append([to_np(y), to_np(x.grad), to_np(lead.grad), to_np(layer.W.grad), to_np(layer.b.grad)])
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_cross_bwd_accumulates():
     """rs_cross_bwd with dx_accumulate = dparams_accumulate = 1 adds onto what is there."""
     from recommendsystem_amd import _lib
