@@ -2,7 +2,7 @@
 // workspace per process, created on the first eligible call (an eager step: graph capture
 // replays the plans a warm-up step made); one plan per (shape, layout, epilogue): matmul
 // descriptor, four matrix layouts and an algorithm, cached.  The algorithm is the fastest of the
-// heuristic's top candidates, each timed on scratch operands of the plan's shape on a private
+// heuristic's top candidates (32; RS_GEMM_BLAS_CANDS), each timed on scratch operands of the plan's shape on a private
 // stream when the plan is made outside a graph capture (the heuristic's first pick otherwise, or
 // with RS_GEMM_BLAS_TUNE=0).  The bias pointer is set on the cached descriptor per call
 // (host-side attribute; a captured launch keeps the one it was recorded with).
@@ -52,6 +52,12 @@ bool init_locked(Ctx& c) {
   }
   c.ok = true;
   return true;
+}
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  if (!e || !*e) return dflt;
+  return (int64_t)strtoll(e, nullptr, 10);
 }
 
 // Times each usable candidate (1 warm-up + 5 timed runs) on zero-filled scratch operands of the
@@ -125,10 +131,14 @@ Plan make_plan(Ctx& c, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_
   const uint64_t wsb = kWsBytes;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                         sizeof(wsb));
-  constexpr int kCand = 8;
+  constexpr int kCand = 32;
+  static const int ncand = [] {  // tuning runs: RS_GEMM_BLAS_CANDS (candidates timed)
+    const int64_t v = env_i64("RS_GEMM_BLAS_CANDS", 32);
+    return (int)(v < 1 ? 1 : (v > kCand ? kCand : v));
+  }();
   hipblasLtMatmulHeuristicResult_t res[kCand];
   int got = 0;
-  const int want = tune ? kCand : 1;
+  const int want = tune ? ncand : 1;
   const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.d, p.d, pref,
                                                              want, res, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
@@ -142,12 +152,6 @@ Plan make_plan(Ctx& c, bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_
   p.algo = res[best].algo;
   p.ok = true;
   return p;
-}
-
-int64_t env_i64(const char* name, int64_t dflt) {
-  const char* e = getenv(name);
-  if (!e || !*e) return dflt;
-  return (int64_t)strtoll(e, nullptr, 10);
 }
 
 }  // namespace
