@@ -540,6 +540,7 @@ __global__ void __launch_bounds__(256) fm_fwd_kernel(FM a, float* __restrict__ Y
   for (int64_t m = (int64_t)blockIdx.x * 4 + wave_id(); m < a.M; m += (int64_t)gridDim.x * 4) {
     float S = 0.f, Q = 0.f;
     if (e < a.E) {
+#pragma unroll 8
       for (int f = fg; f < a.F; f += NG) {
         float y = a.X[m * a.ldx + (int64_t)f * a.fsx + e];
         if (a.A) y *= a.as * a.A[m * a.lda + f];
