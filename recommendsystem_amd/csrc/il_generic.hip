@@ -28,7 +28,9 @@
 // request is RS_ERR_UNSUPPORTED).
 #include "il_kernels.hpp"
 
+#include <map>
 #include <mutex>
+#include <vector>
 
 namespace rs_il {
 namespace gen {
@@ -464,30 +466,31 @@ GArgs make_args(int64_t B, int F, int E, int U, int H, int L, int use_res, float
 }
 
 // GS (global-scratch) mode: workgroups of the grid, and the scratch slab shared by every GS launch
-// of the process (one stream at a time, like the launches themselves).  Grown only outside graph
-// capture (a captured step replays the size its eager warm-up established).
+// of the process on one device (one stream at a time, like the launches themselves).  Grown only
+// outside graph capture (a captured step replays the size its eager warm-up established).  A slab
+// is never freed: a graph captured earlier keeps its address baked in, so growing allocates a new
+// (geometrically larger) slab and retires the old one for the life of the process.
 constexpr int64_t kGsGrid = 256;
 
 float* gs_scratch(size_t floats, hipStream_t s) {
+  struct Slab { float* buf = nullptr; size_t cap = 0; std::vector<float*> retired; };
   static std::mutex mu;
-  static float* buf = nullptr;
-  static size_t cap = 0;
+  static std::map<int, Slab> slabs;  // keyed by device
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lk(mu);
-  if (floats <= cap) return buf;
+  Slab& sl = slabs[dev];
+  if (floats <= sl.cap) return sl.buf;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  if (buf) {
-    if (hipDeviceSynchronize() != hipSuccess) return nullptr;  // (in-flight GS launches)
-    hipFree(buf);
-    buf = nullptr;
-    cap = 0;
-  }
-  if (hipMalloc(&buf, floats * sizeof(float)) != hipSuccess) {
-    buf = nullptr;
-    return nullptr;
-  }
-  cap = floats;
-  return buf;
+  size_t want = sl.cap ? 2 * sl.cap : floats;
+  if (want < floats) want = floats;
+  float* nb = nullptr;
+  if (hipMalloc(&nb, want * sizeof(float)) != hipSuccess) return nullptr;
+  if (sl.buf) sl.retired.push_back(sl.buf);  // still referenced by captured graphs: kept
+  sl.buf = nb;
+  sl.cap = want;
+  return sl.buf;
 }
 
 }  // namespace gen

@@ -1959,27 +1959,55 @@ constexpr bool kSaved4 = kLnPair<C> && C::H * C::FMAX <= 64;
 #define RS_PRAGMA_(x) _Pragma(#x)
 #define RS_UNROLL(n) RS_PRAGMA_(unroll n)
 
+// RS_IL4_ROT (round 6): three rotating buffers instead of two + DY, so the next iteration's input
+// is issued right after the LN backward (when the dy it replaces is consumed) instead of after the
+// K-pass; dq stays in registers through the K-pass; the push rows come to registers
+#ifndef RS_IL4_ROT
+#define RS_IL4_ROT 1
+#endif
+// static priority (cdna guide "two waves per SIMD", item 4): the wave in an odd SIMD slot runs at
+// s_setprio 1, so the two co-resident waves stop trading VALU issue slot by slot (same box, 300
+// steps x 3: IL backward 78.4 -> 77.9 us, profiles/r06/rot/)
+#ifndef RS_IL4_PRIO
+#define RS_IL4_PRIO 1
+#endif
 template <class C>
 struct Bwd4Layout {
-  int ba, bb, pr, dy, pm, st, rows, sv, per_wave;
+  int ba, bb, bc, pr, dy, pm, st, rows, sv, per_wave;
   __host__ __device__ Bwd4Layout(int F) {
     sv = (int)small_save_stride(F, C::U, C::H);
     const int xe = F * C::E;
-    const int xo = ((xe > sv ? xe : sv) + 3) & ~3;
+    const int f16 = (F + 15) & ~15;
+    int xo = ((xe > sv ? xe : sv) + 3) & ~3;
+#if RS_IL4_ROT
+    // a buffer also takes the dx rows of iterations > 0 (exact F: all 16 * ceil(F / 16) rows)
+    const int dyr = (C::EXACT ? f16 : F) * C::U;
+    if (xo < dyr) xo = (dyr + 3) & ~3;
+#endif
     int off = 0;
     ba = off; off += xo;
     bb = off; off += xo;
+#if RS_IL4_ROT
+    bc = off; off += xo;
+#else
+    bc = 0;
+#endif
     // PR's rows F .. 16 * ceil(F / 16) - 1 (written by the unguarded projection stores) land in
     // PM, dead at the projections; DY's (the dx rows of iterations > 0) land in ST / RW / pad,
     // dead in P7 of those iterations
-    const int f16 = (F + 15) & ~15;
     pr = off; off += (C::FMAX * C::PRS + 3) & ~3;
     pm = off; off += (C::H * F * C::PMS + 3) & ~3;
+#if RS_IL4_ROT
+    dy = 0;
+    st = off; off += (C::H * F + 3) & ~3;     // D_i per (head, row)
+    rows = off; off += (F + 3) & ~3;          // the Q-pass's dead-lane P stores
+#else
     dy = off; off += (F * C::U + 3) & ~3;
     st = off; off += (C::H * F + 3) & ~3;     // D_i per (head, row)
     rows = off; off += (F + 3) & ~3;          // the fused push's table rows (int32)
     const int dy_slack = C::EXACT ? (f16 - F) * C::U - (off - dy - F * C::U) : 0;
     if (dy_slack > 0) off += (dy_slack + 3) & ~3;
+#endif
     per_wave = off;
   }
 };
@@ -2123,7 +2151,11 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
   float* XB = base + lay.ba;  // this iteration's input X
   float* SB = base + lay.bb;  // this iteration's save: O | stats, then dO
   float* const PR = base + lay.pr;
+#if RS_IL4_ROT
+  float* DY = base + lay.bc;  // this iteration's dy, then (after P3) the next iteration's X
+#else
   float* const DY = base + lay.dy;
+#endif
   float* const PM = base + lay.pm;
   float* const DL = base + lay.st;
   int32_t* const RW = reinterpret_cast<int32_t*>(base + lay.rows);
@@ -2180,6 +2212,13 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
   mwp.load_proj_lds(WL, BL);
 #endif
 
+#if RS_IL4_PRIO
+  {  // static priority for the wave in an odd SIMD slot (its co-resident partner keeps 0)
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (hw & 1u) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
   IL_STAMP_DECL
   for (int64_t b = b_first; b < a.B; b += b_step) {
     for (int it = a.L - 1; it >= 0; --it) {
@@ -2190,11 +2229,28 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
       const bool has_next = bn < a.B;
       vm_wait_all();  // X, the save (and dy) of this iteration, and the previous push's atomics
       wave_lds_sync();
-      IL_STAMP(1)
+      if (it == a.L - 1) { IL_STAMP(10) } else { IL_STAMP(1) }
       const bool push_now = it == 0 && push;
       float bv[NRT][M::ET][4];
+#if RS_IL4_ROT
+      int32_t rw[NRT][4];
+#endif
       if (push_now) {
+#if RS_IL4_ROT
+        {
+          const int q = lane >> 4;
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int f = 16 * rt + 4 * q + r;
+              rw[rt][r] = __float_as_int(gload_untracked(
+                  reinterpret_cast<const float*>(a.push_rows + b * F + (f < F ? f : F - 1))));
+            }
+        }
+#else
         glds_copy_wave_u32(RW, a.push_rows + b * F, F);
+#endif
         if (with_base) {
           const float* base_g = dx + b * F * C::E;
           const int q = lane >> 4, jx = lane & 15;
@@ -2299,8 +2355,15 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         }
       }
       wave_lds_sync();
+#if RS_IL4_ROT
+      // dy consumed: its buffer takes the next iteration's input now (a Q- and K-pass ahead)
+      if (has_next) glds_copy_wave(DY, x_src(bn, itn), nx4);
+#endif
       IL_STAMP(3)
-      // ---- Q-pass (lane = (h, i)): P -> PM, dq -> DY ----
+      // ---- Q-pass (lane = (h, i)): P -> PM, dq -> DY (ROT: dq stays in registers) ----
+#if RS_IL4_ROT
+      float dqk[DH];
+#endif
       if (RS_IL4_EXP != 3) {
         const bool act = lane < HF;
         const int h = act ? lane / F : 0, i = act ? lane - h * F : 0;
@@ -2315,8 +2378,13 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
         const float* vb = PR + 2 * U + h * DH;
         // lanes past H * F store their P values into DY (dead until this pass's dq stores,
         // which come after the loop in program order and cover DY[0 .. 2U)): an unconditional
-        // ds_write per key instead of an exec-mask save / restore around each
+        // ds_write per key instead of an exec-mask save / restore around each (ROT: into RW,
+        // whose F floats nothing else uses)
+#if RS_IL4_ROT
+        float* pm_row = act ? PM + (h * F + i) * C::PMS : reinterpret_cast<float*>(RW);
+#else
         float* pm_row = act ? PM + (h * F + i) * C::PMS : DY;
+#endif
         const float nm = -stt.x;
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] = 0.f;
@@ -2352,7 +2420,12 @@ RS_UNROLL(RS_IL4_UNROLL_Q)
         }
 #pragma unroll
         for (int d = 0; d < DH; ++d) dq[d] *= a.inv_sdh;
+#if RS_IL4_ROT
+#pragma unroll
+        for (int d = 0; d < DH; ++d) dqk[d] = dq[d];
+#else
         if (act) store_row(DY + i * U + h * DH, dq);
+#endif
       }
       wave_lds_sync();
       IL_STAMP(4)
@@ -2412,12 +2485,27 @@ RS_UNROLL(RS_IL4_UNROLL_K)
       }
       wave_lds_sync();  // every lane's Q-row reads are done
       IL_STAMP(5)
+#if RS_IL4_ROT
+      if (lane < HF) {  // Q <- gQ, lane (h, i) as in the Q-pass
+        const int h = lane / F, i = lane - h * F;
+        float qv[DH];
+        load_row(qv, PR + i * C::PRS + h * DH);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) qv[d] = qv[d] > 0.f ? dqk[d] : 0.f;
+        store_row(PR + i * C::PRS + h * DH, qv);
+      }
+      wave_lds_sync();
+      // dO (SB) is dead: it takes the next sample's dy (iteration 0) or this iteration's dx (P7)
+      if (has_next && it == 0) glds_copy_wave(SB, dy + bn * dy_ld, ny4);
+#else
       for (int k = lane; k < F * U; k += 64) {  // Q <- gQ (dq in DY)
         const int f = k / U, c = k - f * U;
         float* qq = PR + f * C::PRS + c;
         *qq = *qq > 0.f ? DY[k] : 0.f;
       }
       wave_lds_sync();
+#endif
+#if !RS_IL4_ROT
       // dO (SB) and dq (DY) are dead: the next iteration's input (and the next sample's dy)
       if (has_next) {
 #if RS_IL4_EXP == 2
@@ -2428,6 +2516,7 @@ RS_UNROLL(RS_IL4_UNROLL_K)
         if (it == 0) glds_copy_wave(DY, dy + bn * dy_ld, ny4);
 #endif
       }
+#endif  // !RS_IL4_ROT
       IL_STAMP(6)
       // ---- P7: dW += X^T G, db += colsum G; dx = G W^T ----
 #pragma unroll
@@ -2443,7 +2532,12 @@ RS_UNROLL(RS_IL4_UNROLL_K)
 #else
         if (it > 0) {
 #endif
-          auto to_dy = [&](int, int, int, int f, int e, float v) { DY[f * U + e] = v; };
+#if RS_IL4_ROT
+          float* const ndy = SB;  // the next iteration's dy buffer
+#else
+          float* const ndy = DY;
+#endif
+          auto to_dy = [&](int, int, int, int f, int e, float v) { ndy[f * U + e] = v; };
           // (exact F: all NRT * 16 rows, the ones past F land in DY's slack; otherwise the
           // tiles past ceil(F / 16) would not fit it)
           mfma_dx_all<C, decltype(to_dy), C::EXACT>(PR, F, mw, to_dy);
@@ -2466,8 +2560,17 @@ RS_UNROLL(RS_IL4_UNROLL_K)
             for (int et = 0; et < M::ET; ++et)
 #pragma unroll
               for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(bv[rt][et][r]));
-          wave_lds_sync();  // RW landed in LDS
           const int q = lane >> 4;
+#if RS_IL4_ROT
+#pragma unroll
+          for (int rt = 0; rt < NRT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              asm volatile("" : "+v"(rw[rt][r]));
+              if (16 * rt + 4 * q + r >= F) rw[rt][r] = -1;
+            }
+#else
+          wave_lds_sync();  // RW landed in LDS
           int32_t rw[NRT][4];
 #pragma unroll
           for (int rt = 0; rt < NRT; ++rt)
@@ -2476,6 +2579,7 @@ RS_UNROLL(RS_IL4_UNROLL_K)
               const int f = 16 * rt + 4 * q + r;
               rw[rt][r] = f < F ? RW[f] : -1;
             }
+#endif
           mfma_dx_all<C>(PR, F, mw, [&](int rt, int et, int r, int, int e, float v) {
             const int32_t row = rw[rt][r];
             if (row >= 0) {
@@ -2493,9 +2597,16 @@ RS_UNROLL(RS_IL4_UNROLL_K)
       }
       wave_lds_sync();
       if (it > 0) { IL_STAMP(8) } else { IL_STAMP(9) }
+#if RS_IL4_ROT
+      float* const t = XB;  // XB holds the next save, DY the next input, SB the next dy
+      XB = DY;
+      DY = SB;
+      SB = t;
+#else
       float* const t = XB;  // XB holds the next save, SB the next input
       XB = SB;
       SB = t;
+#endif
     }
   }
 

@@ -297,7 +297,10 @@ class _DenseFn(torch.autograd.Function):
         dx = None
         sink = ctx.sink
         if ctx.needs_input_grad[0]:  # data and weight gradients in one launch
-            acc = sink is not None and sink.buf is not None and sink.buf.shape == (M, K)
+            if sink is not None and sink.buf is not None and tuple(sink.buf.shape) != (M, K):
+                raise RuntimeError(f"GradSink holds a {tuple(sink.buf.shape)} gradient for a Dense "
+                                   f"input of {(M, K)}: the producer's gradient would be lost")
+            acc = sink is not None and sink.buf is not None
             dx = sink.buf if acc else torch.empty(M, K, device=x.device, dtype=torch.float32)
             if sink is not None:
                 sink.buf = None

@@ -342,10 +342,10 @@ class MultiHeadRanker(nn.Module):
         B = x0.shape[0]
         # :60-63 the deep tower; its first Dense also adds the interacting layers' dx0 in its
         # backward (GradSink: no separate sum of the two [B, F E] gradients)
-        sink = GradSink()
-        deep = self.deep[0](x0.reshape(B, -1), grad_sink=sink)
-        for layer in self.deep[1:]:
-            deep = layer(deep)
+        sink = GradSink() if self.deep else None
+        deep = x0.reshape(B, -1)
+        for k, layer in enumerate(self.deep):
+            deep = layer(deep, grad_sink=sink) if k == 0 else layer(deep)
         # :54-56 interacting layers, :71 concat [deep, autoint]: the layer writes its output
         # into the concat directly
         result = self.interact.forward_concat(deep, x0, grad_sink=sink)

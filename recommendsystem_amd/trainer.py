@@ -390,6 +390,7 @@ class Trainer:
             self.graphs.append(g)
             self.graph_loss.append(loss.detach())
         self.graph_opt = None
+        self._overflow_words = self._has_overflow_words()
         if self.world > 1:
             self.graph_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_opt, capture_error_mode=mode):  # allocates nothing
@@ -413,14 +414,27 @@ class Trainer:
     # on truncated sparse gradients
     dp_check_every = 256
 
+    def _has_overflow_words(self) -> bool:
+        """Whether a captured step can drop work silently: a fixed-capacity DP exchange
+        (dp_caps) or an owner-sharded table with fixed routing (owner_cap), at any world size."""
+        if getattr(self, "dp_caps", None) is not None:
+            return True
+        return any(is_sharded(t) and t.owner_cap is not None for t in self.tables)
+
     def step_pool(self, i: int):
         k = i % len(self.graphs)
         self.graphs[k].replay()
         if self.graph_opt is not None:
             self._dp_exchange()
             self.graph_opt.replay()
-            if self.dp_caps is not None:
-                self._dp_replays = getattr(self, "_dp_replays", 0) + 1
-                if self._dp_replays % self.dp_check_every == 0:
-                    self.check_dp_overflow()
+        if self._overflow_words:
+            self._dp_replays = getattr(self, "_dp_replays", 0) + 1
+            if self._dp_replays % self.dp_check_every == 0:
+                self.check_dp_overflow()
         return self.graph_loss[k]
+
+    def finish_pool(self) -> None:
+        """Read the sticky overflow words once more (end of a replay run; raises like
+        check_dp_overflow).  step_pool reads them every dp_check_every replays."""
+        if self._has_overflow_words():
+            self.check_dp_overflow()

@@ -462,6 +462,41 @@ def test_interacting_ctor_defaults_train():
     assert losses[-1] < losses[0]
 
 
+def test_generic_scratch_slab_survives_growth_under_graphs():
+    """The generic kernels' global-scratch slab (il_generic.hip gs_scratch) may grow after a graph
+    captured a launch on the smaller slab: the old slab must stay alive (the graph baked its
+    address), so replaying the graph after a larger eager call still equals the eager result."""
+    from recommendsystem_amd._lib import call, ptr, stream_handle
+    F, E, U, H, L = 64, 16, 128, 1, 1            # past the LDS: global-scratch kernels
+    g = torch.Generator(device=DEV).manual_seed(31)
+    W = (torch.rand(E, 4 * U, device=DEV, generator=g) - 0.5) * 0.3
+    bias = torch.zeros(4 * U, device=DEV)
+    gam, bet = torch.ones(U, device=DEV), torch.zeros(U, device=DEV)
+    xs = torch.zeros(1, device=DEV)
+
+    def fwd(x, y):
+        call("rs_il_fwd", stream_handle(), ptr(x), x.shape[0], F, E, U, H, L, ptr(W), ptr(bias),
+             ptr(gam), ptr(bet), 1e-14, 1, 0.0, 0, ptr(y), F * U, ptr(xs))
+
+    xa = torch.rand(3, F, E, device=DEV, generator=g) - 0.5
+    ya_eager, ya_graph = torch.empty(3, F * U, device=DEV), torch.empty(3, F * U, device=DEV)
+    fwd(xa, ya_eager)                                 # sizes the slab for 3 workgroups
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        fwd(xa, ya_graph)
+    xb = torch.rand(300, F, E, device=DEV, generator=g) - 0.5
+    yb = torch.empty(300, F * U, device=DEV)
+    fwd(xb, yb)                                       # grows the slab (256 workgroups)
+    torch.cuda.synchronize()
+    junk = [torch.full((1 << 22,), 7.0, device=DEV) for _ in range(8)]  # reuse freed memory
+    ya_graph.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(ya_graph, ya_eager)
+    del junk
+
+
 @pytest.mark.parametrize("F,L", [(200, 1), (150, 2)])
 def test_interacting_many_fields_dropout(F, L):
     """The config-3 layer as used in training: IL(1, 8, 2, use_dropout=True, dropout_rate=0.2)

@@ -360,6 +360,21 @@ try:
         res.append((losses, params, j.table.weight.cpu().clone()))
     assert res[0][0] == res[1][0], (res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+    # an owner_cap too small for the batches: the captured replays drop ids, and step_pool's
+    # periodic read of the sticky routing word raises (world 1 too: ADVICE r05)
+    j = StaytimeRoughRank(rows=20_011, device=DEV, seed=3, shard_group=pg)
+    trn = Trainer(j, 5e-4, [j.table], process_group=pg)
+    trn.measure_dp_caps(batches)
+    j.table.owner_cap = 32
+    trn.capture_pool(batches, warmup=1)
+    trn.dp_check_every = 2
+    raised = False
+    try:
+        for s in range(4):
+            trn.step_pool(s)
+    except RuntimeError as e:
+        raised = "routing overflow" in str(e)
+    assert raised, "step_pool did not report the owner_cap overflow"
     print("CAPTURED-SHARDED-OK", res[1][0], flush=True)
 except Exception:
     traceback.print_exc()

@@ -28,8 +28,8 @@ for _ in range(3):
         call("rs_il_bwd", s, ptr(x), ptr(xs), ptr(dy), F * U, B, F, E, U, H, L, ptr(W), ptr(bias), ptr(g), ptr(be), 1e-14, 1, 0.0, 0, ptr(dx), 0, None, 0, ptr(ws), wsn)
 torch.cuda.synchronize()
 v = st.cpu().tolist()[:10]
-names = (["wait x/save", "P1 proj + xa", "P3 LN bwd", "Q-pass", "K-pass", "G-Q", "dW (MFMA)",
-          "dx it>0", "dx+push it=0", "-"] if SAVED else
+names = (["wait x/save (it<L-1)", "P1 proj + xa", "P3 LN bwd", "Q-pass", "K-pass", "G-Q", "dW (MFMA)",
+          "dx it>0", "dx+push it=0", "wait (sample start)"] if SAVED else
          ["x load/prefetch", "projection(MFMA)", "attn recompute", "LN bwd", "dV", "dS/dQ", "dK + G", "dW (MFMA)", "dx (MFMA) it>0", "dx+push it=0"])
 tot = sum(v)
 for n, c in zip(names, v):
