@@ -662,7 +662,11 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
                                f"26 fields x emb 16, global batch {B * world} ({scaling} scaling)",
                    "global_batch": B * world, "per_gpu_batch": B, "fields": F, "emb_dim": E,
                    "layer_num": L,
-                   "head_num": H, "parallelism": f"dp{world}"},
+                   "head_num": H, "parallelism": f"dp{world}",
+                   "execution": ("one HIP graph per pool batch" if trainer._one_graph else
+                                 "forward/backward graph + eager all-gather + optimizer graph")
+                                + (" (RCCL all-gather captured in the step graph)"
+                                   if getattr(trainer, "dp_one_graph", False) else "")},
         "roofline": {"bound": "mfma", "kernel": kname
                      + " (InteractingLayer backward over the forward's attention save + fused sparse "
                        "push" + (" + the head's deferred dW1, counted)" if xt else ")"),

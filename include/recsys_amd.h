@@ -392,13 +392,16 @@ int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* dY, int
                  const float* Y, int64_t ldy, int act, const float* W, int64_t M, int K, int N,
                  float* dX, int64_t lddx, int dx_accumulate, float* dW, float* db, int w_accumulate,
                  float* workspace, int64_t workspace_floats);
-/* Large plain GEMMs (M K N >= 2^26 multiply-adds by default; RS_GEMM_BLAS=0 off,
- * RS_GEMM_BLAS_MACS=n threshold) run on hipBLASLt inside the four entries above: forward with
- * its bias / ReLU epilogue (sigmoid stays on the engine), weight gradient and rs_dense_bwd with
- * dZ = dY act'(Y) materialised in the workspace (the workspace query covers it) and db from a
- * fixed-order column reduction, rs_dense_bwd_data only for act 0.  A shape the library declines
- * runs on the engine.  rs_dense_uses_library(M, K, N): 1 when a Dense layer of that shape takes
- * the library route (results then equal the engine's to fp32 rounding, not bitwise). */
+/* Large GEMMs (M K N >= 2^26 multiply-adds by default; RS_GEMM_BIG=0 off, RS_GEMM_BIG_MACS=n
+ * threshold) run the hand-written direct-to-LDS kernels of gemm_big.hip inside the four entries
+ * above: forward with its bias / activation epilogue, data and weight gradients with
+ * dZ = dY act'(Y) applied to the MFMA fragments (no dZ pass), db as the weight product's extra
+ * output row, split-K weight gradients through the workspace (the workspace query covers them)
+ * and a fixed-order column reduction.  rs_dense_uses_big(M, K, N): 1 when a Dense layer of that
+ * shape takes these kernels.  Opt-in comparison route: RS_GEMM_BLAS=1 sends the same shapes to
+ * hipBLASLt (rs_dense_uses_library(M, K, N) says which; results then equal the engine's to fp32
+ * rounding, not bitwise). */
+int rs_dense_uses_big(int64_t M, int K, int N);
 int rs_dense_uses_library(int64_t M, int K, int N);
 /* Grouped Dense: G <= 8 independent layers of one kind in ONE launch (plus one grouped split-K
  * reduce for weight gradients) -- the per-expert / per-task layers that staytime/VideoDnn.py:130-191

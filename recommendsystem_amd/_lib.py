@@ -82,6 +82,7 @@ SIGNATURES: dict[str, tuple] = {
                                  _i32]),
     "rs_dense_bwd_weight_workspace_floats": (_i64, [_i64, _i32, _i32]),
     "rs_dense_uses_library": (_i32, [_i64, _i32, _i32]),
+    "rs_dense_uses_big": (_i32, [_i64, _i32, _i32]),
     "rs_dense_bwd_weight": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _i32,
                                    _vp, _vp, _i32, _vp, _i64]),
     "rs_dense_bwd": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp,

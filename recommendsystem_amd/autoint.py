@@ -139,11 +139,13 @@ class AutoIntTrainer:
     """
 
     def __init__(self, model: AutoInt, batch_size: int, process_group=None,
-                 deterministic: bool = False, metrics=None):
+                 deterministic: bool = False, metrics=None, dp_world1: bool = False):
         """metrics: a metrics.CtrMetrics updated with (p, labels) inside every step (the Keras
         'acc' / AUC() / tn.metric.COPC() of rank/ctr/base_model.py:183-190; one more launch per
         step, captured with the rest), or one CtrMetrics per task for a multi-task head (task t
-        reads column t of p and labels).  None (the benchmark) skips it."""
+        reads column t of p and labels).  None (the benchmark) skips it.
+        dp_world1: run the data-parallel step (exchange, rank-ordered merges) on a world-1 group
+        too (tests: the RCCL path on a one-GPU box)."""
         self.model = m = model
         if metrics is not None and not isinstance(metrics, (list, tuple)):
             metrics = [metrics]
@@ -156,6 +158,7 @@ class AutoIntTrainer:
         self.dev = dev
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.dp = self.world > 1 or (bool(dp_world1) and process_group is not None)
         f32 = dict(device=dev, dtype=torch.float32)
         self.deep_layers = list(m.deep.layers)
         self.logit_layers = list(m.logits.layers)
@@ -234,7 +237,7 @@ class AutoIntTrainer:
         # reduce into a send bucket that also carries the sparse record count, the touched rows
         # are packed into [row | grad] records; two all-gathers, then graph-captured rank-ordered
         # merges and a rank-ordered dense sum fused with Adam
-        self.packed_dp = self.world > 1 and self.push
+        self.packed_dp = self.dp and self.push
         if self.packed_dp:
             n = m.arena.n
             self.dp_n = n
@@ -253,6 +256,13 @@ class AutoIntTrainer:
                 self.dp_send = self.dp_buf[:self.dp_ld]
                 self.dp_recs = self.dp_buf[self.dp_ld:]
                 self.dp_all = torch.zeros(self.world * self.dp_S, **f32)
+                # RCCL: the all-gather is captured with the rest of the step, ONE graph per pool
+                # batch (thread_local capture, dist.capture_error_mode); gloo collectives are host
+                # calls and stay eager between a forward/backward and an optimizer graph
+                # (RS_DP_SPLIT_GRAPH=1 forces that form on RCCL too)
+                from .dist import uses_flat_all_gather
+                self.dp_one_graph = (uses_flat_all_gather(process_group) and
+                                     not os.environ.get("RS_DP_SPLIT_GRAPH"))
             else:
                 self.dp_ld = ld = (n + 1 + 3) // 4 * 4
                 self.dp_cap = B * F
@@ -260,11 +270,16 @@ class AutoIntTrainer:
                 self.dp_recv = torch.zeros(self.world * ld, **f32)
                 self.dp_recs = torch.empty(self.dp_cap * self.dp_rs, **f32)
                 self.dp_recs_all = torch.empty(self.world * self.dp_cap * self.dp_rs, **f32)
-        elif self.world > 1:
+        elif self.dp:
             cap = m.table.touched_cap
             self.x_rows = torch.empty(cap, device=dev, dtype=torch.int32)
             self.x_grads = torch.empty(cap, E, **f32)
             self.x_count = torch.zeros(1, device=dev, dtype=torch.int32)
+
+    @property
+    def _one_graph(self) -> bool:
+        """One captured graph per step: single-GPU, or DP whose collective can be captured."""
+        return not self.dp or getattr(self, "dp_one_graph", False)
 
     def _offset(self, p: torch.Tensor) -> int:
         return (p.data_ptr() - self.model.arena.data.data_ptr()) // 4
@@ -445,7 +460,7 @@ class AutoIntTrainer:
     def _forward_backward_core(self):
         if self.head is not None:
             self._forward_backward_fused()
-            if self.world > 1:
+            if self.dp:
                 self._reduce_dense(adam=False)
             if self.packed_dp:
                 t = self.model.table
@@ -556,7 +571,7 @@ class AutoIntTrainer:
     def _optimize(self):
         m, cfg = self.model, self.model.cfg
         ar = m.arena
-        if self.head is not None and self.world == 1:
+        if self.head is not None and not self.dp:
             # partials -> grads -> Adam, one launch; a scan-mode table's sparse Adam runs in the
             # same launch on blocks of its own
             tail = self._scan_tail(m.table)
@@ -609,7 +624,7 @@ class AutoIntTrainer:
 
     def _step_eager(self):
         self._forward_backward()
-        if self.world > 1:
+        if self.dp:
             self._exchange()
         self._optimize()
 
@@ -650,11 +665,12 @@ class AutoIntTrainer:
 
     def _record(self):
         """Record the step over the CURRENT self.ids / self.labels: one graph for the whole step
-        (N = 1), or the forward/backward half only (N > 1: the collectives stay eager and the
-        optimizer half is recorded once by _record_opt)."""
+        (N = 1, or N > 1 on RCCL: the all-gather inside it), or the forward/backward half only
+        (N > 1 on gloo: the collectives stay eager and the optimizer half is recorded once by
+        _record_opt)."""
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=capture_error_mode()):
-            if self.world == 1:
+            if self._one_graph:
                 self._step_eager()
             else:
                 self._forward_backward()
@@ -669,8 +685,8 @@ class AutoIntTrainer:
     def capture(self, warmup: int = 2) -> None:
         """Capture the step over the trainer's own static ids / labels buffers (``step()``
         replays it).  ``warmup`` eager steps run first and are rolled back (see _warmup)."""
-        self._warmup(warmup)
-        if self.world == 1:
+        self._warmup(max(warmup, 1) if self.dp else warmup)
+        if self._one_graph:
             self.graph = self._record()
         else:
             self.graph_fb = self._record()
@@ -697,7 +713,8 @@ class AutoIntTrainer:
                 raise ValueError("pool ids must be contiguous int64 [B, F]")
             self.pool_batches.append((ids, labels.reshape(self.B, self.T).float().contiguous()))
         own = (self.ids, self.labels)
-        self._warmup(warmup)
+        # (DP: at least one eager step, so the communicator exists before a capture uses it)
+        self._warmup(max(warmup, 1) if self.dp else warmup)
         self.pool_graphs = []
         try:
             for ids, labels in self.pool_batches:
@@ -705,7 +722,7 @@ class AutoIntTrainer:
                 self.pool_graphs.append(self._record())
         finally:
             self.ids, self.labels = own
-        if self.world > 1:
+        if not self._one_graph:
             self._record_opt()
         self._prime_graphs()
 
@@ -721,7 +738,7 @@ class AutoIntTrainer:
         saved = [t.clone() for t in self._state()]
         for g in self.pool_graphs:
             g.replay()
-        if self.world > 1 and self.graph_opt is not None:
+        if not self._one_graph and self.graph_opt is not None:
             self.graph_opt.replay()
         torch.cuda.synchronize()
         for t, v in zip(self._state(), saved):
@@ -731,7 +748,7 @@ class AutoIntTrainer:
     def step_pool(self, i: int) -> torch.Tensor:
         g = self.pool_graphs[i % len(self.pool_graphs)]
         g.replay()
-        if self.world > 1:
+        if not self._one_graph:
             _lib.trace_point("graph_fb")
             self._exchange()
             _lib.trace_point("exchange")
@@ -744,7 +761,7 @@ class AutoIntTrainer:
             self.load_batch(ids, labels)
         if self.graph is None:
             self._step_eager()
-        elif self.world == 1:
+        elif self._one_graph:
             self.graph.replay()
         else:
             self.graph_fb.replay()

@@ -162,7 +162,7 @@ bool rs_blas_wanted(int64_t m, int64_t n, int64_t k) {
   // the timed algorithm choice it also wins from 67 M (config 3 1.586 -> 1.570 ms, config 5
   // 1.791 -> 1.784 ms against the 268 M threshold, profiles/r05/thr/)
   static const int64_t thr = env_i64("RS_GEMM_BLAS_MACS", (int64_t)1 << 26);
-  static const bool on = env_i64("RS_GEMM_BLAS", 1) != 0;
+  static const bool on = env_i64("RS_GEMM_BLAS", 0) != 0;  // opt-in (round 6: gemm_big.hip)
   return on && m > 0 && n > 0 && k > 0 && m * n * k >= thr;
 }
 

@@ -17,6 +17,7 @@
 //                fixed-order reduce (deterministic, no float atomics)
 #include "blas.hpp"
 #include "common.hpp"
+#include "gemm_big.hpp"
 
 #include <cstdint>
 #include <cstdio>
@@ -638,6 +639,63 @@ static int blas_dense_bwd(hipStream_t s, const float* X, int64_t ldx, const floa
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The large GEMMs (>= 2^26 multiply-adds: rs_big::wanted) run the direct-to-LDS kernels of
+// gemm_big.hip; the library route (hipBLASLt, RS_GEMM_BLAS=1) is kept as an opt-in comparison.
+// Each helper returns 0 when it launched, nonzero when the caller runs its own kernels.
+// ---------------------------------------------------------------------------------------------
+static int big_fwd(hipStream_t s, const float* X, int64_t M, int K, int64_t ldx, const float* W,
+                   const float* bias, int N, int act, float* Y, int64_t ldy) {
+  if (!rs_big::wanted(M, N, K)) return 1;
+  return rs_big::fwd(s, X, M, K, ldx, W, bias, N, act, Y, ldy);
+}
+
+static int big_data(hipStream_t s, const float* dY, int64_t lddy, const float* Y, int64_t ldy,
+                    int act, const float* W, int64_t M, int K, int N, float* dX, int64_t lddx,
+                    int accumulate) {
+  if (!rs_big::wanted(M, K, N)) return 1;
+  const bool z = act != RS_ACT_NONE;
+  const rs_big::Plan p = rs_big::plan(M, K, N, false, z);
+  rs_big::Args g{};
+  g.a = rs_big::Operand{dY, z ? Y : nullptr, lddy, ldy, M, 0};
+  g.b = rs_big::Operand{W, nullptr, N, 0, K, 0};
+  g.M = M; g.N = K; g.R = N; g.act_z = act;
+  g.epi = rs_big::EPI_STORE; g.out = dX; g.ldo = lddx; g.accumulate = accumulate; g.Mreal = M;
+  return rs_big::launch(s, rs_big::FORM_DATA, p, g);
+}
+
+// weight gradient dW [K, N] and db [N] as one product of K + 1 output rows (row K: db)
+static rs_big::Plan big_weight_plan(int64_t M, int K, int N, int act) {
+  return rs_big::plan((int64_t)K + 1, N, M, true, act != RS_ACT_NONE);
+}
+static int64_t big_weight_ws(int64_t M, int K, int N, int act) {
+  const rs_big::Plan p = big_weight_plan(M, K, N, act);
+  return p.splits > 1 ? (int64_t)p.splits * ((int64_t)K * N + N) : 0;
+}
+static int big_weight(hipStream_t s, const float* X, int64_t ldx, const float* dY, int64_t lddy,
+                      const float* Y, int64_t ldy, int act, int64_t M, int K, int N, float* dW,
+                      float* db, int accumulate, float* ws, int64_t wsf) {
+  if (!rs_big::wanted(K, N, M)) return 1;
+  const bool z = act != RS_ACT_NONE;
+  const rs_big::Plan p = big_weight_plan(M, K, N, act);
+  const bool split = p.splits > 1;
+  const int64_t total = (int64_t)K * N + N;
+  if (split && (!ws || wsf < (int64_t)p.splits * total)) return 1;
+  rs_big::Args g{};
+  g.a = rs_big::Operand{X, nullptr, ldx, 0, K, 1};
+  g.b = rs_big::Operand{dY, z ? Y : nullptr, lddy, ldy, N, 0};
+  g.M = (int64_t)K + 1; g.N = N; g.R = M; g.act_z = act;
+  g.Mreal = K;
+  if (split) {
+    g.epi = rs_big::EPI_PARTIAL; g.out = ws; g.slab = total;
+  } else {
+    g.epi = rs_big::EPI_STORE; g.out = dW; g.ldo = N; g.db = db; g.accumulate = accumulate;
+  }
+  if (rs_big::launch(s, rs_big::FORM_WEIGHT, p, g)) return 1;
+  if (split) launch_column_reduce(s, ws, p.splits, total, total, (int64_t)K * N, dW, db, accumulate);
+  return 0;
+}
+
 RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t ldx,
                         const float* W, const float* bias, int N, int act, float* Y,
                         int64_t ldy) {
@@ -646,6 +704,8 @@ RS_API int rs_dense_fwd(void* stream, const float* X, int64_t M, int K, int64_t 
   if (act != RS_ACT_SIGMOID && rs_blas_wanted(M, N, K) &&
       rs_blas_gemm_cm(rs_stream(stream), false, false, N, M, K, W, N, X, ldx, 0.f, Y, ldy, bias,
                       act == RS_ACT_RELU) == 0)
+    return rs_status_after_launch();
+  if (big_fwd(rs_stream(stream), X, M, K, ldx, W, bias, N, act, Y, ldy) == 0)
     return rs_status_after_launch();
   GemmArgs g{X, ldx, nullptr, 0, W, N, nullptr, 0, M, N, K, 0, 0, EPI_FWD, act, bias, Y, ldy, 0, nullptr};
   GemmPlan p = plan_gemm(M, N, K, false);
@@ -666,6 +726,8 @@ RS_API int rs_dense_bwd_data(void* stream, const float* dY, int64_t lddy, const 
       rs_blas_gemm_cm(rs_stream(stream), true, false, K, M, N, W, N, dY, lddy,
                       accumulate ? 1.f : 0.f, dX, lddx, nullptr, false) == 0)
     return rs_status_after_launch();
+  if (big_data(rs_stream(stream), dY, lddy, Y, ldy, act, W, M, K, N, dX, lddx, accumulate) == 0)
+    return rs_status_after_launch();
   // C[M, K] = dZ[M, N] . W^T : B(r = n, c = k) = W[k * N + n] (column layout, ldb = N)
   GemmArgs g{dY, lddy, Y, ldy, W, N, nullptr, 0, M, K, N, 0, act, EPI_STORE, 0, nullptr, dX, lddx,
              accumulate, nullptr};
@@ -681,10 +743,19 @@ RS_API int rs_dense_uses_library(int64_t M, int K, int N) {
   return rs_blas_wanted(K, N, M) ? 1 : 0;
 }
 
+RS_API int rs_dense_uses_big(int64_t M, int K, int N) {
+  return !rs_blas_wanted(K, N, M) && rs_big::wanted(K, N, M) ? 1 : 0;
+}
+
 RS_API int64_t rs_dense_bwd_weight_workspace_floats(int64_t M, int K, int N) {
   if (M < 0 || K <= 0 || N <= 0) return 0;  // (rs_dense_bwd_weight rejects these shapes)
   const GemmPlan p = plan_gemm(K, N, M, true);
-  const int64_t own = (int64_t)p.splits * ((int64_t)K * N + N);
+  int64_t own = (int64_t)p.splits * ((int64_t)K * N + N);
+  if (rs_big::wanted(K, N, M)) {  // either activation form (the caller's act is not known here)
+    const int64_t b0 = big_weight_ws(M, K, N, RS_ACT_NONE), b1 = big_weight_ws(M, K, N, RS_ACT_RELU);
+    own = own > b0 ? own : b0;
+    own = own > b1 ? own : b1;
+  }
   if (!rs_blas_wanted(K, N, M)) return own;
   const int64_t lib = blas_bwd_workspace_floats(M, N);  // (or the engine's, if the library declines)
   return lib > own ? lib : own;
@@ -706,6 +777,9 @@ RS_API int rs_dense_bwd_weight(void* stream, const float* X, int64_t ldx, const 
   if (rs_blas_wanted(K, N, M) &&
       blas_dense_bwd(s, X, ldx, dY, lddy, Y, ldy, act, nullptr, M, K, N, nullptr, 0, 0, dW, db,
                      accumulate, workspace, workspace_floats) == 0)
+    return rs_status_after_launch();
+  if (big_weight(s, X, ldx, dY, lddy, Y, ldy, act, M, K, N, dW, db, accumulate, workspace,
+                 workspace_floats) == 0)
     return rs_status_after_launch();
   // C[K, N] = sum_m X[m][k] dZ[m][n]: A(k, m) = X[m * ldx + k] (column layout), B = dZ rows
   const GemmPlan p = plan_gemm(K, N, M, true);
@@ -775,6 +849,18 @@ RS_API int rs_dense_bwd(void* stream, const float* X, int64_t ldx, const float* 
       blas_dense_bwd(rs_stream(stream), X, ldx, dY, lddy, Y, ldy, act, W, M, K, N, dX, lddx,
                      dx_accumulate, dW, db, w_accumulate, workspace, workspace_floats) == 0)
     return rs_status_after_launch();
+  if (M > 0 && rs_big::wanted(K, N, M)) {
+    // two big launches (data, weight); the data gradient of a shape below the big threshold
+    // (M K N is the same product) cannot occur here
+    hipStream_t s = rs_stream(stream);
+    if (big_data(s, dY, lddy, Y, ldy, act, W, M, K, N, dX, lddx, dx_accumulate) == 0) {
+      if (big_weight(s, X, ldx, dY, lddy, Y, ldy, act, M, K, N, dW, db, w_accumulate, workspace,
+                     workspace_floats) == 0)
+        return rs_status_after_launch();
+      return rs_dense_bwd_weight(stream, X, ldx, dY, lddy, Y, ldy, act, M, K, N, dW, db,
+                                 w_accumulate, workspace, workspace_floats);
+    }
+  }
   const GemmPlan pd = plan_gemm(M, K, N, false);
   const GemmPlan pw = plan_gemm(K, N, M, true);
   const bool vec_d = aligned16(dY) && aligned16(Y) && aligned16(W) && lddy % 4 == 0 && ldy % 4 == 0 &&

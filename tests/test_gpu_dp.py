@@ -269,3 +269,73 @@ def test_rccl_flat_all_gather_world1():
         assert torch.equal(recs_all[:3 * rs], recs[:3 * rs])
     finally:
         dist.destroy_process_group()
+
+
+_ONE_GRAPH_CHILD = r"""
+import os, sys, traceback
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch, torch.distributed as dist
+DEV = torch.device("cuda", 0)
+os.environ["MASTER_ADDR"] = "127.0.0.1"
+os.environ["MASTER_PORT"] = sys.argv[2]
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=DEV)
+rc = 0
+try:
+    from recommendsystem_amd.autoint import AutoInt, AutoIntConfig, AutoIntTrainer
+    B, NB, STEPS = 256, 2, 3
+    cfg = AutoIntConfig(vocab_per_field=2000, layer_num=3, lr_dense=1e-3, lr_sparse=1e-3)
+    rng = np.random.default_rng(5)
+    # every (field, id) once per batch: each table row gets one push per step, so the float
+    # atomics of the fused push add in a fixed order and eager == graph bitwise
+    pool = []
+    for k in range(NB):
+        ids = np.stack([rng.permutation(cfg.vocab_per_field)[:B] for _ in range(cfg.num_fields)], 1)
+        pool.append((torch.from_numpy(ids.astype(np.int64)).to(DEV),
+                     torch.from_numpy((rng.uniform(size=(B, 1)) < 0.25).astype(np.float32)).to(DEV)))
+    res = {}
+    for mode in ("eager", "one_graph", "split_graph"):
+        if mode == "split_graph":
+            os.environ["RS_DP_SPLIT_GRAPH"] = "1"
+        model = AutoInt(cfg, device=DEV, seed=21, max_batch=B, world_size=1)
+        trn = AutoIntTrainer(model, B, process_group=dist.group.WORLD, dp_world1=True)
+        assert trn.packed_dp and trn.dp_sync_free
+        assert trn.dp_one_graph == (mode != "split_graph")
+        if mode == "eager":
+            losses = [float(trn.step(*pool[s % NB])) for s in range(STEPS)]
+        else:
+            trn.capture_pool(pool, warmup=1)
+            assert len(trn.pool_graphs) == NB
+            assert (trn.graph_opt is None) == (mode == "one_graph")
+            losses = [float(trn.step_pool(s)) for s in range(STEPS)]
+        torch.cuda.synchronize()
+        params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+        res[mode] = (losses, params, model.table.weight.cpu().clone(), model.table.m.cpu().clone())
+        os.environ.pop("RS_DP_SPLIT_GRAPH", None)
+    e = res["eager"]
+    for mode in ("one_graph", "split_graph"):
+        g = res[mode]
+        assert e[0] == g[0], (mode, e[0], g[0])
+        for a, b in zip(e[1:], g[1:]):
+            assert torch.equal(a, b), mode
+    print("ONE-GRAPH-DP-OK", e[0], flush=True)
+except Exception:
+    traceback.print_exc()
+    rc = 1
+sys.stdout.flush()
+sys.stderr.flush()
+os._exit(rc)
+"""
+
+
+def test_dp_one_graph_rccl_world1():
+    """The AutoInt data-parallel step as ONE captured graph per pool batch on RCCL (the merged
+    all-gather inside the graph, thread_local capture): on a world-1 RCCL group (dp_world1: the
+    DP code path -- exchange, rank-ordered merges, the fused dense sum + Adam) the replays equal
+    the eager DP steps bitwise, and so does the two-graph form (RS_DP_SPLIT_GRAPH=1, what gloo
+    runs).  Child process under a time limit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ONE_GRAPH_CHILD, root, str(_free_port())],
+                       capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0 and "ONE-GRAPH-DP-OK" in r.stdout, (r.stdout[-2000:] + r.stderr[-4000:])

@@ -293,16 +293,20 @@ def test_dense_bwd_one_launch_equals_two(M, K, N, act):
 
 
 @pytest.mark.parametrize("M,K,N,act", [(2048, 1712, 960, 1), (4096, 1616, 273, 0), (2048, 1840, 400, 2),
-                                       (2048, 1712, 256, 1)])
-def test_dense_library_route_matches_engine(M, K, N, act):
-    """The library route (hipBLASLt, rs_dense_uses_library) against the engine forced by
-    RS_GEMM_BLAS=0 in a child process and against float64: forward (bias + activation),
-    rs_dense_bwd (dX accumulated, dW / db accumulated), repeated launches bitwise equal."""
+                                       (2048, 1712, 256, 1), (2085, 530, 333, 1), (4096, 1600, 32, 0),
+                                       (300, 4096, 600, 1), (2048, 1024, 512, 1)])
+def test_dense_big_route_matches_engine(M, K, N, act):
+    """The large-GEMM kernels (gemm_big.hip, rs_dense_uses_big) against the engine forced by
+    RS_GEMM_BIG=0 and the hipBLASLt route (RS_GEMM_BLAS=1), each in a child process, and all
+    against float64: forward (bias + activation), rs_dense_bwd (dX accumulated, dW / db
+    accumulated; split-K weight gradients, ragged and unaligned extents: N = 273 / 333 rows take
+    the 4-B DMA path, K % 128 == 0 puts db in a tile row of its own), repeated launches bitwise
+    equal."""
     import subprocess, sys
     from recommendsystem_amd import _lib
     lib = _lib.load()
-    if not lib.rs_dense_uses_library(M, K, N):
-        pytest.skip("below the library threshold")
+    if not lib.rs_dense_uses_big(M, K, N):
+        pytest.skip("below the large-GEMM threshold")
     code = f"""
 import sys, torch, numpy as np
 sys.path.insert(0, {repr(ROOT)})
@@ -333,10 +337,14 @@ np.savez(sys.argv[1], *[t.numpy() for t in outs[0]])
 """
     import tempfile
     res = {}
-    for mode in ("lib", "engine"):
+    for mode in ("big", "engine", "lib"):
         env = dict(os.environ)
+        env.pop("RS_GEMM_BIG", None)
+        env.pop("RS_GEMM_BLAS", None)
         if mode == "engine":
-            env["RS_GEMM_BLAS"] = "0"
+            env["RS_GEMM_BIG"] = "0"
+        if mode == "lib":
+            env["RS_GEMM_BLAS"] = "1"
         with tempfile.NamedTemporaryFile(suffix=".npz") as f:
             r = subprocess.run([sys.executable, "-c", code, f.name], env=env, capture_output=True,
                                text=True, timeout=120)
@@ -350,10 +358,10 @@ np.savez(sys.argv[1], *[t.numpy() for t in outs[0]])
     dY = (torch.rand(M, N, device="cuda", generator=g) - 0.5).double()
     z = X @ W + b
     Y = torch.relu(z) if act == 1 else torch.sigmoid(z) if act == 2 else z
-    Yf = torch.from_numpy(res["lib"][0]).cuda().double()
+    Yf = torch.from_numpy(res["big"][0]).cuda().double()
     dZ = dY * (Yf > 0) if act == 1 else dY * Yf * (1 - Yf) if act == 2 else dY
     ref = [Y, dZ @ W.T + 0.5, X.T @ dZ + 0.25, dZ.sum(0) + 0.125]
     tols = [1e-7 * K * 0.25 * 8, 1e-7 * N * 0.05 * 8, 1e-7 * M * 0.25 * 8, 1e-7 * M * 8]
     for i, what in enumerate(("y", "dX", "dW", "db")):
-        for mode in ("lib", "engine"):
+        for mode in ("big", "engine", "lib"):
             assert_close(res[mode][i], ref[i].cpu().numpy(), tols[i], 1e-5, what=f"{what} ({mode})")
