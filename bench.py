@@ -623,15 +623,19 @@ def bench_autoint(args, world, rank, dev, pg, compute_dtype, scaling="strong"):
     # this bench's own step), labelled as such
     traffic, traffic_src = None, None
     kname = "rs_il::bwd4_kernel" if B > 1536 else "rs_il::wbwd_kernel"
-    tf_path = os.path.join(ROOT, "profiles", "il_bwd_traffic.json")
-    if compute_dtype == "f32" and os.path.exists(tf_path):
+    # the newest round's committed measurement (profiles/rNN/il_bwd_traffic.json)
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "il_bwd_traffic.json")) +
+                   glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "*", "il_bwd_traffic.json")))
+    tf_path = cands[-1] if cands else ""
+    if compute_dtype == "f32" and tf_path and os.path.exists(tf_path):
         with open(tf_path) as f:
             tj = json.load(f)
         if tj.get("per_gpu_batch") == B and tj.get("kernel", "").split("<")[0] in kname and \
                 tj.get("launch") == ("rs_il_bwd_push_saved_xt" if xt else "rs_il_bwd_push_saved"):
             traffic = tj.get("hbm_bytes_per_launch")
             traffic_src = (f"committed rocprofv3 PMC (FETCH_SIZE x2 + WRITE_SIZE, separate passes) "
-                           f"in profiles/il_bwd_traffic.json ({tj.get('source', '')}), not measured "
+                           f"in {os.path.relpath(tf_path, ROOT)} ({tj.get('source', '')}), not measured "
                            f"in this run")
 
     samples = B * args.steps * world

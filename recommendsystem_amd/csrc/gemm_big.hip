@@ -133,6 +133,9 @@ __device__ __forceinline__ void vm_wait_n(int n) {
 }
 
 __device__ __forceinline__ void lds_sync() {
+#ifdef RS_BIG_NOBAR  // diagnostic builds only (with RS_BIG_NODMA): the barrier's share
+  return;
+#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -202,6 +205,9 @@ struct OpDma {
   }
   // issue the next slab (starting at reduction index r0) into the image at dst
   __device__ void issue(float* dst, int64_t r0, int64_t re, bool tail) {
+#ifdef RS_BIG_NODMA  // diagnostic builds only: the MFMA / LDS pipeline without its loads
+    return;
+#endif
 #pragma unroll
     for (int u = 0; u < IPW; ++u) {
       const float* g = one[u] ? g_consts + 4 : cur[u];
@@ -255,7 +261,7 @@ __global__ void __launch_bounds__(kThreads, NW == 8 ? 1 : 2) big_kernel(Args g) 
   // ---- block -> (split, tile): XCD-contiguous ranges, GM tile rows per group ----
   const int nb = (int)gridDim.x;
   int b = (int)blockIdx.x;
-  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  if (g.xcd && (nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
   const int T = g.tm * g.tn;
   const int z = b / T, tt = b - z * T;
   const int per_group = g.gm * g.tn;
@@ -312,7 +318,11 @@ __global__ void __launch_bounds__(kThreads, NW == 8 ? 1 : 2) big_kernel(Args g) 
 #pragma unroll
     for (int jj = 0; jj < TNW; ++jj) {
       const int x = wc * (BN / WG::WN) + 16 * jj + j;
+#ifdef RS_BIG_DIAG_BR  // diagnostic builds only: B fragments read as R images (wrong values)
+      if constexpr (true) {
+#else
       if constexpr (BMODE == MODE_R) {
+#endif
         const int o = x * BK + 4 * (q ^ sw_r(x));
         const float4 v = *reinterpret_cast<const float4*>(st + SB + o);
         f.b[jj][0] = v.x; f.b[jj][1] = v.y; f.b[jj][2] = v.z; f.b[jj][3] = v.w;
@@ -383,20 +393,15 @@ __global__ void __launch_bounds__(kThreads, NW == 8 ? 1 : 2) big_kernel(Args g) 
   lds_sync();
   read(0, f0, y0);
   zform(f0, y0);
-  auto body = [&](int s, Frag<TMW, TNW> (&fc)[KSUB], Frag<TMW, TNW> (&fn)[KSUB], FY (&yn)[KSUB]) {
-    const bool more = s + 1 < nst;
-    if (more) {
-      // slab s + 1 landed (this wave's DMAs; the barrier publishes all waves' and frees slot s)
-      if (s + STAGES < nst) vm_wait_c<IPS * (STAGES - 2)>();
-      else vm_wait_n(IPS * (nst - s - 2));
-    }
-    lds_sync();
-    if (more) read(s + 1, fn, yn);
+  // One slab step.  STEADY (slab s + STAGES exists): a constant wait count, the next DMA issued
+  // and slab s + 1's fragments read unconditionally -- no branch in front of the MFMAs (behind a
+  // conditional read the compiler's wait pass put an lgkmcnt(0) there, which waited for those
+  // reads before this slab's MFMAs).  The tail steps (the last STAGES or so) count exactly.
+  auto mma_issue = [&](int s, Frag<TMW, TNW> (&fc)[KSUB], bool iss) {
 #if RS_BIG_INTERLEAVE
     // the next DMA pieces issued between the k-step groups of this slab's MFMAs (one wave per
     // SIMD issues in order: a block of address VALU + DMA in front of the MFMAs would not
     // overlap them)
-    const bool iss = s + STAGES < nst;
     constexpr int NPO = 2 + (ZA ? 1 : 0) + (ZB ? 1 : 0);  // pieces per slab
 #pragma unroll
     for (int sub = 0; sub < KSUB; ++sub)
@@ -406,8 +411,12 @@ __global__ void __launch_bounds__(kThreads, NW == 8 ? 1 : 2) big_kernel(Args g) 
         for (int i = 0; i < TMW; ++i)
 #pragma unroll
           for (int jj = 0; jj < TNW; ++jj)
+#ifdef RS_BIG_NOMFMA  // diagnostic builds only: the load pipeline without its MFMAs
+            acc[i][jj][0] += fc[sub].a[i][u] * fc[sub].b[jj][u];
+#else
             acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(fc[sub].a[i][u], fc[sub].b[jj][u],
                                                               acc[i][jj], 0, 0, 0);
+#endif
         __builtin_amdgcn_sched_barrier(0);
         if (iss && u < NPO) {
           const int s2 = s + STAGES;
@@ -422,14 +431,34 @@ __global__ void __launch_bounds__(kThreads, NW == 8 ? 1 : 2) big_kernel(Args g) 
         __builtin_amdgcn_sched_barrier(0);
       }
 #else
-    if (s + STAGES < nst) issue(s + STAGES);
+    if (iss) issue(s + STAGES);
     mma(fc);
 #endif
+  };
+  auto steady = [&](int s, Frag<TMW, TNW> (&fc)[KSUB], Frag<TMW, TNW> (&fn)[KSUB], FY (&yn)[KSUB]) {
+    vm_wait_c<IPS * (STAGES - 2)>();  // slab s + 1 landed (this wave's DMAs)
+    lds_sync();                        // ... every wave's; slot s free
+    read(s + 1, fn, yn);
+    mma_issue(s, fc, true);
+    zform(fn, yn);
+  };
+  auto tail_step = [&](int s, Frag<TMW, TNW> (&fc)[KSUB], Frag<TMW, TNW> (&fn)[KSUB], FY (&yn)[KSUB]) {
+    const bool more = s + 1 < nst;
+    const int issued = s + STAGES < nst ? s + STAGES : nst;
+    if (more) vm_wait_n(IPS * (issued - s - 2));
+    lds_sync();
+    if (more) read(s + 1, fn, yn);
+    mma_issue(s, fc, s + STAGES < nst);
     if (more) zform(fn, yn);
   };
-  for (int s = 0; s < nst; s += 2) {
-    body(s, f0, f1, y1);
-    if (s + 1 < nst) body(s + 1, f1, f0, y0);
+  int s = 0;
+  for (; s + 1 + STAGES < nst; s += 2) {
+    steady(s, f0, f1, y1);
+    steady(s + 1, f1, f0, y0);
+  }
+  for (; s < nst; s += 2) {
+    tail_step(s, f0, f1, y1);
+    if (s + 1 < nst) tail_step(s + 1, f1, f0, y0);
   }
 
   // ---- epilogue: lane (q, j) holds C[16-row tile + 4q + rr][16-col tile + j] ----
@@ -550,7 +579,12 @@ template <int AMODE, int BMODE, bool AV, bool BV, bool ZA, bool ZB>
 static int launch_t(hipStream_t s, const Plan& p, Args g) {
   g.tm = (int)cdiv(g.M, p.bm);
   g.tn = (int)cdiv(g.N, p.bn);
-  g.gm = 4;
+  static const int gm = [] {  // tile rows per group (tuning: RS_GEMM_BIG_GM; 0 = no XCD remap)
+    const char* e = getenv("RS_GEMM_BIG_GM");
+    return e ? atoi(e) : 4;
+  }();
+  g.gm = gm > 0 ? gm : 1;
+  g.xcd = gm > 0;
   g.rchunk = p.rchunk;
   const int64_t blocks = (int64_t)g.tm * g.tn * p.splits;
   if (blocks <= 0 || blocks > (1 << 30)) return 1;
@@ -629,6 +663,14 @@ static float* fwd_scratch(size_t floats, hipStream_t s) {
   return sl.buf;
 }
 
+bool wanted_fwd(int64_t M, int64_t N, int64_t K) {
+  static const bool on = [] {
+    const char* e = getenv("RS_GEMM_BIG");
+    return !e || atoi(e) != 0;
+  }();
+  return wanted(M, N, K) || (on && K >= 1024 && M * N * K >= ((int64_t)1 << 26));
+}
+
 int fwd(hipStream_t s, const float* X, int64_t M, int64_t K, int64_t ldx, const float* W,
         const float* bias, int64_t N, int act, float* Y, int64_t ldy) {
   Plan p = plan(M, N, K, true, false);
@@ -652,10 +694,14 @@ int fwd(hipStream_t s, const float* X, int64_t M, int64_t K, int64_t ldx, const 
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// From 2^29 multiply-adds the big kernels beat the round-4 engine on every configs 3 / 5 product;
+// between 2^26 and 2^29 only the forward with a long reduction (>= 1024: split-K fills the
+// chip) does -- the short-reduction shapes (2048 x 224 x 1152, 2048 x 528 x 400, 2048 x 832 x
+// 128) keep the engine (tools/r06_shapes.sh, profiles/r06/gemm/shapes.txt)
 bool wanted(int64_t m, int64_t n, int64_t k) {
   static const int64_t thr = [] {
     const char* e = getenv("RS_GEMM_BIG_MACS");
-    return e ? (int64_t)atoll(e) : ((int64_t)1 << 26);
+    return e ? (int64_t)atoll(e) : ((int64_t)1 << 29);
   }();
   static const bool on = [] {
     const char* e = getenv("RS_GEMM_BIG");

@@ -29,12 +29,14 @@ struct Args {
   int64_t Mreal;
   int64_t slab;      // EPI_PARTIAL: floats per split
   int tm, tn, gm;    // tile grid (set by the launcher)
+  int xcd;           // re-index blocks so each XCD takes a contiguous tile range
 };
 
 struct Plan { int bm, bn, splits; int64_t rchunk; int stages; };
 
 // the shapes that take these kernels (RS_GEMM_BIG=0 disables, RS_GEMM_BIG_MACS moves the bar)
 bool wanted(int64_t m, int64_t n, int64_t k);
+bool wanted_fwd(int64_t M, int64_t N, int64_t K);
 Plan plan(int64_t M, int64_t N, int64_t R, bool allow_split, bool z);
 // 0: launched; nonzero: not launched (unsupported tile / launch error)
 int launch(hipStream_t s, int form, const Plan& p, const Args& g);

@@ -35,6 +35,11 @@ class _Rec:
                 SEEN[("bwd_data", a[7], a[8], a[9], a[5])] += 1  # M, K, N, act
                 return fn(*a)
             return w
+        if name == "rs_dense_bwd":
+            def w(*a):
+                SEEN[("bwd", a[9], a[10], a[11], a[7])] += 1  # M, K, N, act
+                return fn(*a)
+            return w
         if name == "rs_dense_bwd_weight":
             def w(*a):
                 SEEN[("bwd_weight", a[8], a[9], a[10], a[7])] += 1  # M, K, N, act
@@ -94,6 +99,15 @@ def time_shape(kind, M, K, N, act):
         ours = t_us(lambda: call("rs_dense_bwd_data", s, ptr(dY), N, ptr(Y), N, act, ptr(Wt), M, K, N,
                                  ptr(dX), K, 0))
         blas = t_us(lambda: torch.mm(dY, Wt.t(), out=dX))
+    elif kind == "bwd":
+        dX = torch.empty(M, K, device=dev)
+        dW = torch.empty(K, N, device=dev)
+        db = torch.empty(N, device=dev)
+        wsn = int(lib.rs_dense_bwd_weight_workspace_floats(M, K, N))
+        ws = torch.empty(max(wsn, 1), device=dev)
+        ours = t_us(lambda: call("rs_dense_bwd", s, ptr(X), K, ptr(dY), N, ptr(Y), N, act, ptr(Wt), M,
+                                 K, N, ptr(dX), K, 0, ptr(dW), ptr(db), 0, ptr(ws), wsn))
+        blas = t_us(lambda: (torch.mm(dY, Wt.t(), out=dX), torch.mm(X.t(), dY, out=dW)))
     else:
         dW = torch.empty(K, N, device=dev)
         db = torch.empty(N, device=dev)
