@@ -32,6 +32,9 @@
 // per-sample-wave kernels (partials per wave, combined in wave order): deterministic, within fp32
 // rounding of them.
 #pragma once
+#ifndef RS_ILW_PRIO
+#define RS_ILW_PRIO 0
+#endif
 
 namespace rs_il {
 
@@ -143,6 +146,9 @@ __global__ void __launch_bounds__(kWideThreads, 2) wfwd_kernel(
   float* const PR = smem + lay.pr;
   const int tid = threadIdx.x;
   const int w = wave_id();
+#if RS_ILW_PRIO  // tuning builds: static priority for every other workgroup (all its waves)
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   const int F = C::EXACT ? C::FMAX : a.F;
   const uint64_t seed0 = rs_eff_seed(a.seed, a.seed_off);
 
