@@ -220,6 +220,11 @@ RS_API int rs_sequence_lookup_fwd(void* stream, const int64_t* ids, const int32_
 // differences).  Replicas stay identical because the cross-rank merge (rs_sparse_merge_rows)
 // is rank-ordered and atomic-free.
 // ---------------------------------------------------------------------------------------------
+#ifdef RS_PUSH_KO_FLUSH  // timing experiments only (tools/push_prof.sh): flush by plain stores
+#define RS_FLUSH_ADD(p, v) (*(p) = (v))
+#else
+#define RS_FLUSH_ADD(p, v) atomicAdd((p), (v))
+#endif
 __device__ __forceinline__ void claim_row(int32_t row, int32_t* flag, int32_t* touched,
                                           int32_t* n_touched, int32_t touched_cap) {
   if (atomicCAS(&flag[row], -1, -2) == -1) {
@@ -318,7 +323,7 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
       if (row < 0) continue;
       if (l == 0) scan_mark(flag, row);
       float* dst = grad_table + (int64_t)row * dim;
-      for (int e = l; e < dim; e += G) atomicAdd(dst + e, vals[slot * dim + e]);
+      for (int e = l; e < dim; e += G) RS_FLUSH_ADD(dst + e, vals[slot * dim + e]);
     }
     return;
   }
@@ -339,7 +344,11 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
       rw[u] = slot < cap ? keys[slot] : -1;
     }
 #pragma unroll
+#ifdef RS_PUSH_KO_CLAIM  // timing experiments only: no claim CASes
+    for (int u = 0; u < 4; ++u) old[u] = 0;
+#else
     for (int u = 0; u < 4; ++u) old[u] = rw[u] >= 0 ? atomicCAS(&flag[rw[u]], -1, -2) : 0;
+#endif
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int slot = s0 + u * blockDim.x;
@@ -357,7 +366,7 @@ __global__ void __launch_bounds__(1024) sparse_grad_accum_kernel(
       if (li >= 0 && base + li < touched_cap) touched[base + li] = row;
     }
     float* dst = grad_table + (int64_t)row * dim;
-    for (int e = l; e < dim; e += G) atomicAdd(dst + e, vals[slot * dim + e]);
+    for (int e = l; e < dim; e += G) RS_FLUSH_ADD(dst + e, vals[slot * dim + e]);
   }
 }
 
@@ -502,7 +511,7 @@ __global__ void __launch_bounds__(kThreads) push_elect_kernel(
     const int32_t row = keys[slot];
     if (row < 0) continue;
     float* dst = grad_table + (int64_t)row * dim;
-    for (int e = l2; e < dim; e += G2) atomicAdd(dst + e, vals[slot * dim + e]);
+    for (int e = l2; e < dim; e += G2) RS_FLUSH_ADD(dst + e, vals[slot * dim + e]);
   }
   if (ws_cnt) {
     __syncthreads();
@@ -565,6 +574,18 @@ inline int64_t grid_blocks(int64_t B, int F) {
   return ((B + t - 1) / t) * (int64_t)F;
 }
 
+// this device's per-block LDS (queried once)
+inline int64_t lds_per_block() {
+  static const int64_t v = [] {
+    int dev = 0, x = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+      return (int64_t)64 * 1024;
+    return (int64_t)x;
+  }();
+  return v;
+}
+
 }  // namespace rs_push
 
 RS_API int64_t rs_sparse_push_workspace_bytes(int64_t B, int F) {
@@ -580,15 +601,9 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
                                         int64_t workspace_bytes) {
   using namespace rs_push;
   static const bool elect_off = getenv("RS_PUSH_NO_ELECT") != nullptr;  // A/B: the CAS push
-  // the election push's LDS hash must fit this device's per-block LDS (queried once): larger
-  // shapes, or a part with less LDS, take the CAS push
-  static const int64_t lds_max = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
-      return (int64_t)64 * 1024;
-    return (int64_t)v;
-  }();
+  // the election push's LDS hash must fit this device's per-block LDS: larger shapes, or a part
+  // with less LDS, take the CAS push
+  const int64_t lds_max = lds_per_block();
   const bool ok_shape = !elect_off && !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
                         ((uintptr_t)dout & 15) == 0 && (int64_t)lds_bytes(dim) <= lds_max &&
                         B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;
@@ -626,7 +641,6 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
   return rs_status_after_launch();
 }
 
-
 RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* offsets,
                                      int64_t B, int F, const float* dout, int64_t dout_ld,
                                      int64_t dout_fstride, int dim, int combiner,
@@ -646,7 +660,10 @@ RS_API int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const in
   // often (config-4 history push 55 -> 36 us).  Few fields (config 2's 26 disjoint ranges) keep
   // the 64 KB table: more blocks in flight beat fewer flushes there.
   int cap = 1024;
-  const size_t lds_budget = (!offsets && F >= 32) ? 150 * 1024 : 64 * 1024;
+#ifndef RS_PUSH_MH_BUDGET  // tuning builds only: the multi-hot table's LDS budget (KB)
+#define RS_PUSH_MH_BUDGET 64
+#endif
+  const size_t lds_budget = (!offsets && F >= 32) ? 150 * 1024 : (size_t)RS_PUSH_MH_BUDGET * 1024;
   if (lds_budget > 64 * 1024) cap = 4096;
   while (cap > 32 && (size_t)cap * (dim + 2) * 4 > lds_budget) cap >>= 1;
   const int tile = cap / 2;

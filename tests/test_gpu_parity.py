@@ -150,6 +150,58 @@ def test_single_hot_election_push(mode):
     assert bool((t.flag == -1).all()) and float(t.grad.abs().max()) == 0.0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["list", "scan"])
+@pytest.mark.parametrize("shape", ["short", "long"])
+def test_multi_hot_push(mode, shape):
+    """Multi-hot pushes (rs_sparse_grad_accumulate with offsets): Zipf-hot rows aggregated per
+    block in the LDS hash; "long" lists (up to 1500 ids per segment) overflow a block's table, so
+    those occurrences take the direct global-atomic path and its CAS claims.  Mean / sqrtn
+    scaling, empty segments and padded (-1) ids; two pushes per step and two steps.  Touched
+    list duplicate-free and equal to the oracle row set, gradients equal the oracle sums, flags
+    clean after the optimizer."""
+    from recommendsystem_amd.embedding import SparseAdam, SparseTable
+    rng = np.random.default_rng(5)
+    dim, rows_n = 8, 5000
+    t = SparseTable(rows_n, dim, SparseAdam(1e-2), device=DEV, seed=4)
+    t.mode = mode
+    sizes = ((1, 300, 7), (2, 90, 3)) if shape == "short" else ((1, 40, 3), (2, 12, 2))
+    hi = 4 if shape == "short" else 1500
+    for step in range(2):
+        gsum = np.zeros((rows_n, dim))
+        for combiner, B, F in sizes:
+            lens = rng.integers(0, hi, size=B * F)
+            offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+            ids = np.minimum(rng.zipf(1.2, size=int(offs[-1])) - 1, rows_n - 1).astype(np.int32)
+            ids[rng.uniform(size=ids.size) < 0.05] = -1
+            d = torch.randn(B, F * dim, device=DEV)
+            t.accumulate(torch.from_numpy(ids).to(DEV), torch.from_numpy(offs).to(DEV), B, F, d,
+                         F * dim, dim, combiner)
+            seg = np.repeat(np.arange(B * F), lens)
+            n = np.maximum(lens, 1).astype(np.float64)
+            sc = 1.0 / n if combiner == 1 else 1.0 / np.sqrt(n)
+            contrib = sc[seg][:, None] * _np(d).reshape(B * F, dim).astype(np.float64)[seg]
+            ok = ids >= 0
+            np.add.at(gsum, ids[ok], contrib[ok])
+            touched_rows = set(np.unique(ids[ok]).tolist())
+            gref_rows = touched_rows if combiner == 1 else gref_rows | touched_rows
+        gref = {r: gsum[r] for r in gref_rows}
+        torch.cuda.synchronize()
+        if mode == "list":
+            n = int(t.n_touched[0].item())
+            lst = t.touched[:n].cpu().numpy().tolist()
+            assert len(lst) == len(set(lst)), "a row was claimed twice"
+            assert set(lst) == set(gref)
+        else:
+            assert _scan_marked(t.flag, t.rows) == set(gref)
+        G = t.grad.cpu().numpy()
+        for r, g in gref.items():
+            assert_close(G[r], g, 1e-4, 1e-4, what=f"grad row {r}")
+        t.step()
+        torch.cuda.synchronize()
+        assert bool((t.flag == -1).all()) and float(t.grad.abs().max()) == 0.0
+
+
 def _scan_marked(flag, nrows):
     """Rows marked by a scan-mode push (flag = -2; clean = -1)."""
     f = flag.cpu().numpy()

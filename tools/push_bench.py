@@ -7,6 +7,7 @@ the sparse optimizer run in between (flags / gradient rows reset as in a trainin
           Zipf(1.1), lengths U{1..100} (padded positions row -1), list mode
   c4_q    config 4: the query push, B = 1024 single-hot
   c2      config 2: B = 4096 x 26 single-hot fields over 26 x 100 k, dim 16, scan mode
+  c3_scan config 3's push in scan mode (no claims)
   c5      config 5: B = 2048 x 91 single-hot hashed fields over one 10 M x 32 table, list mode
 
 python tools/push_bench.py [--reps N] [--only c3,c4_hist]  -> one JSON line
@@ -91,7 +92,14 @@ def case_c4_hist_scan(rng, dev):
     return t, fn, ids
 
 
-CASES = {"c5": case_c5, "c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2,
+def case_c3_scan(rng, dev):
+    """config 3's push in scan mode (no claims: the claim cost by difference)"""
+    t, fn, rows = case_c3(rng, dev)
+    t.mode = "scan"
+    return t, fn, rows
+
+
+CASES = {"c3_scan": case_c3_scan, "c5": case_c5, "c3": case_c3, "c4_hist": case_c4_hist, "c4_q": case_c4_q, "c2": case_c2,
          "c4_hist_scan": case_c4_hist_scan}
 
 
