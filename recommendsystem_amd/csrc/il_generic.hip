@@ -40,18 +40,19 @@ constexpr int FMAXG = 256;
 constexpr size_t kLdsMax = 160 * 1024;
 
 struct Layout {
-  int PS, OS;                            // row strides: Q|K|V|R rows, U-wide rows
+  int XS, PS, OS;                        // row strides: x rows, Q|K|V|R rows, U-wide rows
   int QT;                                // query rows per attention tile
   int xs, P, O, G, DK, DV, S, PT, rst, hst, acc, rows, total;  // float offsets
 };
 
 __host__ __device__ inline Layout make_layout(int F, int E, int U, int H, int QT, bool bwd) {
   Layout l;
+  l.XS = E + 1;
   l.PS = 4 * U + 1;
   l.OS = U + 1;
   l.QT = QT;
   int o = 0;
-  l.xs = o; o += F * E;  // (iterations > 0 have E == U)
+  l.xs = o; o += F * l.XS;  // (iterations > 0 have E == U)
   l.P = o; o += F * l.PS;
   l.O = o; o += F * l.OS;
   l.G = o; if (bwd) o += F * l.OS;
@@ -109,25 +110,81 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Q|K|V|R = relu(x W + b) for every (row, column); one fixed fmaf order (forward == backward)
-__device__ __forceinline__ void project(const GArgs& a, const float* xs, float* P) {
-  const int NC = 4 * a.U, XS = a.E;
-  for (int idx = threadIdx.x; idx < a.F * NC; idx += NT) {
-    const int f = idx / NC, c = idx - f * NC;
-    const float* xr = xs + f * XS;
-    float acc = a.bias[c];
-    for (int e = 0; e < a.E; ++e) acc = fmaf(xr[e], a.W[e * NC + c], acc);
-    P[f * a.lay.PS + c] = fmaxf(acc, 0.f);
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// out(m, n) = init + sum_k A(m, k) B(k, n) over an M x N output in 16 x 16 tiles spread over the
+// block's waves (v_mfma_f32_16x16x4_f32, k ascending within each of NACC interleaved chains that
+// are summed at the end), with A(m, k) = a[m ams + k aks], B(k, n) = b[k bks + n bns] read from
+// LDS (or the GS slab / global W); rows, columns and k past the extents read 0.  init(n) seeds
+// every chain-0 row of column n; epi(m, n, v) runs once per in-range output element.
+template <int NACC, class Init, class Epi>
+__device__ __forceinline__ void mm16(const float* a, int ams, int aks, const float* b, int bks,
+                                     int bns, int M, int N, int K, Init init, Epi epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tm = (M + 15) >> 4, tn = (N + 15) >> 4;
+  const int r16 = lane & 15, kq = lane >> 4;
+  for (int t = w; t < tm * tn; t += NT / 64) {
+    const int i0 = (t / tn) << 4, j0 = (t % tn) << 4;
+    const int ar = i0 + r16, bc = j0 + r16;
+    const bool aok = ar < M, bok = bc < N;
+    const float* ap = a + (aok ? ar : 0) * ams + kq * aks;
+    const float* bp = b + (bok ? bc : 0) * bns + kq * bks;
+    f32x4 c[NACC];
+    const float c0 = init(bok ? bc : 0);
+    c[0] = f32x4{c0, c0, c0, c0};
+#pragma unroll
+    for (int q = 1; q < NACC; ++q) c[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int k0 = 0;
+    for (; k0 + 4 * NACC <= K; k0 += 4 * NACC) {
+      float av[NACC], bv[NACC];
+#pragma unroll
+      for (int q = 0; q < NACC; ++q) {
+        av[q] = aok ? ap[(k0 + 4 * q) * aks] : 0.f;
+        bv[q] = bok ? bp[(k0 + 4 * q) * bks] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < NACC; ++q)
+        c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bv[q], c[q], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) {  // the tail: k0 + 4 q + kq may pass K
+      if (k0 + 4 * q >= K) break;
+      const bool kok = k0 + 4 * q + kq < K;
+      const float av = (aok && kok) ? ap[(k0 + 4 * q) * aks] : 0.f;
+      const float bv = (bok && kok) ? bp[(k0 + 4 * q) * bks] : 0.f;
+      c[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, c[q], 0, 0, 0);
+    }
+    f32x4 sum = c[0];
+#pragma unroll
+    for (int q = 1; q < NACC; ++q) sum += c[q];
+    if (bok)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = i0 + 4 * kq + r;
+        if (m < M) epi(m, bc, sum[r]);
+      }
   }
 }
 
-// scaled score (base-2 domain) of query i, key j, head h
-__device__ __forceinline__ float score2(const GArgs& a, const float* P, int i, int j, int h) {
-  const float* q = P + i * a.lay.PS + h * a.DH;
-  const float* k = P + j * a.lay.PS + a.U + h * a.DH;
-  float s = 0.f;
-  for (int d = 0; d < a.DH; ++d) s = fmaf(q[d], k[d], s);
-  return s * a.sc2;
+__device__ __forceinline__ float zero_init(int) { return 0.f; }
+
+// Q|K|V|R = relu(x W + b) for every (row, column) on the matrix cores: each output is bias + one
+// chain over e in ascending order (forward == backward recompute, so the recomputed ReLU masks
+// are the forward's)
+__device__ __forceinline__ void project(const GArgs& a, const float* xs, float* P) {
+  const int NC = 4 * a.U, PS = a.lay.PS;
+  const float* bias = a.bias;
+  mm16<1>(xs, a.lay.XS, 1, a.W, NC, 1, a.F, NC, a.E, [&](int n) { return bias[n]; },
+          [&](int m, int n, float v) { P[m * PS + n] = fmaxf(v, 0.f); });
+}
+
+// scaled scores (base-2 domain) of head h, query rows [i0, i0 + nq) x all keys -> S[nq][F]
+__device__ __forceinline__ void scores(const GArgs& a, const float* P, float* S, int h, int i0,
+                                       int nq) {
+  const int F = a.F, PS = a.lay.PS;
+  const float sc2 = a.sc2;
+  mm16<2>(P + i0 * PS + h * a.DH, PS, 1, P + a.U + h * a.DH, 1, PS, nq, F, a.DH, zero_init,
+          [&](int m, int n, float v) { S[m * F + n] = v * sc2; });
 }
 
 // attention forward of head h, query rows [i0, i0 + nq): O rows (and, with hst, the row stats
@@ -138,10 +195,7 @@ __device__ void attn_tile_fwd(const GArgs& a, float* sm, int h, int i0, int nq, 
   const int F = a.F;
   float* P = sm + l.P;
   float* S = sm + l.S;
-  for (int idx = threadIdx.x; idx < nq * F; idx += NT) {
-    const int ii = idx / F, j = idx - ii * F;
-    S[idx] = score2(a, P, i0 + ii, j, h);
-  }
+  scores(a, P, S, h, i0, nq);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int ii = w; ii < nq; ii += NT / 64) {
@@ -169,15 +223,10 @@ __device__ void attn_tile_fwd(const GArgs& a, float* sm, int h, int i0, int nq, 
     }
   }
   __syncthreads();
-  float* O = sm + l.O;
-  for (int idx = threadIdx.x; idx < nq * a.DH; idx += NT) {
-    const int ii = idx / a.DH, d = idx - ii * a.DH;
-    const float* pr = S + ii * F;
-    const float* v = P + 2 * a.U + h * a.DH + d;
-    float o = 0.f;
-    for (int j = 0; j < F; ++j) o = fmaf(pr[j], v[j * l.PS], o);
-    O[(i0 + ii) * l.OS + h * a.DH + d] = o;
-  }
+  float* O = sm + l.O + i0 * l.OS + h * a.DH;
+  const int OS = l.OS;
+  mm16<1>(S, F, 1, P + 2 * a.U + h * a.DH, l.PS, 1, nq, a.DH, F, zero_init,
+          [&](int m, int n, float v) { O[m * OS + n] = v; });
   __syncthreads();
 }
 
@@ -191,7 +240,7 @@ __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
   const Layout& l = a.lay;
-  const int F = a.F, U = a.U, E = a.E, XS = E;
+  const int F = a.F, U = a.U, E = a.E, XS = l.XS;
   float* xs = sm + l.xs;
   float* P = sm + l.P;
   float* O = sm + l.O;
@@ -260,7 +309,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
   const Layout& l = a.lay;
-  const int F = a.F, U = a.U, E = a.E, DH = a.DH, NC = 4 * U, XS = E;
+  const int F = a.F, U = a.U, E = a.E, DH = a.DH, NC = 4 * U, XS = l.XS, PS = l.PS, OS = l.OS;
   const int NPARAM = E * NC + NC + 2 * U;
   float* xs = sm + l.xs;
   float* P = sm + l.P;
@@ -364,14 +413,16 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
       for (int h = 0; h < a.H; ++h) {
         for (int i0 = 0; i0 < F; i0 += l.QT) {
           const int nq = F - i0 < l.QT ? F - i0 : l.QT;
+          // scores and dP = dO V^T on the matrix cores, then P, dS = P (dP - D) elementwise
+          scores(a, P, S, h, i0, nq);
+          mm16<2>(G + i0 * OS + h * DH, OS, 1, P + 2 * U + h * DH, 1, PS, nq, F, DH, zero_init,
+                  [&](int m, int n, float v) { PT[m * F + n] = v; });
+          __syncthreads();
           for (int idx = threadIdx.x; idx < nq * F; idx += NT) {
             const int ii = idx / F, j = idx - ii * F, i = i0 + ii;
             const float* hs = sm + l.hst + (h * F + i) * 4;
-            const float p = __builtin_amdgcn_exp2f(score2(a, P, i, j, h) - hs[0]) * hs[1];
-            const float* go = G + i * l.OS + h * DH;
-            const float* vv = P + j * l.PS + 2 * U + h * DH;
-            float dp = 0.f;
-            for (int k = 0; k < DH; ++k) dp = fmaf(go[k], vv[k], dp);
+            const float p = __builtin_amdgcn_exp2f(S[idx] - hs[0]) * hs[1];
+            float dp = PT[idx];
             float pd = p;
             if (a.drop) {
               const bool keep = dropout_keep_k(kb, (uint32_t)h, (uint32_t)i, (uint32_t)j, a.drop_rate);
@@ -382,56 +433,41 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
             PT[idx] = pd;
           }
           __syncthreads();
-          for (int idx = threadIdx.x; idx < nq * DH; idx += NT) {  // dQ rows of the tile
-            const int ii = idx / DH, d = idx - ii * DH;
-            const float* ds = S + ii * F;
-            const float* kk = P + U + h * DH + d;
-            float s = 0.f;
-            for (int j = 0; j < F; ++j) s = fmaf(ds[j], kk[j * l.PS], s);
-            O[(i0 + ii) * l.OS + h * DH + d] = s * a.inv_sdh;
-          }
-          for (int idx = threadIdx.x; idx < F * DH; idx += NT) {  // dK, dV over the tile's rows
-            const int j = idx / DH, d = idx - j * DH;
-            float sk = 0.f, sv = 0.f;
-            for (int ii = 0; ii < nq; ++ii) {
-              sk = fmaf(S[ii * F + j], P[(i0 + ii) * l.PS + h * DH + d], sk);
-              sv = fmaf(PT[ii * F + j], G[(i0 + ii) * l.OS + h * DH + d], sv);
-            }
-            DK[j * l.OS + h * DH + d] += sk * a.inv_sdh;
-            DV[j * l.OS + h * DH + d] += sv;
-          }
+          const float isd = a.inv_sdh;
+          // dQ rows of the tile (into O: dead after D), dK / dV over the tile's query rows
+          float* dq = O + i0 * OS + h * DH;
+          mm16<1>(S, F, 1, P + U + h * DH, PS, 1, nq, DH, F, zero_init,
+                  [&](int m, int n, float v) { dq[m * OS + n] = v * isd; });
+          float* dk = DK + h * DH;
+          mm16<1>(S, 1, F, P + i0 * PS + h * DH, PS, 1, F, DH, nq, zero_init,
+                  [&](int m, int n, float v) { dk[m * OS + n] += v * isd; });
+          float* dv = DV + h * DH;
+          mm16<1>(PT, 1, F, G + i0 * OS + h * DH, OS, 1, F, DH, nq, zero_init,
+                  [&](int m, int n, float v) { dv[m * OS + n] += v; });
           __syncthreads();
         }
       }
-      // ---- dZ = [dQ | dK | dV | dR] through the projection ReLUs ----
+      // ---- dZ = [dQ | dK | dV | dR] through the projection ReLUs, into P's columns (Q, K, V are
+      //      dead now): one [F, 4U] operand for dW and dX ----
       for (int idx = threadIdx.x; idx < F * 3 * U; idx += NT) {
         const int f = idx / (3 * U), c = idx - f * 3 * U;
-        float* dst = (c < U ? O : c < 2 * U ? DK : DV) + f * l.OS + (c % U);
-        if (!(P[f * l.PS + c] > 0.f)) *dst = 0.f;
+        const float* src = (c < U ? O : c < 2 * U ? DK : DV) + f * OS + (c % U);
+        float* pz = P + f * PS + c;
+        *pz = *pz > 0.f ? *src : 0.f;
       }
       __syncthreads();
-      auto dzp = [&](int f, int c) -> float {
-        const int g = c / U;
-        return g == 3 ? P[f * l.PS + c] : (g == 0 ? O : g == 1 ? DK : DV)[f * l.OS + c - g * U];
-      };
-      for (int idx = threadIdx.x; idx < E * NC; idx += NT) {  // dW (block partial, RMW)
-        const int e = idx / NC, c = idx - e * NC;
-        float s = 0.f;
-        for (int f = 0; f < F; ++f) s = fmaf(xs[f * XS + e], dzp(f, c), s);
-        part[idx] += s;
-      }
+      mm16<1>(xs, 1, XS, P, PS, 1, E, NC, F, zero_init,  // dW (block partial, RMW)
+              [&](int m, int n, float v) { part[m * NC + n] += v; });
       for (int c = threadIdx.x; c < NC; c += NT) {
         float s = 0.f;
-        for (int f = 0; f < F; ++f) s += dzp(f, c);
+        for (int f = 0; f < F; ++f) s += P[f * PS + c];
         part[E * NC + c] += s;
       }
-      for (int idx = threadIdx.x; idx < F * E; idx += NT) {  // dX = dZ W^T
-        const int f = idx / E, e = idx - f * E;
-        const float* wr = a.W + e * NC;
-        float s = 0.f;
-        for (int c = 0; c < NC; ++c) s = fmaf(dzp(f, c), wr[c], s);
+      // dX = dZ W^T
+      mm16<4>(P, PS, 1, a.W, 1, NC, F, E, NC, zero_init, [&](int f, int e, float s) {
+        const int idx = f * E + e;
         if (it > 0) {
-          G[f * l.OS + e] = s;  // E == U: dY of iteration it - 1
+          G[f * OS + e] = s;  // E == U: dY of iteration it - 1
         } else if (a.push_table) {
           const int32_t row = rows[f];
           if (row >= 0) {
@@ -443,7 +479,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
           float* d = a.dx + b * F * E + idx;
           *d = a.dx_accumulate ? *d + s : s;
         }
-      }
+      });
       __syncthreads();
     }
   }
