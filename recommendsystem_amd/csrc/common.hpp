@@ -40,8 +40,12 @@ const int64_t* rs_seed_offset_now();
 // launch, so the compiler may hoist / merge it.
 __device__ __forceinline__ uint64_t rs_eff_seed(uint64_t seed, uint64_t off_addr) {
   if (!off_addr) return seed;
+  // uniform by construction (a kernel argument); readfirstlane pins it to SGPRs even where
+  // register pressure would otherwise leave it in VGPRs ("s" constraint on a VGPR pair)
+  const uint64_t sa = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(off_addr >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)off_addr);
   uint64_t v;
-  asm("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(off_addr));
+  asm("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(sa));
   return seed + v * 0x9E3779B97F4A7C15ull;
 }
 

@@ -35,7 +35,11 @@
 namespace rs_il {
 namespace gen {
 
-constexpr int NT = 256;
+// threads per workgroup: 256, or 512 where one sample's working set takes more than half the LDS
+// (at most two workgroups per CU either way, so twice the waves hide the MFMA / LDS latencies:
+// ctor defaults backward 1093 -> 833 us, forward 203 -> 156 us; shapes with several workgroups
+// per CU measured 5-15 % slower at 512, profiles/r06/generic/)
+constexpr int kBigLds = 64 * 1024;
 constexpr int FMAXG = 256;
 constexpr size_t kLdsMax = 160 * 1024;
 
@@ -117,7 +121,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // are summed at the end), with A(m, k) = a[m ams + k aks], B(k, n) = b[k bks + n bns] read from
 // LDS (or the GS slab / global W); rows, columns and k past the extents read 0.  init(n) seeds
 // every chain-0 row of column n; epi(m, n, v) runs once per in-range output element.
-template <int NACC, class Init, class Epi>
+template <int NACC, int NT, class Init, class Epi>
 __device__ __forceinline__ void mm16(const float* a, int ams, int aks, const float* b, int bks,
                                      int bns, int M, int N, int K, Init init, Epi epi) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -168,34 +172,38 @@ __device__ __forceinline__ void mm16(const float* a, int ams, int aks, const flo
 
 __device__ __forceinline__ float zero_init(int) { return 0.f; }
 
+
 // Q|K|V|R = relu(x W + b) for every (row, column) on the matrix cores: each output is bias + one
 // chain over e in ascending order (forward == backward recompute, so the recomputed ReLU masks
 // are the forward's)
+template <int NT>
 __device__ __forceinline__ void project(const GArgs& a, const float* xs, float* P) {
   const int NC = 4 * a.U, PS = a.lay.PS;
   const float* bias = a.bias;
-  mm16<1>(xs, a.lay.XS, 1, a.W, NC, 1, a.F, NC, a.E, [&](int n) { return bias[n]; },
+  mm16<1, NT>(xs, a.lay.XS, 1, a.W, NC, 1, a.F, NC, a.E, [&](int n) { return bias[n]; },
           [&](int m, int n, float v) { P[m * PS + n] = fmaxf(v, 0.f); });
 }
 
 // scaled scores (base-2 domain) of head h, query rows [i0, i0 + nq) x all keys -> S[nq][F]
+template <int NT>
 __device__ __forceinline__ void scores(const GArgs& a, const float* P, float* S, int h, int i0,
                                        int nq) {
   const int F = a.F, PS = a.lay.PS;
   const float sc2 = a.sc2;
-  mm16<2>(P + i0 * PS + h * a.DH, PS, 1, P + a.U + h * a.DH, 1, PS, nq, F, a.DH, zero_init,
+  mm16<2, NT>(P + i0 * PS + h * a.DH, PS, 1, P + a.U + h * a.DH, 1, PS, nq, F, a.DH, zero_init,
           [&](int m, int n, float v) { S[m * F + n] = v * sc2; });
 }
 
 // attention forward of head h, query rows [i0, i0 + nq): O rows (and, with hst, the row stats
 // {scaled max, 1 / sum} into hst[(h F + i) 4 + 0..1])
+template <int NT>
 __device__ void attn_tile_fwd(const GArgs& a, float* sm, int h, int i0, int nq, uint32_t kb,
                               bool stats) {
   const Layout& l = a.lay;
   const int F = a.F;
   float* P = sm + l.P;
   float* S = sm + l.S;
-  scores(a, P, S, h, i0, nq);
+  scores<NT>(a, P, S, h, i0, nq);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int ii = w; ii < nq; ii += NT / 64) {
@@ -225,7 +233,7 @@ __device__ void attn_tile_fwd(const GArgs& a, float* sm, int h, int i0, int nq, 
   __syncthreads();
   float* O = sm + l.O + i0 * l.OS + h * a.DH;
   const int OS = l.OS;
-  mm16<1>(S, F, 1, P + 2 * a.U + h * a.DH, l.PS, 1, nq, a.DH, F, zero_init,
+  mm16<1, NT>(S, F, 1, P + 2 * a.U + h * a.DH, l.PS, 1, nq, a.DH, F, zero_init,
           [&](int m, int n, float v) { O[m * OS + n] = v; });
   __syncthreads();
 }
@@ -235,7 +243,7 @@ __device__ __forceinline__ uint32_t layer_key(const GArgs& a, int it, int64_t b)
                 : 0u;
 }
 
-template <bool GS>
+template <bool GS, int NT>
 __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
@@ -261,12 +269,12 @@ __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
     }
     __syncthreads();
     for (int it = 0; it < a.L; ++it) {
-      project(a, xs, P);
+      project<NT>(a, xs, P);
       __syncthreads();
       const uint32_t kb = layer_key(a, it, b);
       for (int h = 0; h < a.H; ++h)
         for (int i0 = 0; i0 < F; i0 += l.QT)
-          attn_tile_fwd(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, false);
+          attn_tile_fwd<NT>(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, false);
       // LN statistics per row
       for (int f = threadIdx.x; f < F; f += NT) {
         float mean = 0.f;
@@ -304,7 +312,7 @@ __global__ void __launch_bounds__(NT) fwd_kernel(GArgs a) {
   }
 }
 
-template <bool GS>
+template <bool GS, int NT>
 __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   float* const sm = GS ? a.gscratch + (int64_t)blockIdx.x * a.lay.total : lds_;
@@ -340,12 +348,12 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
         for (int f = threadIdx.x; f < F; f += NT) rows[f] = a.push_rows[b * F + f];
       for (int idx = threadIdx.x; idx < F * l.OS; idx += NT) { DK[idx] = 0.f; DV[idx] = 0.f; }
       __syncthreads();
-      project(a, xs, P);
+      project<NT>(a, xs, P);
       __syncthreads();
       const uint32_t kb = layer_key(a, it, b);
       for (int h = 0; h < a.H; ++h)
         for (int i0 = 0; i0 < F; i0 += l.QT)
-          attn_tile_fwd(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, true);
+          attn_tile_fwd<NT>(a, sm, h, i0, F - i0 < l.QT ? F - i0 : l.QT, kb, true);
       // ---- epilogue backward: LN, ReLU, residual ----
       for (int f = threadIdx.x; f < F; f += NT) {
         float mean = 0.f;
@@ -414,8 +422,8 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
         for (int i0 = 0; i0 < F; i0 += l.QT) {
           const int nq = F - i0 < l.QT ? F - i0 : l.QT;
           // scores and dP = dO V^T on the matrix cores, then P, dS = P (dP - D) elementwise
-          scores(a, P, S, h, i0, nq);
-          mm16<2>(G + i0 * OS + h * DH, OS, 1, P + 2 * U + h * DH, 1, PS, nq, F, DH, zero_init,
+          scores<NT>(a, P, S, h, i0, nq);
+          mm16<2, NT>(G + i0 * OS + h * DH, OS, 1, P + 2 * U + h * DH, 1, PS, nq, F, DH, zero_init,
                   [&](int m, int n, float v) { PT[m * F + n] = v; });
           __syncthreads();
           for (int idx = threadIdx.x; idx < nq * F; idx += NT) {
@@ -436,13 +444,13 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
           const float isd = a.inv_sdh;
           // dQ rows of the tile (into O: dead after D), dK / dV over the tile's query rows
           float* dq = O + i0 * OS + h * DH;
-          mm16<1>(S, F, 1, P + U + h * DH, PS, 1, nq, DH, F, zero_init,
+          mm16<1, NT>(S, F, 1, P + U + h * DH, PS, 1, nq, DH, F, zero_init,
                   [&](int m, int n, float v) { dq[m * OS + n] = v * isd; });
           float* dk = DK + h * DH;
-          mm16<1>(S, 1, F, P + i0 * PS + h * DH, PS, 1, F, DH, nq, zero_init,
+          mm16<1, NT>(S, 1, F, P + i0 * PS + h * DH, PS, 1, F, DH, nq, zero_init,
                   [&](int m, int n, float v) { dk[m * OS + n] += v * isd; });
           float* dv = DV + h * DH;
-          mm16<1>(PT, 1, F, G + i0 * OS + h * DH, OS, 1, F, DH, nq, zero_init,
+          mm16<1, NT>(PT, 1, F, G + i0 * OS + h * DH, OS, 1, F, DH, nq, zero_init,
                   [&](int m, int n, float v) { dv[m * OS + n] += v; });
           __syncthreads();
         }
@@ -456,7 +464,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
         *pz = *pz > 0.f ? *src : 0.f;
       }
       __syncthreads();
-      mm16<1>(xs, 1, XS, P, PS, 1, E, NC, F, zero_init,  // dW (block partial, RMW)
+      mm16<1, NT>(xs, 1, XS, P, PS, 1, E, NC, F, zero_init,  // dW (block partial, RMW)
               [&](int m, int n, float v) { part[m * NC + n] += v; });
       for (int c = threadIdx.x; c < NC; c += NT) {
         float s = 0.f;
@@ -464,7 +472,7 @@ __global__ void __launch_bounds__(NT) bwd_kernel(GArgs a) {
         part[E * NC + c] += s;
       }
       // dX = dZ W^T
-      mm16<4>(P, PS, 1, a.W, 1, NC, F, E, NC, zero_init, [&](int f, int e, float s) {
+      mm16<4, NT>(P, PS, 1, a.W, 1, NC, F, E, NC, zero_init, [&](int f, int e, float s) {
         const int idx = f * E + e;
         if (it > 0) {
           G[f * OS + e] = s;  // E == U: dY of iteration it - 1
@@ -550,11 +558,14 @@ int il_generic_fwd(const FwdReq& q) {
     const int64_t grid = q.B < kGsGrid ? q.B : kGsGrid;
     a.gscratch = gs_scratch((size_t)grid * a.lay.total, q.stream);
     if (!a.gscratch) return RS_ERR_UNSUPPORTED;
-    fwd_kernel<true><<<(int)grid, NT, 0, q.stream>>>(a);
+    fwd_kernel<true, 256><<<(int)grid, 256, 0, q.stream>>>(a);
     return rs_status_after_launch();
   }
   const int64_t grid = q.B < 4096 ? q.B : 4096;
-  fwd_kernel<false><<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+  if ((size_t)a.lay.total * 4 > kBigLds)
+    fwd_kernel<false, 512><<<(int)grid, 512, (size_t)a.lay.total * 4, q.stream>>>(a);
+  else
+    fwd_kernel<false, 256><<<(int)grid, 256, (size_t)a.lay.total * 4, q.stream>>>(a);
   return rs_status_after_launch();
 }
 
@@ -582,9 +593,12 @@ int il_generic_bwd(const BwdReq& q) {
   if (gs) {
     a.gscratch = gs_scratch((size_t)grid * a.lay.total, q.stream);
     if (!a.gscratch) return RS_ERR_UNSUPPORTED;
-    bwd_kernel<true><<<(int)grid, NT, 0, q.stream>>>(a);
+    bwd_kernel<true, 256><<<(int)grid, 256, 0, q.stream>>>(a);
   } else {
-    bwd_kernel<false><<<(int)grid, NT, (size_t)a.lay.total * 4, q.stream>>>(a);
+    if ((size_t)a.lay.total * 4 > kBigLds)
+      bwd_kernel<false, 512><<<(int)grid, 512, (size_t)a.lay.total * 4, q.stream>>>(a);
+    else
+      bwd_kernel<false, 256><<<(int)grid, 256, (size_t)a.lay.total * 4, q.stream>>>(a);
   }
   int st = rs_status_after_launch();
   if (st || !q.dparams) return st;
