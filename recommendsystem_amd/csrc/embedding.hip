@@ -476,6 +476,10 @@ __global__ void __launch_bounds__(kThreads) push_elect_kernel(
                                  : reinterpret_cast<const float4*>(
                                        dout + (b0 + i) * dout_ld + (int64_t)f * dout_fstride)[e4];
         float* d = vals + slot[u] * dim + 4 * e4;
+#ifdef RS_PUSH_KO_LDSADD  // timing experiments only: the LDS adds as plain LDS stores
+        *reinterpret_cast<float4*>(d) = make_float4(t.x * sc, t.y * sc, t.z * sc, t.w * sc);
+        continue;
+#endif
         atomicAdd(d + 0, t.x * sc); atomicAdd(d + 1, t.y * sc);
         atomicAdd(d + 2, t.z * sc); atomicAdd(d + 3, t.w * sc);
       }
@@ -512,6 +516,160 @@ __global__ void __launch_bounds__(kThreads) push_elect_kernel(
     if (row < 0) continue;
     float* dst = grad_table + (int64_t)row * dim;
     for (int e = l2; e < dim; e += G2) RS_FLUSH_ADD(dst + e, vals[slot * dim + e]);
+  }
+  if (ws_cnt) {
+    __syncthreads();
+    if (tid == 0) ws_cnt[blk] = ctl[0];
+  }
+}
+
+// The same push with the tile's occurrences grouped by row through a counting sort instead of
+// LDS float atomics (tools/push_prof.sh knockouts, profiles/r06/push/: with its LDS adds as plain
+// LDS stores the config-5 91-field push takes 33 instead of 68 us -- a Zipf-hot row puts dozens
+// of lanes of one instruction on the same LDS words, dim atomics per occurrence):
+//   probe + rank (one LDS int atomic per occurrence) -> block scan over the slots (run starts,
+//   kRun-occurrence work items) -> scatter the samples into their runs -> LP lanes per item sum
+//   its occurrences' gradient elements in registers (all loads in flight) into an LDS partial row
+//   -> per distinct row: the election / marks as above and ONE global float-atomic row add of its
+//   items' partial rows summed in item order.
+constexpr int kRun = 8;                        // occurrences per work item
+constexpr int kItems = kTile + kTile / kRun;   // >= sum over rows of ceil(count / kRun)
+static_assert(kCap <= kThreads, "one slot per thread in the scan");
+
+__host__ __device__ constexpr size_t sort_lds_bytes(int dim) {
+  return ((size_t)16 + 4 * (size_t)kCap + 4 * (size_t)kTile + kItems) * 4 +
+         (size_t)kItems * dim * 4;
+}
+
+template <int LP>
+__global__ void __launch_bounds__(kThreads) push_sort_kernel(
+    const int32_t* __restrict__ rows, int64_t B, int F, const float* __restrict__ dout,
+    int64_t dout_ld, int64_t dout_fstride, int dim, float sc, int tile,
+    float* __restrict__ grad_table, int32_t* __restrict__ flag, int32_t* __restrict__ ws_cnt,
+    int32_t* __restrict__ ws_rows) {
+  extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+  int32_t* ctl = sm;                                       // [16]: list count, wave sums
+  float* part = reinterpret_cast<float*>(sm + 16);        // [kItems][dim] item partial rows
+  int32_t* keys = sm + 16 + kItems * dim;                  // [kCap] row of each slot
+  int32_t* cnt = keys + kCap;                              // [kCap] occurrences per slot
+  int32_t* sstart = cnt + kCap;                            // [kCap] run start per slot
+  int32_t* sitem = sstart + kCap;                          // [kCap] first item per slot
+  int32_t* orow = sitem + kCap;                            // [kTile]
+  int32_t* oslot = orow + kTile;                           // [kTile]
+  int32_t* orank = oslot + kTile;                          // [kTile] rank within the row's run
+  int32_t* ssamp = orank + kTile;                          // [kTile] samples sorted by row
+  int32_t* items = ssamp + kTile;                          // [kItems] slot | chunk << 16
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cap = 2 * tile;  // tile is a power of two <= kTile
+  for (int k = tid; k < cap; k += kThreads) {
+    keys[k] = -1;
+    cnt[k] = 0;
+  }
+  if (tid == 0) ctl[0] = 0;
+  const int f = blockIdx.y;
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * tile;
+  const int n = (int)((b0 + tile < B ? b0 + tile : B) - b0);
+  for (int i = tid; i < n; i += kThreads) orow[i] = rows[(b0 + i) * F + f];
+  __syncthreads();
+  for (int i = tid; i < n; i += kThreads) {
+    const int32_t row = orow[i];
+    int slot = -1;
+    if (row >= 0) {
+      int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(cap - 1));
+      for (;;) {  // cap > tile >= distinct rows: terminates
+        const int32_t old = atomicCAS(&keys[h], -1, row);
+        if (old == -1 || old == row) { slot = h; break; }
+        h = (h + 1) & (cap - 1);
+      }
+      orank[i] = atomicAdd(&cnt[slot], 1);
+    }
+    oslot[i] = slot;
+  }
+  __syncthreads();
+  // runs and items: one slot per thread; counts and item counts scanned together (< 2^16 each)
+  const int c = tid < cap ? cnt[tid] : 0;
+  const int nq = (c + kRun - 1) / kRun;
+  const int packed = c + (nq << 16);
+  int inc = packed;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) ctl[8 + wv] = inc;
+  __syncthreads();
+  int pre = inc - packed, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    if (w < wv) pre += ctl[8 + w];
+    tot += ctl[8 + w];
+  }
+  if (tid < cap) {
+    sstart[tid] = pre & 0xffff;
+    sitem[tid] = pre >> 16;
+    for (int q = 0; q < nq; ++q) items[(pre >> 16) + q] = tid | (q << 16);
+  }
+  const int nit = tot >> 16;
+  __syncthreads();
+  for (int i = tid; i < n; i += kThreads) {
+    const int slot = oslot[i];
+    if (slot >= 0) ssamp[sstart[slot] + orank[i]] = i;
+  }
+  __syncthreads();
+  // item partial rows: LP lanes per item, its occurrences' loads all in flight
+  const int ng = kThreads / LP, g = tid / LP, l = tid % LP;
+  const float* dcol = dout + (int64_t)f * dout_fstride;
+  for (int it = g; it < nit; it += ng) {
+    const int slot = items[it] & 0xffff, q = items[it] >> 16;
+    const int kb = sstart[slot] + q * kRun;
+    const int ke = min(kb + kRun, sstart[slot] + cnt[slot]);
+    for (int e = l; e < dim; e += LP) {
+      float v[kRun];
+#pragma unroll
+      for (int u = 0; u < kRun; ++u)
+        v[u] = kb + u < ke ? dcol[(b0 + ssamp[kb + u]) * dout_ld + e] : 0.f;
+      float acc = v[0];
+#pragma unroll
+      for (int u = 1; u < kRun; ++u) acc += v[u];
+      part[it * dim + e] = acc * sc;
+    }
+  }
+  __syncthreads();
+  // election (list mode) or plain marks (scan mode), as push_elect_kernel
+  {
+    int32_t rw[kCap / kThreads], fl[kCap / kThreads];
+#pragma unroll
+    for (int u = 0; u < kCap / kThreads; ++u) {
+      const int slot = tid + u * kThreads;
+      rw[u] = slot < cap ? keys[slot] : -1;
+      fl[u] = (rw[u] >= 0 && ws_cnt) ? flag[rw[u]] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < kCap / kThreads; ++u) {
+      if (rw[u] < 0) continue;
+      if (!ws_cnt) {
+        scan_mark(flag, rw[u]);
+      } else if (fl[u] != -2) {
+        flag[rw[u]] = blk;
+        ws_rows[(int64_t)blk * kCap + atomicAdd(&ctl[0], 1)] = rw[u];
+      }
+    }
+  }
+  // gradient rows: G2 lanes per row, one dword each, the row's item partials summed in order
+  int G2 = 1;
+  while (G2 < dim && G2 < 64) G2 <<= 1;
+  const int per_pass = kThreads / G2, gs = tid / G2, l2 = tid % G2;
+  for (int slot = gs; slot < cap; slot += per_pass) {
+    const int32_t row = keys[slot];
+    if (row < 0) continue;
+    const int i0 = sitem[slot], ni = (cnt[slot] + kRun - 1) / kRun;
+    float* dst = grad_table + (int64_t)row * dim;
+    for (int e = l2; e < dim; e += G2) {
+      float v = part[i0 * dim + e];
+      for (int q = 1; q < ni; ++q) v += part[(i0 + q) * dim + e];
+      RS_FLUSH_ADD(dst + e, v);
+    }
   }
   if (ws_cnt) {
     __syncthreads();
@@ -604,8 +762,17 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
   // the election push's LDS hash must fit this device's per-block LDS: larger shapes, or a part
   // with less LDS, take the CAS push
   const int64_t lds_max = lds_per_block();
+  // rows of >= 32 floats aggregate by counting sort (push_sort_kernel: config-5 91-field push
+  // 69.4 -> 39.3 us), narrower ones with LDS float atomics (push_elect_kernel: config-4 pushes at
+  // dim 16 6.4 / 18.6 / 16.7 us vs 7.5 / 18.6 / 17.3 sorted); RS_PUSH_LDS_ADD=0 / 1 forces either
+  static const int lds_add_env = [] {
+    const char* e = getenv("RS_PUSH_LDS_ADD");
+    return e ? atoi(e) : -1;
+  }();
+  const bool lds_add = lds_add_env >= 0 ? lds_add_env != 0 : dim < 32;
+  const size_t lds = lds_add ? lds_bytes(dim) : sort_lds_bytes(dim);
   const bool ok_shape = !elect_off && !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
-                        ((uintptr_t)dout & 15) == 0 && (int64_t)lds_bytes(dim) <= lds_max &&
+                        ((uintptr_t)dout & 15) == 0 && (int64_t)lds <= lds_max &&
                         B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;
   if (!ok_shape || (touched && (!workspace || workspace_bytes < rs_sparse_push_workspace_bytes(B, F))))
     return rs_sparse_grad_accumulate(stream, rows, offsets, B, F, dout, dout_ld, dout_fstride, dim,
@@ -623,18 +790,33 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
   while (LP < dim / 4 && LP < 64) LP <<= 1;
   const int tile = tile_for(B, F);
   dim3 grid((unsigned)((B + tile - 1) / tile), (unsigned)F);
-  const size_t lds = lds_bytes(dim);
 #define RS_PUSH_E(LL)                                                                             \
   case LL:                                                                                        \
     push_elect_kernel<LL><<<grid, kThreads, lds, s>>>(rows, B, F, dout, dout_ld, dout_fstride,   \
                                                       dim, sc, tile, grad_table, flag, ws_cnt,   \
                                                       ws_rows);                                  \
     break;
-  switch (LP) {
-    RS_PUSH_E(1) RS_PUSH_E(2) RS_PUSH_E(4) RS_PUSH_E(8) RS_PUSH_E(16) RS_PUSH_E(32) RS_PUSH_E(64)
-    default: return RS_ERR_UNSUPPORTED;
+#define RS_PUSH_S(LL)                                                                             \
+  case LL:                                                                                        \
+    push_sort_kernel<LL><<<grid, kThreads, lds, s>>>(rows, B, F, dout, dout_ld, dout_fstride,    \
+                                                     dim, sc, tile, grad_table, flag, ws_cnt,    \
+                                                     ws_rows);                                   \
+    break;
+  if (lds_add) {
+    switch (LP) {
+      RS_PUSH_E(1) RS_PUSH_E(2) RS_PUSH_E(4) RS_PUSH_E(8) RS_PUSH_E(16) RS_PUSH_E(32) RS_PUSH_E(64)
+      default: return RS_ERR_UNSUPPORTED;
+    }
+  } else {
+    int LS = 1;  // lanes per work item: one float each
+    while (LS < dim && LS < 64) LS <<= 1;
+    switch (LS) {
+      RS_PUSH_S(1) RS_PUSH_S(2) RS_PUSH_S(4) RS_PUSH_S(8) RS_PUSH_S(16) RS_PUSH_S(32) RS_PUSH_S(64)
+      default: return RS_ERR_UNSUPPORTED;
+    }
   }
 #undef RS_PUSH_E
+#undef RS_PUSH_S
   if (touched)
     push_claim_kernel<<<(unsigned)nblk, kThreads, 0, s>>>(ws_cnt, ws_rows, flag, touched, n_touched,
                                                           touched_cap);
