@@ -71,9 +71,11 @@ int rs_sparse_grad_accumulate(void* stream, const int32_t* rows, const int32_t* 
 
 /* rs_sparse_grad_accumulate with a caller workspace of >= rs_sparse_push_workspace_bytes(B, F)
  * bytes: single-hot pushes (offsets == NULL) claim rows by election (plain flag stores + a claim
- * kernel, no returning atomics on hot rows' flag words; csrc/embedding.hip rs_push) -- same
- * results and semantics.  Other shapes (multi-hot, unaligned dout) and a NULL / small workspace
- * in list mode run rs_sparse_grad_accumulate.  Graph-capturable. */
+ * kernel, no returning atomics on hot rows' flag words; csrc/embedding.hip rs_push), rows of
+ * >= 32 floats aggregated per block by a counting sort instead of LDS float atomics; multi-hot
+ * pushes (offsets != NULL, no workspace needed) run a counting-sort push with CAS claims -- same
+ * results and semantics.  Unaligned dout and a NULL / small workspace in single-hot list mode run
+ * rs_sparse_grad_accumulate.  Graph-capturable. */
 int64_t rs_sparse_push_workspace_bytes(int64_t B, int F);
 int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const int32_t* offsets,
                                  int64_t B, int F, const float* dout, int64_t dout_ld,

@@ -746,6 +746,255 @@ inline int64_t lds_per_block() {
 
 }  // namespace rs_push
 
+// ---------------------------------------------------------------------------------------------
+// Multi-hot push (rs_sparse_grad_accumulate_mh, offsets != NULL; config 3's 200 fields x U{1..3}
+// ids over disjoint per-field row ranges).  tools/push_prof.sh knockouts on config 3's shape
+// (profiles/r06/push/): the CAS push takes 132 us, 111 with its claim CASes knocked out; a
+// one-thread-per-sample form with the same LDS float-atomic aggregation took 139 us, 73 with those
+// adds as plain LDS stores.  So a block here aggregates without float atomics, by a counting sort
+// of its occurrences by row:
+//   1. one thread per sample of the tile loads its [beg, end); a block scan of the lengths gives
+//      every occurrence a position (a generation holds up to kMhOcc of them);
+//   2. each thread loads its ids (all in flight) into the generation's LDS occurrence list;
+//   3. one lane per occurrence probes the LDS hash (kMhCap > kMhOcc slots: never full) and takes
+//      its rank within the row (one LDS int atomic per occurrence);
+//   4. a block scan over the slots gives each row its run in a sorted occurrence array and
+//      ceil(count / kMhRun) work items; the occurrences are scattered into their runs;
+//   5. LP lanes (one float each) per item sum up to kMhRun occurrences' scale x dout, all loads in
+//      flight, and add the sum to the row with one global float-atomic row segment (a Zipf-hot
+//      row takes count / kMhRun such adds per block, the rest one);
+//   6. claims, per distinct row: a returning CAS (-1 -> -2), as the CAS push (config 3's fields
+//      are disjoint row ranges: few blocks share a row); one n_touched atomic per block and
+//      generation.  Scan mode (touched == NULL): plain marks.
+// Row set exact; the fp32 summation order is not fixed (run order = rank order).
+// ---------------------------------------------------------------------------------------------
+namespace rs_push {
+constexpr int kMhThreads = 256;  // one thread per sample of the tile
+constexpr int kMhTile = kMhThreads;
+constexpr int kMhOcc = 768;      // occurrences per generation (U{1..3} x 256 samples)
+constexpr int kMhCap = 1024;     // LDS hash slots (> kMhOcc >= distinct rows per generation)
+constexpr int kMhRun = 8;        // occurrences summed per work item
+constexpr int kMhItems = kMhOcc + kMhOcc / kMhRun;  // >= sum over rows of ceil(count / kMhRun)
+#ifndef RS_MH_KO  // timing experiments only: 1 no row adds, 2 no claims / marks
+#define RS_MH_KO 0
+#endif
+
+constexpr size_t mh_lds_bytes() {
+  return ((size_t)16 + 3 * (size_t)kMhCap + 4 * (size_t)kMhOcc + kMhItems + kMhTile) * 4;
+}
+
+template <int LP>
+__global__ void __launch_bounds__(kMhThreads) push_mh_kernel(
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ offsets, int64_t B, int F,
+    const float* __restrict__ dout, int64_t dout_ld, int64_t dout_fstride, int dim, int combiner,
+    int tile, float* __restrict__ grad_table, int32_t* __restrict__ flag,
+    int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
+  __shared__ int32_t ctl[16];                 // [0] claims, [1] claim base, [2] items, [4..] waves
+  extern __shared__ __attribute__((aligned(16))) int32_t sm[];
+  int32_t* keys = sm;                         // [kMhCap] row of each slot
+  int32_t* cnt = keys + kMhCap;               // [kMhCap] occurrences per slot
+  int32_t* sstart = cnt + kMhCap;             // [kMhCap] run start per slot
+  int32_t* orow = sstart + kMhCap;            // [kMhOcc] ids, then ranks within their row
+  int32_t* osamp = orow + kMhOcc;             // [kMhOcc] sample of each occurrence
+  int32_t* oslot = osamp + kMhOcc;            // [kMhOcc] slot of each occurrence
+  int32_t* ssamp = oslot + kMhOcc;            // [kMhOcc] samples sorted by row
+  int32_t* items = ssamp + kMhOcc;            // [kMhItems] slot | chunk << 16
+  float* sscale = reinterpret_cast<float*>(items + kMhItems);  // [kMhTile] combiner scale
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = kMhThreads / 64;
+  const int f = blockIdx.y;
+  const int64_t b0 = (int64_t)blockIdx.x * tile;
+  const int n = (int)((b0 + tile < B ? b0 + tile : B) - b0);
+  // block exclusive scan of one int per thread (ctl[4 .. 4 + NW) hold the wave sums)
+  auto block_scan = [&](int x, int& total) {
+    int inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += t;
+    }
+    __syncthreads();  // ctl's wave sums free again
+    if (lane == 63) ctl[4 + wv] = inc;
+    __syncthreads();
+    int pre = inc - x;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      if (w < wv) pre += ctl[4 + w];
+      total += ctl[4 + w];
+    }
+    return pre;
+  };
+  // 1. this thread's sample: its id range, scale and occurrence positions
+  int64_t beg = 0;
+  int len = 0;
+  if (tid < n) {
+    const int64_t sg = (b0 + tid) * F + f;
+    beg = offsets[sg];
+    const int64_t end = offsets[sg + 1];
+    len = end > beg ? (int)(end - beg) : 0;
+    sscale[tid] = combiner_scale(len, combiner);
+  }
+  for (int k = tid; k < kMhCap; k += kMhThreads) {
+    keys[k] = -1;
+    cnt[k] = 0;
+  }
+  if (tid == 0) ctl[0] = 0;
+  int total;
+  const int pos = block_scan(len, total);
+  const int ng = kMhThreads / LP, g = tid / LP, l = tid % LP;
+  constexpr int SPT = kMhCap / kMhThreads;
+  for (int g0 = 0; g0 < total; g0 += kMhOcc) {
+    const int gn = total - g0 < kMhOcc ? total - g0 : kMhOcc;
+    // 2. this generation's ids -> LDS (a thread's loads all issued before its stores)
+    {
+      const int k0 = g0 > pos ? g0 - pos : 0;
+      const int k1 = g0 + gn - pos < len ? g0 + gn - pos : len;
+      for (int k = k0; k < k1; k += 4) {
+        int32_t r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = k + u < k1 ? rows[beg + k + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k + u < k1) {
+            orow[pos + k + u - g0] = r[u];
+            osamp[pos + k + u - g0] = tid;
+          }
+      }
+    }
+    __syncthreads();
+    // 3. probe + rank (padded sequence positions, row < 0, take no slot)
+    for (int j = tid; j < gn; j += kMhThreads) {
+      const int32_t row = orow[j];
+      int slot = -1;
+      if (row >= 0) {
+        int h = (int)(((uint32_t)row * 2654435761u) & (uint32_t)(kMhCap - 1));
+        for (;;) {  // kMhCap > kMhOcc >= distinct rows: terminates
+          const int32_t old = atomicCAS(&keys[h], -1, row);
+          if (old == -1 || old == row) { slot = h; break; }
+          h = (h + 1) & (kMhCap - 1);
+        }
+        orow[j] = atomicAdd(&cnt[slot], 1);
+      }
+      oslot[j] = slot;
+    }
+    __syncthreads();
+    // 4. runs and work items: a thread owns SPT consecutive slots; counts and item counts are
+    //    scanned together (both < 2^16: count in the low half, items in the high half)
+    int c[SPT], packed = 0;
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      c[u] = cnt[tid * SPT + u];
+      packed += c[u] + (((c[u] + kMhRun - 1) / kMhRun) << 16);
+    }
+    int ptot;
+    int pre = block_scan(packed, ptot);
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int slot = tid * SPT + u;
+      const int run0 = pre & 0xffff, it0 = pre >> 16, nch = (c[u] + kMhRun - 1) / kMhRun;
+      sstart[slot] = run0;
+      for (int q = 0; q < nch; ++q) items[it0 + q] = slot | (q << 16);
+      pre += c[u] + (nch << 16);
+    }
+    __syncthreads();
+    const int nit = ptot >> 16;
+    for (int j = tid; j < gn; j += kMhThreads) {
+      const int slot = oslot[j];
+      if (slot >= 0) ssamp[sstart[slot] + orow[j]] = osamp[j];
+    }
+    __syncthreads();
+    // 5. row sums: LP lanes per item, its occurrences' loads all in flight
+    for (int it = g; it < ((RS_MH_KO & 1) ? 0 : nit); it += ng) {
+      const int slot = items[it] & 0xffff, q = items[it] >> 16;
+      const int kb = sstart[slot] + q * kMhRun;
+      const int ke = min(kb + kMhRun, sstart[slot] + cnt[slot]);
+      float* dst = grad_table + (int64_t)keys[slot] * dim;
+      for (int e = l; e < dim; e += LP) {
+        float v[kMhRun];
+#pragma unroll
+        for (int u = 0; u < kMhRun; ++u) {
+          v[u] = 0.f;
+          if (kb + u < ke) {
+            const int i = ssamp[kb + u];
+            v[u] = dout[(b0 + i) * dout_ld + (int64_t)f * dout_fstride + e] * sscale[i];
+          }
+        }
+        float acc = v[0];
+#pragma unroll
+        for (int u = 1; u < kMhRun; ++u) acc += v[u];
+        RS_FLUSH_ADD(dst + e, acc);
+      }
+    }
+    // 6. claims (list mode: a returning CAS -1 -> -2 per distinct row, SPT in flight per thread)
+    //    or marks (scan mode)
+    if (!(RS_MH_KO & 2)) {
+      int32_t rw[SPT], old[SPT], li[SPT];
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) rw[u] = keys[tid * SPT + u];
+      if (touched) {
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) old[u] = rw[u] >= 0 ? atomicCAS(&flag[rw[u]], -1, -2) : 0;
+#pragma unroll
+        for (int u = 0; u < SPT; ++u)
+          li[u] = (rw[u] >= 0 && old[u] == -1) ? atomicAdd(&ctl[0], 1) : -1;
+        __syncthreads();
+        if (tid == 0) ctl[1] = ctl[0] > 0 ? atomicAdd(n_touched, ctl[0]) : 0;
+        __syncthreads();
+        const int base = ctl[1];
+#pragma unroll
+        for (int u = 0; u < SPT; ++u)
+          if (li[u] >= 0 && base + li[u] < touched_cap) touched[base + li[u]] = rw[u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < SPT; ++u)
+          if (rw[u] >= 0) scan_mark(flag, rw[u]);
+      }
+    }
+    if (g0 + kMhOcc < total) {  // next generation: empty table
+      __syncthreads();
+      if (tid == 0) ctl[0] = 0;
+      for (int k = tid; k < kMhCap; k += kMhThreads) {
+        keys[k] = -1;
+        cnt[k] = 0;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// the multi-hot push of rs_sparse_grad_accumulate_ws; nonzero: not launched (the caller takes the
+// CAS push)
+inline int push_mh(hipStream_t s, const int32_t* rows, const int32_t* offsets, int64_t B, int F,
+                   const float* dout, int64_t dout_ld, int64_t dout_fstride, int dim, int combiner,
+                   float* grad_table, int32_t* flag, int32_t* touched, int32_t* n_touched,
+                   int32_t touched_cap) {
+  int tile = kMhTile;  // small launches still spread over >= ~256 blocks
+  while (tile > 32 && ((B + tile - 1) / tile) * (int64_t)F < RS_PUSH_MIN_BLOCKS) tile >>= 1;
+  const int64_t nbx = (B + tile - 1) / tile;
+  if ((int64_t)mh_lds_bytes() > lds_per_block() || F > 65535 || nbx > INT32_MAX) return 1;
+  int LP = 1;
+  while (LP < dim && LP < 64) LP <<= 1;
+  dim3 grid((unsigned)nbx, (unsigned)F);
+  const size_t lds = mh_lds_bytes();
+#define RS_PUSH_MH(LL)                                                                            \
+  case LL:                                                                                        \
+    push_mh_kernel<LL><<<grid, kMhThreads, lds, s>>>(rows, offsets, B, F, dout, dout_ld,         \
+                                                     dout_fstride, dim, combiner, tile,           \
+                                                     grad_table, flag, touched, n_touched,        \
+                                                     touched_cap);                                \
+    return 0;
+  switch (LP) {
+    RS_PUSH_MH(1) RS_PUSH_MH(2) RS_PUSH_MH(4) RS_PUSH_MH(8) RS_PUSH_MH(16) RS_PUSH_MH(32)
+    RS_PUSH_MH(64)
+    default: return 1;
+  }
+#undef RS_PUSH_MH
+}
+
+}  // namespace rs_push
+
+
 RS_API int64_t rs_sparse_push_workspace_bytes(int64_t B, int F) {
   if (B < 0 || F <= 0) return -1;
   return rs_push::grid_blocks(B, F) * (1 + rs_push::kCap) * 4;
@@ -771,6 +1020,13 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
   }();
   const bool lds_add = lds_add_env >= 0 ? lds_add_env != 0 : dim < 32;
   const size_t lds = lds_add ? lds_bytes(dim) : sort_lds_bytes(dim);
+  // multi-hot: the counting-sort push with CAS claims (RS_PUSH_MH_CAS=1: the LDS-atomic CAS push)
+  static const bool mh_off = getenv("RS_PUSH_MH_CAS") != nullptr;
+  if (offsets && !mh_off && rows && dout && grad_table && flag && F > 0 && dim > 0 &&
+      (!touched || n_touched) && B * (int64_t)F > 0 &&
+      rs_push::push_mh(rs_stream(stream), rows, offsets, B, F, dout, dout_ld, dout_fstride, dim,
+                       combiner, grad_table, flag, touched, n_touched, touched_cap) == 0)
+    return rs_status_after_launch();
   const bool ok_shape = !elect_off && !offsets && dim % 4 == 0 && dout_ld % 4 == 0 && dout_fstride % 4 == 0 &&
                         ((uintptr_t)dout & 15) == 0 && (int64_t)lds <= lds_max &&
                         B <= INT32_MAX / 2 && grid_blocks(B, F) <= INT32_MAX;

@@ -154,12 +154,13 @@ def test_single_hot_election_push(mode):
 @pytest.mark.parametrize("mode", ["list", "scan"])
 @pytest.mark.parametrize("shape", ["short", "long"])
 def test_multi_hot_push(mode, shape):
-    """Multi-hot pushes (rs_sparse_grad_accumulate with offsets): Zipf-hot rows aggregated per
-    block in the LDS hash; "long" lists (up to 1500 ids per segment) overflow a block's table, so
-    those occurrences take the direct global-atomic path and its CAS claims.  Mean / sqrtn
-    scaling, empty segments and padded (-1) ids; two pushes per step and two steps.  Touched
-    list duplicate-free and equal to the oracle row set, gradients equal the oracle sums, flags
-    clean after the optimizer."""
+    """Multi-hot pushes (rs_sparse_grad_accumulate_ws with offsets: one thread per sample scans
+    the tile's id lists, a counting sort groups a block's occurrences by row, runs summed in
+    registers, CAS claims).  "long" lists (up to 1500 ids per segment) take several LDS
+    generations per block, so a block adds and claims a row once per generation.  Mean / sqrtn
+    scaling, empty segments and padded (-1) ids; two pushes per step and two steps.  Touched list
+    duplicate-free and equal to the oracle row set, gradients equal the oracle sums, flags clean
+    after the optimizer."""
     from recommendsystem_amd.embedding import SparseAdam, SparseTable
     rng = np.random.default_rng(5)
     dim, rows_n = 8, 5000
