@@ -81,7 +81,8 @@ def build(verbose: bool = False, extra: list[str] | None = None) -> str:
         # a host-sanitizer build (-Xarch_host -fsanitize=...) links the shared sanitizer runtime
         san = [f for f in extra if f.startswith("-fsanitize=")]
         link = [*san, "-shared-libasan"] if san else []
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *link, *objs,
+        os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)  # (RS_LIB_OUT may name a fresh dir)
+        cmd =[_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *link, *objs,
                "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB_PATH]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
