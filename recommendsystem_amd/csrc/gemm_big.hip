@@ -531,12 +531,17 @@ size_t lds_bytes(int bm, int bn, bool za, bool zb) {
          ((size_t)bm * BK * (za ? 2 : 1) + (size_t)bn * BK * (zb ? 2 : 1)) * 4;
 }
 
-// Tile / split choice: the MFMA time of the busiest CU (two blocks per CU) for each candidate
-// tile, plus a split-K's partial round trip; larger tiles win ties (fewer operand bytes per
-// flop).  RS_GEMM_BIG_TILE=BMxBN[,S] forces a choice (tuning runs).
+// Tile / split choice: the multiply-adds of the busiest CU (blocks per CU share its matrix
+// pipes) at the rate the kernel reaches on a busy CU, plus a split-K's partial round trip and
+// reduce launch; larger tiles win ties (fewer operand bytes per flop).  The constants are fitted
+// to a forced tile x split sweep of the configs 3 / 5 trunk shapes (profiles/r06/gemm/
+// tile_sweep.txt): ~150 k MAC/us per busy CU whatever the tile (~49 % of the f32 MFMA peak), a
+// 64 x 64 tile ~10 % above that (4 blocks per CU: two waves per SIMD hide the LDS / barrier
+// waits), a split ~6 us + its partial slabs at ~4 TB/s.  (The round-5 form priced the tiles at
+// the MFMA peak with 64 x 64 at 0.75 and picked 128-row tiles 1 per CU: 10-35 % slower on 6 of
+// the 9 trunk products.)  RS_GEMM_BIG_TILE=BMxBN[,S] forces a choice (tuning runs).
 Plan plan(int64_t M, int64_t N, int64_t R, bool allow_split, bool z) {
   static const Tile cand[4] = {{128, 128}, {128, 64}, {64, 64}, {128, 32}};
-  static const double eff[4] = {1.0, 0.9, 0.75, 0.75};
   Plan best{};
   double bc = 0;
   for (int c = 0; c < 4; ++c) {
@@ -544,13 +549,13 @@ Plan plan(int64_t M, int64_t N, int64_t R, bool allow_split, bool z) {
     if (bn == 32 && N > 32) continue;
     const int64_t tiles = cdiv(M, bm) * cdiv(N, bn);
     for (int64_t s = 1; s <= (allow_split ? 16 : 1); s *= 2) {
-      if (s > 1 && (R / s < 128 || tiles * s > 1024)) break;
+      if (s > 1 && (R / s < 128 || tiles * s > 1536)) break;
       const int64_t rc = cdiv(cdiv(R, s), BK) * BK;
       const int64_t blocks = tiles * cdiv(R, rc);
-      // blocks per CU share its matrix pipes: time ~ blocks on the busiest CU x block MFMA time
       const double per_cu = (double)cdiv(blocks, 256);
-      double cost = per_cu * (double)bm * bn * rc / 307200.0 / eff[c];  // us at 128 MAC/clk/CU
-      if (s > 1) cost += (double)s * M * N * 8.0 / 4.0e6 + 3.0;
+      const double rate = 150000.0 * (bm * bn <= 4096 ? 1.1 : 1.0);  // MAC per us per CU
+      double cost = per_cu * (double)bm * bn * rc / rate;
+      if (s > 1) cost += (double)s * M * N * 8.0 / 4.0e6 + 6.0;
       if (best.bm == 0 || cost < bc * 0.98) {
         bc = cost;
         best = Plan{bm, bn, (int)cdiv(R, rc), rc, stages_of(z)};
