@@ -1971,6 +1971,24 @@ constexpr bool kSaved4 = kLnPair<C> && C::H * C::FMAX <= 64;
 #ifndef RS_IL4_PRIO
 #define RS_IL4_PRIO 1
 #endif
+// RS_IL4_MQ (round 6, opt-in): the Q-pass's score, dP and dq products on the matrix cores (f32,
+// no dropout, two heads of dh = 8, F <= 32, three rotating buffers).  Correct (the whole GPU
+// suite, 338 tests, passed with it on) but SLOWER: same box, 300 steps x 2, the backward launch
+// 77.6 / 78.1 -> 90.4 / 90.2 us (0.1456 / 0.1482 -> 0.1579 / 0.1587 ms per step); one
+// accumulator per key tile (RS_IL4_MQ_SPLIT) 92.3 / 91.3 us (profiles/r06/mq/).  Each 16 x 16
+// tile is a dependent chain (S / dP MFMAs -> exp / dS on the VALU -> 4 dq MFMAs) with 37 % of
+// the tile padding (26 of 32 rows and keys) and the dq^T tile half padding (dh 8 of 16 rows),
+// and the 16 packed dq registers held through the K-pass push the kernel past 256 VGPRs (148 B
+// of scratch); the VALU pass's per-lane key loop keeps two waves per SIMD issuing instead.
+#ifndef RS_IL4_MQ
+#define RS_IL4_MQ 0
+#endif
+#ifndef RS_IL4_MQ_SPLIT
+#define RS_IL4_MQ_SPLIT 0
+#endif
+template <class C, bool DROP>
+constexpr bool kMQ = RS_IL4_MQ && RS_IL4_ROT && !DROP && !C::BF && C::H == 2 && C::DH == 8 &&
+                     C::FMAX <= 32;
 template <class C>
 struct Bwd4Layout {
   int ba, bb, bc, pr, dy, pm, st, rows, sv, per_wave;
@@ -2363,8 +2381,97 @@ __global__ void __launch_bounds__(64 * kWpb3, RS_IL_BWD4_OCC) bwd4_kernel(
       // ---- Q-pass (lane = (h, i)): P -> PM, dq -> DY (ROT: dq stays in registers) ----
 #if RS_IL4_ROT
       float dqk[DH];
+      // MQ: dq per head, packed: lanes of group g < 2 hold query tile 0's d = 4g + r, lanes of
+      // group g >= 2 query tile 1's d = 4(g - 2) + r (the dq^T accumulators' rows d >= 8 are
+      // padding, so the two tiles share one register set)
+      f32x4 dqm[kMQ<C, DROP> ? 2 : 1];
 #endif
-      if (RS_IL4_EXP != 3) {
+      if constexpr (kMQ<C, DROP>) {
+        // Q-pass on the matrix cores (RS_IL4_MQ): per head and 16 x 16 (key j, query i) tile
+        //   S^T = K Q^T, dP^T = V dO^T          two v_mfma_f32_16x16x4_f32 each (dh = 8; lane
+        //                                       group g takes d = 2g + s in instruction s)
+        //   e = exp2(S sc2 - max_i) -> PM,  dS^T = e (dP^T - D_i)    (lane (g, i): j = 4g + r)
+        //   dq^T += K^T dS^T                    the dS^T accumulators ARE the B operand (register
+        //                                       r <-> k-step r: key 4g + r); A = K^T, rows d < 8
+        // Every K / V / Q / dO row is read once per 16 lanes (b64) instead of once per lane and
+        // key (the VALU pass: 4 ds_read_b128 per key and lane).  Rows past F (PR's padded rows
+        // alias PM) read as zeros; invalid (i, j) give e = dS = 0 and store nothing.
+        const int g = lane >> 4, ii = lane & 15;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 dqt[2];
+#pragma unroll
+          for (int it = 0; it < 2; ++it) {
+            f32x4 dq = {0.f, 0.f, 0.f, 0.f};
+#if RS_IL4_MQ_SPLIT
+            f32x4 dq1 = {0.f, 0.f, 0.f, 0.f};
+#endif
+            if (it < nrt) {
+              const int i = 16 * it + ii;
+              const bool iv = i < F;
+              const int ic = iv ? i : 0;
+              float2 qb = *reinterpret_cast<const float2*>(PR + ic * C::PRS + h * DH + 2 * g);
+              float2 ob = *reinterpret_cast<const float2*>(SB + ic * U + h * DH + 2 * g);
+              const float2 stt = *reinterpret_cast<const float2*>(SB + F * U + 2 * (h * F + ic));
+              const float Dv = DL[h * F + ic];  // x 1/sum_i (P3)
+              if (!iv) { qb = make_float2(0.f, 0.f); ob = qb; }
+              float* pm_row = PM + (h * F + ic) * C::PMS;
+#pragma unroll
+              for (int jt = 0; jt < 2; ++jt) {
+                if (jt >= nrt) break;
+                const int ja = 16 * jt + ii;
+                const bool jav = ja < F;
+                const int jc = jav ? ja : 0;
+                float2 ka = *reinterpret_cast<const float2*>(PR + jc * C::PRS + U + h * DH + 2 * g);
+                float2 va = *reinterpret_cast<const float2*>(PR + jc * C::PRS + 2 * U + h * DH + 2 * g);
+                if (!jav) { ka = make_float2(0.f, 0.f); va = ka; }
+                f32x4 s = {0.f, 0.f, 0.f, 0.f}, p = {0.f, 0.f, 0.f, 0.f};
+                s = mfma_16x16x4(ka.x, qb.x, s);
+                p = mfma_16x16x4(va.x, ob.x, p);
+                s = mfma_16x16x4(ka.y, qb.y, s);
+                p = mfma_16x16x4(va.y, ob.y, p);
+                // A of dq^T: K[16 jt + 4g + t][d = ii] (d < 8)
+                float kt[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                  const int j = 16 * jt + 4 * g + t;
+                  kt[t] = (ii < DH && j < F) ? PR[j * C::PRS + U + h * DH + ii] : 0.f;
+                }
+                float ds[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int j = 16 * jt + 4 * g + r;
+                  const bool v = iv && j < F;
+                  const float e = v ? __builtin_amdgcn_exp2f(fmaf(s[r], a.sc2, -stt.x)) : 0.f;
+                  if (v) pm_row[j] = e;
+                  ds[r] = e * (p[r] - Dv);
+                }
+#if RS_IL4_MQ_SPLIT  // one accumulator per key tile: two 4-long MFMA chains instead of one 8-long
+                if (jt == 0) {
+#pragma unroll
+                  for (int t = 0; t < 4; ++t) dq = mfma_16x16x4(kt[t], ds[t], dq);
+                } else {
+#pragma unroll
+                  for (int t = 0; t < 4; ++t) dq1 = mfma_16x16x4(kt[t], ds[t], dq1);
+                }
+#else
+#pragma unroll
+                for (int t = 0; t < 4; ++t) dq = mfma_16x16x4(kt[t], ds[t], dq);
+#endif
+              }
+            }
+#if RS_IL4_MQ_SPLIT
+            dq += dq1;
+#endif
+            dqt[it] = dq;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float t1 = __shfl_xor(dqt[1][r], 32, 64);
+            dqm[kMQ<C, DROP> ? h : 0][r] = (g < 2 ? dqt[0][r] : t1) * a.inv_sdh;
+          }
+        }
+      } else if (RS_IL4_EXP != 3) {
         const bool act = lane < HF;
         const int h = act ? lane / F : 0, i = act ? lane - h * F : 0;
         float qv[DH], dO[DH], dq[DH];
@@ -2486,7 +2593,23 @@ RS_UNROLL(RS_IL4_UNROLL_K)
       wave_lds_sync();  // every lane's Q-row reads are done
       IL_STAMP(5)
 #if RS_IL4_ROT
-      if (lane < HF) {  // Q <- gQ, lane (h, i) as in the Q-pass
+      if constexpr (kMQ<C, DROP>) {  // Q <- gQ from the packed dq registers: lane (g, i)
+        const int g = lane >> 4, ii = lane & 15, it = g >> 1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 16 * it + ii;
+          if (it < nrt && i < F) {
+              float4* qp = reinterpret_cast<float4*>(PR + i * C::PRS + h * DH + 4 * (g & 1));
+              float4 qv = *qp;
+              const f32x4 dq = dqm[kMQ<C, DROP> ? h : 0];
+              qv.x = qv.x > 0.f ? dq[0] : 0.f;
+              qv.y = qv.y > 0.f ? dq[1] : 0.f;
+              qv.z = qv.z > 0.f ? dq[2] : 0.f;
+              qv.w = qv.w > 0.f ? dq[3] : 0.f;
+              *qp = qv;
+          }
+        }
+      } else if (lane < HF) {  // Q <- gQ, lane (h, i) as in the Q-pass
         const int h = lane / F, i = lane - h * F;
         float qv[DH];
         load_row(qv, PR + i * C::PRS + h * DH);
