@@ -769,10 +769,17 @@ inline int64_t lds_per_block() {
 // Row set exact; the fp32 summation order is not fixed (run order = rank order).
 // ---------------------------------------------------------------------------------------------
 namespace rs_push {
-constexpr int kMhThreads = 256;  // one thread per sample of the tile
+// tuning builds: samples per block (a power of two, 64 .. 1024).  Larger tiles aggregate more of
+// a row's occurrences before its global flush (config 3: ~3.2 K -> 2.4 K distinct rows per field
+// at 256 -> 1024 samples) but lengthen each block's serial chain: push 121.7 us at 256, 131.3 at
+// 512, 138.6 at 1024, 142.1 at 128 (list mode; profiles/r06/push/mh_tile_size.txt)
+#ifndef RS_MH_THREADS
+#define RS_MH_THREADS 256
+#endif
+constexpr int kMhThreads = RS_MH_THREADS;  // one thread per sample of the tile
 constexpr int kMhTile = kMhThreads;
-constexpr int kMhOcc = 768;      // occurrences per generation (U{1..3} x 256 samples)
-constexpr int kMhCap = 1024;     // LDS hash slots (> kMhOcc >= distinct rows per generation)
+constexpr int kMhOcc = 3 * kMhThreads;     // occurrences per generation (U{1..3} x the tile)
+constexpr int kMhCap = 4 * kMhThreads;     // LDS hash slots (> kMhOcc >= distinct rows per generation)
 constexpr int kMhRun = 8;        // occurrences summed per work item
 constexpr int kMhItems = kMhOcc + kMhOcc / kMhRun;  // >= sum over rows of ceil(count / kMhRun)
 #ifndef RS_MH_KO  // timing experiments only: 1 no row adds, 2 no claims / marks
@@ -789,7 +796,7 @@ __global__ void __launch_bounds__(kMhThreads) push_mh_kernel(
     const float* __restrict__ dout, int64_t dout_ld, int64_t dout_fstride, int dim, int combiner,
     int tile, float* __restrict__ grad_table, int32_t* __restrict__ flag,
     int32_t* __restrict__ touched, int32_t* __restrict__ n_touched, int32_t touched_cap) {
-  __shared__ int32_t ctl[16];                 // [0] claims, [1] claim base, [2] items, [4..] waves
+  __shared__ int32_t ctl[4 + kMhThreads / 64 > 16 ? 4 + kMhThreads / 64 : 16];  // [0] claims, [1] claim base, [2] items, [4..] waves
   extern __shared__ __attribute__((aligned(16))) int32_t sm[];
   int32_t* keys = sm;                         // [kMhCap] row of each slot
   int32_t* cnt = keys + kMhCap;               // [kMhCap] occurrences per slot
