@@ -83,6 +83,23 @@ int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const int32_
                                  int32_t* flag, int32_t* touched, int32_t* n_touched,
                                  int32_t touched_cap, void* workspace, int64_t workspace_bytes);
 
+/* Several single-hot pushes into ONE table as one launch (+ one claim launch in list mode):
+ * source k pushes rows[k] [B[k], F[k]] with gradient rows dout[k] + b * dout_ld[k] +
+ * f * dout_fstride[k] (16-B aligned, dim >= 32 floats).  Results and claim semantics equal one
+ * rs_sparse_grad_accumulate_ws call per source (a row pushed by several sources is claimed once).
+ * nsrc <= 8; workspace >= rs_sparse_push_group_workspace_bytes(nsrc, B, F) in list mode
+ * (touched != NULL).  RS_ERR_UNSUPPORTED (nothing launched) for rows under 32 floats or unaligned
+ * gradients: push the sources one by one.  Replaces the per-layer pushes of the
+ * EmbeddingFeatures / sequence columns that share one tensornet table in one backward
+ * (staytime/VideoDnn.py:217-244, one table for every feature column).  Graph-capturable. */
+int64_t rs_sparse_push_group_workspace_bytes(int nsrc, const int64_t* B, const int* F);
+int rs_sparse_grad_accumulate_group(void* stream, int nsrc, const int32_t* const* rows,
+                                    const float* const* dout, const int64_t* B, const int* F,
+                                    const int64_t* dout_ld, const int64_t* dout_fstride, int dim,
+                                    float* grad_table, int32_t* flag, int32_t* touched,
+                                    int32_t* n_touched, int32_t touched_cap, void* workspace,
+                                    int64_t workspace_bytes);
+
 /* Deterministic variant of rs_sparse_grad_accumulate: sort by row + segmented sum,
  * so each touched row receives the sum of its occurrences in ascending id order with one plain
  * read-modify-write -- bitwise reproducible run to run (the atomic push reproduces only the row

@@ -35,6 +35,9 @@ SIGNATURES: dict[str, tuple] = {
     "rs_sparse_push_workspace_bytes": (_i64, [_i64, _i32]),
     "rs_sparse_grad_accumulate_ws": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _i32, _i32,
                                             _vp, _vp, _vp, _vp, _i32, _vp, _i64]),
+    "rs_sparse_push_group_workspace_bytes": (_i64, [_i32, _vp, _vp]),
+    "rs_sparse_grad_accumulate_group": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp,
+                                               _vp, _vp, _vp, _i32, _vp, _i64]),
     "rs_sparse_adam": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32, _f32,
                               _f32, _f32]),
     "rs_sparse_adagrad": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f32, _f32]),

@@ -541,12 +541,41 @@ __host__ __device__ constexpr size_t sort_lds_bytes(int dim) {
          (size_t)kItems * dim * 4;
 }
 
+// Push sources of one launch (rs_sparse_grad_accumulate_group): a single-hot push per source
+// ([B, F] rows, dout rows of dout_ld floats with fields dout_fstride apart) into ONE table; the
+// grid's y index runs over every source's fields (source k owns y in [f0, f0 + F)), so the
+// pushes of several layers into a shared table (config 5: 91 fields, 52 fields and three
+// 50-position sequences) run as one launch and one claim launch instead of five of each.
+constexpr int kMaxSrc = 8;
+struct PushSrc {
+  const int32_t* rows;
+  const float* dout;
+  int64_t dout_ld, dout_fstride, B;
+  int F, f0;
+};
+struct PushSrcs {
+  PushSrc s[kMaxSrc];
+  int n;
+};
+
 template <int LP>
 __global__ void __launch_bounds__(kThreads) push_sort_kernel(
-    const int32_t* __restrict__ rows, int64_t B, int F, const float* __restrict__ dout,
-    int64_t dout_ld, int64_t dout_fstride, int dim, float sc, int tile,
+    PushSrcs srcs, int dim, float sc, int tile,
     float* __restrict__ grad_table, int32_t* __restrict__ flag, int32_t* __restrict__ ws_cnt,
     int32_t* __restrict__ ws_rows) {
+  // this block's source (block-uniform; selected field by field so the argument block is never
+  // indexed dynamically)
+  const int y = (int)blockIdx.y;
+  const int32_t* __restrict__ rows = srcs.s[0].rows;
+  const float* __restrict__ dout = srcs.s[0].dout;
+  int64_t dout_ld = srcs.s[0].dout_ld, dout_fstride = srcs.s[0].dout_fstride, B = srcs.s[0].B;
+  int F = srcs.s[0].F, f0 = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxSrc; ++k)
+    if (k < srcs.n && y >= srcs.s[k].f0) {
+      rows = srcs.s[k].rows; dout = srcs.s[k].dout; dout_ld = srcs.s[k].dout_ld;
+      dout_fstride = srcs.s[k].dout_fstride; B = srcs.s[k].B; F = srcs.s[k].F; f0 = srcs.s[k].f0;
+    }
   extern __shared__ __attribute__((aligned(16))) int32_t sm[];
   int32_t* ctl = sm;                                       // [16]: list count, wave sums
   float* part = reinterpret_cast<float*>(sm + 16);        // [kItems][dim] item partial rows
@@ -566,10 +595,11 @@ __global__ void __launch_bounds__(kThreads) push_sort_kernel(
     cnt[k] = 0;
   }
   if (tid == 0) ctl[0] = 0;
-  const int f = blockIdx.y;
+  const int f = y - f0;
   const int blk = blockIdx.y * gridDim.x + blockIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * tile;
-  const int n = (int)((b0 + tile < B ? b0 + tile : B) - b0);
+  // (a source with fewer samples than the grid's widest leaves its last blocks empty: n = 0)
+  const int n = b0 < B ? (int)((b0 + tile < B ? b0 + tile : B) - b0) : 0;
   for (int i = tid; i < n; i += kThreads) orow[i] = rows[(b0 + i) * F + f];
   __syncthreads();
   for (int i = tid; i < n; i += kThreads) {
@@ -1059,11 +1089,13 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
                                                       dim, sc, tile, grad_table, flag, ws_cnt,   \
                                                       ws_rows);                                  \
     break;
+  PushSrcs one{};
+  one.n = 1;
+  one.s[0] = PushSrc{rows, dout, dout_ld, dout_fstride, B, F, 0};
 #define RS_PUSH_S(LL)                                                                             \
   case LL:                                                                                        \
-    push_sort_kernel<LL><<<grid, kThreads, lds, s>>>(rows, B, F, dout, dout_ld, dout_fstride,    \
-                                                     dim, sc, tile, grad_table, flag, ws_cnt,    \
-                                                     ws_rows);                                   \
+    push_sort_kernel<LL><<<grid, kThreads, lds, s>>>(one, dim, sc, tile, grad_table, flag,       \
+                                                     ws_cnt, ws_rows);                           \
     break;
   if (lds_add) {
     switch (LP) {
@@ -1080,6 +1112,85 @@ RS_API int rs_sparse_grad_accumulate_ws(void* stream, const int32_t* rows, const
   }
 #undef RS_PUSH_E
 #undef RS_PUSH_S
+  if (touched)
+    push_claim_kernel<<<(unsigned)nblk, kThreads, 0, s>>>(ws_cnt, ws_rows, flag, touched, n_touched,
+                                                          touched_cap);
+  return rs_status_after_launch();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grouped single-hot pushes into ONE table (rs_push::PushSrcs): the counting-sort push over every
+// source's (tile, field) blocks in one launch, then one claim launch.  Same per-block work, row
+// set and claims as one rs_sparse_grad_accumulate_ws call per source (a row pushed by several
+// sources is claimed once: the election picks one block among all of them).  Rows of >= 32
+// floats only (the sort push); RS_ERR_UNSUPPORTED otherwise (the caller pushes one by one).
+// ---------------------------------------------------------------------------------------------
+static int push_group_shape(int nsrc, const int64_t* B, const int* F, int64_t* bmax, int* ftot) {
+  if (nsrc <= 0 || nsrc > rs_push::kMaxSrc || !B || !F) return RS_ERR_ARG;
+  int64_t bm = 0, ft = 0;
+  for (int k = 0; k < nsrc; ++k) {
+    if (B[k] < 0 || F[k] <= 0) return RS_ERR_ARG;
+    if (B[k] > INT32_MAX / 2) return RS_ERR_UNSUPPORTED;
+    bm = B[k] > bm ? B[k] : bm;
+    ft += F[k];
+  }
+  if (ft > 65535) return RS_ERR_UNSUPPORTED;
+  *bmax = bm;
+  *ftot = (int)ft;
+  return RS_OK;
+}
+
+RS_API int64_t rs_sparse_push_group_workspace_bytes(int nsrc, const int64_t* B, const int* F) {
+  int64_t bmax = 0;
+  int ftot = 0;
+  if (push_group_shape(nsrc, B, F, &bmax, &ftot) != RS_OK) return -1;
+  return rs_push::grid_blocks(bmax, ftot) * (1 + rs_push::kCap) * 4;
+}
+
+RS_API int rs_sparse_grad_accumulate_group(void* stream, int nsrc, const int32_t* const* rows,
+                                           const float* const* dout, const int64_t* B, const int* F,
+                                           const int64_t* dout_ld, const int64_t* dout_fstride,
+                                           int dim, float* grad_table, int32_t* flag,
+                                           int32_t* touched, int32_t* n_touched,
+                                           int32_t touched_cap, void* workspace,
+                                           int64_t workspace_bytes) {
+  using namespace rs_push;
+  if (!rows || !dout || !dout_ld || !dout_fstride || !grad_table || !flag || dim <= 0)
+    return RS_ERR_ARG;
+  if (touched && !n_touched) return RS_ERR_ARG;
+  int64_t bmax = 0;
+  int ftot = 0;
+  const int st = push_group_shape(nsrc, B, F, &bmax, &ftot);
+  if (st != RS_OK) return st;
+  const size_t lds = sort_lds_bytes(dim);
+  if (dim < 32 || dim % 4 != 0 || (int64_t)lds > lds_per_block()) return RS_ERR_UNSUPPORTED;
+  PushSrcs g{};
+  g.n = nsrc;
+  int f0 = 0;
+  for (int k = 0; k < nsrc; ++k) {
+    if (!rows[k] || !dout[k]) return RS_ERR_ARG;
+    if (dout_ld[k] % 4 != 0 || dout_fstride[k] % 4 != 0 || ((uintptr_t)dout[k] & 15) != 0)
+      return RS_ERR_UNSUPPORTED;
+    g.s[k] = PushSrc{rows[k], dout[k], dout_ld[k], dout_fstride[k], B[k], F[k], f0};
+    f0 += F[k];
+  }
+  if (bmax == 0) return RS_OK;
+  const int64_t nblk = grid_blocks(bmax, ftot);
+  if (nblk > INT32_MAX) return RS_ERR_UNSUPPORTED;
+  if (touched && (!workspace || workspace_bytes < nblk * (1 + kCap) * 4)) return RS_ERR_ARG;
+  hipStream_t s = rs_stream(stream);
+  int32_t* ws_cnt = touched ? static_cast<int32_t*>(workspace) : nullptr;
+  int32_t* ws_rows = touched ? ws_cnt + nblk : nullptr;
+  const int tile = tile_for(bmax, ftot);
+  dim3 grid((unsigned)((bmax + tile - 1) / tile), (unsigned)ftot);
+  int LS = 1;
+  while (LS < dim && LS < 64) LS <<= 1;
+  if (LS == 32)
+    push_sort_kernel<32><<<grid, kThreads, lds, s>>>(g, dim, 1.0f, tile, grad_table, flag, ws_cnt, ws_rows);
+  else if (LS == 64)
+    push_sort_kernel<64><<<grid, kThreads, lds, s>>>(g, dim, 1.0f, tile, grad_table, flag, ws_cnt, ws_rows);
+  else
+    return RS_ERR_UNSUPPORTED;
   if (touched)
     push_claim_kernel<<<(unsigned)nblk, kThreads, 0, s>>>(ws_cnt, ws_rows, flag, touched, n_touched,
                                                           touched_cap);

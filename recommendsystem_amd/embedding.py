@@ -17,6 +17,8 @@ claimed once per step); ``SparseAdam.step`` updates exactly the touched rows.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -25,6 +27,9 @@ from torch import nn
 
 from . import _lib
 from ._lib import call, ptr, stream_handle
+
+# grouped single-hot pushes in Trainer steps (RS_PUSH_GROUP=0: one launch per lookup layer, A/B)
+_PUSH_GROUP = os.environ.get("RS_PUSH_GROUP", "1") != "0"
 
 HASH_MODES = {"mod": 0, "splitmix": 1}
 COMBINERS = {"sum": 0, "mean": 1, "sqrtn": 2}
@@ -94,6 +99,10 @@ class SparseTable:
         self.deterministic = False
         self._sorted_ws = None
         self._push_ws = None
+        # grouped pushes (begin_push_group / end_push_group, Trainer steps): the single-hot
+        # pushes of one backward, recorded and issued as ONE rs_sparse_grad_accumulate_group
+        self._deferred = None
+        self._group_ws = None
         # autograd anchor: lets the lookup's backward run (it returns no dense gradient)
         self.anchor = torch.zeros((), device=device, dtype=torch.float32, requires_grad=True)
 
@@ -123,8 +132,57 @@ class SparseTable:
         return torch.cat(parts) if parts else torch.empty(0, dim)
 
     # ---- push / update -----------------------------------------------------------------
+    def _groupable(self, offsets, dout, dout_ld, dout_fstride) -> bool:
+        """rs_sparse_grad_accumulate_group's domain: single-hot, >= 32-float rows, 16-B aligned
+        gradient rows, the non-deterministic push."""
+        return (offsets is None and not self.deterministic and self.dim >= 32 and
+                dout.data_ptr() % 16 == 0 and dout_ld % 4 == 0 and dout_fstride % 4 == 0)
+
+    def begin_push_group(self) -> None:
+        """Record this table's single-hot pushes until end_push_group (one backward's pushes
+        from several lookup layers into this table: staytime/VideoDnn.py:217-244 declares every
+        column of the shared table in ONE tn.layers.EmbeddingFeatures)."""
+        if _PUSH_GROUP:
+            self._deferred = []
+
+    def end_push_group(self) -> None:
+        """Issue the recorded pushes: one grouped launch (+ one claim launch) per <= 8 sources."""
+        d, self._deferred = self._deferred, None
+        if not d:
+            return
+        for k0 in range(0, len(d), 8):
+            chunk = d[k0:k0 + 8]
+            if len(chunk) == 1:
+                rows, B, F, dout, ld, fs = chunk[0]
+                self.accumulate(rows, None, B, F, dout, ld, fs, 0)
+                continue
+            n = len(chunk)
+            keep = [_lib.c_array(ctypes.c_void_p, [ptr(c[0]) for c in chunk]),
+                    _lib.c_array(ctypes.c_void_p, [ptr(c[3]) for c in chunk]),
+                    _lib.c_array(ctypes.c_int64, [c[1] for c in chunk]),
+                    _lib.c_array(ctypes.c_int32, [c[2] for c in chunk]),
+                    _lib.c_array(ctypes.c_int64, [c[4] for c in chunk]),
+                    _lib.c_array(ctypes.c_int64, [c[5] for c in chunk])]  # (alive for the calls)
+            rp, dp, bp, fp, lp, sp = (a for _, a in keep)
+            scan = self.mode == "scan"
+            ws, wsn = None, 0
+            if not scan:
+                need = int(_lib.load().rs_sparse_push_group_workspace_bytes(n, bp, fp))
+                if need < 0:
+                    raise ValueError("grouped push: unsupported source shapes")
+                if self._group_ws is None or self._group_ws.numel() < need:
+                    self._group_ws = torch.empty(need, device=self.weight.device, dtype=torch.uint8)
+                ws, wsn = ptr(self._group_ws), self._group_ws.numel()
+            call("rs_sparse_grad_accumulate_group", stream_handle(), n, rp, dp, bp, fp, lp, sp,
+                 self.dim, ptr(self.grad), ptr(self.flag), None if scan else ptr(self.touched),
+                 None if scan else ptr(self.n_touched), self.touched_cap, ws, wsn)
+
     def accumulate(self, rows: torch.Tensor, offsets: torch.Tensor | None, B: int, F: int,
                    dout: torch.Tensor, dout_ld: int, dout_fstride: int, combiner: int) -> None:
+        if self._deferred is not None and self._groupable(offsets, dout, dout_ld, dout_fstride):
+            # (the record keeps rows / dout alive until the grouped launch reads them)
+            self._deferred.append((rows, int(B), int(F), dout, int(dout_ld), int(dout_fstride)))
+            return
         scan = self.mode == "scan"
         if self.deterministic:
             n = rows.numel()

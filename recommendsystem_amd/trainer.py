@@ -148,11 +148,27 @@ class Trainer:
             ra, rp = _lib.c_array(ctypes.c_float, [float(l2) for _, _, l2 in chunk])
             call("rs_l1l2_grad_grouped", s, n, wp, gp, cp, lp, rp)
 
+    def _backward(self, loss):
+        """loss.backward with each replicated table's single-hot pushes issued as one grouped
+        launch after the backward (SparseTable.begin_push_group; config 5: five pushes into the
+        shared 10 M-row table -> one push + one claim launch)."""
+        grp = [t for t in self.tables if not is_sharded(t) and hasattr(t, "begin_push_group")]
+        for t in grp:
+            t.begin_push_group()
+        try:
+            loss.backward(self._seed)
+        except BaseException:
+            for t in grp:
+                t._deferred = None  # a failed backward pushes nothing
+            raise
+        for t in grp:
+            t.end_push_group()
+
     def _step(self, *batch):
         loss = self.model.loss(*batch)
         if self.bucketer is not None:
             self.bucketer.arm(loss)  # buckets go out as backward produces their gradients
-        loss.backward(self._seed)
+        self._backward(loss)
         if self.bucketer is not None:
             self.bucketer.finish(self._regularise)
         else:
@@ -292,7 +308,7 @@ class Trainer:
             mod._calls = 0
         with _lib.seed_offset(self.step_count):
             loss = self.model.loss(*batch)
-            loss.backward(self._seed)
+            self._backward(loss)
         self._regularise()
         return loss
 
