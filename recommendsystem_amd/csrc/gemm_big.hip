@@ -1,4 +1,4 @@
-// Large fp32 GEMMs of the MLP towers (the Dense layers of >= 2^26 multiply-adds: the config-3
+// Large fp32 GEMMs of the MLP towers (the Dense layers of >= 2^29 multiply-adds, forwards with K >= 1024 from 2^25: the config-3
 // trunk and experts, the config-5 experts, the 400-bin head and the DSSM teacher; reference call
 // sites staytime/VideoDnn.py:130-148,168-169, rank/multi_head/multidnn.py:80-92,
 // rough_rank/model.py:24-27).  Hand-written for gfx950; replaces the round-5 hipBLASLt route.
@@ -542,10 +542,14 @@ size_t lds_bytes(int bm, int bn, bool za, bool zb) {
 // the 9 trunk products.)  RS_GEMM_BIG_TILE=BMxBN[,S] forces a choice (tuning runs).
 Plan plan(int64_t M, int64_t N, int64_t R, bool allow_split, bool z) {
   static const Tile cand[4] = {{128, 128}, {128, 64}, {64, 64}, {128, 32}};
+  // (N <= 32: the 128 x 32 tile first -- it pads the outputs to 32 columns, not 64, so at equal
+  // modelled cost it does half the MFMA work: 2048 x 1456 x 22 forward 16.0 -> 14.8 us)
+  static const Tile cand_narrow[4] = {{128, 32}, {128, 128}, {128, 64}, {64, 64}};
+  const Tile* cands = N <= 32 ? cand_narrow : cand;
   Plan best{};
   double bc = 0;
   for (int c = 0; c < 4; ++c) {
-    const int bm = cand[c].bm, bn = cand[c].bn;
+    const int bm = cands[c].bm, bn = cands[c].bn;
     if (bn == 32 && N > 32) continue;
     const int64_t tiles = cdiv(M, bm) * cdiv(N, bn);
     for (int64_t s = 1; s <= (allow_split ? 16 : 1); s *= 2) {
@@ -673,7 +677,9 @@ bool wanted_fwd(int64_t M, int64_t N, int64_t K) {
     const char* e = getenv("RS_GEMM_BIG");
     return !e || atoi(e) != 0;
   }();
-  return wanted(M, N, K) || (on && K >= 1024 && M * N * K >= ((int64_t)1 << 26));
+  // (from 2^25 multiply-adds: config 5's 2048 x 1456 x 22 forward 26.9 us on the engine, 14.8 on
+  // these kernels -- a long reduction split over the chip; profiles/r06/gemm/tile_small.txt)
+  return wanted(M, N, K) || (on && K >= 1024 && M * N * K >= ((int64_t)1 << 25));
 }
 
 int fwd(hipStream_t s, const float* X, int64_t M, int64_t K, int64_t ldx, const float* W,
@@ -700,7 +706,7 @@ int fwd(hipStream_t s, const float* X, int64_t M, int64_t K, int64_t ldx, const 
 }
 
 // From 2^29 multiply-adds the big kernels beat the round-4 engine on every configs 3 / 5 product;
-// between 2^26 and 2^29 only the forward with a long reduction (>= 1024: split-K fills the
+// between 2^25 and 2^29 only the forward with a long reduction (>= 1024: split-K fills the
 // chip) does -- the short-reduction shapes (2048 x 224 x 1152, 2048 x 528 x 400, 2048 x 832 x
 // 128) keep the engine (tools/r06_shapes.sh, profiles/r06/gemm/shapes.txt)
 bool wanted(int64_t m, int64_t n, int64_t k) {
