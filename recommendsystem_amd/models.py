@@ -18,6 +18,7 @@ three staytime experts' first layers plus the three MMoE gate nets' first layers
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Sequence
 
@@ -309,6 +310,10 @@ class MultiHeadRanker(nn.Module):
         F, E = cfg.num_fields, cfg.embed_dim
         self.table = SparseTable(F * cfg.vocab_per_field, E, SparseAdam(cfg.lr_sparse), device=dev,
                                  seed=seed, max_touched=max_touched)
+        # list mode: the scan form (a 212 MB flag sweep of the 53 M-row table instead of claims +
+        # the touched list) measured 1.72 vs 1.656 ms per step (profiles/r06/push/mh_scan.txt);
+        # RS_MH_SCAN=1 selects it at world 1 (A/B)
+        self.table.prefer_scan = os.environ.get("RS_MH_SCAN", "0") == "1"
         self.embedding = EmbeddingFeatures(self.table, [cfg.vocab_per_field] * F, combiner="mean")
         self.interact = InteractingLayer(1, E, 2, use_dropout=True, dropout_rate=cfg.dropout_rate,
                                          use_res=True, seed=seed + 1, device=dev)
