@@ -566,6 +566,18 @@ Plan plan(int64_t M, int64_t N, int64_t R, bool allow_split, bool z) {
       }
     }
   }
+  // Outputs just past a multiple of 64 columns (config 3's N = 273): 128 x 32 tiles trim >= 10 %
+  // of the padded columns; split so the grid holds ~4 blocks per CU (<= 1536 blocks) -- measured
+  // best of each product's tile x split sweep (forward 4096 x 1616 x 273 71.3 -> 66.9 us, weight
+  // 89.8 -> 73.6 us; profiles/r06/gemm/tile_n273.txt).  The model above ties these tiles (both pad
+  // their work to the same per-CU count) and under-prices the 4-B DMA path at one block per CU.
+  if (allow_split && N > 32 && cdiv(N, 32) * 32 * 10 <= cdiv(N, 64) * 64 * 9) {
+    const int64_t tiles = cdiv(M, 128) * cdiv(N, 32);
+    int64_t s = 1;
+    while (s < 16 && tiles * s * 2 <= 1536 && R / (s * 2) >= 128) s *= 2;
+    const int64_t rc = cdiv(cdiv(R, s), BK) * BK;
+    best = Plan{128, 32, (int)cdiv(R, rc), rc, stages_of(z)};
+  }
   static const int forced = [] {
     const char* e = getenv("RS_GEMM_BIG_TILE");
     int bm = 0, bn = 0, s = 0;
