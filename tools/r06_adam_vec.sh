@@ -1,5 +1,6 @@
 #!/bin/bash
-# vectorised list-mode sparse Adam: whole GPU suite, then config 3 A/B against the scalar kernel
+# vectorised list-mode sparse Adam (built, measured no faster, removed in the same round: this is
+# the script that produced profiles/r06/push/sparse_adam_vec_ab.txt): whole GPU suite, then config 3 A/B
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/adamvec
